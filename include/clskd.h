@@ -1,0 +1,214 @@
+/*
+ * clskd.h — C ABI of libclskd_hip.so, the MI355X (gfx950) hot path of DCCRN + CLSKD.
+ *
+ * The reference has no FFI: its hot path sits behind PyTorch nn.Module calls
+ * (SURVEY.md §8 b).  Each entry point below replaces one reference operator; the Python
+ * package `clskd` (speech-enhancement-clskd_amd/clskd) binds them with ctypes and keeps the
+ * reference's module/function names and signatures.
+ *
+ * Conventions
+ *   - Every pointer is a DEVICE pointer owned by the caller (no allocations are kept across
+ *     calls; no hidden host<->device copies or syncs, so every call is hipGraph-capturable).
+ *   - Activations use the "BFTC" layout: [batch][freq][time][channel], channel fastest.  The
+ *     reference's NCHW tensor x[b][c][f][t] is x_bftc[b][f][t][c].
+ *   - Work is enqueued on `stream` (a hipStream_t; NULL = default stream).
+ *   - Return 0 on success, a negative clskd_status otherwise; clskd_last_error() returns a
+ *     thread-local message.  No exceptions or aborts cross the ABI.
+ *   - fp32 storage; `compute` selects the MFMA operand type of GEMM-shaped ops.
+ */
+#ifndef CLSKD_H
+#define CLSKD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  CLSKD_OK = 0,
+  CLSKD_E_SHAPE = -1,
+  CLSKD_E_DTYPE = -2,
+  CLSKD_E_HIP = -3,
+  CLSKD_E_ARG = -4
+} clskd_status;
+
+typedef enum { CLSKD_F32 = 0, CLSKD_BF16 = 1 } clskd_compute;
+
+const char* clskd_last_error(void);
+int clskd_version(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Implicit-GEMM convolution over BFTC activations.
+ * Replaces: ComplexConv2d.forward (tools_for_model.py:236-262, packed [[Wr,-Wi],[Wi,Wr]]),
+ *           ComplexConvTranspose2d.forward (tools_for_model.py:303-330, polyphase),
+ *           ABF conv1/conv2/att 1x1 & 3x3 convs (framework.py:179-191),
+ *           ConvSTFT / ConviSTFT framing GEMMs (tools_for_model.py:53-67, 90-109),
+ *           nn.LSTM input projections and NavieComplexLSTM Linear projections
+ *           (tools_for_model.py:164-173).
+ *
+ * out[b, fo, to, n] = bias[n] + sum_k A[(b,fo,to), k] * W[n, k]
+ * A is gathered through a K table: for K index k with ktab[k] = {off, dF, dT}, s = kseg[k]:
+ *   fi = fo*stride_f + dF,  ti = to*stride_t + dT
+ *   A[(b,fo,to), k] = seg[s].ptr[b*sB + (fo*stride_f)*sF + (to*stride_t)*sT + off]
+ *                     if 0 <= fi < seg[s].F and 0 <= ti < seg[s].T, else 0
+ * where the host folds the displacement into off (off = cin + dF*sF + dT*sT).  K is padded to a
+ * multiple of 16 with entries whose dF = -32768 (always out of bounds) and zero weights.
+ * ConvTranspose2d(stride (2,1)) runs as two polyphase launches (output fo = 2*j + parity,
+ * of_mul = 2, of_add = parity) with the parity's taps in the K table.
+ * -------------------------------------------------------------------------------------- */
+#define CLSKD_MAX_SEGS 4
+
+typedef struct {
+  const float* ptr; /* segment base (already offset to its first channel / time) */
+  int64_t sB, sF, sT; /* element strides; channel stride is 1 inside a K-table entry */
+  int32_t F, T;       /* bounds for the gathered freq / time index */
+} clskd_seg;
+
+typedef struct {
+  int32_t off; /* element offset added after the row offset (cin*sC + dF*sF + dT*sT) */
+  int16_t dF;  /* freq displacement (bounds check) */
+  int16_t dT;  /* time displacement (bounds check) */
+} clskd_ktab_entry; /* 8 bytes; seg index is stored in ktab_seg[k] */
+
+typedef struct {
+  /* geometry: output rows are (b, fo, to), fo in [0,Fo), to in [0,To) */
+  int32_t B, Fo, To;
+  int32_t N, K;         /* output channels, reduction length */
+  int32_t stride_f;     /* fi = fo*stride_f + dF  (convT polyphase: fo=j, stride 1) */
+  int32_t stride_t;     /* ti = to*stride_t + dT */
+  int32_t nseg;
+  clskd_seg seg[CLSKD_MAX_SEGS];
+  const clskd_ktab_entry* ktab; /* device, K entries */
+  const uint8_t* kseg;          /* device, K entries: segment index of each k */
+  int32_t vec4;                 /* 1: every aligned group of 4 k's is 4 contiguous channels */
+  const float* weight; /* device [N][K] packed */
+  const float* bias;   /* device [N] or NULL */
+  /* output address: out + b*oB + (fo*of_mul+of_add)*oF + to*oT + (n/nlo)*oNhi + (n%nlo)*oNlo */
+  float* out;
+  int64_t oB, oF, oT, oNhi, oNlo;
+  int32_t nlo, of_mul, of_add;
+  int32_t compute; /* clskd_compute */
+} clskd_conv_desc;
+
+int clskd_conv2d_fwd(const clskd_conv_desc* d, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * BatchNorm2d (train or eval) + optional PReLU over a BFTC tensor of `rows` x C.
+ * Replaces nn.BatchNorm2d / nn.PReLU inside the encoder/decoder Sequentials
+ * (DCCRN.py:69-141) and the ABF BNs (framework.py:179-186).
+ *   clskd_bn_stats_partial: per-block fp64 partial sums -> partial[nblk][C][2]
+ *   clskd_bn_finalize: mean/var (biased) -> scale/shift; running stats update (momentum,
+ *                      unbiased var) applied `n_updates` times when running_* != NULL
+ *   clskd_bn_apply: y = x*scale[c] + shift[c]; if alpha: y = y>=0 ? y : alpha*y
+ * -------------------------------------------------------------------------------------- */
+int clskd_bn_stats_partial(const float* x, int64_t rows, int32_t C, double* partial,
+                           int32_t nblk, void* stream);
+int clskd_bn_finalize(const double* partial, int32_t nblk, int64_t rows, int32_t C,
+                      const float* gamma, const float* beta, float eps,
+                      float* running_mean, float* running_var, float momentum,
+                      int32_t n_updates, float* scale, float* shift, float* mean_out,
+                      float* var_out, void* stream);
+int clskd_bn_eval_coeffs(const float* running_mean, const float* running_var,
+                         const float* gamma, const float* beta, float eps, int32_t C,
+                         float* scale, float* shift, void* stream);
+int clskd_bn_apply(const float* x, float* y, int64_t rows, int32_t C, const float* scale,
+                   const float* shift, const float* alpha, void* stream);
+int32_t clskd_bn_partial_blocks(int64_t rows, int32_t C);
+
+/* ------------------------------------------------------------------------------------------
+ * Complex LSTM recurrence (tools_for_model.py:159-174, nn.LSTM gates i,f,g,o, zero state).
+ * gx:  [nws][nseq][T][4H]  precomputed x@W_ih^T + b_ih + b_hh (nws weight sets: real_lstm,
+ *      imag_lstm), with element stride: gx + ws*gx_ws + s*gx_seq + t*gx_t + g
+ * whh: [nws][4H][H];  out: h_t as out + ws*o_ws + s*o_seq + t*o_t + j
+ * -------------------------------------------------------------------------------------- */
+int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_seq, int64_t gx_t,
+                         const float* whh, int32_t nws, int32_t nseq, int32_t T, int32_t H,
+                         float* out, int64_t o_ws, int64_t o_seq, int64_t o_t, void* stream);
+
+/* real = a - b, imag = c + d  (tools_for_model.py:168-169); all [n] contiguous */
+int clskd_complex_combine(const float* rr, const float* ii, const float* ir, const float* ri,
+                          float* real_out, float* imag_out, int64_t n, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * STFT helpers.
+ * clskd_frame_pad: xp[b][j] = x[b][j - pad] with zero (mode 0) or reflect (mode 1) padding,
+ *                  j in [0, Lp); x is [B][L] with row stride ldx.
+ * clskd_mask_e:    DCCRN masking_mode 'E' (DCCRN.py:207-226) from spec [B][T][ldspec] (real
+ *                  bins 0..256 at 0.., imag at 257..) and the last decoder output
+ *                  mask[B][256][Tm][2] read at time t+1; writes est [B][T][ldest] (real at 0..,
+ *                  imag at 257.., zero tail) and optionally mask_r/mask_i [B][T][257].
+ * clskd_ola:       ConviSTFT overlap-add (tools_for_model.py:95-107): frames [B][T][400] ->
+ *                  wav[b][n] = (sum frames) / (sum window^2 + 1e-8), trimmed, clamp(-1,1)
+ *                  (DCCRN.py:235-237) when clamp != 0.
+ * -------------------------------------------------------------------------------------- */
+int clskd_frame_pad(const float* x, int64_t ldx, int32_t B, int32_t L, int32_t pad, int32_t Lp,
+                    int32_t mode, float* xp, void* stream);
+int clskd_mask_e(const float* spec, int32_t ldspec, const float* mask, int32_t Tm, int32_t B,
+                 int32_t T, float* est, int32_t ldest, float* mask_r, float* mask_i,
+                 void* stream);
+int clskd_ola(const float* frames, const float* window, int32_t B, int32_t T, int32_t win,
+              int32_t hop, int32_t out_len, int32_t trim, int32_t clamp, float* wav,
+              void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * ReviewKD ABF attention fusion (framework.py:209-217), mid = 64 channels:
+ *   y_up = nearest-interpolate(res [B][Fr][Tr][64] -> (F, T))
+ *   z = sigmoid(W[2][128] . [x; y_up] + b);  out = x*z0 + y_up*z1
+ * -------------------------------------------------------------------------------------- */
+int clskd_abf_fuse(const float* x, const float* res, int32_t B, int32_t F, int32_t T,
+                   int32_t Fr, int32_t Tr, const float* w, const float* b, float* out,
+                   void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * SPKD / Gram (framework.py:150-172).  A gram job views a tap as z_b = x[b][p][c0 .. c0+Cs)
+ * for p < P positions with position stride Ctot and batch stride sB.
+ * clskd_gram_partial: every job split in chunks of `chunk` positions; one 32x32 fp32 partial
+ *                     Gram slab per chunk; slabs[job_first_slab[j] + i].
+ * clskd_spkd_finalize: per pair (student job, teacher job): sum slabs in order, L1-normalise
+ *                     rows (normalize(G, p=1) — the reference passes 1 as p), loss =
+ *                     ||Gt-Gs||_F^2 (/B^2 if batchmean); writes losses[pair] and grams.
+ * -------------------------------------------------------------------------------------- */
+typedef struct {
+  const float* ptr;
+  int64_t sB;
+  int64_t P;
+  int32_t Ctot, c0, Cs;
+  int32_t chunk;      /* positions per slab */
+  int32_t first_slab; /* index of this job's first slab */
+  int32_t nslab;
+} clskd_gram_job;
+
+int clskd_gram_partial(const clskd_gram_job* jobs_dev, int32_t njobs, int32_t total_slabs,
+                       const int32_t* slab_job_dev, int32_t B, float* slabs, void* stream);
+int clskd_spkd_finalize(const clskd_gram_job* jobs_dev, const int32_t* pairs_dev,
+                        int32_t npairs, int32_t B, int32_t batchmean, const float* slabs,
+                        float* grams_s, float* grams_t, float* losses, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Losses.
+ * clskd_stft_mag_loss: one STFTLoss resolution (framework.py:16-101) from raw spectra
+ *   X, Y [rows][ld] (real part of bin f at f, imaginary at nbins+f); magnitudes
+ *   sqrt(max(re^2+im^2, 1e-7)).  Writes 256 per-block partials acc[256][3] (fp64) =
+ *   {sum (Y-X)^2, sum Y^2, sum |log Y - log X|}.
+ * clskd_stft_loss_finalize: out2[0] = factor_sc*||Y-X||_F/||Y||_F (SpectralConvergenge),
+ *   out2[1] = factor_mag*mean|log Y - log X| (LogSTFTMagnitude) over `count` elements.
+ * clskd_sisnr_rows: tools_for_loss.py:37-47 per row -> out[rows] (dB); two passes, fp64 sums.
+ * clskd_sum_f32: out[0] = scale * sum of a[0..n) (fixed order, fp64).
+ * clskd_stft_loss_finalize with accumulate != 0 adds into out2 (multi-resolution sum).
+ * -------------------------------------------------------------------------------------- */
+int clskd_stft_mag_loss(const float* X, const float* Y, int64_t rows, int32_t ld,
+                        int32_t nbins, double* acc, void* stream);
+int clskd_stft_loss_finalize(const double* acc, int64_t count, float factor_sc,
+                             float factor_mag, int32_t accumulate, float* out2, void* stream);
+int clskd_sisnr_rows(const float* s1, const float* s2, int32_t rows, int32_t L, int64_t ld1,
+                     int64_t ld2, float eps, float* out, void* stream);
+int clskd_sum_f32(const float* a, int32_t n, float scale, float* out, void* stream);
+
+/* small utilities */
+int clskd_zero_f64(double* p, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLSKD_H */

@@ -242,20 +242,26 @@ def mrstft_loss(x, y, fft_sizes=(512,), hop_sizes=(100,), win_lengths=(400,), fa
     return factor_sc * sc, factor_mag * mag
 
 
-def spkd_gram(z):
+def spkd_gram(z, dtype=None):
     """framework.py:155-157: G = normalize(z z^T, 1) over flatten(z,1).
 
     NB the reference passes ``1`` positionally to ``torch.nn.functional.normalize(input, p, dim)``,
     i.e. p=1 along the default dim=1: rows are L1-normalised (G_ij / max(sum_j |G_ij|, 1e-12)),
     not L2.  Pinned by tests/golden/losses.npz and clskd_step.npz."""
     z = torch.flatten(z, 1)
+    if dtype is not None:
+        z = z.to(dtype)
     return F.normalize(torch.matmul(z, torch.t(z)), p=1, dim=1)
 
 
-def spkd_loss(student, teacher, reduction="batchmean"):
-    """framework.py:150-172: ||G_t - G_s||_F^2 (/ B^2 for batchmean)."""
-    g_t = spkd_gram(teacher)
-    g_s = spkd_gram(student)
+def spkd_loss(student, teacher, reduction="batchmean", dtype=None):
+    """framework.py:150-172: ||G_t - G_s||_F^2 (/ B^2 for batchmean).
+
+    dtype=torch.float64 evaluates the same math exactly enough to serve as the parity reference at
+    full size: the reference's fp32 matmul over K ~ 2.6M elements carries ~1e-3 relative error in
+    the loss (measured, tests/diag_spkd_precision.py)."""
+    g_t = spkd_gram(teacher, dtype)
+    g_s = spkd_gram(student, dtype)
     loss = torch.norm(g_t - g_s) ** 2
     b = teacher.shape[0]
     return loss / (b ** 2) if reduction == "batchmean" else loss
@@ -336,7 +342,7 @@ def tap_contract(fwd):
                 clstm_img=fwd["clstm"][1].transpose(0, 1))
 
 
-def clskd_step(pt, ps, pabf, X, y, lstm_fn=lstm_torch):
+def clskd_step(pt, ps, pabf, X, y, lstm_fn=lstm_torch, gram_dtype=None):
     """distill.py:72-148 with local teacher/student.  Returns a dict of every loss term."""
     tf = dccrn_forward(pt, X, train=True, lstm_fn=lstm_fn)
     sf = dccrn_forward(ps, X, train=True, lstm_fn=lstm_fn)
@@ -346,10 +352,10 @@ def clskd_step(pt, ps, pabf, X, y, lstm_fn=lstm_torch):
     s_dec = review_kd_forward(pabf, s["decoder"], "decoder")
     student_preds = sf["out_wav"]  # distill.py:100 (second student forward: identical output)
     base = mrstft_loss(student_preds.squeeze(), y.squeeze())[1]
-    enc_terms = [spkd_loss(a, b) for a, b in zip(s_enc, t["encoder"])]
-    dec_terms = [spkd_loss(a, b) for a, b in zip(s_dec, t["decoder"])]
-    cr = spkd_loss(s["clstm_real"], t["clstm_real"])
-    ci = spkd_loss(s["clstm_img"], t["clstm_img"])
+    enc_terms = [spkd_loss(a, b, dtype=gram_dtype) for a, b in zip(s_enc, t["encoder"])]
+    dec_terms = [spkd_loss(a, b, dtype=gram_dtype) for a, b in zip(s_dec, t["decoder"])]
+    cr = spkd_loss(s["clstm_real"], t["clstm_real"], dtype=gram_dtype)
+    ci = spkd_loss(s["clstm_img"], t["clstm_img"], dtype=gram_dtype)
     total = base + sum(enc_terms) + sum(dec_terms) + cr + ci
     return dict(total=total, base=base, enc=enc_terms, dec=dec_terms, clstm_real=cr,
                 clstm_img=ci, student_wav=student_preds, teacher_wav=tf["out_wav"],

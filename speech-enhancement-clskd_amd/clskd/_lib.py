@@ -1,0 +1,115 @@
+"""ctypes binding of libclskd_hip.so (include/clskd.h).
+
+The product path has no CPU fallback: importing the ops on a machine without the built library
+or without a HIP device raises immediately.
+"""
+import ctypes as C
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libclskd_hip.so")
+
+MAX_SEGS = 4
+F32, BF16 = 0, 1
+
+
+class Seg(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("sB", C.c_int64), ("sF", C.c_int64), ("sT", C.c_int64),
+                ("F", C.c_int32), ("T", C.c_int32)]
+
+
+class KtabEntry(C.Structure):
+    _fields_ = [("off", C.c_int32), ("dF", C.c_int16), ("dT", C.c_int16)]
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [("B", C.c_int32), ("Fo", C.c_int32), ("To", C.c_int32), ("N", C.c_int32),
+                ("K", C.c_int32), ("stride_f", C.c_int32), ("stride_t", C.c_int32),
+                ("nseg", C.c_int32), ("seg", Seg * MAX_SEGS), ("ktab", C.c_void_p),
+                ("kseg", C.c_void_p), ("vec4", C.c_int32), ("weight", C.c_void_p),
+                ("bias", C.c_void_p), ("out", C.c_void_p), ("oB", C.c_int64), ("oF", C.c_int64),
+                ("oT", C.c_int64), ("oNhi", C.c_int64), ("oNlo", C.c_int64), ("nlo", C.c_int32),
+                ("of_mul", C.c_int32), ("of_add", C.c_int32), ("compute", C.c_int32)]
+
+
+class GramJob(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("sB", C.c_int64), ("P", C.c_int64), ("Ctot", C.c_int32),
+                ("c0", C.c_int32), ("Cs", C.c_int32), ("chunk", C.c_int32),
+                ("first_slab", C.c_int32), ("nslab", C.c_int32)]
+
+
+assert C.sizeof(KtabEntry) == 8
+assert C.sizeof(GramJob) == 48
+
+_p, _i32, _i64, _f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float
+
+SIGNATURES = {
+    "clskd_last_error": (C.c_char_p, []),
+    "clskd_version": (_i32, []),
+    "clskd_conv2d_fwd": (_i32, [C.POINTER(ConvDesc), _p]),
+    "clskd_bn_partial_blocks": (_i32, [_i64, _i32]),
+    "clskd_bn_stats_partial": (_i32, [_p, _i64, _i32, _p, _i32, _p]),
+    "clskd_bn_finalize": (_i32, [_p, _i32, _i64, _i32, _p, _p, _f32, _p, _p, _f32, _i32, _p, _p,
+                                 _p, _p, _p]),
+    "clskd_bn_eval_coeffs": (_i32, [_p, _p, _p, _p, _f32, _i32, _p, _p, _p]),
+    "clskd_bn_apply": (_i32, [_p, _p, _i64, _i32, _p, _p, _p, _p]),
+    "clskd_lstm_recurrent": (_i32, [_p, _i64, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _i64,
+                                    _i64, _i64, _p]),
+    "clskd_complex_combine": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p]),
+    "clskd_frame_pad": (_i32, [_p, _i64, _i32, _i32, _i32, _i32, _i32, _p, _p]),
+    "clskd_mask_e": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p]),
+    "clskd_ola": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p]),
+    "clskd_abf_fuse": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p]),
+    "clskd_gram_partial": (_i32, [_p, _i32, _i32, _p, _i32, _p, _p]),
+    "clskd_spkd_finalize": (_i32, [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
+    "clskd_stft_mag_loss": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p]),
+    "clskd_stft_loss_finalize": (_i32, [_p, _i64, _f32, _f32, _i32, _p, _p]),
+    "clskd_sisnr_rows": (_i32, [_p, _p, _i32, _i32, _i64, _i64, _f32, _p, _p]),
+    "clskd_sum_f32": (_i32, [_p, _i32, _f32, _p, _p]),
+    "clskd_zero_f64": (_i32, [_p, _i64, _p]),
+}
+
+
+def header_symbols():
+    """Function names declared in include/clskd.h (parsed, for the export test)."""
+    import re
+    hdr = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "clskd.h")
+    src = open(hdr).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(clskd_[a-z0-9_]+)\s*\(", src)))
+
+
+_LIB = None
+
+
+def load(require_gpu=True):
+    """Load the shared library.  Raises (never falls back) when missing."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libclskd_hip.so not built at {LIB_PATH}; run __graft_entry__.build()")
+        lib = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = lib
+    if require_gpu and not torch.cuda.is_available():
+        raise RuntimeError("clskd: no HIP device visible; the MI355X path has no CPU fallback")
+    return _LIB
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = _LIB.clskd_last_error().decode() if _LIB is not None else ""
+        raise RuntimeError(f"clskd {what} failed ({rc}): {msg}")
+
+
+def stream_ptr(device=None):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)

@@ -1,0 +1,52 @@
+"""In-tree build of libclskd_hip.so for gfx950 (hipcc, no JIT cache): the built .so lives next to
+this file so it travels with the repo snapshot to the GPU box."""
+import concurrent.futures as cf
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(os.path.dirname(HERE), "csrc")
+OUT = os.path.join(HERE, "libclskd_hip.so")
+OBJDIR = os.path.join(os.path.dirname(HERE), "build", "obj")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+SOURCES = ["capi.cpp", "conv_igemm.hip", "norm.hip", "lstm.hip", "loss.hip"]
+FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
+
+
+def _newer(src_files, target):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in src_files)
+
+
+def build(verbose=False, force=False):
+    os.makedirs(OBJDIR, exist_ok=True)
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    headers.append(os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "clskd.h"))
+    objs = []
+    jobs = []
+    for s in SOURCES:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(OBJDIR, s + ".o")
+        objs.append(obj)
+        if force or _newer([src] + headers, obj):
+            lang = ["-x", "hip"] if s.endswith(".hip") else []
+            jobs.append([HIPCC] + FLAGS + lang + ["-c", src, "-o", obj])
+    with cf.ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
+        for cmd, res in zip(jobs, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs)):
+            if res.returncode != 0:
+                raise RuntimeError(f"hipcc failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
+            if verbose and res.stderr.strip():
+                print(res.stderr)
+    if force or jobs or _newer(objs, OUT):
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", OUT] + objs
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(verbose=True))

@@ -1,0 +1,156 @@
+"""KnowledgeDistillation (distill.py:38-148) and the SPKD-output variant (distill_SPKD.py:37-87)
+as MI355X-native training-step objects.
+
+``KnowledgeDistillation.training_step((X, y), batch_idx)`` returns the same scalar loss as the
+reference: MRSTFT log-magnitude base loss + 14 SPKD terms (6 encoder ReviewKD pairs, 6 decoder
+ReviewKD pairs, clstm real/imag), with the local-DCCRN tap contract of SURVEY.md §8 a11.
+The whole fwd+loss step is HIP kernels: one shared ConvSTFT, the teacher and student
+forwards (train-mode BN), both ReviewKD fusions, ONE batched-Gram launch over all 28 taps,
+one SPKD finalize launch, the MRSTFT GEMM + reduction and a final sum.
+
+Deliberate equivalences (documented in DESIGN.md):
+  * distill.py:85 and :100 run the student forward twice on the same input in train mode; the
+    outputs are identical, so the step runs it once and applies the BN running-stat update twice.
+  * Teacher and student share the fixed ConvSTFT kernel (tools_for_model.py:44-47), so the input
+    spectrum is computed once.
+  * The reference builds NEW random ABF modules each step (distill.py:92-96); here the ABF
+    modules are built once (``abf_reinit='once'``) or re-drawn every step on the device
+    (``abf_reinit='step'``, kaiming_uniform(a=1) like framework.py:194-195).
+"""
+import torch
+import torch.nn as nn
+
+from . import config as cfg
+from . import ops
+from .framework import MultiResolutionSTFTLoss, SPKDLoss, build_review_kd
+from .model import DCCRN
+
+
+def _gram_bftc(t, c0=0, Cs=None):
+    B, Fn, Tn, Ct = t.shape
+    Cs = Ct if Cs is None else Cs
+    return ops.GramView(t, 0, Fn * Tn * Ct, Fn * Tn, Ct, c0, Cs)
+
+
+class KnowledgeDistillation(nn.Module):
+    """distill.py:38-229 without Lightning: same constructor and step signature."""
+
+    def __init__(self, teacher, student, sftf_loss=MultiResolutionSTFTLoss, spkd_loss=SPKDLoss,
+                 cfg=cfg, abf_reinit="once"):
+        super().__init__()
+        self.automatic_optimization = True
+        self.teacher = teacher
+        for p in self.teacher.parameters():
+            p.requires_grad = False
+        self.student = student
+        self.spkd_loss = spkd_loss
+        self.stft_loss = sftf_loss(fft_sizes=[512], win_lengths=[400], hop_sizes=[100])
+        self.cfg = cfg
+        self.abf_reinit = abf_reinit
+        self.review_encoder = build_review_kd(None, "encoder")
+        self.review_decoder = build_review_kd(None, "decoder")
+        self.last = None
+
+    def forward(self, x):
+        return self.student(x)
+
+    def configure_optimizers(self):
+        return torch.optim.Adam(self.student.parameters(), lr=self.cfg.learning_rate)
+
+    def _reinit_abf(self):
+        if self.abf_reinit != "step":
+            return
+        with torch.no_grad():
+            for rk in (self.review_encoder, self.review_decoder):
+                for abf in rk.abfs:
+                    nn.init.kaiming_uniform_(abf.conv1[0].weight, a=1)
+                    nn.init.kaiming_uniform_(abf.conv2[0].weight, a=1)
+                    if abf.att_conv is not None:
+                        abf.att_conv[0].reset_parameters()
+
+    def training_step(self, batch, batch_idx=0, return_parts=False):
+        X, y = batch
+        out = clskd_step(self.teacher, self.student, self.review_encoder, self.review_decoder,
+                         self.stft_loss, X, y, reinit=self._reinit_abf)
+        self.last = out
+        if return_parts:
+            return out
+        return out["loss"]
+
+
+@torch.no_grad()
+def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y, reinit=None):
+    """One CLSKD fwd+loss step (distill.py:72-148).  Returns a dict of device tensors."""
+    if not (isinstance(teacher, DCCRN) and isinstance(student, DCCRN)):
+        raise TypeError("clskd_step expects clskd.DCCRN teacher and student")
+    X = X.float()
+    if X.dim() == 3:
+        X = X.squeeze(1)
+    X = X.contiguous()
+    y = y.float().reshape(X.shape[0], -1).contiguous()
+    B = X.shape[0]
+    if reinit is not None:
+        reinit()
+    dev = X.device
+    spec = teacher.spectrum(X)
+    # both ConvSTFTs are the fixed (win 400, hop 100, fft 512) kernel of the same window type
+    s_spec = spec if teacher.win_type == student.win_type else None
+    tf = teacher.run(X, train=teacher.training, bn_updates=1, spec=spec, want_masks=False)
+    sf = student.run(X, train=student.training, bn_updates=2 if student.training else 0,
+                     spec=s_spec, want_masks=False)
+    # ReviewKD on the student taps (distill.py:92-96); tap contract SURVEY.md §8 a11
+    s_enc = review_encoder.forward_bftc(sf["enc"])
+    s_dec = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5])
+    t_dec = [tf["dec_in"]] + tf["dec"][:5]
+    pairs = [(_gram_bftc(a), _gram_bftc(b)) for a, b in zip(s_enc, tf["enc"])]
+    pairs += [(_gram_bftc(a), _gram_bftc(b)) for a, b in zip(s_dec, t_dec)]
+    Chs = sf["dec_in"].shape[-1] // 2
+    Cht = tf["dec_in"].shape[-1] // 2
+    pairs += [(_gram_bftc(sf["dec_in"], 0, Chs), _gram_bftc(tf["dec_in"], 0, Cht)),
+              (_gram_bftc(sf["dec_in"], Chs, Chs), _gram_bftc(tf["dec_in"], Cht, Cht))]
+    buf = torch.empty(2 + len(pairs), dtype=torch.float32, device=dev)  # [sc, mag, spkd...]
+    ops.spkd_losses(pairs, B, batchmean=True, out=buf[2:])
+    # MRSTFT base loss on (student wav, clean) (distill.py:100-101) -> buf[0:2]
+    stft_loss(sf["out_wav"], y, out2=buf[0:2])
+    total = torch.empty((), dtype=torch.float32, device=dev)
+    ops.sum_f32(buf[1:], total)
+    return dict(loss=total, base=buf[1], sc=buf[0], spkd=buf[2:], enc=buf[2:8], dec=buf[8:14],
+                clstm_real=buf[14], clstm_img=buf[15], student_wav=sf["out_wav"],
+                teacher_wav=tf["out_wav"], s_enc=s_enc, s_dec=s_dec, t=tf, s=sf)
+
+
+class SPKDDistillation(nn.Module):
+    """distill_SPKD.py:37-87: MRSTFT base + SPKD on the output waveforms (config C4)."""
+
+    def __init__(self, teacher, student, sftf_loss=MultiResolutionSTFTLoss, spkd_loss=SPKDLoss,
+                 cfg=cfg):
+        super().__init__()
+        self.teacher = teacher
+        for p in self.teacher.parameters():
+            p.requires_grad = False
+        self.student = student
+        self.spkd_loss = spkd_loss
+        self.stft_loss = sftf_loss(fft_sizes=[512], win_lengths=[400], hop_sizes=[100])
+        self.cfg = cfg
+
+    def forward(self, x):
+        return self.student(x)
+
+    @torch.no_grad()
+    def training_step(self, batch, batch_idx=0, return_parts=False):
+        X, y = batch
+        X = X.float().reshape(X.shape[0], -1).contiguous()
+        y = y.float().reshape(X.shape[0], -1).contiguous()
+        spec = self.teacher.spectrum(X)
+        s = self.student.run(X, train=self.student.training, bn_updates=1, spec=spec,
+                             want_masks=False)["out_wav"]
+        t = self.teacher.run(X, train=self.teacher.training, bn_updates=1, spec=spec,
+                             want_masks=False)["out_wav"]
+        buf = torch.empty(3, dtype=torch.float32, device=X.device)
+        self.stft_loss(s, y, out2=buf[0:2])
+        ops.spkd_losses([(ops.gram_view(s), ops.gram_view(t))], X.shape[0], out=buf[2:3])
+        total = torch.empty((), dtype=torch.float32, device=X.device)
+        ops.sum_f32(buf[1:], total)
+        if return_parts:
+            return dict(loss=total, base=buf[1], spkd=buf[2], student_wav=s, teacher_wav=t)
+        return total

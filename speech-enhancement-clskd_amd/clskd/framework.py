@@ -1,0 +1,288 @@
+"""framework.py drop-in: MultiResolutionSTFTLoss, SPKDLoss, ABF / ReviewKD / build_review_kd.
+
+Same class names, constructor arguments and return conventions as the reference
+(``framework.py:16-284``); arithmetic runs in libclskd_hip.so.  Feature maps may be any NCHW
+tensors; BFTC buffers produced by ``clskd.DCCRN`` (exposed as permuted NCHW views) are consumed
+without copies.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import ops
+from .ops import OutMap, Seg, SegGeom, seg_bftc
+
+# --------------------------------------------------------------------------------------------
+# helpers
+# --------------------------------------------------------------------------------------------
+
+
+def to_bftc(x):
+    """NCHW tensor -> contiguous BFTC tensor (no copy when x is a permuted BFTC buffer)."""
+    if x.dim() != 4:
+        raise ValueError(f"expected an NCHW feature map, got shape {tuple(x.shape)}")
+    B, Cn, Fn, Tn = x.shape
+    if x.stride() == (Fn * Tn * Cn, 1, Tn * Cn, Cn):
+        return x.permute(0, 2, 3, 1)  # contiguous view of the underlying BFTC storage
+    return x.permute(0, 2, 3, 1).contiguous().float()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2)
+
+
+def _pv(*ts):
+    return tuple((t.data_ptr(), t._version) for t in ts)
+
+
+# --------------------------------------------------------------------------------------------
+# STFT losses (framework.py:16-146)
+# --------------------------------------------------------------------------------------------
+class _StftPlan:
+    """Framing GEMM plan of one resolution: torch.stft(center=True, reflect, onesided) with a
+    win_length window centred in fft_size, as a hop-grouped conv over the reflect-padded signal."""
+
+    def __init__(self, fft_size, hop, win, window):
+        self.fft, self.hop, self.win = fft_size, hop, win
+        self.off = (fft_size - win) // 2
+        self.KT = -(-win // hop)
+        w = np.zeros(self.KT * hop, np.float64)
+        w[:win] = window.double().cpu().numpy()
+        n = np.arange(self.KT * hop, dtype=np.float64) + self.off
+        f = np.arange(fft_size // 2 + 1, dtype=np.float64)[:, None]
+        ang = 2.0 * np.pi * f * n[None, :] / fft_size
+        basis = np.concatenate([np.cos(ang) * w, -np.sin(ang) * w], 0)  # [fft+2, KT*hop]
+        self.basis_cpu = torch.from_numpy(basis.astype(np.float32))
+        self._dev = {}
+
+    def basis(self, dev):
+        if dev not in self._dev:
+            self._dev[dev] = ops.pack_weight(self.basis_cpu.to(dev).unsqueeze(1), self.KT * self.hop)
+        return self._dev[dev]
+
+    def spectrum(self, x):
+        B, L = x.shape
+        nb = self.fft // 2 + 1
+        Tm = 1 + L // self.hop
+        pad = self.fft // 2
+        Lr = L + 2 * pad + self.KT * self.hop
+        Lr += (-Lr) % 4
+        xr = torch.empty(B, Lr, device=x.device, dtype=torch.float32)
+        ops.frame_pad(x, pad, Lr, 1, xr)
+        X = torch.empty(B, Tm, 2 * nb, device=x.device, dtype=torch.float32)
+        seg = Seg(xr, self.off, SegGeom(self.hop, Lr, 0, self.hop, 1, Tm + self.KT))
+        ops.conv([seg], [(0, kt) for kt in range(self.KT)], B, 1, Tm, 2 * nb,
+                 self.basis(x.device), None, X, OutMap(Tm * 2 * nb, 0, 2 * nb))
+        return X
+
+
+class STFTLoss(nn.Module):
+    """framework.py:72-101."""
+
+    def __init__(self, fft_size=1024, shift_size=120, win_length=600, window="hann_window"):
+        super().__init__()
+        self.fft_size, self.shift_size, self.win_length = fft_size, shift_size, win_length
+        self.register_buffer("window", getattr(torch, window)(win_length))
+        self._plan = _StftPlan(fft_size, shift_size, win_length, self.window)
+
+    def accumulate(self, x, y, out2, factor_sc, factor_mag, accumulate):
+        x = x.reshape(-1, x.shape[-1]).float().contiguous()
+        y = y.reshape(-1, y.shape[-1]).float().contiguous()
+        X = self._plan.spectrum(x)
+        Y = self._plan.spectrum(y)
+        return ops.stft_mag_loss(X, Y, self.fft_size // 2 + 1, factor_sc, factor_mag, out2,
+                                 accumulate)
+
+    def forward(self, x, y):
+        out2 = self.accumulate(x, y, None, 1.0, 1.0, False)
+        return out2[0], out2[1]
+
+
+class MultiResolutionSTFTLoss(nn.Module):
+    """framework.py:104-146: returns (factor_sc * mean sc, factor_mag * mean log-mag L1)."""
+
+    def __init__(self, fft_sizes=[1024, 2048, 512], hop_sizes=[120, 240, 50],
+                 win_lengths=[600, 1200, 240], window="hann_window", factor_sc=0.1,
+                 factor_mag=0.1):
+        super().__init__()
+        assert len(fft_sizes) == len(hop_sizes) == len(win_lengths)
+        self.stft_losses = nn.ModuleList()
+        for fs, ss, wl in zip(fft_sizes, hop_sizes, win_lengths):
+            self.stft_losses += [STFTLoss(fs, ss, wl, window)]
+        self.factor_sc = factor_sc
+        self.factor_mag = factor_mag
+
+    def forward(self, x, y, out2=None):
+        R = len(self.stft_losses)
+        for r, f in enumerate(self.stft_losses):
+            out2 = f.accumulate(x, y, out2, self.factor_sc / R, self.factor_mag / R, r > 0)
+        return out2[0], out2[1]
+
+
+# --------------------------------------------------------------------------------------------
+# SPKD (framework.py:150-172)
+# --------------------------------------------------------------------------------------------
+class SPKDLoss(nn.Module):
+    """Similarity-preserving KD: G = normalize(z z^T, p=1) per side, ||G_t - G_s||_F^2 (/ B^2).
+
+    NB the reference's ``normalize(torch.matmul(z, torch.t(z)), 1)`` passes 1 as p (L1 rows)."""
+
+    def __init__(self, student_output, teacher_output, reduction, **kwargs):
+        super().__init__()
+        self.student_outputs = student_output
+        self.teacher_outputs = teacher_output
+        self.reduction = reduction
+
+    def matmul_and_normalize(self, z):
+        _, gs, _ = ops.spkd_losses([(ops.gram_view(z), ops.gram_view(z))], z.shape[0], True, True)
+        return gs[0]
+
+    def compute_spkd_loss(self, teacher_outputs, student_outputs):
+        B = teacher_outputs.shape[0]
+        loss = ops.spkd_losses([(ops.gram_view(student_outputs), ops.gram_view(teacher_outputs))],
+                               B, batchmean=False)
+        return loss[0]
+
+    def forward(self, *args, **kwargs):
+        B = self.teacher_outputs.shape[0]
+        loss = ops.spkd_losses([(ops.gram_view(self.student_outputs),
+                                 ops.gram_view(self.teacher_outputs))], B,
+                               batchmean=self.reduction == "batchmean")
+        return loss[0]
+
+
+# --------------------------------------------------------------------------------------------
+# ABF / ReviewKD (framework.py:176-284)
+# --------------------------------------------------------------------------------------------
+class ABF(nn.Module):
+    """framework.py:176-222.  Parameters are standard Conv2d/BatchNorm2d containers; forward
+    runs conv1(1x1)+BN -> [nearest upsample + attention fuse] -> conv2(3x3)+BN in HIP."""
+
+    def __init__(self, in_channel, mid_channel, out_channel, fuse):
+        super().__init__()
+        self.conv1 = nn.Sequential(nn.Conv2d(in_channel, mid_channel, kernel_size=1, bias=False),
+                                   nn.BatchNorm2d(mid_channel))
+        self.conv2 = nn.Sequential(nn.Conv2d(mid_channel, out_channel, kernel_size=3, stride=1,
+                                             padding=1, bias=False),
+                                   nn.BatchNorm2d(out_channel))
+        if fuse:
+            self.att_conv = nn.Sequential(nn.Conv2d(mid_channel * 2, 2, kernel_size=1), nn.Sigmoid())
+        else:
+            self.att_conv = None
+        nn.init.kaiming_uniform_(self.conv1[0].weight, a=1)
+        nn.init.kaiming_uniform_(self.conv2[0].weight, a=1)
+        self._wcache = {}
+
+    def _weights(self):
+        ps = [self.conv1[0].weight, self.conv2[0].weight]
+        if self.att_conv is not None:
+            ps += [self.att_conv[0].weight, self.att_conv[0].bias]
+        ver = _pv(*ps)
+        ent = self._wcache.get("w")
+        if ent is None or ent[0] != ver:
+            with torch.no_grad():
+                w1 = self.conv1[0].weight  # [mid, in, 1, 1]
+                w1p = ops.pack_weight(w1.reshape(w1.shape[0], 1, w1.shape[1]), w1.shape[1])
+                w2 = self.conv2[0].weight  # [out, mid, 3, 3]
+                w2p = ops.pack_weight(w2.permute(0, 2, 3, 1).reshape(w2.shape[0], 9, w2.shape[1]),
+                                      9 * w2.shape[1])
+                att = None
+                if self.att_conv is not None:
+                    att = (self.att_conv[0].weight.reshape(2, -1).float().contiguous(),
+                           self.att_conv[0].bias.float().contiguous())
+            ent = (ver, (w1p, w2p, att))
+            self._wcache["w"] = ent
+        return ent[1]
+
+    def forward_bftc(self, x, y=None, shape=None, out_shape=None, train=None):
+        """x: BFTC [B][F][T][Cin]; y: BFTC residual [B][Fr][Tr][mid].  Returns (out, x_fused) BFTC."""
+        train = self.training if train is None else train
+        B, Fn, Tn, Cin = x.shape
+        w1p, w2p, att = self._weights()
+        mid = w1p.shape[0]
+        dev = x.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        x1 = torch.empty(B, Fn, Tn, mid, **f32)
+        ops.conv([seg_bftc(x)], [(0, 0)], B, Fn, Tn, mid, w1p, None, x1,
+                 OutMap(Fn * Tn * mid, Tn * mid, mid))
+        bn = self.conv1[1]
+        ops.batch_norm_bftc(x1, x1, bn.weight, bn.bias, bn.running_mean, bn.running_var, train,
+                            bn.momentum, bn.eps, 1)
+        if self.att_conv is not None:
+            if shape != Fn:  # the reference's torch.cat would fail as well (framework.py:213-216)
+                raise ValueError(f"ABF fuse: residual upsampled to F={shape} but x has F={Fn}")
+            xf = torch.empty_like(x1)
+            ops.abf_fuse(x1, y, att[0], att[1], xf)
+            x1 = xf
+        if Tn != out_shape and Fn != out_shape:
+            raise NotImplementedError(
+                f"ABF output interpolation to ({out_shape}, {Tn}) from F={Fn} is not on the CLSKD path")
+        Cout = w2p.shape[0]
+        out = torch.empty(B, Fn, Tn, Cout, **f32)
+        ops.conv([seg_bftc(x1)], [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], B, Fn,
+                 Tn, Cout, w2p, None, out, OutMap(Fn * Tn * Cout, Tn * Cout, Cout))
+        bn = self.conv2[1]
+        ops.batch_norm_bftc(out, out, bn.weight, bn.bias, bn.running_mean, bn.running_var, train,
+                            bn.momentum, bn.eps, 1)
+        return out, x1
+
+    def forward(self, x, y=None, shape=None, out_shape=None, feature_type=None):
+        out, xf = self.forward_bftc(to_bftc(x), to_bftc(y) if y is not None else None, shape,
+                                    out_shape)
+        return nchw(out), nchw(xf)
+
+
+class ReviewKD(nn.Module):
+    """framework.py:226-263."""
+
+    def __init__(self, in_channels, out_channels, shapes, out_shapes, feature_maps, ft_type):
+        super().__init__()
+        self.shapes = shapes
+        self.out_shapes = shapes if out_shapes is None else out_shapes
+        self.feature_maps = feature_maps
+        self.ft_type = ft_type
+        abfs = nn.ModuleList()
+        mid_channel = min(512, in_channels[-1])
+        for idx, in_channel in enumerate(in_channels):
+            abfs.append(ABF(in_channel, mid_channel, out_channels[idx], idx < len(in_channels) - 1))
+        self.abfs = abfs[::-1]
+
+    def forward_bftc(self, feats):
+        """feats: BFTC student features in the reference's list order.  Returns BFTC outputs."""
+        xs = feats[::-1] if self.ft_type == "encoder" else list(feats)
+        results = []
+        out, res = self.abfs[0].forward_bftc(xs[0], out_shape=self.out_shapes[0])
+        results.append(out)
+        for feature, abf, shape, out_shape in zip(xs[1:], self.abfs[1:], self.shapes[1:],
+                                                  self.out_shapes[1:]):
+            out, res = abf.forward_bftc(feature, res, shape, out_shape)
+            if self.ft_type == "encoder":
+                results.insert(0, out)
+            else:
+                results.append(out)
+        return results
+
+    def forward(self, x=None):
+        feats = [to_bftc(f) for f in self.feature_maps]
+        return [nchw(r) for r in self.forward_bftc(feats)]
+
+
+def build_review_kd(feature_maps, ft_type):
+    """framework.py:266-284."""
+    in_channels = [8, 16, 32, 64, 64, 64]
+    out_channels = [32, 64, 128, 256, 256, 256]
+    shapes = [4, 8, 16, 32, 64, 128]
+    out_shapes = [4, 8, 16, 32, 64, 128]
+    if ft_type not in ("encoder", "decoder"):
+        raise ValueError(ft_type)
+    model = ReviewKD(in_channels, out_channels, shapes, out_shapes, feature_maps, ft_type)
+    dev = None
+    for f in feature_maps or []:
+        if torch.is_tensor(f):
+            dev = f.device
+            break
+    if dev is not None:
+        model = model.to(dev)
+    return model

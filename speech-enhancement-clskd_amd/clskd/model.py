@@ -1,0 +1,468 @@
+"""DCCRN on MI355X: reference-compatible module tree, HIP forward.
+
+``DCCRN`` keeps the constructor signature, submodule names and ``state_dict`` keys of the
+reference (``DCCRN.py:14-147``; ``tools_for_model.py:35-330``), so reference checkpoints load
+unchanged and ``feature_extraction``-style taps are available.  The submodules (nn.Conv2d,
+nn.LSTM, …) are parameter containers only: ``DCCRN.forward`` runs the whole network through
+libclskd_hip.so on BFTC ([batch][freq][time][channel]) buffers, never through torch compute.
+
+Supported configuration = the one the reference trains and distils: masking_mode 'E',
+use_clstm=True, use_cbn=False, kernel_size 5, fft 512 / win 400 / hop 100.  Anything else raises.
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+from scipy.signal import get_window
+
+from . import config as cfg
+from . import ops
+from .ops import OutMap, Seg, SegGeom, seg_bftc
+
+# --------------------------------------------------------------------------------------------
+# fixed STFT kernels (tools_for_model.py:15-32)
+# --------------------------------------------------------------------------------------------
+
+
+def init_kernels(win_len, win_inc, fft_len, win_type=None, invers=False):
+    """Same construction as tools_for_model.py:15-32 (float64, then fp32)."""
+    if win_type == "None" or win_type is None:
+        window = np.ones(win_len)
+    else:
+        window = get_window(win_type, win_len, fftbins=True)
+    basis = np.fft.rfft(np.eye(fft_len))[:win_len]
+    kernel = np.concatenate([np.real(basis), np.imag(basis)], 1).T
+    if invers:
+        kernel = np.linalg.pinv(kernel).T
+    kernel = kernel * window
+    return (torch.from_numpy(kernel[:, None, :].astype(np.float32)),
+            torch.from_numpy(window[None, :, None].astype(np.float32)))
+
+
+class ConvSTFT(nn.Module):
+    """tools_for_model.py:35-67 (buffer ``weight`` [N+2, 1, win])."""
+
+    def __init__(self, win_len, win_inc, fft_len=None, win_type="hamming", feature_type="real",
+                 fix=True):
+        super().__init__()
+        self.fft_len = fft_len if fft_len is not None else int(2 ** np.ceil(np.log2(win_len)))
+        kernel, _ = init_kernels(win_len, win_inc, self.fft_len, win_type)
+        self.register_buffer("weight", kernel)
+        self.feature_type = feature_type
+        self.stride = win_inc
+        self.win_len = win_len
+        self.dim = self.fft_len
+
+
+class ConviSTFT(nn.Module):
+    """tools_for_model.py:70-109 (buffers ``weight``, ``window``, ``enframe``)."""
+
+    def __init__(self, win_len, win_inc, fft_len=None, win_type="hamming", feature_type="real",
+                 fix=True):
+        super().__init__()
+        self.fft_len = fft_len if fft_len is not None else int(2 ** np.ceil(np.log2(win_len)))
+        kernel, window = init_kernels(win_len, win_inc, self.fft_len, win_type, invers=True)
+        self.register_buffer("weight", kernel)
+        self.feature_type = feature_type
+        self.win_type = win_type
+        self.win_len = win_len
+        self.stride = win_inc
+        self.dim = self.fft_len
+        self.register_buffer("window", window)
+        self.register_buffer("enframe", torch.eye(win_len)[:, None, :])
+
+
+class ComplexConv2d(nn.Module):
+    """Parameter container for tools_for_model.py:193-262 (real_conv / imag_conv)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=(1, 1), stride=(1, 1),
+                 padding=(0, 0), dilation=1, groups=1, causal=True, complex_axis=1):
+        super().__init__()
+        self.in_channels = in_channels // 2
+        self.out_channels = out_channels // 2
+        self.kernel_size, self.stride, self.padding = kernel_size, stride, padding
+        self.causal, self.complex_axis = causal, complex_axis
+        self.real_conv = nn.Conv2d(self.in_channels, self.out_channels, kernel_size, stride,
+                                   padding=[padding[0], 0], dilation=dilation, groups=groups)
+        self.imag_conv = nn.Conv2d(self.in_channels, self.out_channels, kernel_size, stride,
+                                   padding=[padding[0], 0], dilation=dilation, groups=groups)
+        nn.init.normal_(self.real_conv.weight.data, std=0.05)
+        nn.init.normal_(self.imag_conv.weight.data, std=0.05)
+        nn.init.constant_(self.real_conv.bias, 0.0)
+        nn.init.constant_(self.imag_conv.bias, 0.0)
+
+    def forward(self, x):
+        raise NotImplementedError("ComplexConv2d runs inside DCCRN.forward (HIP executor)")
+
+
+class ComplexConvTranspose2d(nn.Module):
+    """Parameter container for tools_for_model.py:265-330."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=(1, 1), stride=(1, 1),
+                 padding=(0, 0), output_padding=(0, 0), causal=False, complex_axis=1, groups=1):
+        super().__init__()
+        self.in_channels = in_channels // 2
+        self.out_channels = out_channels // 2
+        self.kernel_size, self.stride, self.padding = kernel_size, stride, padding
+        self.output_padding = output_padding
+        self.real_conv = nn.ConvTranspose2d(self.in_channels, self.out_channels, kernel_size,
+                                            stride, padding=padding,
+                                            output_padding=output_padding, groups=groups)
+        self.imag_conv = nn.ConvTranspose2d(self.in_channels, self.out_channels, kernel_size,
+                                            stride, padding=padding,
+                                            output_padding=output_padding, groups=groups)
+        self.complex_axis = complex_axis
+        nn.init.normal_(self.real_conv.weight, std=0.05)
+        nn.init.normal_(self.imag_conv.weight, std=0.05)
+        nn.init.constant_(self.real_conv.bias, 0.0)
+        nn.init.constant_(self.imag_conv.bias, 0.0)
+
+    def forward(self, x):
+        raise NotImplementedError("ComplexConvTranspose2d runs inside DCCRN.forward (HIP executor)")
+
+
+class NavieComplexLSTM(nn.Module):
+    """Parameter container for tools_for_model.py:138-178 (name kept from the reference)."""
+
+    def __init__(self, input_size, hidden_size, projection_dim=None, bidirectional=False,
+                 batch_first=False):
+        super().__init__()
+        assert not bidirectional, "bidirectional complex LSTM is not on the DCCRN-CL path"
+        self.input_dim = input_size // 2
+        self.rnn_units = hidden_size // 2
+        self.real_lstm = nn.LSTM(self.input_dim, self.rnn_units, num_layers=1, batch_first=False)
+        self.imag_lstm = nn.LSTM(self.input_dim, self.rnn_units, num_layers=1, batch_first=False)
+        if projection_dim is not None:
+            self.projection_dim = projection_dim // 2
+            self.r_trans = nn.Linear(self.rnn_units, self.projection_dim)
+            self.i_trans = nn.Linear(self.rnn_units, self.projection_dim)
+        else:
+            self.projection_dim = None
+
+    def forward(self, x):
+        raise NotImplementedError("NavieComplexLSTM runs inside DCCRN.forward (HIP executor)")
+
+
+def _pv(*tensors):
+    """Cache key of a parameter group: storage pointers and in-place versions."""
+    return tuple((t.data_ptr(), t._version) for t in tensors)
+
+
+# --------------------------------------------------------------------------------------------
+# DCCRN
+# --------------------------------------------------------------------------------------------
+class DCCRN(nn.Module):
+    def __init__(self, rnn_layers=cfg.rnn_layers, rnn_units=cfg.rnn_units, win_len=cfg.win_len,
+                 win_inc=cfg.win_inc, fft_len=cfg.fft_len, win_type=cfg.window_type,
+                 masking_mode="E", use_clstm=False, use_cbn=False, kernel_size=5,
+                 kernel_num=[16, 32, 64, 128, 256, 256]):
+        super().__init__()
+        if masking_mode != "E" or not use_clstm or use_cbn or kernel_size != 5:
+            raise NotImplementedError(
+                "clskd.DCCRN builds the DCCRN-CL path of the reference (masking_mode='E', "
+                "use_clstm=True, use_cbn=False, kernel_size=5)")
+        if (win_len, win_inc, fft_len) != (400, 100, 512):
+            raise NotImplementedError("clskd.DCCRN is built for win 400 / hop 100 / fft 512")
+        self.win_len, self.win_inc, self.fft_len, self.win_type = win_len, win_inc, fft_len, win_type
+        self.rnn_units = rnn_units
+        self.input_dim = self.output_dim = win_len
+        self.hidden_layers = rnn_layers
+        self.kernel_size = kernel_size
+        self.kernel_num = [2] + list(kernel_num)
+        self.masking_mode = masking_mode
+        self.use_clstm = use_clstm
+        self.fix = True
+        self.stft = ConvSTFT(win_len, win_inc, fft_len, win_type, "complex", fix=True)
+        self.istft = ConviSTFT(win_len, win_inc, fft_len, win_type, "complex", fix=True)
+        self.encoder = nn.ModuleList()
+        self.decoder = nn.ModuleList()
+        kn = self.kernel_num
+        for idx in range(len(kn) - 1):
+            self.encoder.append(nn.Sequential(
+                ComplexConv2d(kn[idx], kn[idx + 1], kernel_size=(kernel_size, 2), stride=(2, 1),
+                              padding=(2, 1)),
+                nn.BatchNorm2d(kn[idx + 1]),
+                nn.PReLU()))
+        hidden_dim = fft_len // (2 ** len(kn))
+        rnns = []
+        for idx in range(rnn_layers):
+            rnns.append(NavieComplexLSTM(
+                input_size=hidden_dim * kn[-1] if idx == 0 else rnn_units,
+                hidden_size=rnn_units,
+                projection_dim=hidden_dim * kn[-1] if idx == rnn_layers - 1 else None))
+        self.enhance = nn.Sequential(*rnns)
+        for idx in range(len(kn) - 1, 0, -1):
+            mods = [ComplexConvTranspose2d(kn[idx] * 2, kn[idx - 1], kernel_size=(kernel_size, 2),
+                                           stride=(2, 1), padding=(2, 0), output_padding=(1, 0))]
+            if idx != 1:
+                mods += [nn.BatchNorm2d(kn[idx - 1]), nn.PReLU()]
+            self.decoder.append(nn.Sequential(*mods))
+        self._wcache = {}
+        self._tap_sinks = []
+
+    # ---------------------------------------------------------------- reference helpers
+    def flatten_parameters(self):
+        pass
+
+    def get_params(self, weight_decay=0.0):
+        """DCCRN.py:242-257."""
+        weights, biases = [], []
+        for name, param in self.named_parameters():
+            (biases if "bias" in name else weights).append(param)
+        return [{"params": weights, "weight_decay": weight_decay},
+                {"params": biases, "weight_decay": 0.0}]
+
+    def loss(self, inputs, labels, real_spec=None, img_spec=None, loss_mode="SI-SNR"):
+        """DCCRN.py:259-411 — the SI-SNR / MSE modes (the others need asteroid PMSQE / mel)."""
+        from .tools_for_loss import si_snr
+        if loss_mode == "SI-SNR":
+            return -si_snr(inputs, labels)
+        raise NotImplementedError(f"loss_mode {loss_mode!r} is not on the CLSKD hot path")
+
+    # ---------------------------------------------------------------- packed weights
+    def _packed(self, key, params, build):
+        ent = self._wcache.get(key)
+        ver = _pv(*params)
+        if ent is None or ent[0] != ver:
+            with torch.no_grad():
+                ent = (ver, build())
+            self._wcache[key] = ent
+        return ent[1]
+
+    def _enc_w(self, i):
+        cc = self.encoder[i][0]
+
+        def build():
+            wr, wi = cc.real_conv.weight, cc.imag_conv.weight  # [Co/2, Ci/2, 5, 2]
+            top = torch.cat([wr, -wi], 1)
+            bot = torch.cat([wi, wr], 1)
+            w = torch.cat([top, bot], 0)  # [Co, Ci, 5, 2]
+            Co, Ci = w.shape[:2]
+            w = w.permute(0, 2, 3, 1).reshape(Co, 10, Ci)  # tap = kf*2 + kt
+            bias = torch.cat([cc.real_conv.bias - cc.imag_conv.bias,
+                              cc.imag_conv.bias + cc.real_conv.bias]).float().contiguous()
+            return ops.pack_weight(w, 10 * Ci), bias
+        return self._packed(("enc", i), (cc.real_conv.weight, cc.imag_conv.weight,
+                                         cc.real_conv.bias, cc.imag_conv.bias), build)
+
+    _DEC_TAPS = {0: ((0, 1), (2, 0), (4, -1)), 1: ((1, 1), (3, 0))}  # parity -> (kf, dF)
+
+    def _dec_w(self, d, parity):
+        cc = self.decoder[d][0]
+
+        def build():
+            wr, wi = cc.real_conv.weight, cc.imag_conv.weight  # [Ci/2, Co/2, 5, 2]
+            top = torch.cat([wr, wi], 1)   # real input -> [real out | imag out]
+            bot = torch.cat([-wi, wr], 1)  # imag input -> [real out | imag out]
+            w = torch.cat([top, bot], 0)   # [Ci, Co, 5, 2]
+            Ci, Co = w.shape[:2]
+            taps = [(kf, kt) for kf, _ in self._DEC_TAPS[parity] for kt in (0, 1)]
+            w = torch.stack([w[:, :, kf, kt] for kf, kt in taps], 0)  # [ntap, Ci, Co]
+            w = w.permute(2, 0, 1)  # [Co, ntap, Ci]
+            bias = torch.cat([cc.real_conv.bias - cc.imag_conv.bias,
+                              cc.imag_conv.bias + cc.real_conv.bias]).float().contiguous()
+            return ops.pack_weight(w, len(taps) * Ci), bias
+        return self._packed(("dec", d, parity), (cc.real_conv.weight, cc.imag_conv.weight,
+                                                 cc.real_conv.bias, cc.imag_conv.bias), build)
+
+    def _lstm_w(self, li):
+        m = self.enhance[li]
+        R, I = m.real_lstm, m.imag_lstm
+
+        def build():
+            H = R.hidden_size
+            wih = torch.cat([R.weight_ih_l0, I.weight_ih_l0], 0)  # [8H, D]
+            if li == 0:
+                D = wih.shape[1]
+                Ch = D // 4
+                w = wih.reshape(8 * H, Ch, 4).permute(0, 2, 1)  # [8H, tap=f, Ch]
+                wp = ops.pack_weight(w, D)
+            else:
+                wp = ops.pack_weight(wih.unsqueeze(1), wih.shape[1])
+            bias = torch.cat([R.bias_ih_l0 + R.bias_hh_l0, I.bias_ih_l0 + I.bias_hh_l0]).float().contiguous()
+            whh = torch.stack([R.weight_hh_l0, I.weight_hh_l0], 0).float().contiguous()
+            out = [wp, bias, whh]
+            if m.projection_dim is not None:
+                for lin in (m.r_trans, m.i_trans):
+                    out += [ops.pack_weight(lin.weight.unsqueeze(1), lin.weight.shape[1]),
+                            lin.bias.float().contiguous()]
+            return out
+        ps = [R.weight_ih_l0, I.weight_ih_l0, R.weight_hh_l0, I.weight_hh_l0, R.bias_ih_l0,
+              R.bias_hh_l0, I.bias_ih_l0, I.bias_hh_l0]
+        if m.projection_dim is not None:
+            ps += [m.r_trans.weight, m.r_trans.bias, m.i_trans.weight, m.i_trans.bias]
+        return self._packed(("lstm", li), ps, build)
+
+    def _stft_w(self):
+        def build():
+            return self.stft.weight[:, 0, :].float().contiguous()  # [514, 400]
+        return self._packed(("stft",), (self.stft.weight,), build)
+
+    def _istft_w(self):
+        def build():
+            inv = self.istft.weight[:, 0, :].float()  # [514, 400]
+            w = inv.t().contiguous()  # [400, 514]
+            w = torch.cat([w, w.new_zeros(400, 2)], 1)  # K = 516 (est buffer has 2 zero columns)
+            return ops.pack_weight(w.unsqueeze(1), 516), self.istft.window[0, :, 0].float().contiguous()
+        return self._packed(("istft",), (self.istft.weight, self.istft.window), build)
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, inputs, lens=None, is_feat=None):
+        """DCCRN.py:149-240.  inputs [B, L] fp32 on the HIP device."""
+        res = self.run(inputs, train=self.training, bn_updates=1 if self.training else 0)
+        for sink in list(self._tap_sinks):
+            sink(res)
+        if is_feat:
+            return res["out_wav"]
+        return res["mask_real"], res["mask_imag"], res["real"], res["imag"], res["out_wav"]
+
+    def spectrum(self, x):
+        """ConvSTFT (tools_for_model.py:53-67) -> spec [B][T][514] (frame-major)."""
+        B, L = x.shape
+        T = cfg.n_frames(L)
+        Lp = 100 * (T + 3)
+        dev = x.device
+        xp = torch.empty(B, Lp, device=dev, dtype=torch.float32)
+        ops.frame_pad(x, 300, Lp, 0, xp)
+        spec = torch.empty(B, T, 514, device=dev, dtype=torch.float32)
+        seg = Seg(xp, 0, SegGeom(100, Lp, 0, 100, 1, T + 3))
+        ops.conv([seg], [(0, kt) for kt in range(4)], B, 1, T, 514, self._stft_w(), None, spec,
+                 OutMap(T * 514, 0, 514))
+        return spec
+
+    def run(self, x, train=True, bn_updates=1, spec=None, want_masks=True):
+        """Full forward on the HIP device.  Returns a dict of BFTC buffers and NCHW views."""
+        if not x.is_cuda:
+            raise RuntimeError("clskd.DCCRN.forward needs inputs on the HIP device")
+        x = x.float()
+        if x.dim() == 3:
+            x = x.squeeze(1)
+        x = x.contiguous()
+        B, L = x.shape
+        T = cfg.n_frames(L)
+        dev = x.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        if spec is None:
+            spec = self.spectrum(x)
+        kn = self.kernel_num
+        nl = len(kn) - 1
+        # ---------------- encoder (DCCRN.py:171-176, tools_for_model.py:236-262)
+        enc = []
+        F = 256
+        for i in range(nl):
+            Co = kn[i + 1]
+            Fo = F // 2
+            wp, bias = self._enc_w(i)
+            if i == 0:
+                segs = [Seg(spec, 1, SegGeom(1, T * 514, 1, 514, 256, T)),
+                        Seg(spec, 258, SegGeom(1, T * 514, 1, 514, 256, T))]
+            else:
+                segs = [seg_bftc(enc[-1])]
+            taps = [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)]
+            raw = torch.empty(B, Fo, T, Co, **f32)
+            ops.conv(segs, taps, B, Fo, T, Co, wp, bias, raw, OutMap(Fo * T * Co, T * Co, Co),
+                     stride_f=2)
+            bn, pr = self.encoder[i][1], self.encoder[i][2]
+            ops.batch_norm_bftc(raw, raw, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                train, bn.momentum, bn.eps, bn_updates, alpha=pr.weight)
+            enc.append(raw)
+            F = Fo
+        # ---------------- complex LSTM (DCCRN.py:178-199, tools_for_model.py:159-174)
+        C6 = kn[-1]
+        Ch = C6 // 2
+        act6 = enc[-1]
+        D4 = act6.shape[1]
+        H = self.rnn_units // 2
+        r_in = None
+        lstm_io = []
+        for li in range(self.hidden_layers):
+            packs = self._lstm_w(li)
+            wp, bias, whh = packs[:3]
+            gx = torch.empty(2, B, T, 8 * H, **f32)
+            for half in range(2):
+                if li == 0:
+                    segs = [seg_bftc(act6, c0=half * Ch, C=Ch)]
+                    taps = [(f, 0) for f in range(D4)]
+                else:
+                    src = r_in[half]
+                    segs = [Seg(src, 0, SegGeom(H, T * H, 0, H, 1, T))]
+                    taps = [(0, 0)]
+                ops.conv(segs, taps, B, 1, T, 8 * H, wp, bias, gx[half],
+                         OutMap(T * 8 * H, 0, 8 * H))
+            hs = torch.empty(2, 2 * B, T, H, **f32)
+            ops.lstm_recurrent(gx, 4 * H, T * 8 * H, 8 * H, whh, 2, 2 * B, T, H, hs,
+                               2 * B * T * H, T * H, H)
+            ro = torch.empty(B, T, H, **f32)
+            io = torch.empty(B, T, H, **f32)
+            ops.complex_combine(hs[0, :B], hs[1, B:], hs[0, B:], hs[1, :B], ro, io)
+            r_in = (ro, io)
+            lstm_io.append((ro, io))
+        # projection into the decoder input [B][D4][T][C6] (DCCRN.py:188-199)
+        dec_in = torch.empty(B, D4, T, C6, **f32)
+        m = self.enhance[self.hidden_layers - 1]
+        packs = self._lstm_w(self.hidden_layers - 1)
+        P = m.projection_dim
+        for half in range(2):
+            wpp, bp = packs[3 + 2 * half], packs[4 + 2 * half]
+            src = r_in[half]
+            ops.conv([Seg(src, 0, SegGeom(H, T * H, 0, H, 1, T))], [(0, 0)], B, 1, T, P, wpp, bp,
+                     dec_in, OutMap(D4 * T * C6, 0, C6, 1, T * C6, D4), out_offset=half * Ch)
+        # ---------------- decoder (DCCRN.py:201-206, tools_for_model.py:303-330), polyphase
+        dec = []
+        out_t, out_t0, out_T = dec_in, 0, T
+        F = D4
+        for d in range(nl):
+            skip = enc[-1 - d]
+            Cof = out_t.shape[-1]
+            Csk = skip.shape[-1]
+            segs = [seg_bftc(out_t, 0, Cof // 2, out_t0, out_T), seg_bftc(skip, 0, Csk // 2),
+                    seg_bftc(out_t, Cof // 2, Cof // 2, out_t0, out_T),
+                    seg_bftc(skip, Csk // 2, Csk // 2)]
+            Co = self.decoder[d][0].out_channels * 2
+            raw = torch.empty(B, 2 * F, T + 1, Co, **f32)
+            for parity in (0, 1):
+                wp, bias = self._dec_w(d, parity)
+                taps = [(dF, -kt) for _, dF in self._DEC_TAPS[parity] for kt in (0, 1)]
+                ops.conv(segs, taps, B, F, T + 1, Co, wp, bias, raw,
+                         OutMap(2 * F * (T + 1) * Co, (T + 1) * Co, Co, of_mul=2, of_add=parity))
+            if len(self.decoder[d]) > 1:
+                bn, pr = self.decoder[d][1], self.decoder[d][2]
+                ops.batch_norm_bftc(raw, raw, bn.weight, bn.bias, bn.running_mean,
+                                    bn.running_var, train, bn.momentum, bn.eps, bn_updates,
+                                    alpha=pr.weight)
+            dec.append(raw)
+            out_t, out_t0, out_T = raw, 1, T
+            F = 2 * F
+        # ---------------- mask 'E' + ConviSTFT + clamp (DCCRN.py:207-237)
+        mask = dec[-1]  # [B][256][T+1][2]
+        est = torch.empty(B, T, 516, **f32)
+        mr = mi = None
+        if want_masks:
+            mr = torch.empty(B, T, 257, **f32)
+            mi = torch.empty(B, T, 257, **f32)
+        ops.mask_e(spec, mask, T, est, mr, mi)
+        winv, window = self._istft_w()
+        frames = torch.empty(B, T, 400, **f32)
+        ops.conv([Seg(est, 0, SegGeom(516, T * 516, 0, 516, 1, T))], [(0, 0)], B, 1, T, 400, winv,
+                 None, frames, OutMap(T * 400, 0, 400))
+        out_len = (T + 1) * 100 - 400
+        wav = torch.empty(B, out_len, **f32)
+        ops.ola_hop(frames, window, 100, out_len, 300, True, wav)
+        nchw = lambda t: t.permute(0, 3, 1, 2)
+        return dict(
+            out_wav=wav,
+            real=est[:, :, :257].permute(0, 2, 1),
+            imag=est[:, :, 257:514].permute(0, 2, 1),
+            mask_real=mr.permute(0, 2, 1) if mr is not None else None,
+            mask_imag=mi.permute(0, 2, 1) if mi is not None else None,
+            enc=enc, dec=dec, dec_in=dec_in, spec=spec, est=est, T=T,
+            enc_nchw=[nchw(t) for t in enc], dec_nchw=[nchw(t) for t in dec],
+            lstm_io=lstm_io)
+
+    @staticmethod
+    def clstm_from_dec_in(dec_in):
+        """[T,B,P] real/imag enhance outputs (DCCRN.py:186) from the BFTC decoder input."""
+        B, D4, T, C6 = dec_in.shape
+        Ch = C6 // 2
+        r = dec_in[..., :Ch].permute(2, 0, 3, 1).reshape(T, B, Ch * D4)
+        i = dec_in[..., Ch:].permute(2, 0, 3, 1).reshape(T, B, Ch * D4)
+        return r, i

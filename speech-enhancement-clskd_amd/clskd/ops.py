@@ -1,0 +1,334 @@
+"""Thin torch-facing wrappers over libclskd_hip.so.
+
+torch is plumbing here (device memory, streams); every arithmetic op runs in a HIP kernel of
+the library.  Tensors are BFTC ([batch][freq][time][channel]) unless noted.
+"""
+import ctypes as C
+from dataclasses import dataclass
+from functools import lru_cache
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, ptr
+
+BK = 16
+ZERO_DF = -32768
+
+
+def lib():
+    return _lib.load()
+
+
+def _stream():
+    return _lib.stream_ptr()
+
+
+# ------------------------------------------------------------------------------------------
+# implicit-GEMM convolution
+# ------------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class SegGeom:
+    """Gather geometry of one channel segment (pointer supplied at call time)."""
+    C: int      # channels in this segment (contiguous, stride 1)
+    sB: int
+    sF: int
+    sT: int
+    F: int
+    T: int
+
+
+@dataclass
+class Seg:
+    tensor: torch.Tensor  # storage owner
+    offset: int           # element offset of the segment's (b=0, f=0, t=0, c=0)
+    geom: SegGeom
+
+
+def seg_bftc(t, c0=0, C=None, t0=0, T=None):
+    """Segment over a contiguous BFTC tensor t[B][F][T][Ct], channels [c0, c0+C), time from t0."""
+    B, F, Tt, Ct = t.shape
+    assert t.is_contiguous()
+    C = Ct - c0 if C is None else C
+    T = Tt - t0 if T is None else T
+    return Seg(t, c0 + t0 * Ct, SegGeom(C, F * Tt * Ct, Tt * Ct, Ct, F, T))
+
+
+@lru_cache(maxsize=1024)
+def _ktab(geoms, taps, device_index):
+    """K table for segments `geoms` and spatial taps [(dF, dT)], K order (tap, seg, cin)."""
+    ent, kseg = [], []
+    for dF, dT in taps:
+        for s, g in enumerate(geoms):
+            for c in range(g.C):
+                ent.append((c + dF * g.sF + dT * g.sT, dF, dT))
+                kseg.append(s)
+    K = len(ent)
+    Kp = -(-K // BK) * BK
+    for _ in range(Kp - K):
+        ent.append((0, ZERO_DF, 0))
+        kseg.append(0)
+    arr = np.zeros(Kp, dtype=[("off", "<i4"), ("dF", "<i2"), ("dT", "<i2")])
+    offs = np.array([e[0] for e in ent], np.int64)
+    assert np.all(np.abs(offs) < 2 ** 31), "K-table offset overflow"
+    arr["off"] = offs
+    arr["dF"] = [e[1] for e in ent]
+    arr["dT"] = [e[2] for e in ent]
+    dev = torch.device("cuda", device_index)
+    kt = torch.from_numpy(arr.view(np.uint8).copy()).to(dev)
+    ks = torch.tensor(kseg, dtype=torch.uint8, device=dev)
+    vec4 = all(g.C % 4 == 0 and g.sB % 4 == 0 and g.sF % 4 == 0 and g.sT % 4 == 0 for g in geoms)
+    return kt, ks, K, Kp, vec4
+
+
+def pack_weight(w, K):
+    """w: [N, ntaps, Cin] (K order tap-major, channel-minor) -> [N, Kp] contiguous fp32, zero pad."""
+    N = w.shape[0]
+    w = w.reshape(N, -1).float()
+    assert w.shape[1] == K, (w.shape, K)
+    Kp = -(-K // BK) * BK
+    if Kp != K:
+        w = torch.cat([w, w.new_zeros(N, Kp - K)], 1)
+    return w.contiguous()
+
+
+@dataclass(frozen=True)
+class OutMap:
+    oB: int
+    oF: int
+    oT: int
+    oNhi: int = 0
+    oNlo: int = 1
+    nlo: int = 1 << 30
+    of_mul: int = 1
+    of_add: int = 0
+
+
+def out_bftc(t, c0=0, of_mul=1, of_add=0):
+    """Output map for a contiguous BFTC tensor (channels from c0)."""
+    B, F, T, Ct = t.shape
+    return OutMap(F * T * Ct, T * Ct, Ct, 0, 1, 1 << 30, of_mul, of_add), c0
+
+
+def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, stride_f=1,
+         stride_t=1):
+    """out[b, fo*of_mul+of_add, to, n] = bias[n] + sum_k A[(b,fo,to),k] W[n,k]."""
+    dev = out.device
+    geoms = tuple(s.geom for s in segs)
+    kt, ks, K, Kp, vec4 = _ktab(geoms, tuple(taps), dev.index or 0)
+    assert wpacked.shape == (N, Kp) and wpacked.is_contiguous() and wpacked.dtype == torch.float32
+    for s in segs:
+        if (s.tensor.data_ptr() + 4 * s.offset) % 16 != 0:
+            vec4 = False
+    d = _lib.ConvDesc()
+    d.B, d.Fo, d.To, d.N, d.K = B, Fo, To, N, Kp
+    d.stride_f, d.stride_t = stride_f, stride_t
+    d.nseg = len(segs)
+    for i, s in enumerate(segs):
+        g = s.geom
+        d.seg[i] = _lib.Seg(s.tensor.data_ptr() + 4 * s.offset, g.sB, g.sF, g.sT, g.F, g.T)
+    for i in range(len(segs), _lib.MAX_SEGS):
+        d.seg[i] = d.seg[0]
+    d.ktab, d.kseg, d.vec4 = kt.data_ptr(), ks.data_ptr(), int(vec4)
+    d.weight = wpacked.data_ptr()
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.out = out.data_ptr() + 4 * out_offset
+    d.oB, d.oF, d.oT, d.oNhi, d.oNlo = omap.oB, omap.oF, omap.oT, omap.oNhi, omap.oNlo
+    d.nlo = min(omap.nlo, 1 << 30)
+    d.of_mul, d.of_add = omap.of_mul, omap.of_add
+    d.compute = _lib.F32
+    check(lib().clskd_conv2d_fwd(C.byref(d), _stream()), "conv2d")
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# BatchNorm (+ PReLU)
+# ------------------------------------------------------------------------------------------
+def batch_norm_bftc(x, y, gamma, beta, running_mean, running_var, train, momentum=0.1,
+                    eps=1e-5, n_updates=1, alpha=None, stats_out=None):
+    """nn.BatchNorm2d over a BFTC tensor (channels last), then optional PReLU (single alpha).
+    train: batch statistics (biased var), running stats updated n_updates times (if given)."""
+    L = lib()
+    Cn = x.shape[-1]
+    rows = x.numel() // Cn
+    dev = x.device
+    scale = torch.empty(Cn, device=dev, dtype=torch.float32)
+    shift = torch.empty(Cn, device=dev, dtype=torch.float32)
+    st = _stream()
+    if train:
+        nblk = L.clskd_bn_partial_blocks(rows, Cn)
+        part = torch.empty(nblk * Cn * 2, device=dev, dtype=torch.float64)
+        check(L.clskd_bn_stats_partial(ptr(x), rows, Cn, ptr(part), nblk, st), "bn_stats")
+        mean_o = var_o = None
+        if stats_out is not None:
+            mean_o, var_o = stats_out
+        upd = running_mean is not None and running_var is not None and n_updates > 0
+        check(L.clskd_bn_finalize(ptr(part), nblk, rows, Cn, ptr(gamma), ptr(beta), eps,
+                                  ptr(running_mean) if upd else None,
+                                  ptr(running_var) if upd else None, momentum, n_updates,
+                                  ptr(scale), ptr(shift), ptr(mean_o), ptr(var_o), st),
+              "bn_finalize")
+    else:
+        check(L.clskd_bn_eval_coeffs(ptr(running_mean), ptr(running_var), ptr(gamma), ptr(beta),
+                                     eps, Cn, ptr(scale), ptr(shift), st), "bn_eval")
+    check(L.clskd_bn_apply(ptr(x), ptr(y), rows, Cn, ptr(scale), ptr(shift), ptr(alpha), st),
+          "bn_apply")
+    return y
+
+
+# ------------------------------------------------------------------------------------------
+# LSTM, STFT helpers, ABF fuse
+# ------------------------------------------------------------------------------------------
+def lstm_recurrent(gx, gx_ws, gx_seq, gx_t, whh, nws, nseq, T, H, out, o_ws, o_seq, o_t):
+    check(lib().clskd_lstm_recurrent(ptr(gx), gx_ws, gx_seq, gx_t, ptr(whh), nws, nseq, T, H,
+                                     ptr(out), o_ws, o_seq, o_t, _stream()), "lstm")
+    return out
+
+
+def complex_combine(rr, ii, ir, ri, ro, io):
+    check(lib().clskd_complex_combine(ptr(rr), ptr(ii), ptr(ir), ptr(ri), ptr(ro), ptr(io),
+                                      ro.numel(), _stream()), "complex_combine")
+
+
+def frame_pad(x, pad, Lp, mode, out):
+    B, L = x.shape
+    check(lib().clskd_frame_pad(ptr(x), x.stride(0), B, L, pad, Lp, mode, ptr(out), _stream()),
+          "frame_pad")
+    return out
+
+
+def mask_e(spec, mask, T, est, mask_r=None, mask_i=None):
+    B = spec.shape[0]
+    Tm = mask.shape[2]
+    check(lib().clskd_mask_e(ptr(spec), spec.shape[-1], ptr(mask), Tm, B, T, ptr(est),
+                             est.shape[-1], ptr(mask_r), ptr(mask_i), _stream()), "mask_e")
+
+
+def ola_hop(frames, window, hop, out_len, trim, clamp, wav):
+    B, T, win = frames.shape
+    check(lib().clskd_ola(ptr(frames), ptr(window), B, T, win, hop, out_len, trim, int(clamp),
+                          ptr(wav), _stream()), "ola")
+
+
+def abf_fuse(x, res, w, b, out):
+    B, F, T, Cm = x.shape
+    _, Fr, Tr, Cr = res.shape
+    assert Cm == 64 and Cr == 64, "ABF fuse is built for mid_channel = 64 (framework.py:235)"
+    check(lib().clskd_abf_fuse(ptr(x), ptr(res), B, F, T, Fr, Tr, ptr(w), ptr(b), ptr(out),
+                               _stream()), "abf_fuse")
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# Gram / SPKD
+# ------------------------------------------------------------------------------------------
+@dataclass
+class GramView:
+    tensor: torch.Tensor
+    offset: int
+    sB: int
+    P: int
+    Ctot: int
+    c0: int
+    Cs: int
+
+
+def gram_view(t):
+    """View of a tensor as z_b (any tensor whose per-sample block is contiguous)."""
+    B = t.shape[0]
+    if t.is_contiguous():
+        n = t.numel() // B
+        if n % 4 == 0:
+            return GramView(t, 0, n, n // 4, 4, 0, 4)
+    # BFTC buffer exposed as an NCHW permuted view: underlying storage contiguous
+    if t.dim() == 4 and t.stride(1) == 1:
+        Bn, Cn, Fn, Tn = t.shape
+        if t.stride() == (Fn * Tn * Cn, 1, Tn * Cn, Cn) and (Fn * Tn * Cn) % 4 == 0:
+            n = Fn * Tn * Cn
+            return GramView(t, 0, n, n // 4, 4, 0, 4)
+    tc = t.contiguous()
+    n = tc.numel() // B
+    if n % 4 != 0:
+        tc = torch.cat([tc.reshape(B, n), tc.new_zeros(B, 4 - n % 4)], 1)
+        n = tc.shape[1]
+    return GramView(tc, 0, n, n // 4, 4, 0, 4)
+
+
+def spkd_losses(pairs_views, B, batchmean=True, return_grams=False, chunk_elems=16384, out=None):
+    """pairs_views: list of (student GramView, teacher GramView).  One gram launch for every
+    view, one finalize launch for every pair.  Returns losses [npairs] (and grams)."""
+    views = [v for pr in pairs_views for v in pr]
+    dev = views[0].tensor.device
+    jobs = (_lib.GramJob * len(views))()
+    slab_job = []
+    first = 0
+    for j, v in enumerate(views):
+        chunk = max(1, chunk_elems // v.Cs)
+        ns = -(-v.P // chunk)
+        jobs[j] = _lib.GramJob(v.tensor.data_ptr() + 4 * v.offset, v.sB, v.P, v.Ctot, v.c0, v.Cs,
+                               chunk, first, ns)
+        slab_job += [j] * ns
+        first += ns
+    jobs_t = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(dev, non_blocking=False)
+    slab_t = torch.tensor(slab_job, dtype=torch.int32, device=dev)
+    pairs = torch.tensor([[2 * i, 2 * i + 1] for i in range(len(pairs_views))], dtype=torch.int32,
+                         device=dev)
+    slabs = torch.empty(first * 1024, dtype=torch.float32, device=dev)
+    losses = out if out is not None else torch.empty(len(pairs_views), dtype=torch.float32, device=dev)
+    assert losses.is_contiguous() and losses.numel() == len(pairs_views)
+    gs = gt = None
+    if return_grams:
+        gs = torch.empty(len(pairs_views), B, B, dtype=torch.float32, device=dev)
+        gt = torch.empty_like(gs)
+    L = lib()
+    st = _stream()
+    check(L.clskd_gram_partial(ptr(jobs_t), len(views), first, ptr(slab_t), B, ptr(slabs), st),
+          "gram_partial")
+    check(L.clskd_spkd_finalize(ptr(jobs_t), ptr(pairs), len(pairs_views), B, int(batchmean),
+                                ptr(slabs), ptr(gs), ptr(gt), ptr(losses), st), "spkd_finalize")
+    # keep the job tables alive until the kernels have consumed them
+    losses._clskd_keep = (jobs_t, slab_t, pairs, slabs)
+    if return_grams:
+        return losses, gs, gt
+    return losses
+
+
+# ------------------------------------------------------------------------------------------
+# losses
+# ------------------------------------------------------------------------------------------
+def stft_mag_loss(X, Y, nbins, factor_sc=0.1, factor_mag=0.1, out2=None, accumulate=False):
+    """X, Y: raw spectra [..., 2*nbins] (re | im).  Returns out2 = [sc, mag] (device);
+    accumulate=True adds into out2 (multi-resolution sums)."""
+    rows = X.numel() // X.shape[-1]
+    dev = X.device
+    acc = torch.empty(256 * 3, dtype=torch.float64, device=dev)
+    if out2 is None:
+        out2 = torch.empty(2, dtype=torch.float32, device=dev)
+    L = lib()
+    st = _stream()
+    check(L.clskd_stft_mag_loss(ptr(X), ptr(Y), rows, X.shape[-1], nbins, ptr(acc), st), "stft_mag_loss")
+    check(L.clskd_stft_loss_finalize(ptr(acc), rows * nbins, factor_sc, factor_mag,
+                                     int(accumulate), ptr(out2), st),
+          "stft_loss_finalize")
+    return out2
+
+
+def sisnr_rows(s1, s2, eps=1e-8):
+    """Per-row SI-SNR (tools_for_loss.py:37-47) of [rows, L] tensors -> [rows] (device)."""
+    s1 = s1.reshape(-1, s1.shape[-1])
+    s2 = s2.reshape(-1, s2.shape[-1])
+    if s1.stride(-1) != 1:
+        s1 = s1.contiguous()
+    if s2.stride(-1) != 1:
+        s2 = s2.contiguous()
+    out = torch.empty(s1.shape[0], dtype=torch.float32, device=s1.device)
+    check(lib().clskd_sisnr_rows(ptr(s1), ptr(s2), s1.shape[0], s1.shape[1], s1.stride(0),
+                                 s2.stride(0), eps, ptr(out), _stream()), "sisnr")
+    return out
+
+
+def sum_f32(a, out, scale=1.0):
+    """out[0] = scale * sum(a) for a contiguous (or 1-D strided-1) tensor a."""
+    check(lib().clskd_sum_f32(ptr(a), a.numel(), scale, ptr(out), _stream()), "sum_f32")
+    return out

@@ -99,3 +99,18 @@ TEACHER_SEED = 1001
 STUDENT_SEED = 2002
 ABF_SEED = 7
 DATA_SEED = 20231015
+
+
+def apply_recipe(module, seed, prefix=""):
+    """Load the recipe into a torch module whose state_dict keys (optionally prefixed, e.g.
+    ``"encoder."`` for a ReviewKD) are reference keys.  Returns the module."""
+    import torch
+
+    shapes = {prefix + k: tuple(v.shape) for k, v in module.state_dict().items()}
+    sd = recipe_state_dict(shapes, seed)
+    dev = next(iter(module.state_dict().values())).device
+    missing, unexpected = module.load_state_dict(
+        {k[len(prefix):]: torch.from_numpy(v).to(dev) for k, v in sd.items()}, strict=False)
+    assert not unexpected, unexpected
+    assert all(k.startswith(("stft.", "istft.")) for k in missing), missing
+    return module

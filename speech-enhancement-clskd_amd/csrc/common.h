@@ -1,0 +1,62 @@
+// Shared device/host helpers for libclskd_hip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/clskd.h"
+
+namespace clskd {
+
+// ---- host-side error plumbing (thread-local message; no exceptions across the C ABI) ----------
+void set_error(const char* fmt, ...);
+
+#define CLSKD_CHECK_ARG(cond, ...)                 \
+  do {                                             \
+    if (!(cond)) {                                 \
+      ::clskd::set_error(__VA_ARGS__);             \
+      return CLSKD_E_ARG;                          \
+    }                                              \
+  } while (0)
+
+#define CLSKD_CHECK_SHAPE(cond, ...)               \
+  do {                                             \
+    if (!(cond)) {                                 \
+      ::clskd::set_error(__VA_ARGS__);             \
+      return CLSKD_E_SHAPE;                        \
+    }                                              \
+  } while (0)
+
+#define CLSKD_LAUNCH_CHECK(name)                                                  \
+  do {                                                                            \
+    hipError_t e_ = hipGetLastError();                                            \
+    if (e_ != hipSuccess) {                                                       \
+      ::clskd::set_error("%s: launch failed: %s", name, hipGetErrorString(e_));   \
+      return CLSKD_E_HIP;                                                         \
+    }                                                                             \
+  } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---- device helpers ---------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+}  // namespace clskd

@@ -1,0 +1,251 @@
+// Implicit-GEMM convolution engine for BFTC activations (gfx950, fp32 MFMA 32x32x2).
+//
+// One engine serves every GEMM-shaped op on the DCCRN/CLSKD path (see include/clskd.h):
+// complex Conv2d (packed [[Wr,-Wi],[Wi,Wr]] weights), polyphase ConvTranspose2d, ABF 1x1/3x3
+// convs, the ConvSTFT/ConviSTFT/MRSTFT framing GEMMs and the LSTM input/output projections.
+//
+// Tile: BM=128 output rows x BN output channels x BK=16, 256 threads = 4 waves; wave w owns
+// rows [32w, 32w+32) x all BN columns as BN/32 accumulators of v_mfma_f32_32x32x2_f32.
+// The K loop is register-prefetched one tile ahead into a second LDS buffer (one barrier per
+// K-tile).  Inside a K-tile the reduction order is permuted so each lane reads its MFMA
+// operands as 8 contiguous floats (two ds_read_b128): step s uses k = 8*(lane>>5) + s.
+// LDS rows are 64 B; 16-B chunks are XOR-swizzled by ((row>>2)&3) so the ds_read_b128 lane
+// groups hit 16 distinct bank slots.
+#include "common.h"
+
+namespace clskd {
+
+constexpr int BM = 128;
+constexpr int BK = 16;
+
+struct ConvArgs {
+  clskd_conv_desc d;
+};
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+
+// select the per-segment value without runtime-indexed arrays (which would go to scratch)
+template <typename T>
+__device__ __forceinline__ T sel4(int s, T a0, T a1, T a2, T a3) {
+  return s == 0 ? a0 : (s == 1 ? a1 : (s == 2 ? a2 : a3));
+}
+
+template <int BN, bool VEC4>
+__global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
+  const clskd_conv_desc& d = args.d;
+  constexpr int NT = BN / 32;
+  __shared__ __attribute__((aligned(16))) float As[2][BM * BK];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * BK];
+  __shared__ int64_t out_row[BM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int64_t M = (int64_t)d.B * d.Fo * d.To;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int nk = d.K / BK;  // host pads K to a multiple of BK
+  const int64_t FoTo = (int64_t)d.Fo * d.To;
+
+  // ---- per-block output row offsets ----
+  if (tid < BM) {
+    int64_t m = m0 + tid;
+    int64_t off = -1;
+    if (m < M) {
+      int64_t b = m / FoTo;
+      int64_t r = m - b * FoTo;
+      int fo = (int)(r / d.To);
+      int to = (int)(r - (int64_t)fo * d.To);
+      off = b * d.oB + (int64_t)(fo * d.of_mul + d.of_add) * d.oF + (int64_t)to * d.oT;
+    }
+    out_row[tid] = off;
+  }
+
+  // ---- A-gather rows owned by this thread: rows (tid>>2) and (tid>>2)+64, k-quad (tid&3) ----
+  const int kq = tid & 3;
+  bool rvalid[2];
+  int rb[2], rfi[2], rti[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    int64_t m = m0 + (tid >> 2) + 64 * i;
+    rvalid[i] = m < M;
+    int64_t mm = rvalid[i] ? m : 0;
+    int64_t b = mm / FoTo;
+    int64_t r = mm - b * FoTo;
+    int fo = (int)(r / d.To);
+    int to = (int)(r - (int64_t)fo * d.To);
+    rb[i] = (int)b;
+    rfi[i] = fo * d.stride_f;
+    rti[i] = to * d.stride_t;
+  }
+
+  auto load_a = [&](int kt, f32x4 (&ra)[2]) {
+    if constexpr (VEC4) {
+      const int k = kt * BK + kq * 4;
+      const clskd_ktab_entry e = d.ktab[k];
+      const int s = d.kseg[k];
+      const float* sp = sel4(s, d.seg[0].ptr, d.seg[1].ptr, d.seg[2].ptr, d.seg[3].ptr);
+      const int64_t sB = sel4(s, d.seg[0].sB, d.seg[1].sB, d.seg[2].sB, d.seg[3].sB);
+      const int64_t sF = sel4(s, d.seg[0].sF, d.seg[1].sF, d.seg[2].sF, d.seg[3].sF);
+      const int64_t sT = sel4(s, d.seg[0].sT, d.seg[1].sT, d.seg[2].sT, d.seg[3].sT);
+      const int Fb = sel4(s, d.seg[0].F, d.seg[1].F, d.seg[2].F, d.seg[3].F);
+      const int Tb = sel4(s, d.seg[0].T, d.seg[1].T, d.seg[2].T, d.seg[3].T);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int fi = rfi[i] + e.dF;
+        const int ti = rti[i] + e.dT;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (rvalid[i] && fi >= 0 && fi < Fb && ti >= 0 && ti < Tb) {
+          const float* p = sp + (int64_t)rb[i] * sB + (int64_t)rfi[i] * sF + (int64_t)rti[i] * sT + e.off;
+          v = *reinterpret_cast<const f32x4*>(p);
+        }
+        ra[i] = v;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int k = kt * BK + kq * 4 + q;
+          const clskd_ktab_entry e = d.ktab[k];
+          const int s = d.kseg[k];
+          const float* sp = sel4(s, d.seg[0].ptr, d.seg[1].ptr, d.seg[2].ptr, d.seg[3].ptr);
+          const int64_t sB = sel4(s, d.seg[0].sB, d.seg[1].sB, d.seg[2].sB, d.seg[3].sB);
+          const int64_t sF = sel4(s, d.seg[0].sF, d.seg[1].sF, d.seg[2].sF, d.seg[3].sF);
+          const int64_t sT = sel4(s, d.seg[0].sT, d.seg[1].sT, d.seg[2].sT, d.seg[3].sT);
+          const int Fb = sel4(s, d.seg[0].F, d.seg[1].F, d.seg[2].F, d.seg[3].F);
+          const int Tb = sel4(s, d.seg[0].T, d.seg[1].T, d.seg[2].T, d.seg[3].T);
+          const int fi = rfi[i] + e.dF;
+          const int ti = rti[i] + e.dT;
+          if (rvalid[i] && fi >= 0 && fi < Fb && ti >= 0 && ti < Tb) {
+            v[q] = sp[(int64_t)rb[i] * sB + (int64_t)rfi[i] * sF + (int64_t)rti[i] * sT + e.off];
+          }
+        }
+        ra[i] = v;
+      }
+    }
+  };
+
+  constexpr int NBL = (BN * 4 + 255) / 256;  // float4 B loads per thread
+  auto load_b = [&](int kt, f32x4 (&rbv)[NBL]) {
+#pragma unroll
+    for (int i = 0; i < NBL; ++i) {
+      const int idx = tid + 256 * i;
+      const int n = n0 + (idx >> 2);
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if ((idx >> 2) < BN && n < d.N)
+        v = *reinterpret_cast<const f32x4*>(d.weight + (int64_t)n * d.K + kt * BK + (idx & 3) * 4);
+      rbv[i] = v;
+    }
+  };
+
+  auto store_tiles = [&](int buf, const f32x4 (&ra)[2], const f32x4 (&rbv)[NBL]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (tid >> 2) + 64 * i;
+      *reinterpret_cast<f32x4*>(&As[buf][row * BK + swz(row, kq) * 4]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NBL; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx >> 2;
+      if (row < BN) *reinterpret_cast<f32x4*>(&Bs[buf][row * BK + swz(row, idx & 3) * 4]) = rbv[i];
+    }
+  };
+
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  f32x4 ra[2];
+  f32x4 rbv[NBL];
+  load_a(0, ra);
+  load_b(0, rbv);
+  store_tiles(0, ra, rbv);
+  __syncthreads();
+
+  const int arow = wave * 32 + (lane & 31);
+  const int h = lane >> 5;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) {
+      load_a(kt + 1, ra);
+      load_b(kt + 1, rbv);
+    }
+    const float* as = &As[buf][0];
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(as + arow * BK + swz(arow, 2 * h) * 4);
+    const f32x4 a1 = *reinterpret_cast<const f32x4*>(as + arow * BK + swz(arow, 2 * h + 1) * 4);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int brow = t * 32 + (lane & 31);
+      const float* bs = &Bs[buf][0];
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(bs + brow * BK + swz(brow, 2 * h) * 4);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(bs + brow * BK + swz(brow, 2 * h + 1) * 4);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc[t], 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc[t], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_tiles(buf ^ 1, ra, rbv);
+    __syncthreads();
+  }
+
+  // ---- epilogue: bias + scatter store ----
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int n = n0 + t * 32 + (lane & 31);
+    if (n >= d.N) continue;
+    const float bias = d.bias ? d.bias[n] : 0.f;
+    const int64_t coff = (int64_t)(n / d.nlo) * d.oNhi + (int64_t)(n % d.nlo) * d.oNlo;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int64_t ro = out_row[row];
+      if (ro >= 0) d.out[ro + coff] = acc[t][r] + bias;
+    }
+  }
+}
+
+}  // namespace clskd
+
+using namespace clskd;
+
+extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
+  CLSKD_CHECK_ARG(dp != nullptr, "conv2d: null descriptor");
+  const clskd_conv_desc& d = *dp;
+  CLSKD_CHECK_ARG(d.compute == CLSKD_F32, "conv2d: only CLSKD_F32 compute is built in this version");
+  CLSKD_CHECK_SHAPE(d.B > 0 && d.Fo > 0 && d.To > 0 && d.N > 0 && d.K > 0, "conv2d: empty shape");
+  CLSKD_CHECK_SHAPE(d.K % BK == 0, "conv2d: K=%d must be padded to a multiple of %d", d.K, BK);
+  CLSKD_CHECK_SHAPE(d.nseg >= 1 && d.nseg <= CLSKD_MAX_SEGS, "conv2d: nseg=%d", d.nseg);
+  CLSKD_CHECK_ARG(d.weight && d.out && d.ktab && d.kseg, "conv2d: null pointer");
+  CLSKD_CHECK_SHAPE(d.nlo >= 1, "conv2d: nlo must be >= 1");
+  CLSKD_CHECK_ARG(((uintptr_t)d.weight & 15) == 0, "conv2d: weight must be 16-byte aligned");
+  for (int s = 0; s < d.nseg; ++s) CLSKD_CHECK_ARG(d.seg[s].ptr != nullptr, "conv2d: null segment %d", s);
+  if (d.vec4) {
+    for (int s = 0; s < d.nseg; ++s) {
+      const clskd_seg& g = d.seg[s];
+      CLSKD_CHECK_ARG(((uintptr_t)g.ptr & 15) == 0 && g.sB % 4 == 0 && g.sF % 4 == 0 && g.sT % 4 == 0,
+                      "conv2d: vec4 segment %d not 16-byte aligned", s);
+    }
+  }
+  const int64_t M = (int64_t)d.B * d.Fo * d.To;
+  CLSKD_CHECK_SHAPE(M < (int64_t)INT32_MAX * 64, "conv2d: too many rows");
+  ConvArgs a{d};
+  hipStream_t st = as_stream(stream);
+  const unsigned gx = (unsigned)cdiv(M, BM);
+#define LAUNCH(BN_, V_)                                                                      \
+  hipLaunchKernelGGL((conv_igemm_f32<BN_, V_>), dim3(gx, (unsigned)cdiv(d.N, BN_)), dim3(256), 0, st, a)
+  if (d.N <= 32) {
+    if (d.vec4) LAUNCH(32, true); else LAUNCH(32, false);
+  } else if (d.N <= 64) {
+    if (d.vec4) LAUNCH(64, true); else LAUNCH(64, false);
+  } else {
+    if (d.vec4) LAUNCH(128, true); else LAUNCH(128, false);
+  }
+#undef LAUNCH
+  CLSKD_LAUNCH_CHECK("conv2d");
+  return CLSKD_OK;
+}

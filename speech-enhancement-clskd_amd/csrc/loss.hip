@@ -1,0 +1,331 @@
+// CLSKD losses: batched Gram (SPKD, framework.py:150-172), MRSTFT log-magnitude / spectral
+// convergence reductions (framework.py:16-101) and SI-SNR (tools_for_loss.py:22-47).
+//
+// Gram: memory-bound (arithmetic intensity = B FLOP/byte).  One launch serves every tap of the
+// step: the host flattens all taps into "slabs" (chunk positions of one tap); each workgroup
+// streams 16 (or 32) batch rows of its slab with 16-B loads straight into the
+// v_mfma_f32_16x16x4_f32 operand layout (lane l: row l&15, 4 consecutive elements at 4*(l>>4));
+// A and B operands are the same register, so one load feeds both.  Partial 32x32 slabs are
+// summed in a fixed order by the finalize kernel: bitwise reproducible, no atomics.
+#include "common.h"
+
+namespace clskd {
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 load_row4(const clskd_gram_job& j, int b, int B, int64_t e,
+                                           int64_t p0, int64_t p1) {
+  // element e of this slab (p0-relative), 4-aligned, Cs % 4 == 0
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (b < B) {
+    const int64_t p = p0 + e / j.Cs;
+    const int c = (int)(e % j.Cs);
+    if (p < p1) v = *reinterpret_cast<const f32x4*>(j.ptr + (int64_t)b * j.sB + p * j.Ctot + j.c0 + c);
+  }
+  return v;
+}
+
+template <int NB>  // row blocks of 16: B <= 16*NB
+__global__ __launch_bounds__(256) void gram_partial_kernel(const clskd_gram_job* __restrict__ jobs,
+                                                           const int32_t* __restrict__ slab_job,
+                                                           int B, float* __restrict__ slabs) {
+  const int slab = blockIdx.x;
+  const clskd_gram_job j = jobs[slab_job[slab]];
+  const int si = slab - j.first_slab;
+  const int64_t p0 = (int64_t)si * j.chunk;
+  const int64_t p1 = min(j.P, p0 + j.chunk);
+  const int64_t nel = (p1 - p0) * j.Cs;  // elements per row in this slab
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = lane & 15;
+  const int g = lane >> 4;
+  f32x4 acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
+  // each wave step covers 16 elements per row; 4 waves interleave; unroll 4 steps for MLP
+  constexpr int U = 4;
+  for (int64_t base = (int64_t)wave * 16; base < nel; base += 64 * U) {
+    f32x4 v0[U], v1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = base + (int64_t)u * 64 + 4 * g;
+      const bool ok = e < nel;
+      v0[u] = ok ? load_row4(j, r, B, e, p0, p1) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (NB == 2) v1[u] = ok ? load_row4(j, r + 16, B, e, p0, p1) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc00 = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[u][q], v0[u][q], acc00, 0, 0, 0);
+        if constexpr (NB == 2) {
+          acc01 = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[u][q], v1[u][q], acc01, 0, 0, 0);
+          acc11 = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[u][q], v1[u][q], acc11, 0, 0, 0);
+        }
+      }
+    }
+  }
+  // reduce the 4 waves' accumulators in a fixed order; C layout: col = l&15, row = 4*(l>>4)+i
+  __shared__ float red[4][3][256];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    red[wave][0][lane * 4 + i] = acc00[i];
+    red[wave][1][lane * 4 + i] = acc01[i];
+    red[wave][2][lane * 4 + i] = acc11[i];
+  }
+  __syncthreads();
+  float* out = slabs + (int64_t)slab * 1024;
+  for (int idx = threadIdx.x; idx < 1024; idx += 256) {
+    const int row = idx >> 5, col = idx & 31;
+    const int I = row >> 4, J = col >> 4;
+    float v = 0.f;
+    if (!(I == 1 && J == 0)) {
+      const int t = (I == 0 && J == 0) ? 0 : ((I == 0) ? 1 : 2);
+      const int rr = row & 15, cc = col & 15;
+      const int l = cc + 16 * (rr >> 2);
+      const int i = rr & 3;
+      v = red[0][t][l * 4 + i] + red[1][t][l * 4 + i] + red[2][t][l * 4 + i] + red[3][t][l * 4 + i];
+    } else {
+      // lower-left block = transpose of the upper-right block
+      const int rr = col & 15, cc = row & 15;  // element (row, col) = G01[col-?]: G10[r][c] = G01[c][r]
+      const int l = cc + 16 * (rr >> 2);
+      const int i = rr & 3;
+      v = red[0][1][l * 4 + i] + red[1][1][l * 4 + i] + red[2][1][l * 4 + i] + red[3][1][l * 4 + i];
+    }
+    out[idx] = v;
+  }
+}
+
+// One block per pair: Gs = sum of the student job's slabs, Gt likewise, L1-normalise rows,
+// loss = ||Gt - Gs||_F^2 (/ B^2).  256 threads; B <= 32.
+__global__ __launch_bounds__(256) void spkd_finalize_kernel(const clskd_gram_job* __restrict__ jobs,
+                                                            const int32_t* __restrict__ pairs, int B,
+                                                            int batchmean,
+                                                            const float* __restrict__ slabs,
+                                                            float* grams_s, float* grams_t,
+                                                            float* losses) {
+  const int pr = blockIdx.x;
+  const clskd_gram_job js = jobs[pairs[2 * pr]];
+  const clskd_gram_job jt = jobs[pairs[2 * pr + 1]];
+  __shared__ double Gs[32 * 32], Gt[32 * 32];
+  __shared__ double rs[32], rt[32];
+  __shared__ double red[256];
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < B * B; idx += 256) {
+    const int i = idx / B, k = idx % B;
+    double s = 0.0, t = 0.0;
+    for (int q = 0; q < js.nslab; ++q) s += (double)slabs[(int64_t)(js.first_slab + q) * 1024 + i * 32 + k];
+    for (int q = 0; q < jt.nslab; ++q) t += (double)slabs[(int64_t)(jt.first_slab + q) * 1024 + i * 32 + k];
+    Gs[idx] = s;
+    Gt[idx] = t;
+  }
+  __syncthreads();
+  if (tid < B) {
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < B; ++k) {
+      a += fabs(Gs[tid * B + k]);
+      b += fabs(Gt[tid * B + k]);
+    }
+    rs[tid] = a > 1e-12 ? a : 1e-12;
+    rt[tid] = b > 1e-12 ? b : 1e-12;
+  }
+  __syncthreads();
+  double acc = 0.0;
+  for (int idx = tid; idx < B * B; idx += 256) {
+    const int i = idx / B;
+    const float gs = (float)(Gs[idx] / rs[i]);
+    const float gt = (float)(Gt[idx] / rt[i]);
+    if (grams_s) grams_s[(int64_t)pr * B * B + idx] = gs;
+    if (grams_t) grams_t[(int64_t)pr * B * B + idx] = gt;
+    const double dlt = (double)gt - (double)gs;
+    acc += dlt * dlt;
+  }
+  red[tid] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) losses[pr] = (float)(batchmean ? red[0] / ((double)B * B) : red[0]);
+}
+
+// MRSTFT partials: per block {sum (Y-X)^2, sum Y^2, sum |log Y - log X|} over its elements.
+__global__ __launch_bounds__(256) void stft_mag_loss_kernel(const float* __restrict__ X,
+                                                            const float* __restrict__ Y,
+                                                            int64_t rows, int ld, int nb,
+                                                            double* __restrict__ partial) {
+  const int64_t total = rows * nb;
+  double a = 0, b = 0, c = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / nb;
+    const int f = (int)(i - r * nb);
+    const float xr = X[r * ld + f], xi = X[r * ld + nb + f];
+    const float yr = Y[r * ld + f], yi = Y[r * ld + nb + f];
+    const float xm = sqrtf(fmaxf(xr * xr + xi * xi, 1e-7f));
+    const float ym = sqrtf(fmaxf(yr * yr + yi * yi, 1e-7f));
+    const float d = ym - xm;
+    a += (double)d * d;
+    b += (double)ym * ym;
+    c += fabs((double)logf(ym) - (double)logf(xm));
+  }
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
+  c = wave_sum_d(c);
+  __shared__ double red[4][3];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[w][0] = a;
+    red[w][1] = b;
+    red[w][2] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int k = threadIdx.x;
+    partial[blockIdx.x * 3 + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+  }
+}
+
+// out[0] = factor_sc * sqrt(sum (Y-X)^2) / sqrt(sum Y^2) ; out[1] = factor_mag * sum|..| / count
+__global__ void stft_loss_finalize_kernel(const double* partial, int nblk, int64_t count,
+                                          float factor_sc, float factor_mag, int accumulate,
+                                          float* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double a = 0, b = 0, c = 0;
+  for (int i = 0; i < nblk; ++i) {
+    a += partial[i * 3];
+    b += partial[i * 3 + 1];
+    c += partial[i * 3 + 2];
+  }
+  const float sc = (float)(factor_sc * (sqrt(a) / sqrt(b)));
+  const float mag = (float)(factor_mag * (c / (double)count));
+  out[0] = accumulate ? out[0] + sc : sc;
+  out[1] = accumulate ? out[1] + mag : mag;
+}
+
+// SI-SNR per row, two passes over the row (tools_for_loss.py:37-47, eps as given).
+__global__ __launch_bounds__(256) void sisnr_rows_kernel(const float* __restrict__ s1,
+                                                         const float* __restrict__ s2, int L,
+                                                         int64_t ld1, int64_t ld2, float eps,
+                                                         float* __restrict__ out) {
+  const int row = blockIdx.x;
+  const float* a = s1 + row * ld1;
+  const float* b = s2 + row * ld2;
+  __shared__ double red[4][2];
+  __shared__ float alpha_s;
+  double d12 = 0, d22 = 0;
+  for (int i = threadIdx.x; i < L; i += 256) {
+    d12 += (double)a[i] * b[i];
+    d22 += (double)b[i] * b[i];
+  }
+  d12 = wave_sum_d(d12);
+  d22 = wave_sum_d(d22);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[w][0] = d12;
+    red[w][1] = d22;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double s12 = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    const double s22 = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+    alpha_s = (float)s12 / ((float)s22 + eps);
+  }
+  __syncthreads();
+  const float alpha = alpha_s;
+  double tt = 0, ee = 0;
+  for (int i = threadIdx.x; i < L; i += 256) {
+    const float st = alpha * b[i];
+    const float e = a[i] - st;
+    tt += (double)st * st;
+    ee += (double)e * e;
+  }
+  tt = wave_sum_d(tt);
+  ee = wave_sum_d(ee);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    red[w][0] = tt;
+    red[w][1] = ee;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float T2 = (float)(red[0][0] + red[1][0] + red[2][0] + red[3][0]);
+    const float E2 = (float)(red[0][1] + red[1][1] + red[2][1] + red[3][1]);
+    out[row] = 10.f * log10f(T2 / (E2 + eps) + eps);
+  }
+}
+
+__global__ void sum_f32_kernel(const float* a, int n, float scale, float* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0;
+  for (int i = 0; i < n; ++i) s += a[i];
+  out[0] = (float)(s * scale);
+}
+
+}  // namespace clskd
+
+using namespace clskd;
+
+extern "C" int clskd_gram_partial(const clskd_gram_job* jobs_dev, int32_t njobs, int32_t total_slabs,
+                                  const int32_t* slab_job_dev, int32_t B, float* slabs,
+                                  void* stream) {
+  CLSKD_CHECK_ARG(jobs_dev && slab_job_dev && slabs, "gram_partial: null pointer");
+  CLSKD_CHECK_SHAPE(B >= 1 && B <= 32, "gram_partial: batch %d must be in [1, 32]", B);
+  CLSKD_CHECK_SHAPE(njobs >= 1 && total_slabs >= 1, "gram_partial: empty job list");
+  hipStream_t st = as_stream(stream);
+  if (B <= 16)
+    hipLaunchKernelGGL(gram_partial_kernel<1>, dim3(total_slabs), dim3(256), 0, st, jobs_dev,
+                       slab_job_dev, B, slabs);
+  else
+    hipLaunchKernelGGL(gram_partial_kernel<2>, dim3(total_slabs), dim3(256), 0, st, jobs_dev,
+                       slab_job_dev, B, slabs);
+  CLSKD_LAUNCH_CHECK("gram_partial");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_spkd_finalize(const clskd_gram_job* jobs_dev, const int32_t* pairs_dev,
+                                   int32_t npairs, int32_t B, int32_t batchmean, const float* slabs,
+                                   float* grams_s, float* grams_t, float* losses, void* stream) {
+  CLSKD_CHECK_ARG(jobs_dev && pairs_dev && slabs && losses, "spkd_finalize: null pointer");
+  CLSKD_CHECK_SHAPE(B >= 1 && B <= 32 && npairs >= 1, "spkd_finalize: shape");
+  hipLaunchKernelGGL(spkd_finalize_kernel, dim3(npairs), dim3(256), 0, as_stream(stream), jobs_dev,
+                     pairs_dev, B, batchmean, slabs, grams_s, grams_t, losses);
+  CLSKD_LAUNCH_CHECK("spkd_finalize");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_stft_mag_loss(const float* X, const float* Y, int64_t rows, int32_t ld,
+                                   int32_t nbins, double* acc, void* stream) {
+  // acc: [256][3] partials (caller-owned); finalize with clskd_stft_loss_finalize
+  CLSKD_CHECK_ARG(X && Y && acc, "stft_mag_loss: null pointer");
+  CLSKD_CHECK_SHAPE(rows > 0 && ld >= 2 * nbins, "stft_mag_loss: shape");
+  hipLaunchKernelGGL(stft_mag_loss_kernel, dim3(256), dim3(256), 0, as_stream(stream), X, Y, rows,
+                     ld, nbins, acc);
+  CLSKD_LAUNCH_CHECK("stft_mag_loss");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_stft_loss_finalize(const double* acc, int64_t count, float factor_sc,
+                                        float factor_mag, int32_t accumulate, float* out2,
+                                        void* stream) {
+  CLSKD_CHECK_ARG(acc && out2, "stft_loss_finalize: null pointer");
+  hipLaunchKernelGGL(stft_loss_finalize_kernel, dim3(1), dim3(64), 0, as_stream(stream), acc, 256,
+                     count, factor_sc, factor_mag, accumulate, out2);
+  CLSKD_LAUNCH_CHECK("stft_loss_finalize");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_sisnr_rows(const float* s1, const float* s2, int32_t rows, int32_t L,
+                                int64_t ld1, int64_t ld2, float eps, float* out, void* stream) {
+  CLSKD_CHECK_ARG(s1 && s2 && out, "sisnr: null pointer");
+  CLSKD_CHECK_SHAPE(rows >= 1 && L >= 1, "sisnr: shape");
+  hipLaunchKernelGGL(sisnr_rows_kernel, dim3(rows), dim3(256), 0, as_stream(stream), s1, s2, L, ld1,
+                     ld2, eps, out);
+  CLSKD_LAUNCH_CHECK("sisnr_rows");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_sum_f32(const float* a, int32_t n, float scale, float* out, void* stream) {
+  CLSKD_CHECK_ARG(a && out && n >= 1, "sum_f32: bad args");
+  hipLaunchKernelGGL(sum_f32_kernel, dim3(1), dim3(64), 0, as_stream(stream), a, n, scale, out);
+  CLSKD_LAUNCH_CHECK("sum_f32");
+  return CLSKD_OK;
+}

@@ -1,0 +1,443 @@
+// BatchNorm (train/eval) + PReLU, masking mode 'E', ConviSTFT overlap-add, framing pads,
+// complex-LSTM combine and the ReviewKD ABF attention fusion.  All HBM-bound elementwise /
+// reduction work: float4 (16 B/lane) loads, fp64 accumulation for statistics, deterministic
+// two-level reductions (no float atomics).
+#include "common.h"
+
+namespace clskd {
+
+// ------------------------------------------------------------------------------------------
+// BatchNorm statistics: block `blk` reduces rows [blk*rpb, (blk+1)*rpb) of x[rows][C] into
+// partial[blk][C][2] = {sum, sumsq} (fp64).  Threads map to (row-lane, channel quad).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __restrict__ x,
+                                                               int64_t rows, int C, int64_t rpb,
+                                                               double* __restrict__ partial) {
+  const int CG = C >> 2;                 // channel quads
+  const int RP = 256 / CG;               // rows in flight per pass
+  const int tid = threadIdx.x;
+  const int cg = tid % CG;
+  const int rl = tid / CG;
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = min(rows, r0 + rpb);
+  double s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+  if (rl < RP) {
+    for (int64_t r = r0 + rl; r < r1; r += RP) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(x + r * C + cg * 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[j] += (double)v[j];
+        q[j] += (double)v[j] * (double)v[j];
+      }
+    }
+  }
+  __shared__ double red[256][9];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    red[tid][j] = s[j];
+    red[tid][4 + j] = q[j];
+  }
+  __syncthreads();
+  if (tid < CG) {
+    double S[4] = {0, 0, 0, 0}, Q[4] = {0, 0, 0, 0};
+    for (int l = 0; l < RP; ++l) {
+      const int t = l * CG + tid;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        S[j] += red[t][j];
+        Q[j] += red[t][4 + j];
+      }
+    }
+    double* p = partial + ((int64_t)blockIdx.x * C + tid * 4) * 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      p[2 * j] = S[j];
+      p[2 * j + 1] = Q[j];
+    }
+  }
+}
+
+// one block per channel: sum partials in a fixed order, then scale/shift & running stats.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(
+    const double* __restrict__ partial, int nblk, int64_t rows, int C, const float* gamma,
+    const float* beta, float eps, float* running_mean, float* running_var, float momentum,
+    int n_updates, float* scale, float* shift, float* mean_out, float* var_out) {
+  const int c = blockIdx.x;
+  const int tid = threadIdx.x;
+  double S = 0, Q = 0;
+  for (int b = tid; b < nblk; b += 256) {
+    S += partial[((int64_t)b * C + c) * 2];
+    Q += partial[((int64_t)b * C + c) * 2 + 1];
+  }
+  __shared__ double rs[256], rq[256];
+  rs[tid] = S;
+  rq[tid] = Q;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      rs[tid] += rs[tid + o];
+      rq[tid] += rq[tid + o];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const double n = (double)rows;
+    const double mean = rs[0] / n;
+    double var = rq[0] / n - mean * mean;
+    if (var < 0) var = 0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float g = gamma ? gamma[c] : 1.f;
+    const float bb = beta ? beta[c] : 0.f;
+    const float sc = invstd * g;
+    scale[c] = sc;
+    shift[c] = bb - (float)mean * sc;
+    if (mean_out) mean_out[c] = (float)mean;
+    if (var_out) var_out[c] = (float)var;
+    if (running_mean && running_var) {
+      const float unb = (float)(rows > 1 ? var * n / (n - 1.0) : var);
+      float rm = running_mean[c], rv = running_var[c];
+      for (int u = 0; u < n_updates; ++u) {
+        rm = (1.f - momentum) * rm + momentum * (float)mean;
+        rv = (1.f - momentum) * rv + momentum * unb;
+      }
+      running_mean[c] = rm;
+      running_var[c] = rv;
+    }
+  }
+}
+
+__global__ void bn_eval_coeffs_kernel(const float* rm, const float* rv, const float* gamma,
+                                      const float* beta, float eps, int C, float* scale,
+                                      float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = 1.f / sqrtf(rv[c] + eps);
+  const float sc = invstd * (gamma ? gamma[c] : 1.f);
+  scale[c] = sc;
+  shift[c] = (beta ? beta[c] : 0.f) - rm[c] * sc;
+}
+
+__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ x,
+                                                       float* __restrict__ y, int64_t n4, int C,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const float* __restrict__ alpha) {
+  const float a = alpha ? alpha[0] : 0.f;
+  const bool act = alpha != nullptr;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)((i * 4) % C);
+    f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float t = v[j] * scale[c0 + j] + shift[c0 + j];
+      if (act) t = t >= 0.f ? t : a * t;
+      v[j] = t;
+    }
+    reinterpret_cast<f32x4*>(y)[i] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// framing pad: zero (mode 0) or reflect (mode 1, torch.stft center=True pad_mode='reflect')
+// ------------------------------------------------------------------------------------------
+__global__ void frame_pad_kernel(const float* __restrict__ x, int64_t ldx, int B, int L, int pad,
+                                 int Lp, int mode, float* __restrict__ xp) {
+  const int64_t total = (int64_t)B * Lp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(i / Lp);
+    const int j = (int)(i - (int64_t)b * Lp);
+    int src = j - pad;
+    float v = 0.f;
+    if (mode == 0) {
+      if (src >= 0 && src < L) v = x[(int64_t)b * ldx + src];
+    } else {
+      if (src >= -pad && src < L + pad) {
+        if (src < 0) src = -src;
+        if (src >= L) src = 2 * (L - 1) - src;
+        v = x[(int64_t)b * ldx + src];
+      }
+    }
+    xp[i] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// masking mode 'E' (DCCRN.py:150-159, 207-226)
+// ------------------------------------------------------------------------------------------
+__global__ void mask_e_kernel(const float* __restrict__ spec, int ldspec,
+                              const float* __restrict__ mask, int Tm, int B, int T,
+                              float* __restrict__ est, int ldest, float* __restrict__ mask_r,
+                              float* __restrict__ mask_i) {
+  const int64_t total = (int64_t)B * T * 257;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int f = (int)(i % 257);
+    const int64_t bt = i / 257;
+    const int t = (int)(bt % T);
+    const int b = (int)(bt / T);
+    const float re = spec[bt * ldspec + f];
+    const float im = spec[bt * ldspec + 257 + f];
+    const float mags = sqrtf(re * re + im * im + 1e-8f);
+    const float phase = atan2f(im, re);
+    float mr = 0.f, mi = 0.f;
+    if (f > 0) {
+      const float* mp = mask + (((int64_t)b * 256 + (f - 1)) * Tm + (t + 1)) * 2;
+      mr = mp[0];
+      mi = mp[1];
+    }
+    const float mm = sqrtf(mr * mr + mi * mi);
+    const float rp = mr / (mm + 1e-8f);
+    const float ip = mi / (mm + 1e-8f);
+    const float mphase = atan2f(ip, rp);
+    const float em = tanhf(mm) * mags;
+    const float ep = phase + mphase;
+    est[bt * ldest + f] = em * cosf(ep);
+    est[bt * ldest + 257 + f] = em * sinf(ep);
+    if (f < ldest - 514) est[bt * ldest + 514 + f] = 0.f;
+    if (mask_r) {
+      mask_r[bt * 257 + f] = mr;
+      mask_i[bt * 257 + f] = mi;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// ConviSTFT overlap-add + window-energy normalisation + trim (+ clamp)
+// ------------------------------------------------------------------------------------------
+__global__ void ola_kernel(const float* __restrict__ frames, const float* __restrict__ window,
+                           int B, int T, int win, int hop, int out_len, int trim, int clamp,
+                           float* __restrict__ wav) {
+  const int64_t total = (int64_t)B * out_len;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(i / out_len);
+    const int n = (int)(i - (int64_t)b * out_len);
+    const int p = n + trim;
+    int t_hi = p / hop;
+    if (t_hi > T - 1) t_hi = T - 1;
+    int t_lo = p - win + 1 <= 0 ? 0 : (p - win + 1 + hop - 1) / hop;
+    float acc = 0.f, coff = 0.f;
+    for (int t = t_lo; t <= t_hi; ++t) {
+      const int o = p - t * hop;
+      acc += frames[((int64_t)b * T + t) * win + o];
+      const float w = window[o];
+      coff += w * w;
+    }
+    float v = acc / (coff + 1e-8f);
+    if (clamp) v = fminf(fmaxf(v, -1.f), 1.f);
+    wav[i] = v;
+  }
+}
+
+// real = rr - ii ; imag = ir + ri   (tools_for_model.py:168-169)
+__global__ void complex_combine_kernel(const float* rr, const float* ii, const float* ir,
+                                       const float* ri, float* ro, float* io, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    ro[i] = rr[i] - ii[i];
+    io[i] = ir[i] + ri[i];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// ABF attention fusion, mid = 64 channels: 16 lanes per pixel, 4 channels per lane.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int nearest_src(int dst, int in_size, int out_size) {
+  // ATen nearest_idx (UpSample.h): identity / >>1 fast paths, else floorf(dst*scale), scale in f32
+  if (out_size == in_size) return dst;
+  if (out_size == 2 * in_size) return dst >> 1;
+  const float scale = (float)in_size / (float)out_size;
+  const int s = (int)floorf((float)dst * scale);
+  return s < in_size - 1 ? s : in_size - 1;
+}
+
+__global__ __launch_bounds__(256) void abf_fuse_kernel(const float* __restrict__ x,
+                                                       const float* __restrict__ res, int B,
+                                                       int F, int T, int Fr, int Tr,
+                                                       const float* __restrict__ w,
+                                                       const float* __restrict__ bias,
+                                                       float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & 15;  // channel quad
+  const int c = sub * 4;
+  f32x4 w0x, w0y, w1x, w1y;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    w0x[j] = w[c + j];
+    w0y[j] = w[64 + c + j];
+    w1x[j] = w[128 + c + j];
+    w1y[j] = w[192 + c + j];
+  }
+  const float b0 = bias[0], b1 = bias[1];
+  const int64_t npix = (int64_t)B * F * T;
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;  // pixel slot
+  const int64_t nslots = ((int64_t)gridDim.x * blockDim.x) >> 4;
+  for (int64_t p = gw; p < npix; p += nslots) {
+    const int t = (int)(p % T);
+    const int64_t bf = p / T;
+    const int f = (int)(bf % F);
+    const int b = (int)(bf / F);
+    const int fr = nearest_src(f, Fr, F);
+    const int tr = nearest_src(t, Tr, T);
+    const f32x4 xv = *reinterpret_cast<const f32x4*>(x + p * 64 + c);
+    const f32x4 yv = *reinterpret_cast<const f32x4*>(res + (((int64_t)b * Fr + fr) * Tr + tr) * 64 + c);
+    float d0 = 0.f, d1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      d0 += w0x[j] * xv[j] + w0y[j] * yv[j];
+      d1 += w1x[j] * xv[j] + w1y[j] * yv[j];
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      d0 += __shfl_xor(d0, o, 16);
+      d1 += __shfl_xor(d1, o, 16);
+    }
+    const float z0 = sigmoidf_(d0 + b0);
+    const float z1 = sigmoidf_(d1 + b1);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = xv[j] * z0 + yv[j] * z1;
+    *reinterpret_cast<f32x4*>(out + p * 64 + c) = o;
+  }
+}
+
+__global__ void zero_f64_kernel(double* p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = 0.0;
+}
+
+inline unsigned grid_for(int64_t n, int block = 256, int64_t cap = 8192) {
+  int64_t g = cdiv(n, block);
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+}  // namespace clskd
+
+using namespace clskd;
+
+extern "C" int32_t clskd_bn_partial_blocks(int64_t rows, int32_t C) {
+  int64_t work = rows * (int64_t)C / (256 * 64);
+  if (work < 1) work = 1;
+  if (work > 2048) work = 2048;
+  if (work > rows) work = rows;
+  return (int32_t)work;
+}
+
+extern "C" int clskd_bn_stats_partial(const float* x, int64_t rows, int32_t C, double* partial,
+                                      int32_t nblk, void* stream) {
+  CLSKD_CHECK_ARG(x && partial, "bn_stats: null pointer");
+  CLSKD_CHECK_SHAPE(rows > 0 && C >= 4 && C % 4 == 0 && C <= 1024, "bn_stats: bad C=%d", C);
+  CLSKD_CHECK_SHAPE(nblk >= 1, "bn_stats: nblk");
+  CLSKD_CHECK_ARG(((uintptr_t)x & 15) == 0, "bn_stats: x must be 16-byte aligned");
+  const int64_t rpb = cdiv(rows, nblk);
+  hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(nblk), dim3(256), 0, as_stream(stream), x, rows,
+                     C, rpb, partial);
+  CLSKD_LAUNCH_CHECK("bn_stats_partial");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_bn_finalize(const double* partial, int32_t nblk, int64_t rows, int32_t C,
+                                 const float* gamma, const float* beta, float eps,
+                                 float* running_mean, float* running_var, float momentum,
+                                 int32_t n_updates, float* scale, float* shift, float* mean_out,
+                                 float* var_out, void* stream) {
+  CLSKD_CHECK_ARG(partial && scale && shift, "bn_finalize: null pointer");
+  CLSKD_CHECK_SHAPE(C > 0 && nblk > 0 && rows > 0, "bn_finalize: shape");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, as_stream(stream), partial, nblk,
+                     rows, C, gamma, beta, eps, running_mean, running_var, momentum, n_updates,
+                     scale, shift, mean_out, var_out);
+  CLSKD_LAUNCH_CHECK("bn_finalize");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_bn_eval_coeffs(const float* running_mean, const float* running_var,
+                                    const float* gamma, const float* beta, float eps, int32_t C,
+                                    float* scale, float* shift, void* stream) {
+  CLSKD_CHECK_ARG(running_mean && running_var && scale && shift, "bn_eval: null pointer");
+  hipLaunchKernelGGL(bn_eval_coeffs_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0,
+                     as_stream(stream), running_mean, running_var, gamma, beta, eps, C, scale,
+                     shift);
+  CLSKD_LAUNCH_CHECK("bn_eval_coeffs");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_bn_apply(const float* x, float* y, int64_t rows, int32_t C,
+                              const float* scale, const float* shift, const float* alpha,
+                              void* stream) {
+  CLSKD_CHECK_ARG(x && y && scale && shift, "bn_apply: null pointer");
+  CLSKD_CHECK_SHAPE(C % 4 == 0 && rows > 0, "bn_apply: C=%d must be a multiple of 4", C);
+  CLSKD_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0, "bn_apply: alignment");
+  const int64_t n4 = rows * C / 4;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), x, y, n4,
+                     C, scale, shift, alpha);
+  CLSKD_LAUNCH_CHECK("bn_apply");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_frame_pad(const float* x, int64_t ldx, int32_t B, int32_t L, int32_t pad,
+                               int32_t Lp, int32_t mode, float* xp, void* stream) {
+  CLSKD_CHECK_ARG(x && xp, "frame_pad: null pointer");
+  CLSKD_CHECK_SHAPE(B > 0 && L > 0 && Lp > 0 && pad >= 0, "frame_pad: shape");
+  CLSKD_CHECK_SHAPE(mode == 0 || pad < L, "frame_pad: reflect pad %d needs L > pad", pad);
+  hipLaunchKernelGGL(frame_pad_kernel, dim3(grid_for((int64_t)B * Lp)), dim3(256), 0,
+                     as_stream(stream), x, ldx, B, L, pad, Lp, mode, xp);
+  CLSKD_LAUNCH_CHECK("frame_pad");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_mask_e(const float* spec, int32_t ldspec, const float* mask, int32_t Tm,
+                            int32_t B, int32_t T, float* est, int32_t ldest, float* mask_r,
+                            float* mask_i, void* stream) {
+  CLSKD_CHECK_ARG(spec && mask && est, "mask_e: null pointer");
+  CLSKD_CHECK_SHAPE(ldspec >= 514 && ldest >= 514 && ldest - 514 <= 257 && Tm >= T + 1,
+                    "mask_e: bad strides");
+  hipLaunchKernelGGL(mask_e_kernel, dim3(grid_for((int64_t)B * T * 257)), dim3(256), 0,
+                     as_stream(stream), spec, ldspec, mask, Tm, B, T, est, ldest, mask_r, mask_i);
+  CLSKD_LAUNCH_CHECK("mask_e");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_ola(const float* frames, const float* window, int32_t B, int32_t T,
+                         int32_t win, int32_t hop, int32_t out_len, int32_t trim, int32_t clamp,
+                         float* wav, void* stream) {
+  CLSKD_CHECK_ARG(frames && window && wav, "ola: null pointer");
+  CLSKD_CHECK_SHAPE(out_len > 0 && T > 0 && hop > 0 && win >= hop, "ola: shape");
+  hipLaunchKernelGGL(ola_kernel, dim3(grid_for((int64_t)B * out_len)), dim3(256), 0,
+                     as_stream(stream), frames, window, B, T, win, hop, out_len, trim, clamp, wav);
+  CLSKD_LAUNCH_CHECK("ola");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_complex_combine(const float* rr, const float* ii, const float* ir,
+                                     const float* ri, float* real_out, float* imag_out,
+                                     int64_t n, void* stream) {
+  CLSKD_CHECK_ARG(rr && ii && ir && ri && real_out && imag_out, "complex_combine: null pointer");
+  hipLaunchKernelGGL(complex_combine_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), rr,
+                     ii, ir, ri, real_out, imag_out, n);
+  CLSKD_LAUNCH_CHECK("complex_combine");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_abf_fuse(const float* x, const float* res, int32_t B, int32_t F, int32_t T,
+                              int32_t Fr, int32_t Tr, const float* w, const float* b, float* out,
+                              void* stream) {
+  CLSKD_CHECK_ARG(x && res && w && b && out, "abf_fuse: null pointer");
+  CLSKD_CHECK_SHAPE(B > 0 && F > 0 && T > 0 && Fr > 0 && Tr > 0, "abf_fuse: shape");
+  const int64_t npix = (int64_t)B * F * T;
+  hipLaunchKernelGGL(abf_fuse_kernel, dim3(grid_for(npix * 16)), dim3(256), 0, as_stream(stream), x,
+                     res, B, F, T, Fr, Tr, w, b, out);
+  CLSKD_LAUNCH_CHECK("abf_fuse");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_zero_f64(double* p, int64_t n, void* stream) {
+  CLSKD_CHECK_ARG(p, "zero_f64: null pointer");
+  hipLaunchKernelGGL(zero_f64_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, n);
+  CLSKD_LAUNCH_CHECK("zero_f64");
+  return CLSKD_OK;
+}

@@ -1,0 +1,86 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads and exports every symbol that
+include/clskd.h declares; host-side plumbing (K tables, packing, module trees) is consistent.
+No GPU compute is called here."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from clskd import _lib, config as cfg
+
+
+def test_library_exports_every_header_symbol():
+    assert os.path.exists(_lib.LIB_PATH), "run __graft_entry__.build() first"
+    lib = _lib.load(require_gpu=False)
+    syms = _lib.header_symbols()
+    assert len(syms) >= 20
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    # every bound signature is a header symbol and vice versa
+    assert set(_lib.SIGNATURES) == set(syms)
+    assert lib.clskd_version() == 1
+    assert isinstance(lib.clskd_last_error(), bytes)
+
+
+def test_struct_layouts_match_header():
+    # clskd_seg: ptr + 3 int64 + 2 int32 = 40 B; desc must be 8-aligned
+    assert ctypes.sizeof(_lib.Seg) == 40
+    assert ctypes.sizeof(_lib.KtabEntry) == 8
+    assert ctypes.sizeof(_lib.GramJob) == 48
+    assert ctypes.sizeof(_lib.ConvDesc) % 8 == 0
+
+
+def test_error_path_reports_without_gpu():
+    lib = _lib.load(require_gpu=False)
+    rc = lib.clskd_conv2d_fwd(None, None)
+    assert rc == -4
+    assert b"null descriptor" in lib.clskd_last_error()
+    rc = lib.clskd_lstm_recurrent(None, 0, 0, 0, None, 1, 1, 1, 32, None, 0, 0, 0, None)
+    assert rc < 0
+
+
+def test_ktab_construction():
+    from clskd import ops
+    g1 = ops.SegGeom(8, 1000, 100, 8, 5, 12)
+    g2 = ops.SegGeom(4, 500, 40, 4, 5, 12)
+    entries = []
+    taps = [(-1, 0), (0, -1)]
+    for dF, dT in taps:
+        for s, g in enumerate((g1, g2)):
+            for c in range(g.C):
+                entries.append((c + dF * g.sF + dT * g.sT, dF, dT, s))
+    assert len(entries) == 24  # padded to 32 in the device table
+    # K order is (tap, segment, channel): the packer must follow it
+    w = torch.arange(3 * 2 * 12, dtype=torch.float32).reshape(3, 2, 12)
+    wp = ops.pack_weight(w, 24)
+    assert wp.shape == (3, 32) and torch.all(wp[:, 24:] == 0)
+    assert torch.equal(wp[:, :24], w.reshape(3, 24))
+
+
+def test_module_tree_matches_reference_state_dict():
+    from clskd.model import DCCRN
+    for spec in (cfg.STUDENT, cfg.TEACHER):
+        m = DCCRN(masking_mode="E", use_clstm=True, **spec)
+        keys = [k for k in m.state_dict() if not k.startswith(("stft.", "istft."))]
+        assert keys == list(cfg.dccrn_param_shapes(**spec))
+    with pytest.raises(NotImplementedError):
+        DCCRN(masking_mode="C", use_clstm=True, **cfg.STUDENT)
+
+
+def test_stft_kernels_match_oracle():
+    from clskd.model import ConvSTFT, ConviSTFT
+    from oracle import ref_cpu
+    fwd, inv, win = ref_cpu._kernels()
+    assert torch.equal(ConvSTFT(400, 100, 512, "hamming", "complex").weight, fwd)
+    i = ConviSTFT(400, 100, 512, "hamming", "complex")
+    assert torch.equal(i.weight, inv) and torch.equal(i.window, win)
+
+
+def test_synthetic_data_recipe():
+    from clskd.data import synthetic_pairs
+    a, b = synthetic_pairs(2, 16000, seed=3)
+    a2, _ = synthetic_pairs(2, 16000, seed=3)
+    assert a.shape == (2, 16000) and np.array_equal(a, a2)
+    assert np.abs(a).max() <= 1.0 and np.abs(b).max() < 1.0
