@@ -1,0 +1,179 @@
+"""Benchmark: DCCRN-CLSKD fwd+loss step (configuration C2 of BASELINE.json) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+
+A step = one KnowledgeDistillation.training_step (distill.py:72-148) over B=16 synthetic 16 kHz
+4 s noisy/clean pairs per GPU: teacher + student DCCRN forwards (train-mode BN), ReviewKD
+fusions, 14 SPKD Gram losses and the MRSTFT base loss; frames = B * T with T = L/100 + 3 = 643.
+Each rank processes its own batch shard (weak scaling; forward+loss has no exchange step).
+Prints one JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "speech-enhancement-clskd_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from clskd import config as cfg  # noqa: E402
+
+METRIC = "frames/sec/GPU DCCRN-CLSKD fwd+loss @16k 4s; SI-SNR parity ±0.01 dB"
+PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (f32-in MFMA), dense
+B_PER_GPU = 16
+L = 64000
+
+
+def build_kd(dev, abf_reinit):
+    from clskd.distill import KnowledgeDistillation
+    from clskd.model import DCCRN
+    from clskd.weights import ABF_SEED, STUDENT_SEED, TEACHER_SEED, apply_recipe
+    teacher = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.TEACHER), TEACHER_SEED)
+    student = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.STUDENT), STUDENT_SEED)
+    kd = KnowledgeDistillation(teacher, student, abf_reinit=abf_reinit).to(dev).train()
+    apply_recipe(kd.review_encoder, ABF_SEED, "encoder.")
+    apply_recipe(kd.review_decoder, ABF_SEED, "decoder.")
+    return kd
+
+
+def cpu_baseline(seconds):
+    """The CPU oracle (fp32 PyTorch-CPU restatement of the reference, oracle/ref_cpu.py) timed on
+    this host on a bounded sample of the same workload: B=2 x 4 s clips per step, repeated until
+    `seconds` of CPU work."""
+    from oracle import ref_cpu as R
+    from clskd.data import synthetic_pairs
+    from clskd.weights import ABF_SEED, STUDENT_SEED, TEACHER_SEED, recipe_state_dict
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    pt = R.to_torch_params(recipe_state_dict(cfg.dccrn_param_shapes(**cfg.TEACHER), TEACHER_SEED))
+    ps = R.to_torch_params(recipe_state_dict(cfg.dccrn_param_shapes(**cfg.STUDENT), STUDENT_SEED))
+    pa = R.to_torch_params(recipe_state_dict(
+        {**cfg.review_param_shapes("encoder"), **cfg.review_param_shapes("decoder")}, ABF_SEED))
+    Bc = 2
+    noisy, clean = synthetic_pairs(Bc, L, seed=99)
+    X, Y = torch.from_numpy(noisy), torch.from_numpy(clean)
+    with torch.no_grad():
+        R.clskd_step(pt, ps, pa, X, Y)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            R.clskd_step(pt, ps, pa, X, Y)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    frames = n * Bc * cfg.n_frames(L)
+    return dict(value=round(frames / el, 2), unit="frames/s", cores=threads, kind="port",
+                sample=f"oracle/ref_cpu.clskd_step, B={Bc} x 4 s @16 kHz, {n} step(s) in {el:.1f} s, "
+                       f"fp32, torch CPU {threads} threads")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--abf-reinit", default="step", choices=["step", "once"])
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world == 1:
+        raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from clskd import ops
+    from clskd.data import synthetic_pairs
+    kd = build_kd(dev, args.abf_reinit)
+    noisy, clean = synthetic_pairs(B_PER_GPU, L, seed=1000 + rank)
+    X = torch.from_numpy(noisy).to(dev)
+    Y = torch.from_numpy(clean).to(dev)
+    T = cfg.n_frames(L)
+
+    for _ in range(args.warmup):
+        kd.training_step((X, Y), 0)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # ---- timed region: exactly K steps, barrier + sync on both sides --------------------
+    barrier()
+    ops.KernelTimer.start()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = kd.training_step((X, Y), i)
+    barrier()
+    el = time.perf_counter() - t0
+    ktimes = ops.KernelTimer.stop()
+    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = float(el_t.item())
+    loss_v = float(loss.item())
+
+    if rank == 0:
+        frames = world * B_PER_GPU * T * args.steps
+        # dominant kernel = conv engine variant with the largest total time
+        name, (n_l, ms, flops) = max(ktimes.items(), key=lambda kv: kv[1][1])
+        conv_total_ms = sum(v[1] for v in ktimes.values())
+        conv_total_fl = sum(v[2] for v in ktimes.values())
+        avg_ms = ms / n_l
+        achieved = flops / n_l / (avg_ms * 1e-3) / 1e12
+        roof = dict(bound="mfma", kernel=name, achieved=round(achieved, 2),
+                    peak=PEAK_F32_MFMA_TFLOPS, unit="TFLOP/s",
+                    frac=round(achieved / PEAK_F32_MFMA_TFLOPS, 4), traffic=None,
+                    launches_per_step=n_l // args.steps, avg_launch_us=round(avg_ms * 1e3, 2),
+                    algorithmic_gflop_per_launch=round(flops / n_l / 1e9, 3),
+                    conv_engine_all_variants=dict(
+                        ms_per_step=round(conv_total_ms / args.steps, 3),
+                        tflops=round(conv_total_fl / (conv_total_ms * 1e-3) / 1e12, 2)))
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_seconds)
+        out = {
+            "metric": METRIC,
+            "value": round(frames / el, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (seeded 16 kHz enveloped-sinusoid clean + noise at 0-10 dB SNR; "
+                    "recipe weights, SURVEY.md §8 d)",
+            "config": {"workload": "C2: DCCRN-CLSKD fwd+loss (teacher 3.67M + student 0.23M "
+                                   "params, ReviewKD enc+dec, 14 SPKD Grams, MRSTFT)",
+                       "global_batch": world * B_PER_GPU, "per_gpu_batch": B_PER_GPU,
+                       "clip_samples": L, "frames_per_clip": T, "parallelism": f"dp{world}",
+                       "abf_reinit": args.abf_reinit, "loss": round(loss_v, 6)},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -21,6 +21,36 @@ def lib():
     return _lib.load()
 
 
+class KernelTimer:
+    """Live per-launch timing of the conv engine with HIP events on the launching stream.
+    Enabled by bench.py over its timed region; records (kernel variant, flops, start, end)."""
+    active = False
+    records = []
+
+    @classmethod
+    def start(cls):
+        cls.active, cls.records = True, []
+
+    @classmethod
+    def stop(cls):
+        cls.active = False
+        torch.cuda.synchronize()
+        out = {}
+        for name, flops, e0, e1 in cls.records:
+            ms = e0.elapsed_time(e1)
+            agg = out.setdefault(name, [0, 0.0, 0.0])
+            agg[0] += 1
+            agg[1] += ms
+            agg[2] += flops
+        cls.records = []
+        return out  # name -> [launches, total_ms, total_flops]
+
+
+def conv_kernel_name(N, vec4):
+    bn = 32 if N <= 32 else (64 if N <= 64 else 128)
+    return f"conv_igemm_f32<{bn},{'true' if vec4 else 'false'}>"
+
+
 def _stream():
     return _lib.stream_ptr()
 
@@ -138,7 +168,15 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
     d.nlo = min(omap.nlo, 1 << 30)
     d.of_mul, d.of_add = omap.of_mul, omap.of_add
     d.compute = _lib.F32
-    check(lib().clskd_conv2d_fwd(C.byref(d), _stream()), "conv2d")
+    if KernelTimer.active:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        check(lib().clskd_conv2d_fwd(C.byref(d), _stream()), "conv2d")
+        e1.record()
+        KernelTimer.records.append((conv_kernel_name(N, vec4), 2.0 * B * Fo * To * N * K, e0, e1))
+    else:
+        check(lib().clskd_conv2d_fwd(C.byref(d), _stream()), "conv2d")
     return out
 
 
