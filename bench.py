@@ -84,22 +84,18 @@ def main():
     ap.add_argument("--abf-reinit", default="step", choices=["step", "once"])
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    from clskd import dist as cdist
+    rank, world, local_rank = cdist.env_rank()
     if args.gpus > 1 and world == 1:
         raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+    cdist.init("nccl", dev)
 
     from clskd import ops
     from clskd.data import synthetic_pairs
     kd = build_kd(dev, args.abf_reinit)
-    noisy, clean = synthetic_pairs(B_PER_GPU, L, seed=1000 + rank)
+    noisy, clean = synthetic_pairs(B_PER_GPU, L, seed=cdist.shard_seed(1000, rank))
     X = torch.from_numpy(noisy).to(dev)
     Y = torch.from_numpy(clean).to(dev)
     T = cfg.n_frames(L)
@@ -108,24 +104,16 @@ def main():
         kd.training_step((X, Y), 0)
     torch.cuda.synchronize()
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-
     # ---- timed region: exactly K steps, barrier + sync on both sides --------------------
-    barrier()
+    cdist.barrier(dev)
     ops.KernelTimer.start()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = kd.training_step((X, Y), i)
-    barrier()
+    cdist.barrier(dev)
     el = time.perf_counter() - t0
     ktimes = ops.KernelTimer.stop()
-    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if dist is not None:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    el = float(el_t.item())
+    el = cdist.max_over_ranks(el, dev)
     loss_v = float(loss.item())
 
     if rank == 0:
@@ -170,9 +158,9 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    if world > 1:
+        cdist.barrier(dev)
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":
