@@ -27,17 +27,19 @@ from clskd import config as cfg  # noqa: E402
 
 METRIC = "frames/sec/GPU DCCRN-CLSKD fwd+loss @16k 4s; SI-SNR parity ±0.01 dB"
 PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (f32-in MFMA), dense
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
 B_PER_GPU = 16
 L = 64000
 
 
-def build_kd(dev, abf_reinit):
+def build_kd(dev, abf_reinit, precision="fp32"):
     from clskd.distill import KnowledgeDistillation
     from clskd.model import DCCRN
     from clskd.weights import ABF_SEED, STUDENT_SEED, TEACHER_SEED, apply_recipe
     teacher = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.TEACHER), TEACHER_SEED)
     student = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.STUDENT), STUDENT_SEED)
-    kd = KnowledgeDistillation(teacher, student, abf_reinit=abf_reinit).to(dev).train()
+    kd = KnowledgeDistillation(teacher, student, abf_reinit=abf_reinit,
+                               precision=precision).to(dev).train()
     apply_recipe(kd.review_encoder, ABF_SEED, "encoder.")
     apply_recipe(kd.review_decoder, ABF_SEED, "decoder.")
     return kd
@@ -82,6 +84,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--abf-reinit", default="step", choices=["step", "once"])
+    ap.add_argument("--precision", default="mixed", choices=["mixed", "fp32"],
+                    help="mixed: teacher + ReviewKD GEMMs on bf16 MFMA operands (fp32 accumulate), "
+                         "student fp32; fp32: every GEMM on exact-f32 MFMA")
     args = ap.parse_args()
 
     from clskd import dist as cdist
@@ -94,7 +99,7 @@ def main():
 
     from clskd import ops
     from clskd.data import synthetic_pairs
-    kd = build_kd(dev, args.abf_reinit)
+    kd = build_kd(dev, args.abf_reinit, args.precision)
     noisy, clean = synthetic_pairs(B_PER_GPU, L, seed=cdist.shard_seed(1000, rank))
     X = torch.from_numpy(noisy).to(dev)
     Y = torch.from_numpy(clean).to(dev)
@@ -124,9 +129,10 @@ def main():
         conv_total_fl = sum(v[2] for v in ktimes.values())
         avg_ms = ms / n_l
         achieved = flops / n_l / (avg_ms * 1e-3) / 1e12
+        peak = PEAK_BF16_MFMA_TFLOPS if "bf16" in name else PEAK_F32_MFMA_TFLOPS
         roof = dict(bound="mfma", kernel=name, achieved=round(achieved, 2),
-                    peak=PEAK_F32_MFMA_TFLOPS, unit="TFLOP/s",
-                    frac=round(achieved / PEAK_F32_MFMA_TFLOPS, 4), traffic=None,
+                    peak=peak, unit="TFLOP/s",
+                    frac=round(achieved / peak, 4), traffic=None,
                     launches_per_step=n_l // args.steps, avg_launch_us=round(avg_ms * 1e3, 2),
                     algorithmic_gflop_per_launch=round(flops / n_l / 1e9, 3),
                     conv_engine_all_variants=dict(
@@ -146,14 +152,17 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "bf16" if args.precision == "mixed" else "fp32",
             "data": "synthetic (seeded 16 kHz enveloped-sinusoid clean + noise at 0-10 dB SNR; "
                     "recipe weights, SURVEY.md §8 d)",
             "config": {"workload": "C2: DCCRN-CLSKD fwd+loss (teacher 3.67M + student 0.23M "
                                    "params, ReviewKD enc+dec, 14 SPKD Grams, MRSTFT)",
                        "global_batch": world * B_PER_GPU, "per_gpu_batch": B_PER_GPU,
                        "clip_samples": L, "frames_per_clip": T, "parallelism": f"dp{world}",
-                       "abf_reinit": args.abf_reinit, "loss": round(loss_v, 6)},
+                       "abf_reinit": args.abf_reinit, "loss": round(loss_v, 6),
+                       "precision": ("teacher+ReviewKD GEMMs bf16 MFMA operands / fp32 accumulate; "
+                                     "student, STFT/iSTFT, LSTM recurrence, BN, losses fp32")
+                       if args.precision == "mixed" else "fp32 MFMA everywhere"},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

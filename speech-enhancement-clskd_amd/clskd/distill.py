@@ -26,6 +26,18 @@ from .framework import MultiResolutionSTFTLoss, SPKDLoss, build_review_kd
 from .model import DCCRN
 
 
+_SIDE = {}
+
+
+def _side_stream(dev):
+    """A second HIP stream per device: the student forward runs there, overlapping the teacher's
+    latency-bound LSTM recurrence and small kernels with the other model's GEMMs."""
+    key = torch.device(dev).index
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=dev)
+    return _SIDE[key]
+
+
 def _gram_bftc(t, c0=0, Cs=None):
     B, Fn, Tn, Ct = t.shape
     Cs = Ct if Cs is None else Cs
@@ -36,7 +48,7 @@ class KnowledgeDistillation(nn.Module):
     """distill.py:38-229 without Lightning: same constructor and step signature."""
 
     def __init__(self, teacher, student, sftf_loss=MultiResolutionSTFTLoss, spkd_loss=SPKDLoss,
-                 cfg=cfg, abf_reinit="once"):
+                 cfg=cfg, abf_reinit="once", precision="fp32"):
         super().__init__()
         self.automatic_optimization = True
         self.teacher = teacher
@@ -50,6 +62,22 @@ class KnowledgeDistillation(nn.Module):
         self.review_encoder = build_review_kd(None, "encoder")
         self.review_decoder = build_review_kd(None, "decoder")
         self.last = None
+        self.set_precision(precision)
+
+    def set_precision(self, precision):
+        """"fp32": every GEMM on exact-f32 MFMA.  "mixed": the frozen teacher and the ReviewKD
+        fusions (95 % of the step's FLOPs; they only feed the SPKD similarity Grams) run bf16
+        MFMA operands with fp32 accumulation; the student — whose waveform is the product and
+        the SI-SNR / RMS parity target — stays fp32."""
+        if precision not in ("fp32", "mixed"):
+            raise ValueError(precision)
+        self.precision = precision
+        c = "bf16" if precision == "mixed" else "fp32"
+        self.teacher.compute = c
+        self.review_encoder.set_compute(c)
+        self.review_decoder.set_compute(c)
+        self.student.compute = "fp32"
+        return self
 
     def forward(self, x):
         return self.student(x)
@@ -95,9 +123,14 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     spec = teacher.spectrum(X)
     # both ConvSTFTs are the fixed (win 400, hop 100, fft 512) kernel of the same window type
     s_spec = spec if teacher.win_type == student.win_type else None
+    main = torch.cuda.current_stream(dev)
+    side = _side_stream(dev)
+    side.wait_stream(main)  # spec ready; previous step's work on main is done before reuse
+    with torch.cuda.stream(side):
+        sf = student.run(X, train=student.training, bn_updates=2 if student.training else 0,
+                         spec=s_spec, want_masks=False)
     tf = teacher.run(X, train=teacher.training, bn_updates=1, spec=spec, want_masks=False)
-    sf = student.run(X, train=student.training, bn_updates=2 if student.training else 0,
-                     spec=s_spec, want_masks=False)
+    main.wait_stream(side)
     # ReviewKD on the student taps (distill.py:92-96); tap contract SURVEY.md §8 a11
     s_enc = review_encoder.forward_bftc(sf["enc"])
     s_dec = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5])

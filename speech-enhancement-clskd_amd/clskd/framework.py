@@ -174,20 +174,22 @@ class ABF(nn.Module):
         nn.init.kaiming_uniform_(self.conv1[0].weight, a=1)
         nn.init.kaiming_uniform_(self.conv2[0].weight, a=1)
         self._wcache = {}
+        self.compute = "fp32"  # MFMA operand type of conv1/conv2 ("fp32" | "bf16")
 
     def _weights(self):
         ps = [self.conv1[0].weight, self.conv2[0].weight]
         if self.att_conv is not None:
             ps += [self.att_conv[0].weight, self.att_conv[0].bias]
-        ver = _pv(*ps)
+        ver = _pv(*ps) + (self.compute,)
         ent = self._wcache.get("w")
         if ent is None or ent[0] != ver:
             with torch.no_grad():
+                c1 = self.compute if self.conv1[0].weight.shape[1] >= 64 else "fp32"
                 w1 = self.conv1[0].weight  # [mid, in, 1, 1]
-                w1p = ops.pack_weight(w1.reshape(w1.shape[0], 1, w1.shape[1]), w1.shape[1])
+                w1p = ops.pack_weight(w1.reshape(w1.shape[0], 1, w1.shape[1]), w1.shape[1], c1)
                 w2 = self.conv2[0].weight  # [out, mid, 3, 3]
                 w2p = ops.pack_weight(w2.permute(0, 2, 3, 1).reshape(w2.shape[0], 9, w2.shape[1]),
-                                      9 * w2.shape[1])
+                                      9 * w2.shape[1], self.compute)
                 att = None
                 if self.att_conv is not None:
                     att = (self.att_conv[0].weight.reshape(2, -1).float().contiguous(),
@@ -205,6 +207,8 @@ class ABF(nn.Module):
         dev = x.device
         f32 = dict(device=dev, dtype=torch.float32)
         x1 = torch.empty(B, Fn, Tn, mid, **f32)
+        if w1p.dtype == torch.bfloat16 and not ops.bf16_eligible([seg_bftc(x)]):
+            raise RuntimeError("ABF conv1 input is not vec4-gatherable for bf16")
         ops.conv([seg_bftc(x)], [(0, 0)], B, Fn, Tn, mid, w1p, None, x1,
                  OutMap(Fn * Tn * mid, Tn * mid, mid))
         bn = self.conv1[1]
@@ -248,6 +252,11 @@ class ReviewKD(nn.Module):
         for idx, in_channel in enumerate(in_channels):
             abfs.append(ABF(in_channel, mid_channel, out_channels[idx], idx < len(in_channels) - 1))
         self.abfs = abfs[::-1]
+
+    def set_compute(self, compute):
+        for abf in self.abfs:
+            abf.compute = compute
+        return self
 
     def forward_bftc(self, feats):
         """feats: BFTC student features in the reference's list order.  Returns BFTC outputs."""

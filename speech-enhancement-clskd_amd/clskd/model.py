@@ -198,6 +198,9 @@ class DCCRN(nn.Module):
             self.decoder.append(nn.Sequential(*mods))
         self._wcache = {}
         self._tap_sinks = []
+        # MFMA operand type of the large GEMMs: "fp32" (exact-f32 MFMA) or "bf16" (bf16 operands,
+        # fp32 accumulation).  STFT/iSTFT framing GEMMs always run fp32.
+        self.compute = "fp32"
 
     # ---------------------------------------------------------------- reference helpers
     def flatten_parameters(self):
@@ -219,6 +222,12 @@ class DCCRN(nn.Module):
         raise NotImplementedError(f"loss_mode {loss_mode!r} is not on the CLSKD hot path")
 
     # ---------------------------------------------------------------- packed weights
+    def _cmp(self, segs, K):
+        """Operand type for one GEMM: bf16 only where the model asks for it and the gather allows."""
+        if self.compute == "bf16" and K >= 64 and ops.bf16_eligible(segs):
+            return "bf16"
+        return "fp32"
+
     def _packed(self, key, params, build):
         ent = self._wcache.get(key)
         ver = _pv(*params)
@@ -228,7 +237,7 @@ class DCCRN(nn.Module):
             self._wcache[key] = ent
         return ent[1]
 
-    def _enc_w(self, i):
+    def _enc_w(self, i, compute="fp32"):
         cc = self.encoder[i][0]
 
         def build():
@@ -240,13 +249,13 @@ class DCCRN(nn.Module):
             w = w.permute(0, 2, 3, 1).reshape(Co, 10, Ci)  # tap = kf*2 + kt
             bias = torch.cat([cc.real_conv.bias - cc.imag_conv.bias,
                               cc.imag_conv.bias + cc.real_conv.bias]).float().contiguous()
-            return ops.pack_weight(w, 10 * Ci), bias
-        return self._packed(("enc", i), (cc.real_conv.weight, cc.imag_conv.weight,
-                                         cc.real_conv.bias, cc.imag_conv.bias), build)
+            return ops.pack_weight(w, 10 * Ci, compute), bias
+        return self._packed(("enc", i, compute), (cc.real_conv.weight, cc.imag_conv.weight,
+                                                  cc.real_conv.bias, cc.imag_conv.bias), build)
 
     _DEC_TAPS = {0: ((0, 1), (2, 0), (4, -1)), 1: ((1, 1), (3, 0))}  # parity -> (kf, dF)
 
-    def _dec_w(self, d, parity):
+    def _dec_w(self, d, parity, compute="fp32"):
         cc = self.decoder[d][0]
 
         def build():
@@ -260,11 +269,11 @@ class DCCRN(nn.Module):
             w = w.permute(2, 0, 1)  # [Co, ntap, Ci]
             bias = torch.cat([cc.real_conv.bias - cc.imag_conv.bias,
                               cc.imag_conv.bias + cc.real_conv.bias]).float().contiguous()
-            return ops.pack_weight(w, len(taps) * Ci), bias
-        return self._packed(("dec", d, parity), (cc.real_conv.weight, cc.imag_conv.weight,
-                                                 cc.real_conv.bias, cc.imag_conv.bias), build)
+            return ops.pack_weight(w, len(taps) * Ci, compute), bias
+        return self._packed(("dec", d, parity, compute), (cc.real_conv.weight, cc.imag_conv.weight,
+                                                          cc.real_conv.bias, cc.imag_conv.bias), build)
 
-    def _lstm_w(self, li):
+    def _lstm_w(self, li, compute="fp32"):
         m = self.enhance[li]
         R, I = m.real_lstm, m.imag_lstm
 
@@ -275,22 +284,22 @@ class DCCRN(nn.Module):
                 D = wih.shape[1]
                 Ch = D // 4
                 w = wih.reshape(8 * H, Ch, 4).permute(0, 2, 1)  # [8H, tap=f, Ch]
-                wp = ops.pack_weight(w, D)
+                wp = ops.pack_weight(w, D, compute)
             else:
-                wp = ops.pack_weight(wih.unsqueeze(1), wih.shape[1])
+                wp = ops.pack_weight(wih.unsqueeze(1), wih.shape[1], compute)
             bias = torch.cat([R.bias_ih_l0 + R.bias_hh_l0, I.bias_ih_l0 + I.bias_hh_l0]).float().contiguous()
             whh = torch.stack([R.weight_hh_l0, I.weight_hh_l0], 0).float().contiguous()
             out = [wp, bias, whh]
             if m.projection_dim is not None:
                 for lin in (m.r_trans, m.i_trans):
-                    out += [ops.pack_weight(lin.weight.unsqueeze(1), lin.weight.shape[1]),
+                    out += [ops.pack_weight(lin.weight.unsqueeze(1), lin.weight.shape[1], compute),
                             lin.bias.float().contiguous()]
             return out
         ps = [R.weight_ih_l0, I.weight_ih_l0, R.weight_hh_l0, I.weight_hh_l0, R.bias_ih_l0,
               R.bias_hh_l0, I.bias_ih_l0, I.bias_hh_l0]
         if m.projection_dim is not None:
             ps += [m.r_trans.weight, m.r_trans.bias, m.i_trans.weight, m.i_trans.bias]
-        return self._packed(("lstm", li), ps, build)
+        return self._packed(("lstm", li, compute), ps, build)
 
     def _stft_w(self):
         def build():
@@ -351,12 +360,12 @@ class DCCRN(nn.Module):
         for i in range(nl):
             Co = kn[i + 1]
             Fo = F // 2
-            wp, bias = self._enc_w(i)
             if i == 0:
                 segs = [Seg(spec, 1, SegGeom(1, T * 514, 1, 514, 256, T)),
                         Seg(spec, 258, SegGeom(1, T * 514, 1, 514, 256, T))]
             else:
                 segs = [seg_bftc(enc[-1])]
+            wp, bias = self._enc_w(i, self._cmp(segs, 10 * kn[i]))
             taps = [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)]
             raw = torch.empty(B, Fo, T, Co, **f32)
             ops.conv(segs, taps, B, Fo, T, Co, wp, bias, raw, OutMap(Fo * T * Co, T * Co, Co),
@@ -375,8 +384,6 @@ class DCCRN(nn.Module):
         r_in = None
         lstm_io = []
         for li in range(self.hidden_layers):
-            packs = self._lstm_w(li)
-            wp, bias, whh = packs[:3]
             gx = torch.empty(2, B, T, 8 * H, **f32)
             for half in range(2):
                 if li == 0:
@@ -386,6 +393,8 @@ class DCCRN(nn.Module):
                     src = r_in[half]
                     segs = [Seg(src, 0, SegGeom(H, T * H, 0, H, 1, T))]
                     taps = [(0, 0)]
+                packs = self._lstm_w(li, self._cmp(segs, len(taps) * segs[0].geom.C))
+                wp, bias, whh = packs[:3]
                 ops.conv(segs, taps, B, 1, T, 8 * H, wp, bias, gx[half],
                          OutMap(T * 8 * H, 0, 8 * H))
             hs = torch.empty(2, 2 * B, T, H, **f32)
@@ -399,12 +408,12 @@ class DCCRN(nn.Module):
         # projection into the decoder input [B][D4][T][C6] (DCCRN.py:188-199)
         dec_in = torch.empty(B, D4, T, C6, **f32)
         m = self.enhance[self.hidden_layers - 1]
-        packs = self._lstm_w(self.hidden_layers - 1)
         P = m.projection_dim
         for half in range(2):
+            segs = [Seg(r_in[half], 0, SegGeom(H, T * H, 0, H, 1, T))]
+            packs = self._lstm_w(self.hidden_layers - 1, self._cmp(segs, H))
             wpp, bp = packs[3 + 2 * half], packs[4 + 2 * half]
-            src = r_in[half]
-            ops.conv([Seg(src, 0, SegGeom(H, T * H, 0, H, 1, T))], [(0, 0)], B, 1, T, P, wpp, bp,
+            ops.conv(segs, [(0, 0)], B, 1, T, P, wpp, bp,
                      dec_in, OutMap(D4 * T * C6, 0, C6, 1, T * C6, D4), out_offset=half * Ch)
         # ---------------- decoder (DCCRN.py:201-206, tools_for_model.py:303-330), polyphase
         dec = []
@@ -419,9 +428,10 @@ class DCCRN(nn.Module):
                     seg_bftc(skip, Csk // 2, Csk // 2)]
             Co = self.decoder[d][0].out_channels * 2
             raw = torch.empty(B, 2 * F, T + 1, Co, **f32)
+            Ci = sum(sg.geom.C for sg in segs)
             for parity in (0, 1):
-                wp, bias = self._dec_w(d, parity)
                 taps = [(dF, -kt) for _, dF in self._DEC_TAPS[parity] for kt in (0, 1)]
+                wp, bias = self._dec_w(d, parity, self._cmp(segs, len(taps) * Ci))
                 ops.conv(segs, taps, B, F, T + 1, Co, wp, bias, raw,
                          OutMap(2 * F * (T + 1) * Co, (T + 1) * Co, Co, of_mul=2, of_add=parity))
             if len(self.decoder[d]) > 1:

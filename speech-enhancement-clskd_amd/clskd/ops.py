@@ -46,8 +46,10 @@ class KernelTimer:
         return out  # name -> [launches, total_ms, total_flops]
 
 
-def conv_kernel_name(N, vec4):
+def conv_kernel_name(N, vec4, bf16=False):
     bn = 32 if N <= 32 else (64 if N <= 64 else 128)
+    if bf16:
+        return f"conv_igemm_bf16<{bn}>"
     return f"conv_igemm_f32<{bn},{'true' if vec4 else 'false'}>"
 
 
@@ -85,9 +87,13 @@ def seg_bftc(t, c0=0, C=None, t0=0, T=None):
     return Seg(t, c0 + t0 * Ct, SegGeom(C, F * Tt * Ct, Tt * Ct, Ct, F, T))
 
 
+BK_BF16 = 64
+
+
 @lru_cache(maxsize=1024)
-def _ktab(geoms, taps, device_index):
-    """K table for segments `geoms` and spatial taps [(dF, dT)], K order (tap, seg, cin)."""
+def _ktab(geoms, taps, device_index, bk=BK):
+    """K table for segments `geoms` and spatial taps [(dF, dT)], K order (tap, seg, cin),
+    padded to a multiple of `bk` with always-out-of-bounds entries."""
     ent, kseg = [], []
     for dF, dT in taps:
         for s, g in enumerate(geoms):
@@ -95,7 +101,7 @@ def _ktab(geoms, taps, device_index):
                 ent.append((c + dF * g.sF + dT * g.sT, dF, dT))
                 kseg.append(s)
     K = len(ent)
-    Kp = -(-K // BK) * BK
+    Kp = -(-K // bk) * bk
     for _ in range(Kp - K):
         ent.append((0, ZERO_DF, 0))
         kseg.append(0)
@@ -112,15 +118,25 @@ def _ktab(geoms, taps, device_index):
     return kt, ks, K, Kp, vec4
 
 
-def pack_weight(w, K):
-    """w: [N, ntaps, Cin] (K order tap-major, channel-minor) -> [N, Kp] contiguous fp32, zero pad."""
+def pack_weight(w, K, compute="fp32"):
+    """w: [N, ntaps, Cin] (K order tap-major, channel-minor) -> [N, Kp] contiguous, zero pad.
+    fp32: Kp multiple of 16, float32; bf16: Kp multiple of 64, bfloat16 (RNE)."""
     N = w.shape[0]
     w = w.reshape(N, -1).float()
     assert w.shape[1] == K, (w.shape, K)
-    Kp = -(-K // BK) * BK
+    bk = BK_BF16 if compute == "bf16" else BK
+    Kp = -(-K // bk) * bk
     if Kp != K:
         w = torch.cat([w, w.new_zeros(N, Kp - K)], 1)
+    if compute == "bf16":
+        return w.to(torch.bfloat16).contiguous()
     return w.contiguous()
+
+
+def bf16_eligible(segs):
+    """The bf16 engine needs the vec4 gather (channel runs of 4, 16-B aligned strides)."""
+    return all(s.geom.C % 4 == 0 and s.geom.sB % 4 == 0 and s.geom.sF % 4 == 0 and
+               s.geom.sT % 4 == 0 and (s.tensor.data_ptr() + 4 * s.offset) % 16 == 0 for s in segs)
 
 
 @dataclass(frozen=True)
@@ -143,11 +159,14 @@ def out_bftc(t, c0=0, of_mul=1, of_add=0):
 
 def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, stride_f=1,
          stride_t=1):
-    """out[b, fo*of_mul+of_add, to, n] = bias[n] + sum_k A[(b,fo,to),k] W[n,k]."""
+    """out[b, fo*of_mul+of_add, to, n] = bias[n] + sum_k A[(b,fo,to),k] W[n,k].
+    The MFMA operand type follows the packed weight's dtype (float32 or bfloat16)."""
     dev = out.device
     geoms = tuple(s.geom for s in segs)
-    kt, ks, K, Kp, vec4 = _ktab(geoms, tuple(taps), dev.index or 0)
-    assert wpacked.shape == (N, Kp) and wpacked.is_contiguous() and wpacked.dtype == torch.float32
+    bf16 = wpacked.dtype == torch.bfloat16
+    kt, ks, K, Kp, vec4 = _ktab(geoms, tuple(taps), dev.index or 0, BK_BF16 if bf16 else BK)
+    assert wpacked.shape == (N, Kp) and wpacked.is_contiguous(), (wpacked.shape, N, Kp)
+    assert wpacked.dtype in (torch.float32, torch.bfloat16)
     for s in segs:
         if (s.tensor.data_ptr() + 4 * s.offset) % 16 != 0:
             vec4 = False
@@ -167,14 +186,16 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
     d.oB, d.oF, d.oT, d.oNhi, d.oNlo = omap.oB, omap.oF, omap.oT, omap.oNhi, omap.oNlo
     d.nlo = min(omap.nlo, 1 << 30)
     d.of_mul, d.of_add = omap.of_mul, omap.of_add
-    d.compute = _lib.F32
+    d.compute = _lib.BF16 if bf16 else _lib.F32
+    if bf16 and not vec4:
+        raise RuntimeError("bf16 conv needs the vec4 gather; pack this layer as fp32")
     if KernelTimer.active:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
         check(lib().clskd_conv2d_fwd(C.byref(d), _stream()), "conv2d")
         e1.record()
-        KernelTimer.records.append((conv_kernel_name(N, vec4), 2.0 * B * Fo * To * N * K, e0, e1))
+        KernelTimer.records.append((conv_kernel_name(N, vec4, bf16), 2.0 * B * Fo * To * N * K, e0, e1))
     else:
         check(lib().clskd_conv2d_fwd(C.byref(d), _stream()), "conv2d")
     return out

@@ -209,6 +209,8 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
   }
 }
 
+int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st);
+
 }  // namespace clskd
 
 using namespace clskd;
@@ -216,9 +218,12 @@ using namespace clskd;
 extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
   CLSKD_CHECK_ARG(dp != nullptr, "conv2d: null descriptor");
   const clskd_conv_desc& d = *dp;
-  CLSKD_CHECK_ARG(d.compute == CLSKD_F32, "conv2d: only CLSKD_F32 compute is built in this version");
+  CLSKD_CHECK_ARG(d.compute == CLSKD_F32 || d.compute == CLSKD_BF16, "conv2d: unknown compute %d",
+                  d.compute);
   CLSKD_CHECK_SHAPE(d.B > 0 && d.Fo > 0 && d.To > 0 && d.N > 0 && d.K > 0, "conv2d: empty shape");
-  CLSKD_CHECK_SHAPE(d.K % BK == 0, "conv2d: K=%d must be padded to a multiple of %d", d.K, BK);
+  const int kmul = d.compute == CLSKD_BF16 ? 64 : BK;
+  CLSKD_CHECK_SHAPE(d.K % kmul == 0, "conv2d: K=%d must be padded to a multiple of %d", d.K, kmul);
+  CLSKD_CHECK_ARG(d.compute == CLSKD_F32 || d.vec4, "conv2d: bf16 compute needs the vec4 gather");
   CLSKD_CHECK_SHAPE(d.nseg >= 1 && d.nseg <= CLSKD_MAX_SEGS, "conv2d: nseg=%d", d.nseg);
   CLSKD_CHECK_ARG(d.weight && d.out && d.ktab && d.kseg, "conv2d: null pointer");
   CLSKD_CHECK_SHAPE(d.nlo >= 1, "conv2d: nlo must be >= 1");
@@ -233,8 +238,13 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
   }
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
   CLSKD_CHECK_SHAPE(M < (int64_t)INT32_MAX * 64, "conv2d: too many rows");
-  ConvArgs a{d};
   hipStream_t st = as_stream(stream);
+  if (d.compute == CLSKD_BF16) {
+    launch_conv_bf16(d, st);
+    CLSKD_LAUNCH_CHECK("conv2d_bf16");
+    return CLSKD_OK;
+  }
+  ConvArgs a{d};
   const unsigned gx = (unsigned)cdiv(M, BM);
 #define LAUNCH(BN_, V_)                                                                      \
   hipLaunchKernelGGL((conv_igemm_f32<BN_, V_>), dim3(gx, (unsigned)cdiv(d.N, BN_)), dim3(256), 0, st, a)

@@ -46,16 +46,18 @@ __global__ __launch_bounds__(8 * H) void lstm_recurrent_kernel(
   for (int t = 0; t < T; ++t) {
     const float gcur = gnext;
     if (ks == 0 && t + 1 < T) gnext = gp[(int64_t)(t + 1) * gx_t];
-    float acc = 0.f;
+    // four independent FMA chains (latency), summed in a fixed order
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     const float* hp = h_s + ks * HK;
 #pragma unroll
     for (int c = 0; c < HK; c += 4) {
       const f32x4 hv = *reinterpret_cast<const f32x4*>(hp + c);
-      acc += w[c] * hv[0];
-      acc += w[c + 1] * hv[1];
-      acc += w[c + 2] * hv[2];
-      acc += w[c + 3] * hv[3];
+      a0 = fmaf(w[c], hv[0], a0);
+      a1 = fmaf(w[c + 1], hv[1], a1);
+      a2 = fmaf(w[c + 2], hv[2], a2);
+      a3 = fmaf(w[c + 3], hv[3], a3);
     }
+    float acc = (a0 + a1) + (a2 + a3);
     acc += __shfl_xor(acc, 1, 64);
     if (ks == 0) pre[g] = gcur + acc;
     __syncthreads();

@@ -293,3 +293,26 @@ def test_clskd_step_full_batch_properties():
     assert rms(_np(o3["student_wav"]), _np(w1[perm])) <= 1e-5
     # SPKD Grams are permutation-equivariant -> loss invariant
     assert abs(o3["loss"].item() - l1) <= 1e-4 * abs(l1)
+
+
+def test_clskd_step_mixed_precision():
+    """precision='mixed' (bf16 MFMA operands for the teacher and ReviewKD GEMMs): the student —
+    waveform, base loss — is untouched (bitwise), SPKD terms stay within 2 % of the fp32 step."""
+    from clskd.data import synthetic_pairs
+    noisy, clean = synthetic_pairs(4, 64000, seed=5)
+    X, y = torch.from_numpy(noisy).to(DEV), torch.from_numpy(clean).to(DEV)
+    kd = _kd()
+    sd_t = {k: v.clone() for k, v in kd.teacher.state_dict().items()}
+    sd_s = {k: v.clone() for k, v in kd.student.state_dict().items()}
+    ref = kd.training_step((X, y), 0, return_parts=True)
+    r_spkd, r_wav, r_base = _np(ref["spkd"]), ref["student_wav"].clone(), ref["base"].item()
+    kd.teacher.load_state_dict(sd_t)
+    kd.student.load_state_dict(sd_s)
+    kd.set_precision("mixed")
+    out = kd.training_step((X, y), 0, return_parts=True)
+    assert torch.equal(out["student_wav"], r_wav)
+    assert out["base"].item() == r_base
+    rel = np.abs(_np(out["spkd"]) - r_spkd) / r_spkd
+    print("mixed-precision SPKD relative deviation per term:", np.array2string(rel, precision=2))
+    assert rel.max() <= 2e-2, rel
+    assert abs(out["loss"].item() - ref["loss"].item()) <= 2e-3 * ref["loss"].item()
