@@ -14,7 +14,7 @@
  *   - Work is enqueued on `stream` (a hipStream_t; NULL = default stream).
  *   - Return 0 on success, a negative clskd_status otherwise; clskd_last_error() returns a
  *     thread-local message.  No exceptions or aborts cross the ABI.
- *   - fp32 storage; `compute` selects the MFMA operand type of GEMM-shaped ops.
+ *   - Storage is fp32 or bf16 per tensor (dtype arguments); GEMM-shaped ops accumulate in fp32.
  */
 #ifndef CLSKD_H
 #define CLSKD_H
@@ -82,13 +82,16 @@ typedef struct {
   const clskd_ktab_entry* ktab; /* device, K entries */
   const uint8_t* kseg;          /* device, K entries: segment index of each k */
   int32_t vec4;                 /* 1: every aligned group of 4 k's is 4 contiguous channels */
-  const float* weight; /* device [N][K] packed */
+  const void* weight;  /* device [N][K] packed, fp32 (compute F32) or bf16 (compute BF16) */
   const float* bias;   /* device [N] or NULL */
   /* output address: out + b*oB + (fo*of_mul+of_add)*oF + to*oT + (n/nlo)*oNhi + (n%nlo)*oNlo */
-  float* out;
+  void* out;
   int64_t oB, oF, oT, oNhi, oNlo;
   int32_t nlo, of_mul, of_add;
-  int32_t compute; /* clskd_compute */
+  int32_t compute;   /* clskd_compute: MFMA operand type */
+  int32_t in_dtype;  /* CLSKD_F32 / CLSKD_BF16 storage of every segment (bf16 <=> bf16 compute;
+                        bf16 needs segment channel runs of 8 and strides % 8) */
+  int32_t out_dtype; /* CLSKD_F32 / CLSKD_BF16 storage of `out` */
 } clskd_conv_desc;
 
 int clskd_conv2d_fwd(const clskd_conv_desc* d, void* stream);
@@ -101,9 +104,10 @@ int clskd_conv2d_fwd(const clskd_conv_desc* d, void* stream);
  *   clskd_bn_finalize: mean/var (biased) -> scale/shift; running stats update (momentum,
  *                      unbiased var) applied `n_updates` times when running_* != NULL
  *   clskd_bn_apply: y = x*scale[c] + shift[c]; if alpha: y = y>=0 ? y : alpha*y
+ *   x / y storage is fp32 or bf16 (`dtype`, clskd_compute values); statistics are fp64/fp32.
  * -------------------------------------------------------------------------------------- */
-int clskd_bn_stats_partial(const float* x, int64_t rows, int32_t C, double* partial,
-                           int32_t nblk, void* stream);
+int clskd_bn_stats_partial(const void* x, int64_t rows, int32_t C, double* partial,
+                           int32_t nblk, int32_t dtype, void* stream);
 int clskd_bn_finalize(const double* partial, int32_t nblk, int64_t rows, int32_t C,
                       const float* gamma, const float* beta, float eps,
                       float* running_mean, float* running_var, float momentum,
@@ -112,8 +116,8 @@ int clskd_bn_finalize(const double* partial, int32_t nblk, int64_t rows, int32_t
 int clskd_bn_eval_coeffs(const float* running_mean, const float* running_var,
                          const float* gamma, const float* beta, float eps, int32_t C,
                          float* scale, float* shift, void* stream);
-int clskd_bn_apply(const float* x, float* y, int64_t rows, int32_t C, const float* scale,
-                   const float* shift, const float* alpha, void* stream);
+int clskd_bn_apply(const void* x, void* y, int64_t rows, int32_t C, const float* scale,
+                   const float* shift, const float* alpha, int32_t dtype, void* stream);
 int32_t clskd_bn_partial_blocks(int64_t rows, int32_t C);
 
 /* ------------------------------------------------------------------------------------------
@@ -156,9 +160,9 @@ int clskd_ola(const float* frames, const float* window, int32_t B, int32_t T, in
  *   y_up = nearest-interpolate(res [B][Fr][Tr][64] -> (F, T))
  *   z = sigmoid(W[2][128] . [x; y_up] + b);  out = x*z0 + y_up*z1
  * -------------------------------------------------------------------------------------- */
-int clskd_abf_fuse(const float* x, const float* res, int32_t B, int32_t F, int32_t T,
-                   int32_t Fr, int32_t Tr, const float* w, const float* b, float* out,
-                   void* stream);
+int clskd_abf_fuse(const void* x, const void* res, int32_t B, int32_t F, int32_t T,
+                   int32_t Fr, int32_t Tr, const float* w, const float* b, void* out,
+                   int32_t dtype, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * SPKD / Gram (framework.py:150-172).  A gram job views a tap as z_b = x[b][p][c0 .. c0+Cs)
@@ -170,13 +174,15 @@ int clskd_abf_fuse(const float* x, const float* res, int32_t B, int32_t F, int32
  *                     ||Gt-Gs||_F^2 (/B^2 if batchmean); writes losses[pair] and grams.
  * -------------------------------------------------------------------------------------- */
 typedef struct {
-  const float* ptr;
+  const void* ptr;
   int64_t sB;
   int64_t P;
   int32_t Ctot, c0, Cs;
   int32_t chunk;      /* positions per slab */
   int32_t first_slab; /* index of this job's first slab */
   int32_t nslab;
+  int32_t dtype;      /* CLSKD_F32 (Cs % 4 == 0) or CLSKD_BF16 (Cs % 8 == 0) storage */
+  int32_t reserved;
 } clskd_gram_job;
 
 int clskd_gram_partial(const clskd_gram_job* jobs_dev, int32_t njobs, int32_t total_slabs,

@@ -31,17 +31,19 @@ class ConvDesc(C.Structure):
                 ("kseg", C.c_void_p), ("vec4", C.c_int32), ("weight", C.c_void_p),
                 ("bias", C.c_void_p), ("out", C.c_void_p), ("oB", C.c_int64), ("oF", C.c_int64),
                 ("oT", C.c_int64), ("oNhi", C.c_int64), ("oNlo", C.c_int64), ("nlo", C.c_int32),
-                ("of_mul", C.c_int32), ("of_add", C.c_int32), ("compute", C.c_int32)]
+                ("of_mul", C.c_int32), ("of_add", C.c_int32), ("compute", C.c_int32),
+                ("in_dtype", C.c_int32), ("out_dtype", C.c_int32)]
 
 
 class GramJob(C.Structure):
     _fields_ = [("ptr", C.c_void_p), ("sB", C.c_int64), ("P", C.c_int64), ("Ctot", C.c_int32),
                 ("c0", C.c_int32), ("Cs", C.c_int32), ("chunk", C.c_int32),
-                ("first_slab", C.c_int32), ("nslab", C.c_int32)]
+                ("first_slab", C.c_int32), ("nslab", C.c_int32), ("dtype", C.c_int32),
+                ("reserved", C.c_int32)]
 
 
 assert C.sizeof(KtabEntry) == 8
-assert C.sizeof(GramJob) == 48
+assert C.sizeof(GramJob) == 56
 
 _p, _i32, _i64, _f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float
 
@@ -50,18 +52,18 @@ SIGNATURES = {
     "clskd_version": (_i32, []),
     "clskd_conv2d_fwd": (_i32, [C.POINTER(ConvDesc), _p]),
     "clskd_bn_partial_blocks": (_i32, [_i64, _i32]),
-    "clskd_bn_stats_partial": (_i32, [_p, _i64, _i32, _p, _i32, _p]),
+    "clskd_bn_stats_partial": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p]),
     "clskd_bn_finalize": (_i32, [_p, _i32, _i64, _i32, _p, _p, _f32, _p, _p, _f32, _i32, _p, _p,
                                  _p, _p, _p]),
     "clskd_bn_eval_coeffs": (_i32, [_p, _p, _p, _p, _f32, _i32, _p, _p, _p]),
-    "clskd_bn_apply": (_i32, [_p, _p, _i64, _i32, _p, _p, _p, _p]),
+    "clskd_bn_apply": (_i32, [_p, _p, _i64, _i32, _p, _p, _p, _i32, _p]),
     "clskd_lstm_recurrent": (_i32, [_p, _i64, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _i64,
                                     _i64, _i64, _p]),
     "clskd_complex_combine": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p]),
     "clskd_frame_pad": (_i32, [_p, _i64, _i32, _i32, _i32, _i32, _i32, _p, _p]),
     "clskd_mask_e": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p]),
     "clskd_ola": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p]),
-    "clskd_abf_fuse": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p]),
+    "clskd_abf_fuse": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _i32, _p]),
     "clskd_gram_partial": (_i32, [_p, _i32, _i32, _p, _i32, _p, _p]),
     "clskd_spkd_finalize": (_i32, [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
     "clskd_stft_mag_loss": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p]),

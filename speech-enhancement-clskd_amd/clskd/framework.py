@@ -24,9 +24,11 @@ def to_bftc(x):
     if x.dim() != 4:
         raise ValueError(f"expected an NCHW feature map, got shape {tuple(x.shape)}")
     B, Cn, Fn, Tn = x.shape
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        x = x.float()
     if x.stride() == (Fn * Tn * Cn, 1, Tn * Cn, Cn):
         return x.permute(0, 2, 3, 1)  # contiguous view of the underlying BFTC storage
-    return x.permute(0, 2, 3, 1).contiguous().float()
+    return x.permute(0, 2, 3, 1).contiguous()
 
 
 def nchw(t):
@@ -176,15 +178,19 @@ class ABF(nn.Module):
         self._wcache = {}
         self.compute = "fp32"  # MFMA operand type of conv1/conv2 ("fp32" | "bf16")
 
-    def _weights(self):
+    @property
+    def act_dtype(self):
+        return torch.bfloat16 if self.compute == "bf16" else torch.float32
+
+    def _weights(self, in_dtype):
         ps = [self.conv1[0].weight, self.conv2[0].weight]
         if self.att_conv is not None:
             ps += [self.att_conv[0].weight, self.att_conv[0].bias]
-        ver = _pv(*ps) + (self.compute,)
+        ver = _pv(*ps) + (self.compute, in_dtype)
         ent = self._wcache.get("w")
         if ent is None or ent[0] != ver:
             with torch.no_grad():
-                c1 = self.compute if self.conv1[0].weight.shape[1] >= 64 else "fp32"
+                c1 = "bf16" if in_dtype == torch.bfloat16 else "fp32"
                 w1 = self.conv1[0].weight  # [mid, in, 1, 1]
                 w1p = ops.pack_weight(w1.reshape(w1.shape[0], 1, w1.shape[1]), w1.shape[1], c1)
                 w2 = self.conv2[0].weight  # [out, mid, 3, 3]
@@ -202,13 +208,11 @@ class ABF(nn.Module):
         """x: BFTC [B][F][T][Cin]; y: BFTC residual [B][Fr][Tr][mid].  Returns (out, x_fused) BFTC."""
         train = self.training if train is None else train
         B, Fn, Tn, Cin = x.shape
-        w1p, w2p, att = self._weights()
+        w1p, w2p, att = self._weights(x.dtype)
         mid = w1p.shape[0]
         dev = x.device
-        f32 = dict(device=dev, dtype=torch.float32)
-        x1 = torch.empty(B, Fn, Tn, mid, **f32)
-        if w1p.dtype == torch.bfloat16 and not ops.bf16_eligible([seg_bftc(x)]):
-            raise RuntimeError("ABF conv1 input is not vec4-gatherable for bf16")
+        act = dict(device=dev, dtype=self.act_dtype)
+        x1 = torch.empty(B, Fn, Tn, mid, **act)
         ops.conv([seg_bftc(x)], [(0, 0)], B, Fn, Tn, mid, w1p, None, x1,
                  OutMap(Fn * Tn * mid, Tn * mid, mid))
         bn = self.conv1[1]
@@ -217,6 +221,8 @@ class ABF(nn.Module):
         if self.att_conv is not None:
             if shape != Fn:  # the reference's torch.cat would fail as well (framework.py:213-216)
                 raise ValueError(f"ABF fuse: residual upsampled to F={shape} but x has F={Fn}")
+            if y.dtype != x1.dtype:  # user-supplied residual of another storage type
+                y = y.to(x1.dtype).contiguous()
             xf = torch.empty_like(x1)
             ops.abf_fuse(x1, y, att[0], att[1], xf)
             x1 = xf
@@ -224,7 +230,7 @@ class ABF(nn.Module):
             raise NotImplementedError(
                 f"ABF output interpolation to ({out_shape}, {Tn}) from F={Fn} is not on the CLSKD path")
         Cout = w2p.shape[0]
-        out = torch.empty(B, Fn, Tn, Cout, **f32)
+        out = torch.empty(B, Fn, Tn, Cout, **act)
         ops.conv([seg_bftc(x1)], [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], B, Fn,
                  Tn, Cout, w2p, None, out, OutMap(Fn * Tn * Cout, Tn * Cout, Cout))
         bn = self.conv2[1]

@@ -222,11 +222,16 @@ class DCCRN(nn.Module):
         raise NotImplementedError(f"loss_mode {loss_mode!r} is not on the CLSKD hot path")
 
     # ---------------------------------------------------------------- packed weights
-    def _cmp(self, segs, K):
-        """Operand type for one GEMM: bf16 only where the model asks for it and the gather allows."""
-        if self.compute == "bf16" and K >= 64 and ops.bf16_eligible(segs):
-            return "bf16"
-        return "fp32"
+    @staticmethod
+    def _cmp(segs, K=None):
+        """MFMA operand type of one GEMM = storage type of its input segments."""
+        return "bf16" if segs[0].tensor.dtype == torch.bfloat16 else "fp32"
+
+    @property
+    def act_dtype(self):
+        """Storage of the BFTC activations: bf16 when the model computes in bf16 (the frozen
+        teacher in precision='mixed'), fp32 otherwise."""
+        return torch.bfloat16 if self.compute == "bf16" else torch.float32
 
     def _packed(self, key, params, build):
         ent = self._wcache.get(key)
@@ -350,6 +355,7 @@ class DCCRN(nn.Module):
         T = cfg.n_frames(L)
         dev = x.device
         f32 = dict(device=dev, dtype=torch.float32)
+        act = dict(device=dev, dtype=self.act_dtype)
         if spec is None:
             spec = self.spectrum(x)
         kn = self.kernel_num
@@ -367,7 +373,7 @@ class DCCRN(nn.Module):
                 segs = [seg_bftc(enc[-1])]
             wp, bias = self._enc_w(i, self._cmp(segs, 10 * kn[i]))
             taps = [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)]
-            raw = torch.empty(B, Fo, T, Co, **f32)
+            raw = torch.empty(B, Fo, T, Co, **act)
             ops.conv(segs, taps, B, Fo, T, Co, wp, bias, raw, OutMap(Fo * T * Co, T * Co, Co),
                      stride_f=2)
             bn, pr = self.encoder[i][1], self.encoder[i][2]
@@ -406,7 +412,7 @@ class DCCRN(nn.Module):
             r_in = (ro, io)
             lstm_io.append((ro, io))
         # projection into the decoder input [B][D4][T][C6] (DCCRN.py:188-199)
-        dec_in = torch.empty(B, D4, T, C6, **f32)
+        dec_in = torch.empty(B, D4, T, C6, **act)
         m = self.enhance[self.hidden_layers - 1]
         P = m.projection_dim
         for half in range(2):
@@ -427,7 +433,8 @@ class DCCRN(nn.Module):
                     seg_bftc(out_t, Cof // 2, Cof // 2, out_t0, out_T),
                     seg_bftc(skip, Csk // 2, Csk // 2)]
             Co = self.decoder[d][0].out_channels * 2
-            raw = torch.empty(B, 2 * F, T + 1, Co, **f32)
+            last = d == nl - 1
+            raw = torch.empty(B, 2 * F, T + 1, Co, **(f32 if last else act))
             Ci = sum(sg.geom.C for sg in segs)
             for parity in (0, 1):
                 taps = [(dF, -kt) for _, dF in self._DEC_TAPS[parity] for kt in (0, 1)]

@@ -133,10 +133,17 @@ def pack_weight(w, K, compute="fp32"):
     return w.contiguous()
 
 
-def bf16_eligible(segs):
-    """The bf16 engine needs the vec4 gather (channel runs of 4, 16-B aligned strides)."""
-    return all(s.geom.C % 4 == 0 and s.geom.sB % 4 == 0 and s.geom.sF % 4 == 0 and
-               s.geom.sT % 4 == 0 and (s.tensor.data_ptr() + 4 * s.offset) % 16 == 0 for s in segs)
+def _dt(t):
+    """clskd storage-type code of a tensor (0 = fp32, 1 = bf16)."""
+    if t.dtype == torch.float32:
+        return _lib.F32
+    if t.dtype == torch.bfloat16:
+        return _lib.BF16
+    raise TypeError(f"clskd kernels take float32 or bfloat16 tensors, got {t.dtype}")
+
+
+def seg_addr(s):
+    return s.tensor.data_ptr() + s.tensor.element_size() * s.offset
 
 
 @dataclass(frozen=True)
@@ -160,35 +167,42 @@ def out_bftc(t, c0=0, of_mul=1, of_add=0):
 def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, stride_f=1,
          stride_t=1):
     """out[b, fo*of_mul+of_add, to, n] = bias[n] + sum_k A[(b,fo,to),k] W[n,k].
-    The MFMA operand type follows the packed weight's dtype (float32 or bfloat16)."""
+    bf16 segments run the LDS-DMA bf16-MFMA engine (weights packed bf16, K % 64); fp32 segments
+    the fp32-MFMA engine (weights fp32, K % 16).  `out` may be fp32 or bf16 storage."""
     dev = out.device
     geoms = tuple(s.geom for s in segs)
-    bf16 = wpacked.dtype == torch.bfloat16
+    in_dt = {_dt(s.tensor) for s in segs}
+    assert len(in_dt) == 1, "all segments of one conv share a storage type"
+    in_dt = in_dt.pop()
+    bf16 = in_dt == _lib.BF16
     kt, ks, K, Kp, vec4 = _ktab(geoms, tuple(taps), dev.index or 0, BK_BF16 if bf16 else BK)
     assert wpacked.shape == (N, Kp) and wpacked.is_contiguous(), (wpacked.shape, N, Kp)
-    assert wpacked.dtype in (torch.float32, torch.bfloat16)
+    assert wpacked.dtype == (torch.bfloat16 if bf16 else torch.float32), wpacked.dtype
     for s in segs:
-        if (s.tensor.data_ptr() + 4 * s.offset) % 16 != 0:
+        if seg_addr(s) % 16 != 0:
             vec4 = False
+    if bf16 and not all(g.C % 8 == 0 and g.sB % 8 == 0 and g.sF % 8 == 0 and g.sT % 8 == 0
+                        for g in geoms):
+        raise RuntimeError("bf16 conv segments need channel runs of 8 and strides % 8")
     d = _lib.ConvDesc()
     d.B, d.Fo, d.To, d.N, d.K = B, Fo, To, N, Kp
     d.stride_f, d.stride_t = stride_f, stride_t
     d.nseg = len(segs)
     for i, s in enumerate(segs):
         g = s.geom
-        d.seg[i] = _lib.Seg(s.tensor.data_ptr() + 4 * s.offset, g.sB, g.sF, g.sT, g.F, g.T)
+        d.seg[i] = _lib.Seg(seg_addr(s), g.sB, g.sF, g.sT, g.F, g.T)
     for i in range(len(segs), _lib.MAX_SEGS):
         d.seg[i] = d.seg[0]
     d.ktab, d.kseg, d.vec4 = kt.data_ptr(), ks.data_ptr(), int(vec4)
     d.weight = wpacked.data_ptr()
     d.bias = bias.data_ptr() if bias is not None else None
-    d.out = out.data_ptr() + 4 * out_offset
+    d.out = out.data_ptr() + out.element_size() * out_offset
     d.oB, d.oF, d.oT, d.oNhi, d.oNlo = omap.oB, omap.oF, omap.oT, omap.oNhi, omap.oNlo
     d.nlo = min(omap.nlo, 1 << 30)
     d.of_mul, d.of_add = omap.of_mul, omap.of_add
     d.compute = _lib.BF16 if bf16 else _lib.F32
-    if bf16 and not vec4:
-        raise RuntimeError("bf16 conv needs the vec4 gather; pack this layer as fp32")
+    d.in_dtype = in_dt
+    d.out_dtype = _dt(out)
     if KernelTimer.active:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
@@ -218,7 +232,7 @@ def batch_norm_bftc(x, y, gamma, beta, running_mean, running_var, train, momentu
     if train:
         nblk = L.clskd_bn_partial_blocks(rows, Cn)
         part = torch.empty(nblk * Cn * 2, device=dev, dtype=torch.float64)
-        check(L.clskd_bn_stats_partial(ptr(x), rows, Cn, ptr(part), nblk, st), "bn_stats")
+        check(L.clskd_bn_stats_partial(ptr(x), rows, Cn, ptr(part), nblk, _dt(x), st), "bn_stats")
         mean_o = var_o = None
         if stats_out is not None:
             mean_o, var_o = stats_out
@@ -231,7 +245,8 @@ def batch_norm_bftc(x, y, gamma, beta, running_mean, running_var, train, momentu
     else:
         check(L.clskd_bn_eval_coeffs(ptr(running_mean), ptr(running_var), ptr(gamma), ptr(beta),
                                      eps, Cn, ptr(scale), ptr(shift), st), "bn_eval")
-    check(L.clskd_bn_apply(ptr(x), ptr(y), rows, Cn, ptr(scale), ptr(shift), ptr(alpha), st),
+    assert x.dtype == y.dtype
+    check(L.clskd_bn_apply(ptr(x), ptr(y), rows, Cn, ptr(scale), ptr(shift), ptr(alpha), _dt(x), st),
           "bn_apply")
     return y
 
@@ -274,8 +289,9 @@ def abf_fuse(x, res, w, b, out):
     B, F, T, Cm = x.shape
     _, Fr, Tr, Cr = res.shape
     assert Cm == 64 and Cr == 64, "ABF fuse is built for mid_channel = 64 (framework.py:235)"
+    assert x.dtype == res.dtype == out.dtype
     check(lib().clskd_abf_fuse(ptr(x), ptr(res), B, F, T, Fr, Tr, ptr(w), ptr(b), ptr(out),
-                               _stream()), "abf_fuse")
+                               _dt(x), _stream()), "abf_fuse")
     return out
 
 
@@ -296,22 +312,25 @@ class GramView:
 def gram_view(t):
     """View of a tensor as z_b (any tensor whose per-sample block is contiguous)."""
     B = t.shape[0]
+    if t.dtype not in (torch.float32, torch.bfloat16):
+        t = t.float()
+    g = 8 if t.dtype == torch.bfloat16 else 4
     if t.is_contiguous():
         n = t.numel() // B
-        if n % 4 == 0:
-            return GramView(t, 0, n, n // 4, 4, 0, 4)
+        if n % g == 0:
+            return GramView(t, 0, n, n // g, g, 0, g)
     # BFTC buffer exposed as an NCHW permuted view: underlying storage contiguous
     if t.dim() == 4 and t.stride(1) == 1:
         Bn, Cn, Fn, Tn = t.shape
-        if t.stride() == (Fn * Tn * Cn, 1, Tn * Cn, Cn) and (Fn * Tn * Cn) % 4 == 0:
+        if t.stride() == (Fn * Tn * Cn, 1, Tn * Cn, Cn) and (Fn * Tn * Cn) % g == 0:
             n = Fn * Tn * Cn
-            return GramView(t, 0, n, n // 4, 4, 0, 4)
+            return GramView(t, 0, n, n // g, g, 0, g)
     tc = t.contiguous()
     n = tc.numel() // B
-    if n % 4 != 0:
-        tc = torch.cat([tc.reshape(B, n), tc.new_zeros(B, 4 - n % 4)], 1)
+    if n % g != 0:  # zero padding adds nothing to z z^T
+        tc = torch.cat([tc.reshape(B, n), tc.new_zeros(B, g - n % g)], 1)
         n = tc.shape[1]
-    return GramView(tc, 0, n, n // 4, 4, 0, 4)
+    return GramView(tc, 0, n, n // g, g, 0, g)
 
 
 def spkd_losses(pairs_views, B, batchmean=True, return_grams=False, chunk_elems=16384, out=None):
@@ -325,8 +344,10 @@ def spkd_losses(pairs_views, B, batchmean=True, return_grams=False, chunk_elems=
     for j, v in enumerate(views):
         chunk = max(1, chunk_elems // v.Cs)
         ns = -(-v.P // chunk)
-        jobs[j] = _lib.GramJob(v.tensor.data_ptr() + 4 * v.offset, v.sB, v.P, v.Ctot, v.c0, v.Cs,
-                               chunk, first, ns)
+        dt = _dt(v.tensor)
+        assert v.Cs % (8 if dt == _lib.BF16 else 4) == 0
+        jobs[j] = _lib.GramJob(v.tensor.data_ptr() + v.tensor.element_size() * v.offset, v.sB, v.P,
+                               v.Ctot, v.c0, v.Cs, chunk, first, ns, dt, 0)
         slab_job += [j] * ns
         first += ns
     jobs_t = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(dev, non_blocking=False)

@@ -1,56 +1,100 @@
-// Implicit-GEMM convolution engine, bf16 MFMA operands / fp32 accumulation (gfx950).
+// Implicit-GEMM convolution engine for bf16 BFTC activations (gfx950).
 //
-// Same descriptor and K-table gather as conv_igemm.hip (include/clskd.h), selected with
-// compute = CLSKD_BF16 for the large-K layers (teacher encoder/decoder, ReviewKD 3x3 convs).
-// Activations stay fp32 in HBM and are rounded to bf16 (RNE, v_cvt_pk_bf16_f32) while staging
-// into LDS; weights are pre-packed bf16 [N][K] with K padded to a multiple of 64.
+// Selected by in_dtype = CLSKD_BF16 (descriptor in include/clskd.h): the frozen teacher and the
+// ReviewKD fusions keep their activations in bf16, so the A operand can be staged straight from
+// HBM into LDS by LDS-DMA (global_load_lds_dwordx4, 16 B per lane) without a register round trip.
+// The K-table gather becomes a per-lane SOURCE address (the LDS destination of one wave
+// instruction is linear: 8 rows x 128 B); out-of-bounds taps read a zero page.
 //
-// Tile BM=128 x BN x BK=64, 256 threads = 4 waves, v_mfma_f32_32x32x16_bf16.  Waves are laid out
-// 2x2 (BN=128: 64x64 per wave) or 4x1 (BN<=64: 32xBN per wave).  LDS rows are 64 bf16 = 128 B;
-// the 16-B chunk index is XOR-swizzled with ((row>>1)&7) so each ds_read_b128 lane group
-// (16 rows, same chunk) hits 16 distinct bank slots.  One register-prefetched K-tile in flight,
-// two LDS buffers, one barrier per K-tile.
+// Tile BM=128 x BN x BK=64, 256 threads = 4 waves, v_mfma_f32_32x32x16_bf16 (fp32 accumulate).
+// Three LDS stages, two K-tiles in flight: per K-tile every wave waits on a COUNTED vmcnt (its
+// own DMAs for the tile it is about to read), then a raw s_barrier makes every wave's DMA
+// visible; no __syncthreads (which would drain vmcnt to 0).  LDS rows are 128 B with the 16-B
+// chunk XOR-swizzled by ((row>>1)&7): the DMA applies the inverse permutation on the source
+// address, the ds_read_b128 fragment reads apply it on the LDS address (same involution), so
+// every read lane group of 16 rows hits 16 distinct bank slots.  All LDS is one dynamic array.
 #include "common.h"
 
 namespace clskd {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
 
-namespace bf {
+__device__ __attribute__((aligned(64))) unsigned char g_zero_page[64];
+
+namespace v2 {
 constexpr int BM = 128;
 constexpr int BK = 64;
-constexpr int ROWB = BK * 2;  // bytes per LDS row
+constexpr int ROWB = 128;  // bytes per LDS row (64 bf16)
+constexpr int STAGES = 3;
 
-__device__ __forceinline__ int chunk_swz(int row, int c) { return c ^ ((row >> 1) & 7); }
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
 template <typename T>
 __device__ __forceinline__ T sel4(int s, T a0, T a1, T a2, T a3) {
   return s == 0 ? a0 : (s == 1 ? a1 : (s == 2 ? a2 : a3));
 }
-}  // namespace bf
 
-struct ConvArgsBF {
+template <typename OutT>
+__device__ __forceinline__ void store_out(OutT* p, float v);
+template <>
+__device__ __forceinline__ void store_out<float>(float* p, float v) { *p = v; }
+template <>
+__device__ __forceinline__ void store_out<__bf16>(__bf16* p, float v) { *p = (__bf16)v; }
+
+__host__ __device__ constexpr int stage_bytes(int BN) { return BM * ROWB + BN * ROWB; }
+
+// One 1-KiB LDS-DMA wave instruction: lane l copies 16 B from gsrc to lds_base + 16*l.
+// Inline asm (cdna_hip_programming.md §5.7): hipcc neither tracks nor waits for it, so the
+// pipeline's counted vmcnt waits are the only synchronisation.  M0 is set and restored inside.
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+}  // namespace v2
+
+struct ConvArgsV2 {
   clskd_conv_desc d;
 };
 
-template <int BN>
-__global__ __launch_bounds__(256) void conv_igemm_bf16(const ConvArgsBF args) {
-  using namespace bf;
+template <int BN, typename OutT>
+__global__ __launch_bounds__(256) void conv_igemm_bf16_dma(const ConvArgsV2 args) {
+  using namespace v2;
   const clskd_conv_desc& d = args.d;
-  constexpr int WN = (BN == 128) ? 2 : 1;   // waves along N
-  constexpr int WM = 4 / WN;                // waves along M
-  constexpr int TM = BM / WM / 32;          // 32x32 tiles per wave along M
-  constexpr int TN = BN / WN / 32;          // 32x32 tiles per wave along N
-  __shared__ __attribute__((aligned(16))) unsigned char As[2][BM * ROWB];
-  __shared__ __attribute__((aligned(16))) unsigned char Bs[2][BN * ROWB];
-  __shared__ int64_t out_row[BM];
+  constexpr int WN = (BN >= 128) ? 2 : 1;
+  constexpr int WM = 4 / WN;
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  constexpr int SB = stage_bytes(BN);
+  constexpr int NGA = BM / 8 / 4;   // A DMA instructions per wave per K-tile (4)
+  constexpr int NGB = BN / 8 / 4;   // B DMA instructions per wave per K-tile (>= 1)
+  constexpr int NG = NGA + NGB;
+  static_assert(NGB >= 1, "BN >= 32");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* stages = smem;
+  int* rowinfo = reinterpret_cast<int*>(smem + STAGES * SB);        // [BM][4]: fi0, ti0, valid, -
+  int* rowbase = rowinfo + BM * 4;                                   // [4 seg][BM] element offsets
+  int64_t* out_row = reinterpret_cast<int64_t*>(rowbase + 4 * BM);   // [BM]
+  int4* segtab = reinterpret_cast<int4*>(out_row + BM);              // [4]: ptr lo, ptr hi, F, T
+  int2* ctab = reinterpret_cast<int2*>(segtab + 4);                  // [K/8] chunk entries
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
   const int64_t m0 = (int64_t)blockIdx.x * BM;
@@ -58,116 +102,108 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16(const ConvArgsBF args) {
   const int nk = d.K / BK;
   const int64_t FoTo = (int64_t)d.Fo * d.To;
 
+  // ---- per-block tables -------------------------------------------------------------------
   if (tid < BM) {
-    int64_t m = m0 + tid;
-    int64_t off = -1;
-    if (m < M) {
-      int64_t b = m / FoTo;
-      int64_t r = m - b * FoTo;
-      int fo = (int)(r / d.To);
-      int to = (int)(r - (int64_t)fo * d.To);
-      off = b * d.oB + (int64_t)(fo * d.of_mul + d.of_add) * d.oF + (int64_t)to * d.oT;
-    }
-    out_row[tid] = off;
+    const int64_t m = m0 + tid;
+    const bool valid = m < M;
+    const int64_t mm = valid ? m : 0;
+    const int64_t b = mm / FoTo;
+    const int64_t r = mm - b * FoTo;
+    const int fo = (int)(r / d.To);
+    const int to = (int)(r - (int64_t)fo * d.To);
+    const int fi0 = fo * d.stride_f, ti0 = to * d.stride_t;
+    rowinfo[tid * 4 + 0] = fi0;
+    rowinfo[tid * 4 + 1] = ti0;
+    rowinfo[tid * 4 + 2] = valid ? 1 : 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      rowbase[s * BM + tid] = (int)(b * d.seg[s].sB + (int64_t)fi0 * d.seg[s].sF + (int64_t)ti0 * d.seg[s].sT);
+    out_row[tid] = valid ? b * d.oB + (int64_t)(fo * d.of_mul + d.of_add) * d.oF + (int64_t)to * d.oT : -1;
   }
-
-  // A staging: thread -> row (tid>>1), 32 consecutive k (8 quads) at (tid&1)*32
-  const int arow = tid >> 1;
-  const int ahalf = tid & 1;
-  int rb, rfi, rti;
-  bool rvalid;
-  {
-    int64_t m = m0 + arow;
-    rvalid = m < M;
-    int64_t mm = rvalid ? m : 0;
-    int64_t b = mm / FoTo;
-    int64_t r = mm - b * FoTo;
-    int fo = (int)(r / d.To);
-    int to = (int)(r - (int64_t)fo * d.To);
-    rb = (int)b;
-    rfi = fo * d.stride_f;
-    rti = to * d.stride_t;
+  if (tid < 4) {
+    const clskd_seg& g = d.seg[tid];
+    const uint64_t pv = (uint64_t)(uintptr_t)g.ptr;
+    segtab[tid] = make_int4((int)(unsigned)pv, (int)(unsigned)(pv >> 32), g.F, g.T);
   }
-  const int64_t rowbase0 = (int64_t)rb * d.seg[0].sB + (int64_t)rfi * d.seg[0].sF + (int64_t)rti * d.seg[0].sT;
-  const int64_t rowbase1 = (int64_t)rb * d.seg[1].sB + (int64_t)rfi * d.seg[1].sF + (int64_t)rti * d.seg[1].sT;
-  const int64_t rowbase2 = (int64_t)rb * d.seg[2].sB + (int64_t)rfi * d.seg[2].sF + (int64_t)rti * d.seg[2].sT;
-  const int64_t rowbase3 = (int64_t)rb * d.seg[3].sB + (int64_t)rfi * d.seg[3].sF + (int64_t)rti * d.seg[3].sT;
-
-  auto load_a = [&](int kt, f32x4 (&ra)[8]) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int k = kt * BK + ahalf * 32 + q * 4;
-      const clskd_ktab_entry e = d.ktab[k];
-      const int s = d.kseg[k];
-      const float* sp = sel4(s, d.seg[0].ptr, d.seg[1].ptr, d.seg[2].ptr, d.seg[3].ptr);
-      const int64_t rbase = sel4(s, rowbase0, rowbase1, rowbase2, rowbase3);
-      const int Fb = sel4(s, d.seg[0].F, d.seg[1].F, d.seg[2].F, d.seg[3].F);
-      const int Tb = sel4(s, d.seg[0].T, d.seg[1].T, d.seg[2].T, d.seg[3].T);
-      const int fi = rfi + e.dF;
-      const int ti = rti + e.dT;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (rvalid && fi >= 0 && fi < Fb && ti >= 0 && ti < Tb)
-        v = *reinterpret_cast<const f32x4*>(sp + rbase + e.off);
-      ra[q] = v;
-    }
-  };
-
-  constexpr int NBL = BN * ROWB / 16 / 256;  // 16-B weight chunks per thread (BN*8/256)
-  const __bf16* wgt = reinterpret_cast<const __bf16*>(d.weight);
-  auto load_b = [&](int kt, u32x4 (&rbv)[NBL > 0 ? NBL : 1]) {
-#pragma unroll
-    for (int i = 0; i < NBL; ++i) {
-      const int idx = tid + 256 * i;  // chunk index: row = idx>>3, chunk = idx&7
-      const int n = n0 + (idx >> 3);
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (n < d.N) v = *reinterpret_cast<const u32x4*>(wgt + (int64_t)n * d.K + kt * BK + (idx & 7) * 8);
-      rbv[i] = v;
-    }
-  };
-
-  auto store_tiles = [&](int buf, const f32x4 (&ra)[8], const u32x4 (&rbv)[NBL > 0 ? NBL : 1]) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int kq = ahalf * 8 + q;  // quad index 0..15 within the 64-wide row
-      const int c = kq >> 1;
-      bf16x4 h;
-      h[0] = (__bf16)ra[q][0];
-      h[1] = (__bf16)ra[q][1];
-      h[2] = (__bf16)ra[q][2];
-      h[3] = (__bf16)ra[q][3];
-      *reinterpret_cast<bf16x4*>(&As[buf][arow * ROWB + chunk_swz(arow, c) * 16 + (kq & 1) * 8]) = h;
-    }
-#pragma unroll
-    for (int i = 0; i < NBL; ++i) {
-      const int idx = tid + 256 * i;
-      const int row = idx >> 3;
-      *reinterpret_cast<u32x4*>(&Bs[buf][row * ROWB + chunk_swz(row, idx & 7) * 16]) = rbv[i];
-    }
-  };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  f32x4 ra[8];
-  u32x4 rbv[NBL > 0 ? NBL : 1];
-  load_a(0, ra);
-  load_b(0, rbv);
-  store_tiles(0, ra, rbv);
+  for (int q = tid; q < d.K / 8; q += 256) {
+    const clskd_ktab_entry e = d.ktab[q * 8];
+    const int s = d.kseg[q * 8];
+    ctab[q] = make_int2(e.off, (int)(((unsigned)e.dF & 0xFFFFu) | (((unsigned)e.dT & 0xFFu) << 16) |
+                                     ((unsigned)s << 24)));
+  }
   __syncthreads();
 
+  const unsigned short* wgt = reinterpret_cast<const unsigned short*>(d.weight);
+  const int prow = lane >> 3;  // row within an 8-row DMA group
+  const int ppos = lane & 7;   // 16-B chunk position within the LDS row
+
+  const uint64_t zero_addr = (uint64_t)(uintptr_t)g_zero_page;
+  const unsigned stage_lds0 = __builtin_amdgcn_readfirstlane(lds_addr(stages));
+  auto issue = [&](int kt, int stage) {
+    // phase 1: every source address of this K-tile (LDS table reads only)
+    uint64_t srcA[NGA], srcB[NGB];
+#pragma unroll
+    for (int i = 0; i < NGA; ++i) {
+      const int r = (wave * NGA + i) * 8 + prow;
+      const int c = ppos ^ swz(r);
+      const int2 ce = ctab[kt * 8 + c];
+      const int s = (int)((unsigned)ce.y >> 24);
+      const int dF = (int)(short)(ce.y & 0xFFFF);
+      const int dT = (int)(signed char)((ce.y >> 16) & 0xFF);
+      const int4 ri = reinterpret_cast<const int4*>(rowinfo)[r];
+      const int4 sg = segtab[s];
+      const int fi = ri.x + dF;
+      const int ti = ri.y + dT;
+      const bool ok = ri.z && (unsigned)fi < (unsigned)sg.z && (unsigned)ti < (unsigned)sg.w;
+      const uint64_t base = ((uint64_t)(unsigned)sg.y << 32) | (uint64_t)(unsigned)sg.x;
+      const int64_t eoff = (int64_t)rowbase[s * BM + r] + ce.x;
+      srcA[i] = ok ? base + (uint64_t)(eoff * 2) : zero_addr;
+    }
+#pragma unroll
+    for (int i = 0; i < NGB; ++i) {
+      const int r = (wave + 4 * i) * 8 + prow;
+      const int c = ppos ^ swz(r);
+      const int n = n0 + r;
+      srcB[i] = n < d.N ? (uint64_t)(uintptr_t)(wgt + (int64_t)n * d.K + kt * BK + c * 8) : zero_addr;
+    }
+    // phase 2: the DMAs, back to back
+    const unsigned sl = stage_lds0 + stage * SB;
+#pragma unroll
+    for (int i = 0; i < NGA; ++i) glds16((const void*)srcA[i], sl + (wave * NGA + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < NGB; ++i) glds16((const void*)srcB[i], sl + BM * ROWB + (wave + 4 * i) * 1024);
+  };
+
+  // accumulators start at the bias (its loads are waited for here, once, before the pipeline)
   const int h = lane >> 5;
   const int l32 = lane & 31;
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * (BN / WN) + j * 32 + l32;
+    const float bv = (d.bias && n < d.N) ? d.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = bv;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
     if (kt + 1 < nk) {
-      load_a(kt + 1, ra);
-      load_b(kt + 1, rbv);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % STAGES);
+    const unsigned char* sa = stages + (kt % STAGES) * SB;
+    const unsigned char* sb = sa + BM * ROWB;
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
       const int c = 2 * s + h;  // lane half h takes k = 16s + 8h .. +8
@@ -175,12 +211,12 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16(const ConvArgsBF args) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * (BM / WM) + i * 32 + l32;
-        af[i] = *reinterpret_cast<const bf16x8*>(&As[buf][row * ROWB + chunk_swz(row, c) * 16]);
+        af[i] = *reinterpret_cast<const bf16x8*>(sa + row * ROWB + ((c ^ swz(row)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * (BN / WN) + j * 32 + l32;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(&Bs[buf][row * ROWB + chunk_swz(row, c) * 16]);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(sb + row * ROWB + ((c ^ swz(row)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -188,15 +224,13 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16(const ConvArgsBF args) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_tiles(buf ^ 1, ra, rbv);
-    __syncthreads();
   }
 
+  OutT* out = reinterpret_cast<OutT*>(d.out);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * (BN / WN) + j * 32 + l32;
     if (n >= d.N) continue;
-    const float bias = d.bias ? d.bias[n] : 0.f;
     const int64_t coff = (int64_t)(n / d.nlo) * d.oNhi + (int64_t)(n % d.nlo) * d.oNlo;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -204,23 +238,39 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16(const ConvArgsBF args) {
       for (int r = 0; r < 16; ++r) {
         const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int64_t ro = out_row[row];
-        if (ro >= 0) d.out[ro + coff] = acc[i][j][r] + bias;
+        if (ro >= 0) store_out<OutT>(out + ro + coff, acc[i][j][r]);
       }
     }
   }
 }
 
-int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
-  ConvArgsBF a{d};
+template <int BN, typename OutT>
+static int launch_v2(const clskd_conv_desc& d, hipStream_t st) {
+  using namespace v2;
+  const size_t lds = (size_t)STAGES * stage_bytes(BN) + BM * 16 + 4 * BM * 4 + BM * 8 + 64 +
+                     (size_t)(d.K / 8) * 8;
+  if (lds > 160 * 1024) {
+    set_error("conv2d(bf16): K=%d needs %zu B of LDS", d.K, lds);
+    return CLSKD_E_SHAPE;
+  }
+  auto kern = conv_igemm_bf16_dma<BN, OutT>;
+  static bool attr_set = false;  // per instantiation
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
-  const unsigned gx = (unsigned)cdiv(M, bf::BM);
-  if (d.N <= 32)
-    hipLaunchKernelGGL(conv_igemm_bf16<32>, dim3(gx, (unsigned)cdiv(d.N, 32)), dim3(256), 0, st, a);
-  else if (d.N <= 64)
-    hipLaunchKernelGGL(conv_igemm_bf16<64>, dim3(gx, (unsigned)cdiv(d.N, 64)), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL(conv_igemm_bf16<128>, dim3(gx, (unsigned)cdiv(d.N, 128)), dim3(256), 0, st, a);
-  return 0;
+  ConvArgsV2 a{d};
+  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, BM), (unsigned)cdiv(d.N, BN)), dim3(256), lds, st, a);
+  return CLSKD_OK;
+}
+
+int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
+  const bool f32out = d.out_dtype == CLSKD_F32;
+  if (d.N <= 32) return f32out ? launch_v2<32, float>(d, st) : launch_v2<32, __bf16>(d, st);
+  if (d.N <= 64) return f32out ? launch_v2<64, float>(d, st) : launch_v2<64, __bf16>(d, st);
+  if (d.N <= 128) return f32out ? launch_v2<128, float>(d, st) : launch_v2<128, __bf16>(d, st);
+  return f32out ? launch_v2<256, float>(d, st) : launch_v2<256, __bf16>(d, st);
 }
 
 }  // namespace clskd

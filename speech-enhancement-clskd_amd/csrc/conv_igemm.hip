@@ -30,7 +30,10 @@ __device__ __forceinline__ T sel4(int s, T a0, T a1, T a2, T a3) {
   return s == 0 ? a0 : (s == 1 ? a1 : (s == 2 ? a2 : a3));
 }
 
-template <int BN, bool VEC4>
+template <typename OutT>
+__device__ __forceinline__ void store_val(OutT* p, float v) { *p = (OutT)v; }
+
+template <int BN, bool VEC4, typename OutT>
 __global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
   const clskd_conv_desc& d = args.d;
   constexpr int NT = BN / 32;
@@ -135,7 +138,8 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
       const int n = n0 + (idx >> 2);
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if ((idx >> 2) < BN && n < d.N)
-        v = *reinterpret_cast<const f32x4*>(d.weight + (int64_t)n * d.K + kt * BK + (idx & 3) * 4);
+        v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(d.weight) + (int64_t)n * d.K +
+                                            kt * BK + (idx & 3) * 4);
       rbv[i] = v;
     }
   };
@@ -154,11 +158,15 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
     }
   };
 
+  // accumulators start at the bias: no loads are left for the epilogue's store branches
   f32x16 acc[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t)
+  for (int t = 0; t < NT; ++t) {
+    const int n = n0 + t * 32 + (lane & 31);
+    const float bv = (d.bias && n < d.N) ? d.bias[n] : 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    for (int r = 0; r < 16; ++r) acc[t][r] = bv;
+  }
 
   f32x4 ra[2];
   f32x4 rbv[NBL];
@@ -193,18 +201,18 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
     __syncthreads();
   }
 
-  // ---- epilogue: bias + scatter store ----
+  // ---- epilogue: predicated scatter stores (bias already in the accumulators) ----
+  OutT* outp = reinterpret_cast<OutT*>(d.out);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int n = n0 + t * 32 + (lane & 31);
     if (n >= d.N) continue;
-    const float bias = d.bias ? d.bias[n] : 0.f;
     const int64_t coff = (int64_t)(n / d.nlo) * d.oNhi + (int64_t)(n % d.nlo) * d.oNlo;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
       const int64_t ro = out_row[row];
-      if (ro >= 0) d.out[ro + coff] = acc[t][r] + bias;
+      if (ro >= 0) store_val<OutT>(outp + ro + coff, acc[t][r]);
     }
   }
 }
@@ -223,13 +231,22 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
   CLSKD_CHECK_SHAPE(d.B > 0 && d.Fo > 0 && d.To > 0 && d.N > 0 && d.K > 0, "conv2d: empty shape");
   const int kmul = d.compute == CLSKD_BF16 ? 64 : BK;
   CLSKD_CHECK_SHAPE(d.K % kmul == 0, "conv2d: K=%d must be padded to a multiple of %d", d.K, kmul);
-  CLSKD_CHECK_ARG(d.compute == CLSKD_F32 || d.vec4, "conv2d: bf16 compute needs the vec4 gather");
+  CLSKD_CHECK_SHAPE(d.compute != CLSKD_BF16 || d.K <= 8192, "conv2d(bf16): K=%d > 8192", d.K);
+  CLSKD_CHECK_ARG((d.in_dtype == CLSKD_BF16) == (d.compute == CLSKD_BF16),
+                  "conv2d: bf16 MFMA operands come from bf16 activations (in_dtype) only");
+  CLSKD_CHECK_ARG(d.out_dtype == CLSKD_F32 || d.out_dtype == CLSKD_BF16, "conv2d: out_dtype");
   CLSKD_CHECK_SHAPE(d.nseg >= 1 && d.nseg <= CLSKD_MAX_SEGS, "conv2d: nseg=%d", d.nseg);
   CLSKD_CHECK_ARG(d.weight && d.out && d.ktab && d.kseg, "conv2d: null pointer");
   CLSKD_CHECK_SHAPE(d.nlo >= 1, "conv2d: nlo must be >= 1");
   CLSKD_CHECK_ARG(((uintptr_t)d.weight & 15) == 0, "conv2d: weight must be 16-byte aligned");
   for (int s = 0; s < d.nseg; ++s) CLSKD_CHECK_ARG(d.seg[s].ptr != nullptr, "conv2d: null segment %d", s);
-  if (d.vec4) {
+  if (d.in_dtype == CLSKD_BF16) {
+    for (int s = 0; s < d.nseg; ++s) {
+      const clskd_seg& g = d.seg[s];
+      CLSKD_CHECK_ARG(((uintptr_t)g.ptr & 15) == 0 && g.sB % 8 == 0 && g.sF % 8 == 0 && g.sT % 8 == 0,
+                      "conv2d(bf16): segment %d must be 16-byte aligned with strides %% 8", s);
+    }
+  } else if (d.vec4) {
     for (int s = 0; s < d.nseg; ++s) {
       const clskd_seg& g = d.seg[s];
       CLSKD_CHECK_ARG(((uintptr_t)g.ptr & 15) == 0 && g.sB % 4 == 0 && g.sF % 4 == 0 && g.sT % 4 == 0,
@@ -240,21 +257,25 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
   CLSKD_CHECK_SHAPE(M < (int64_t)INT32_MAX * 64, "conv2d: too many rows");
   hipStream_t st = as_stream(stream);
   if (d.compute == CLSKD_BF16) {
-    launch_conv_bf16(d, st);
+    const int rc = launch_conv_bf16(d, st);
+    if (rc != CLSKD_OK) return rc;
     CLSKD_LAUNCH_CHECK("conv2d_bf16");
     return CLSKD_OK;
   }
   ConvArgs a{d};
   const unsigned gx = (unsigned)cdiv(M, BM);
-#define LAUNCH(BN_, V_)                                                                      \
-  hipLaunchKernelGGL((conv_igemm_f32<BN_, V_>), dim3(gx, (unsigned)cdiv(d.N, BN_)), dim3(256), 0, st, a)
+#define LAUNCH(BN_, V_, O_)                                                                  \
+  hipLaunchKernelGGL((conv_igemm_f32<BN_, V_, O_>), dim3(gx, (unsigned)cdiv(d.N, BN_)), dim3(256), 0, st, a)
+#define LAUNCH_O(BN_, V_) \
+  do { if (d.out_dtype == CLSKD_BF16) LAUNCH(BN_, V_, __bf16); else LAUNCH(BN_, V_, float); } while (0)
   if (d.N <= 32) {
-    if (d.vec4) LAUNCH(32, true); else LAUNCH(32, false);
+    if (d.vec4) LAUNCH_O(32, true); else LAUNCH_O(32, false);
   } else if (d.N <= 64) {
-    if (d.vec4) LAUNCH(64, true); else LAUNCH(64, false);
+    if (d.vec4) LAUNCH_O(64, true); else LAUNCH_O(64, false);
   } else {
-    if (d.vec4) LAUNCH(128, true); else LAUNCH(128, false);
+    if (d.vec4) LAUNCH_O(128, true); else LAUNCH_O(128, false);
   }
+#undef LAUNCH_O
 #undef LAUNCH
   CLSKD_LAUNCH_CHECK("conv2d");
   return CLSKD_OK;

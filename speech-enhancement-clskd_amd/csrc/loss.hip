@@ -15,12 +15,21 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x4 load_row4(const clskd_gram_job& j, int b, int B, int64_t e,
                                            int64_t p0, int64_t p1) {
-  // element e of this slab (p0-relative), 4-aligned, Cs % 4 == 0
+  // element e of this slab (p0-relative), 4-aligned, Cs % 4 == 0 (fp32) / % 8 == 0 (bf16)
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
   if (b < B) {
     const int64_t p = p0 + e / j.Cs;
     const int c = (int)(e % j.Cs);
-    if (p < p1) v = *reinterpret_cast<const f32x4*>(j.ptr + (int64_t)b * j.sB + p * j.Ctot + j.c0 + c);
+    if (p < p1) {
+      const int64_t off = (int64_t)b * j.sB + p * j.Ctot + j.c0 + c;
+      if (j.dtype == CLSKD_BF16) {
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        const bf16x4 h = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(j.ptr) + off);
+        v = f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+      } else {
+        v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(j.ptr) + off);
+      }
+    }
   }
   return v;
 }

@@ -6,11 +6,41 @@
 
 namespace clskd {
 
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ f32x4 load4(const T* p);
+template <>
+__device__ __forceinline__ f32x4 load4<float>(const float* p) {
+  return *reinterpret_cast<const f32x4*>(p);
+}
+template <>
+__device__ __forceinline__ f32x4 load4<__bf16>(const __bf16* p) {
+  const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+template <typename T>
+__device__ __forceinline__ void store4(T* p, f32x4 v);
+template <>
+__device__ __forceinline__ void store4<float>(float* p, f32x4 v) {
+  *reinterpret_cast<f32x4*>(p) = v;
+}
+template <>
+__device__ __forceinline__ void store4<__bf16>(__bf16* p, f32x4 v) {
+  bf16x4 o;
+  o[0] = (__bf16)v[0];
+  o[1] = (__bf16)v[1];
+  o[2] = (__bf16)v[2];
+  o[3] = (__bf16)v[3];
+  *reinterpret_cast<bf16x4*>(p) = o;
+}
+
 // ------------------------------------------------------------------------------------------
 // BatchNorm statistics: block `blk` reduces rows [blk*rpb, (blk+1)*rpb) of x[rows][C] into
 // partial[blk][C][2] = {sum, sumsq} (fp64).  Threads map to (row-lane, channel quad).
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __restrict__ x,
+template <typename T>
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(const T* __restrict__ x,
                                                                int64_t rows, int C, int64_t rpb,
                                                                double* __restrict__ partial) {
   const int CG = C >> 2;                 // channel quads
@@ -23,7 +53,7 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float* __re
   double s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
   if (rl < RP) {
     for (int64_t r = r0 + rl; r < r1; r += RP) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(x + r * C + cg * 4);
+      const f32x4 v = load4<T>(x + r * C + cg * 4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         s[j] += (double)v[j];
@@ -117,8 +147,9 @@ __global__ void bn_eval_coeffs_kernel(const float* rm, const float* rv, const fl
   shift[c] = (beta ? beta[c] : 0.f) - rm[c] * sc;
 }
 
-__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ x,
-                                                       float* __restrict__ y, int64_t n4, int C,
+template <typename T>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
+                                                       T* __restrict__ y, int64_t n4, int C,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
                                                        const float* __restrict__ alpha) {
@@ -127,14 +158,14 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int c0 = (int)((i * 4) % C);
-    f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+    f32x4 v = load4<T>(x + i * 4);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float t = v[j] * scale[c0 + j] + shift[c0 + j];
       if (act) t = t >= 0.f ? t : a * t;
       v[j] = t;
     }
-    reinterpret_cast<f32x4*>(y)[i] = v;
+    store4<T>(y + i * 4, v);
   }
 }
 
@@ -253,12 +284,13 @@ __device__ __forceinline__ int nearest_src(int dst, int in_size, int out_size) {
   return s < in_size - 1 ? s : in_size - 1;
 }
 
-__global__ __launch_bounds__(256) void abf_fuse_kernel(const float* __restrict__ x,
-                                                       const float* __restrict__ res, int B,
+template <typename DT>
+__global__ __launch_bounds__(256) void abf_fuse_kernel(const DT* __restrict__ x,
+                                                       const DT* __restrict__ res, int B,
                                                        int F, int T, int Fr, int Tr,
                                                        const float* __restrict__ w,
                                                        const float* __restrict__ bias,
-                                                       float* __restrict__ out) {
+                                                       DT* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int sub = lane & 15;  // channel quad
   const int c = sub * 4;
@@ -281,8 +313,8 @@ __global__ __launch_bounds__(256) void abf_fuse_kernel(const float* __restrict__
     const int b = (int)(bf / F);
     const int fr = nearest_src(f, Fr, F);
     const int tr = nearest_src(t, Tr, T);
-    const f32x4 xv = *reinterpret_cast<const f32x4*>(x + p * 64 + c);
-    const f32x4 yv = *reinterpret_cast<const f32x4*>(res + (((int64_t)b * Fr + fr) * Tr + tr) * 64 + c);
+    const f32x4 xv = load4<DT>(x + p * 64 + c);
+    const f32x4 yv = load4<DT>(res + (((int64_t)b * Fr + fr) * Tr + tr) * 64 + c);
     float d0 = 0.f, d1 = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -299,7 +331,7 @@ __global__ __launch_bounds__(256) void abf_fuse_kernel(const float* __restrict__
     f32x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = xv[j] * z0 + yv[j] * z1;
-    *reinterpret_cast<f32x4*>(out + p * 64 + c) = o;
+    store4<DT>(out + p * 64 + c, o);
   }
 }
 
@@ -328,15 +360,20 @@ extern "C" int32_t clskd_bn_partial_blocks(int64_t rows, int32_t C) {
   return (int32_t)work;
 }
 
-extern "C" int clskd_bn_stats_partial(const float* x, int64_t rows, int32_t C, double* partial,
-                                      int32_t nblk, void* stream) {
+extern "C" int clskd_bn_stats_partial(const void* x, int64_t rows, int32_t C, double* partial,
+                                      int32_t nblk, int32_t dtype, void* stream) {
   CLSKD_CHECK_ARG(x && partial, "bn_stats: null pointer");
   CLSKD_CHECK_SHAPE(rows > 0 && C >= 4 && C % 4 == 0 && C <= 1024, "bn_stats: bad C=%d", C);
   CLSKD_CHECK_SHAPE(nblk >= 1, "bn_stats: nblk");
   CLSKD_CHECK_ARG(((uintptr_t)x & 15) == 0, "bn_stats: x must be 16-byte aligned");
+  CLSKD_CHECK_ARG(dtype == CLSKD_F32 || dtype == CLSKD_BF16, "bn_stats: dtype");
   const int64_t rpb = cdiv(rows, nblk);
-  hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(nblk), dim3(256), 0, as_stream(stream), x, rows,
-                     C, rpb, partial);
+  if (dtype == CLSKD_BF16)
+    hipLaunchKernelGGL(bn_stats_partial_kernel<__bf16>, dim3(nblk), dim3(256), 0, as_stream(stream),
+                       (const __bf16*)x, rows, C, rpb, partial);
+  else
+    hipLaunchKernelGGL(bn_stats_partial_kernel<float>, dim3(nblk), dim3(256), 0, as_stream(stream),
+                       (const float*)x, rows, C, rpb, partial);
   CLSKD_LAUNCH_CHECK("bn_stats_partial");
   return CLSKD_OK;
 }
@@ -366,15 +403,20 @@ extern "C" int clskd_bn_eval_coeffs(const float* running_mean, const float* runn
   return CLSKD_OK;
 }
 
-extern "C" int clskd_bn_apply(const float* x, float* y, int64_t rows, int32_t C,
+extern "C" int clskd_bn_apply(const void* x, void* y, int64_t rows, int32_t C,
                               const float* scale, const float* shift, const float* alpha,
-                              void* stream) {
+                              int32_t dtype, void* stream) {
   CLSKD_CHECK_ARG(x && y && scale && shift, "bn_apply: null pointer");
   CLSKD_CHECK_SHAPE(C % 4 == 0 && rows > 0, "bn_apply: C=%d must be a multiple of 4", C);
-  CLSKD_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0, "bn_apply: alignment");
+  CLSKD_CHECK_ARG(((uintptr_t)x & 7) == 0 && ((uintptr_t)y & 7) == 0, "bn_apply: alignment");
+  CLSKD_CHECK_ARG(dtype == CLSKD_F32 || dtype == CLSKD_BF16, "bn_apply: dtype");
   const int64_t n4 = rows * C / 4;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream), x, y, n4,
-                     C, scale, shift, alpha);
+  if (dtype == CLSKD_BF16)
+    hipLaunchKernelGGL(bn_apply_kernel<__bf16>, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream),
+                       (const __bf16*)x, (__bf16*)y, n4, C, scale, shift, alpha);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream),
+                       (const float*)x, (float*)y, n4, C, scale, shift, alpha);
   CLSKD_LAUNCH_CHECK("bn_apply");
   return CLSKD_OK;
 }
@@ -423,14 +465,21 @@ extern "C" int clskd_complex_combine(const float* rr, const float* ii, const flo
   return CLSKD_OK;
 }
 
-extern "C" int clskd_abf_fuse(const float* x, const float* res, int32_t B, int32_t F, int32_t T,
-                              int32_t Fr, int32_t Tr, const float* w, const float* b, float* out,
-                              void* stream) {
+extern "C" int clskd_abf_fuse(const void* x, const void* res, int32_t B, int32_t F, int32_t T,
+                              int32_t Fr, int32_t Tr, const float* w, const float* b, void* out,
+                              int32_t dtype, void* stream) {
   CLSKD_CHECK_ARG(x && res && w && b && out, "abf_fuse: null pointer");
   CLSKD_CHECK_SHAPE(B > 0 && F > 0 && T > 0 && Fr > 0 && Tr > 0, "abf_fuse: shape");
+  CLSKD_CHECK_ARG(dtype == CLSKD_F32 || dtype == CLSKD_BF16, "abf_fuse: dtype");
   const int64_t npix = (int64_t)B * F * T;
-  hipLaunchKernelGGL(abf_fuse_kernel, dim3(grid_for(npix * 16)), dim3(256), 0, as_stream(stream), x,
-                     res, B, F, T, Fr, Tr, w, b, out);
+  if (dtype == CLSKD_BF16)
+    hipLaunchKernelGGL(abf_fuse_kernel<__bf16>, dim3(grid_for(npix * 16)), dim3(256), 0,
+                       as_stream(stream), (const __bf16*)x, (const __bf16*)res, B, F, T, Fr, Tr, w, b,
+                       (__bf16*)out);
+  else
+    hipLaunchKernelGGL(abf_fuse_kernel<float>, dim3(grid_for(npix * 16)), dim3(256), 0,
+                       as_stream(stream), (const float*)x, (const float*)res, B, F, T, Fr, Tr, w, b,
+                       (float*)out);
   CLSKD_LAUNCH_CHECK("abf_fuse");
   return CLSKD_OK;
 }

@@ -28,7 +28,7 @@ def test_struct_layouts_match_header():
     # clskd_seg: ptr + 3 int64 + 2 int32 = 40 B; desc must be 8-aligned
     assert ctypes.sizeof(_lib.Seg) == 40
     assert ctypes.sizeof(_lib.KtabEntry) == 8
-    assert ctypes.sizeof(_lib.GramJob) == 48
+    assert ctypes.sizeof(_lib.GramJob) == 56
     assert ctypes.sizeof(_lib.ConvDesc) % 8 == 0
 
 
