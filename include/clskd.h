@@ -92,6 +92,9 @@ typedef struct {
   int32_t in_dtype;  /* CLSKD_F32 / CLSKD_BF16 storage of every segment (bf16 <=> bf16 compute;
                         bf16 needs segment channel runs of 8 and strides % 8) */
   int32_t out_dtype; /* CLSKD_F32 / CLSKD_BF16 storage of `out` */
+  double* stats;     /* optional fused BatchNorm statistics: per M-block (128 output rows) fp64
+                        partials stats[blockIdx.x][N][2] = {sum, sumsq} of the biased outputs,
+                        consumed by clskd_bn_finalize (nblk = number of M-blocks) */
 } clskd_conv_desc;
 
 int clskd_conv2d_fwd(const clskd_conv_desc* d, void* stream);

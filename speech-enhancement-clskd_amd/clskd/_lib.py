@@ -32,7 +32,7 @@ class ConvDesc(C.Structure):
                 ("bias", C.c_void_p), ("out", C.c_void_p), ("oB", C.c_int64), ("oF", C.c_int64),
                 ("oT", C.c_int64), ("oNhi", C.c_int64), ("oNlo", C.c_int64), ("nlo", C.c_int32),
                 ("of_mul", C.c_int32), ("of_add", C.c_int32), ("compute", C.c_int32),
-                ("in_dtype", C.c_int32), ("out_dtype", C.c_int32)]
+                ("in_dtype", C.c_int32), ("out_dtype", C.c_int32), ("stats", C.c_void_p)]
 
 
 class GramJob(C.Structure):

@@ -213,11 +213,14 @@ class ABF(nn.Module):
         dev = x.device
         act = dict(device=dev, dtype=self.act_dtype)
         x1 = torch.empty(B, Fn, Tn, mid, **act)
+        nmb = ops.conv_mblocks(B, Fn, Tn)
+        f64 = dict(device=dev, dtype=torch.float64)
+        part = torch.empty(nmb * mid * 2, **f64) if train else None
         ops.conv([seg_bftc(x)], [(0, 0)], B, Fn, Tn, mid, w1p, None, x1,
-                 OutMap(Fn * Tn * mid, Tn * mid, mid))
+                 OutMap(Fn * Tn * mid, Tn * mid, mid), stats=part)
         bn = self.conv1[1]
         ops.batch_norm_bftc(x1, x1, bn.weight, bn.bias, bn.running_mean, bn.running_var, train,
-                            bn.momentum, bn.eps, 1)
+                            bn.momentum, bn.eps, 1, partial=(part, nmb) if train else None)
         if self.att_conv is not None:
             if shape != Fn:  # the reference's torch.cat would fail as well (framework.py:213-216)
                 raise ValueError(f"ABF fuse: residual upsampled to F={shape} but x has F={Fn}")
@@ -231,11 +234,12 @@ class ABF(nn.Module):
                 f"ABF output interpolation to ({out_shape}, {Tn}) from F={Fn} is not on the CLSKD path")
         Cout = w2p.shape[0]
         out = torch.empty(B, Fn, Tn, Cout, **act)
+        part2 = torch.empty(nmb * Cout * 2, **f64) if train else None
         ops.conv([seg_bftc(x1)], [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], B, Fn,
-                 Tn, Cout, w2p, None, out, OutMap(Fn * Tn * Cout, Tn * Cout, Cout))
+                 Tn, Cout, w2p, None, out, OutMap(Fn * Tn * Cout, Tn * Cout, Cout), stats=part2)
         bn = self.conv2[1]
         ops.batch_norm_bftc(out, out, bn.weight, bn.bias, bn.running_mean, bn.running_var, train,
-                            bn.momentum, bn.eps, 1)
+                            bn.momentum, bn.eps, 1, partial=(part2, nmb) if train else None)
         return out, x1
 
     def forward(self, x, y=None, shape=None, out_shape=None, feature_type=None):

@@ -374,11 +374,14 @@ class DCCRN(nn.Module):
             wp, bias = self._enc_w(i, self._cmp(segs, 10 * kn[i]))
             taps = [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)]
             raw = torch.empty(B, Fo, T, Co, **act)
+            nmb = ops.conv_mblocks(B, Fo, T)
+            part = torch.empty(nmb * Co * 2, device=dev, dtype=torch.float64) if train else None
             ops.conv(segs, taps, B, Fo, T, Co, wp, bias, raw, OutMap(Fo * T * Co, T * Co, Co),
-                     stride_f=2)
+                     stride_f=2, stats=part)
             bn, pr = self.encoder[i][1], self.encoder[i][2]
             ops.batch_norm_bftc(raw, raw, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                                train, bn.momentum, bn.eps, bn_updates, alpha=pr.weight)
+                                train, bn.momentum, bn.eps, bn_updates, alpha=pr.weight,
+                                partial=(part, nmb) if train else None)
             enc.append(raw)
             F = Fo
         # ---------------- complex LSTM (DCCRN.py:178-199, tools_for_model.py:159-174)
@@ -436,16 +439,21 @@ class DCCRN(nn.Module):
             last = d == nl - 1
             raw = torch.empty(B, 2 * F, T + 1, Co, **(f32 if last else act))
             Ci = sum(sg.geom.C for sg in segs)
+            has_bn = len(self.decoder[d]) > 1
+            nmb = ops.conv_mblocks(B, F, T + 1)
+            part = (torch.empty(2 * nmb * Co * 2, device=dev, dtype=torch.float64)
+                    if (train and has_bn) else None)
             for parity in (0, 1):
                 taps = [(dF, -kt) for _, dF in self._DEC_TAPS[parity] for kt in (0, 1)]
                 wp, bias = self._dec_w(d, parity, self._cmp(segs, len(taps) * Ci))
                 ops.conv(segs, taps, B, F, T + 1, Co, wp, bias, raw,
-                         OutMap(2 * F * (T + 1) * Co, (T + 1) * Co, Co, of_mul=2, of_add=parity))
-            if len(self.decoder[d]) > 1:
+                         OutMap(2 * F * (T + 1) * Co, (T + 1) * Co, Co, of_mul=2, of_add=parity),
+                         stats=part, stats_offset=parity * nmb * Co * 2)
+            if has_bn:
                 bn, pr = self.decoder[d][1], self.decoder[d][2]
                 ops.batch_norm_bftc(raw, raw, bn.weight, bn.bias, bn.running_mean,
                                     bn.running_var, train, bn.momentum, bn.eps, bn_updates,
-                                    alpha=pr.weight)
+                                    alpha=pr.weight, partial=(part, 2 * nmb) if part is not None else None)
             dec.append(raw)
             out_t, out_t0, out_T = raw, 1, T
             F = 2 * F

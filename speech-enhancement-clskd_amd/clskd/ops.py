@@ -164,8 +164,13 @@ def out_bftc(t, c0=0, of_mul=1, of_add=0):
     return OutMap(F * T * Ct, T * Ct, Ct, 0, 1, 1 << 30, of_mul, of_add), c0
 
 
+def conv_mblocks(B, Fo, To):
+    """Number of 128-row M-blocks of a conv launch (= fused-statistics partial count)."""
+    return -(-(B * Fo * To) // 128)
+
+
 def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, stride_f=1,
-         stride_t=1):
+         stride_t=1, stats=None, stats_offset=0):
     """out[b, fo*of_mul+of_add, to, n] = bias[n] + sum_k A[(b,fo,to),k] W[n,k].
     bf16 segments run the LDS-DMA bf16-MFMA engine (weights packed bf16, K % 64); fp32 segments
     the fp32-MFMA engine (weights fp32, K % 16).  `out` may be fp32 or bf16 storage."""
@@ -203,6 +208,11 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
     d.compute = _lib.BF16 if bf16 else _lib.F32
     d.in_dtype = in_dt
     d.out_dtype = _dt(out)
+    if stats is not None:
+        assert stats.dtype == torch.float64 and stats.numel() >= stats_offset + conv_mblocks(B, Fo, To) * N * 2
+        d.stats = stats.data_ptr() + 8 * stats_offset
+    else:
+        d.stats = None
     if KernelTimer.active:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
@@ -219,9 +229,10 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
 # BatchNorm (+ PReLU)
 # ------------------------------------------------------------------------------------------
 def batch_norm_bftc(x, y, gamma, beta, running_mean, running_var, train, momentum=0.1,
-                    eps=1e-5, n_updates=1, alpha=None, stats_out=None):
+                    eps=1e-5, n_updates=1, alpha=None, stats_out=None, partial=None):
     """nn.BatchNorm2d over a BFTC tensor (channels last), then optional PReLU (single alpha).
-    train: batch statistics (biased var), running stats updated n_updates times (if given)."""
+    train: batch statistics (biased var), running stats updated n_updates times (if given).
+    partial=(tensor, nblk): statistics already produced by the conv epilogue (fused)."""
     L = lib()
     Cn = x.shape[-1]
     rows = x.numel() // Cn
@@ -230,9 +241,12 @@ def batch_norm_bftc(x, y, gamma, beta, running_mean, running_var, train, momentu
     shift = torch.empty(Cn, device=dev, dtype=torch.float32)
     st = _stream()
     if train:
-        nblk = L.clskd_bn_partial_blocks(rows, Cn)
-        part = torch.empty(nblk * Cn * 2, device=dev, dtype=torch.float64)
-        check(L.clskd_bn_stats_partial(ptr(x), rows, Cn, ptr(part), nblk, _dt(x), st), "bn_stats")
+        if partial is not None:
+            part, nblk = partial
+        else:
+            nblk = L.clskd_bn_partial_blocks(rows, Cn)
+            part = torch.empty(nblk * Cn * 2, device=dev, dtype=torch.float64)
+            check(L.clskd_bn_stats_partial(ptr(x), rows, Cn, ptr(part), nblk, _dt(x), st), "bn_stats")
         mean_o = var_o = None
         if stats_out is not None:
             mean_o, var_o = stats_out

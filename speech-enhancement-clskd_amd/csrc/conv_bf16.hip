@@ -226,6 +226,46 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16_dma(const ConvArgsV2 args
     }
   }
 
+  if (d.stats) {  // fused BatchNorm statistics of this block's valid rows
+    __syncthreads();  // all DMAs retired (vmcnt(0) on the last K-tile); stage LDS is free
+    double* red = reinterpret_cast<double*>(smem);  // [WM][BN][2]
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * (BN / WN) + j * 32 + l32;
+      float sm = 0.f, sq = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (out_row[row] >= 0) {
+            const float v = acc[i][j][r];
+            sm += v;
+            sq = fmaf(v, v, sq);
+          }
+        }
+      double ds = (double)sm + (double)__shfl_xor(sm, 32, 64);
+      double dq = (double)sq + (double)__shfl_xor(sq, 32, 64);
+      if (h == 0) {
+        red[(wm * BN + col) * 2] = ds;
+        red[(wm * BN + col) * 2 + 1] = dq;
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      const int n = n0 + c;
+      if (n >= d.N) continue;
+      double S = 0.0, Q = 0.0;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        S += red[(w * BN + c) * 2];
+        Q += red[(w * BN + c) * 2 + 1];
+      }
+      d.stats[((int64_t)blockIdx.x * d.N + n) * 2] = S;
+      d.stats[((int64_t)blockIdx.x * d.N + n) * 2 + 1] = Q;
+    }
+  }
+
   OutT* out = reinterpret_cast<OutT*>(d.out);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {

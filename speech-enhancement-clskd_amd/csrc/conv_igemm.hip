@@ -201,6 +201,41 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
     __syncthreads();
   }
 
+  if (d.stats) {  // fused BatchNorm statistics (fp32 per lane, fp64 across lanes/waves)
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(&As[0][0]);  // [4 waves][BN][2]
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = t * 32 + (lane & 31);
+      float sm = 0.f, sq = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (out_row[row] >= 0) {
+          const float v = acc[t][r];
+          sm += v;
+          sq = fmaf(v, v, sq);
+        }
+      }
+      const double ds = (double)sm + (double)__shfl_xor(sm, 32, 64);
+      const double dq = (double)sq + (double)__shfl_xor(sq, 32, 64);
+      if (h == 0) {
+        red[(wave * BN + col) * 2] = ds;
+        red[(wave * BN + col) * 2 + 1] = dq;
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      const int n = n0 + c;
+      if (n >= d.N) continue;
+      const double S = red[c * 2] + red[(BN + c) * 2] + red[(2 * BN + c) * 2] + red[(3 * BN + c) * 2];
+      const double Q = red[c * 2 + 1] + red[(BN + c) * 2 + 1] + red[(2 * BN + c) * 2 + 1] +
+                       red[(3 * BN + c) * 2 + 1];
+      d.stats[((int64_t)blockIdx.x * d.N + n) * 2] = S;
+      d.stats[((int64_t)blockIdx.x * d.N + n) * 2 + 1] = Q;
+    }
+  }
+
   // ---- epilogue: predicated scatter stores (bias already in the accumulators) ----
   OutT* outp = reinterpret_cast<OutT*>(d.out);
 #pragma unroll

@@ -148,24 +148,79 @@ __global__ void bn_eval_coeffs_kernel(const float* rm, const float* rv, const fl
 }
 
 template <typename T>
+struct Vec8;
+template <>
+struct Vec8<float> {
+  __device__ static void load(const float* p, float (&v)[8]) {
+    const f32x4 a = reinterpret_cast<const f32x4*>(p)[0], b = reinterpret_cast<const f32x4*>(p)[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = a[j];
+      v[4 + j] = b[j];
+    }
+  }
+  __device__ static void store(float* p, const float (&v)[8]) {
+    reinterpret_cast<f32x4*>(p)[0] = f32x4{v[0], v[1], v[2], v[3]};
+    reinterpret_cast<f32x4*>(p)[1] = f32x4{v[4], v[5], v[6], v[7]};
+  }
+};
+template <>
+struct Vec8<__bf16> {
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  __device__ static void load(const __bf16* p, float (&v)[8]) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)a[j];
+  }
+  __device__ static void store(__bf16* p, const float (&v)[8]) {
+    bf16x8 a;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = (__bf16)v[j];
+    *reinterpret_cast<bf16x8*>(p) = a;
+  }
+};
+
+// y = x*scale[c] + shift[c] (+ PReLU).  8 channels per thread; with C/8 dividing the grid
+// stride each thread keeps one channel group, so scale/shift stay in registers.
+template <typename T>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
-                                                       T* __restrict__ y, int64_t n4, int C,
+                                                       T* __restrict__ y, int64_t items, int CG,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
                                                        const float* __restrict__ alpha) {
   const float a = alpha ? alpha[0] : 0.f;
   const bool act = alpha != nullptr;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)((i * 4) % C);
-    f32x4 v = load4<T>(x + i * 4);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int cg = (int)(i % CG);
+  float sc[8], sh[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float t = v[j] * scale[c0 + j] + shift[c0 + j];
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = scale[cg * 8 + j];
+    sh[j] = shift[cg * 8 + j];
+  }
+  const bool fixed = (stride % CG) == 0;
+  for (; i < items; i += stride) {
+    if (!fixed) {
+      const int c2 = (int)(i % CG);
+      if (c2 != cg) {
+        cg = c2;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sc[j] = scale[cg * 8 + j];
+          sh[j] = shift[cg * 8 + j];
+        }
+      }
+    }
+    float v[8];
+    Vec8<T>::load(x + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = fmaf(v[j], sc[j], sh[j]);
       if (act) t = t >= 0.f ? t : a * t;
       v[j] = t;
     }
-    store4<T>(y + i * 4, v);
+    Vec8<T>::store(y + i * 8, v);
   }
 }
 
@@ -407,16 +462,20 @@ extern "C" int clskd_bn_apply(const void* x, void* y, int64_t rows, int32_t C,
                               const float* scale, const float* shift, const float* alpha,
                               int32_t dtype, void* stream) {
   CLSKD_CHECK_ARG(x && y && scale && shift, "bn_apply: null pointer");
-  CLSKD_CHECK_SHAPE(C % 4 == 0 && rows > 0, "bn_apply: C=%d must be a multiple of 4", C);
-  CLSKD_CHECK_ARG(((uintptr_t)x & 7) == 0 && ((uintptr_t)y & 7) == 0, "bn_apply: alignment");
+  CLSKD_CHECK_SHAPE(C % 8 == 0 && rows > 0, "bn_apply: C=%d must be a multiple of 8", C);
+  CLSKD_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0, "bn_apply: alignment");
   CLSKD_CHECK_ARG(dtype == CLSKD_F32 || dtype == CLSKD_BF16, "bn_apply: dtype");
-  const int64_t n4 = rows * C / 4;
+  const int64_t items = rows * C / 8;
+  const int CG = C / 8;
+  // grid a multiple of CG-friendly size: 256 threads/block, stride = 256*grid
+  int64_t g = cdiv(items, 256);
+  if (g > 4096) g = 4096;
   if (dtype == CLSKD_BF16)
-    hipLaunchKernelGGL(bn_apply_kernel<__bf16>, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream),
-                       (const __bf16*)x, (__bf16*)y, n4, C, scale, shift, alpha);
+    hipLaunchKernelGGL(bn_apply_kernel<__bf16>, dim3((unsigned)g), dim3(256), 0, as_stream(stream),
+                       (const __bf16*)x, (__bf16*)y, items, CG, scale, shift, alpha);
   else
-    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(grid_for(n4)), dim3(256), 0, as_stream(stream),
-                       (const float*)x, (float*)y, n4, C, scale, shift, alpha);
+    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3((unsigned)g), dim3(256), 0, as_stream(stream),
+                       (const float*)x, (float*)y, items, CG, scale, shift, alpha);
   CLSKD_LAUNCH_CHECK("bn_apply");
   return CLSKD_OK;
 }
