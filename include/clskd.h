@@ -168,14 +168,22 @@ int clskd_abf_fuse(const void* x, const void* res, int32_t B, int32_t F, int32_t
                    int32_t dtype, void* stream);
 
 /* ------------------------------------------------------------------------------------------
- * SPKD / Gram (framework.py:150-172).  A gram job views a tap as z_b = x[b][p][c0 .. c0+Cs)
- * for p < P positions with position stride Ctot and batch stride sB.
- * clskd_gram_partial: every job split in chunks of `chunk` positions; one 32x32 fp32 partial
- *                     Gram slab per chunk; slabs[job_first_slab[j] + i].
- * clskd_spkd_finalize: per pair (student job, teacher job): sum slabs in order, L1-normalise
- *                     rows (normalize(G, p=1) — the reference passes 1 as p), loss =
- *                     ||Gt-Gs||_F^2 (/B^2 if batchmean); writes losses[pair] and grams.
+ * SPKD / Gram (framework.py:150-172; replaces SPKDLoss.forward / get_similarity_matrix, the
+ * per-tap torch.mm(z, z.t()) of framework.py:156-160, for every tap of a step at once).
+ * A gram job views a tap as z_b = x[b][p][c0 .. c0+Cs) for p < P positions with position
+ * stride Ctot and batch stride sB (elements).  Job arrays are HOST memory: the library passes
+ * them to the kernels as kernel arguments (no device upload; launches are graph-capturable).
+ * clskd_gram_partial: job k covers slabs [first_slab, first_slab + nslab), nslab = ceil(P/chunk),
+ *                     jobs contiguous from slab 0; one 32x32 fp32 partial Gram per slab into
+ *                     slabs[slab][32][32] (device, caller-owned).
+ * clskd_spkd_finalize: per pair (student job pairs[2i], teacher job pairs[2i+1], host array):
+ *                     sum the slabs in order (fp64), L1-normalise rows (normalize(G, p=1) — the
+ *                     reference passes 1 as p), loss = ||Gt-Gs||_F^2 (/B^2 if batchmean);
+ *                     writes losses[i] and, if non-null, grams_s/grams_t[i][B][B].
  * -------------------------------------------------------------------------------------- */
+#define CLSKD_GRAM_MAX_JOBS 32   /* jobs per kernel launch (the library splits larger lists) */
+#define CLSKD_SPKD_MAX_PAIRS 64  /* pairs per finalize launch (likewise) */
+
 typedef struct {
   const void* ptr;
   int64_t sB;
@@ -188,9 +196,9 @@ typedef struct {
   int32_t reserved;
 } clskd_gram_job;
 
-int clskd_gram_partial(const clskd_gram_job* jobs_dev, int32_t njobs, int32_t total_slabs,
-                       const int32_t* slab_job_dev, int32_t B, float* slabs, void* stream);
-int clskd_spkd_finalize(const clskd_gram_job* jobs_dev, const int32_t* pairs_dev,
+int clskd_gram_partial(const clskd_gram_job* jobs, int32_t njobs, int32_t B, float* slabs,
+                       void* stream);
+int clskd_spkd_finalize(const clskd_gram_job* jobs, int32_t njobs, const int32_t* pairs,
                         int32_t npairs, int32_t B, int32_t batchmean, const float* slabs,
                         float* grams_s, float* grams_t, float* losses, void* stream);
 

@@ -9,6 +9,7 @@ Drop-in counterparts of the reference modules (KhanhNguyen4999/Speech-Enhancemen
   distill.py              -> clskd.distill.KnowledgeDistillation (training_step)
   distill_SPKD.py         -> clskd.distill.SPKDDistillation
   config.py               -> clskd.config
+A whole step can be captured and replayed as one hipGraph (clskd.graph.StepGraph).
 All arithmetic runs in libclskd_hip.so (gfx950); there is no CPU fallback.
 """
 from . import config  # noqa: F401
@@ -26,4 +27,7 @@ def __getattr__(name):
     if name in ("MultiResolutionSTFTLoss", "SPKDLoss", "build_review_kd", "ReviewKD", "ABF"):
         from . import framework
         return getattr(framework, name)
+    if name == "StepGraph":
+        from .graph import StepGraph
+        return StepGraph
     raise AttributeError(name)

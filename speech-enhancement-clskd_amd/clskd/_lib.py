@@ -64,8 +64,8 @@ SIGNATURES = {
     "clskd_mask_e": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p]),
     "clskd_ola": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p]),
     "clskd_abf_fuse": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _i32, _p]),
-    "clskd_gram_partial": (_i32, [_p, _i32, _i32, _p, _i32, _p, _p]),
-    "clskd_spkd_finalize": (_i32, [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
+    "clskd_gram_partial": (_i32, [_p, _i32, _i32, _p, _p]),
+    "clskd_spkd_finalize": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
     "clskd_stft_mag_loss": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p]),
     "clskd_stft_loss_finalize": (_i32, [_p, _i64, _f32, _f32, _i32, _p, _p]),
     "clskd_sisnr_rows": (_i32, [_p, _p, _i32, _i32, _i64, _i64, _f32, _p, _p]),

@@ -213,7 +213,7 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
         d.stats = stats.data_ptr() + 8 * stats_offset
     else:
         d.stats = None
-    if KernelTimer.active:
+    if KernelTimer.active and not torch.cuda.is_current_stream_capturing():
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -353,7 +353,6 @@ def spkd_losses(pairs_views, B, batchmean=True, return_grams=False, chunk_elems=
     views = [v for pr in pairs_views for v in pr]
     dev = views[0].tensor.device
     jobs = (_lib.GramJob * len(views))()
-    slab_job = []
     first = 0
     for j, v in enumerate(views):
         chunk = max(1, chunk_elems // v.Cs)
@@ -362,12 +361,8 @@ def spkd_losses(pairs_views, B, batchmean=True, return_grams=False, chunk_elems=
         assert v.Cs % (8 if dt == _lib.BF16 else 4) == 0
         jobs[j] = _lib.GramJob(v.tensor.data_ptr() + v.tensor.element_size() * v.offset, v.sB, v.P,
                                v.Ctot, v.c0, v.Cs, chunk, first, ns, dt, 0)
-        slab_job += [j] * ns
         first += ns
-    jobs_t = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(dev, non_blocking=False)
-    slab_t = torch.tensor(slab_job, dtype=torch.int32, device=dev)
-    pairs = torch.tensor([[2 * i, 2 * i + 1] for i in range(len(pairs_views))], dtype=torch.int32,
-                         device=dev)
+    pairs = (C.c_int32 * (2 * len(pairs_views)))(*range(2 * len(pairs_views)))
     slabs = torch.empty(first * 1024, dtype=torch.float32, device=dev)
     losses = out if out is not None else torch.empty(len(pairs_views), dtype=torch.float32, device=dev)
     assert losses.is_contiguous() and losses.numel() == len(pairs_views)
@@ -377,12 +372,10 @@ def spkd_losses(pairs_views, B, batchmean=True, return_grams=False, chunk_elems=
         gt = torch.empty_like(gs)
     L = lib()
     st = _stream()
-    check(L.clskd_gram_partial(ptr(jobs_t), len(views), first, ptr(slab_t), B, ptr(slabs), st),
-          "gram_partial")
-    check(L.clskd_spkd_finalize(ptr(jobs_t), ptr(pairs), len(pairs_views), B, int(batchmean),
+    # job / pair tables are host arrays passed as kernel arguments (no upload, capturable)
+    check(L.clskd_gram_partial(jobs, len(views), B, ptr(slabs), st), "gram_partial")
+    check(L.clskd_spkd_finalize(jobs, len(views), pairs, len(pairs_views), B, int(batchmean),
                                 ptr(slabs), ptr(gs), ptr(gt), ptr(losses), st), "spkd_finalize")
-    # keep the job tables alive until the kernels have consumed them
-    losses._clskd_keep = (jobs_t, slab_t, pairs, slabs)
     if return_grams:
         return losses, gs, gt
     return losses

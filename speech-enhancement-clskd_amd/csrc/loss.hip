@@ -11,35 +11,85 @@
 
 namespace clskd {
 
-typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ f32x4 load_row4(const clskd_gram_job& j, int b, int B, int64_t e,
-                                           int64_t p0, int64_t p1) {
-  // element e of this slab (p0-relative), 4-aligned, Cs % 4 == 0 (fp32) / % 8 == 0 (bf16)
+// Kernel-argument job tables: no device-side descriptor upload, so a step is graph-capturable
+// and the host never waits on a copy.
+struct GramJobsArg {
+  clskd_gram_job j[CLSKD_GRAM_MAX_JOBS];
+  int32_t n;      // jobs in this launch
+  int32_t slab0;  // absolute slab index of blockIdx.x == 0
+};
+
+struct SpkdPairsArg {
+  int32_t s_first[CLSKD_SPKD_MAX_PAIRS], s_n[CLSKD_SPKD_MAX_PAIRS];
+  int32_t t_first[CLSKD_SPKD_MAX_PAIRS], t_n[CLSKD_SPKD_MAX_PAIRS];
+  int32_t pair0;  // absolute pair index of blockIdx.x == 0
+};
+
+__device__ __forceinline__ f32x4 load_row4_f32(const clskd_gram_job& j, int b, int B, int64_t e,
+                                               int64_t p0, int64_t p1) {
+  // 4 fp32 elements at slab-relative element e (Cs % 4 == 0, e % 4 == 0)
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
   if (b < B) {
     const int64_t p = p0 + e / j.Cs;
     const int c = (int)(e % j.Cs);
-    if (p < p1) {
-      const int64_t off = (int64_t)b * j.sB + p * j.Ctot + j.c0 + c;
-      if (j.dtype == CLSKD_BF16) {
-        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-        const bf16x4 h = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(j.ptr) + off);
-        v = f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
-      } else {
-        v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(j.ptr) + off);
-      }
-    }
+    if (p < p1)
+      v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(j.ptr) +
+                                          (int64_t)b * j.sB + p * j.Ctot + j.c0 + c);
   }
   return v;
 }
 
+__device__ __forceinline__ bf16x8g load_row8_bf16(const clskd_gram_job& j, int b, int B, int64_t e,
+                                                  int64_t p0, int64_t p1) {
+  // 8 bf16 elements (one 16-B load) at slab-relative element e (Cs % 8 == 0, e % 8 == 0)
+  bf16x8g v = {};
+  if (b < B) {
+    const int64_t p = p0 + e / j.Cs;
+    const int c = (int)(e % j.Cs);
+    if (p < p1)
+      v = *reinterpret_cast<const bf16x8g*>(reinterpret_cast<const __bf16*>(j.ptr) +
+                                            (int64_t)b * j.sB + p * j.Ctot + j.c0 + c);
+  }
+  return v;
+}
+
+// Fixed-order reduction of the 4 waves' 16x16 accumulators into the 32x32 slab.
+// C layout (16x16 MFMA): col = l&15, row = 4*(l>>4)+i.
+__device__ __forceinline__ void gram_store_slab(float (*red)[3][256], const f32x4& acc00,
+                                                const f32x4& acc01, const f32x4& acc11,
+                                                float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    red[wave][0][lane * 4 + i] = acc00[i];
+    red[wave][1][lane * 4 + i] = acc01[i];
+    red[wave][2][lane * 4 + i] = acc11[i];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 1024; idx += 256) {
+    const int row = idx >> 5, col = idx & 31;
+    const int I = row >> 4, J = col >> 4;
+    // the lower-left block is the transpose of the upper-right one
+    const bool lower = (I == 1 && J == 0);
+    const int t = lower ? 1 : ((I == 0 && J == 0) ? 0 : (I == 0 ? 1 : 2));
+    const int rr = lower ? (col & 15) : (row & 15), cc = lower ? (row & 15) : (col & 15);
+    const int l = cc + 16 * (rr >> 2), i = rr & 3;
+    out[idx] = red[0][t][l * 4 + i] + red[1][t][l * 4 + i] + red[2][t][l * 4 + i] +
+               red[3][t][l * 4 + i];
+  }
+}
+
 template <int NB>  // row blocks of 16: B <= 16*NB
-__global__ __launch_bounds__(256) void gram_partial_kernel(const clskd_gram_job* __restrict__ jobs,
-                                                           const int32_t* __restrict__ slab_job,
-                                                           int B, float* __restrict__ slabs) {
-  const int slab = blockIdx.x;
-  const clskd_gram_job j = jobs[slab_job[slab]];
+__global__ __launch_bounds__(256) void gram_partial_kernel(const GramJobsArg jobs, int B,
+                                                           float* __restrict__ slabs) {
+  const int slab = jobs.slab0 + blockIdx.x;
+  // uniform scan of the (<= 32) kernel-argument jobs for the one owning this slab
+  int q = 0;
+  for (int k = 1; k < jobs.n; ++k)
+    if (slab >= jobs.j[k].first_slab) q = k;
+  const clskd_gram_job j = jobs.j[q];
   const int si = slab - j.first_slab;
   const int64_t p0 = (int64_t)si * j.chunk;
   const int64_t p1 = min(j.P, p0 + j.chunk);
@@ -49,71 +99,68 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const clskd_gram_job*
   const int r = lane & 15;
   const int g = lane >> 4;
   f32x4 acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
-  // each wave step covers 16 elements per row; 4 waves interleave; unroll 4 steps for MLP
-  constexpr int U = 4;
-  for (int64_t base = (int64_t)wave * 16; base < nel; base += 64 * U) {
-    f32x4 v0[U], v1[U];
+  if (j.dtype == CLSKD_BF16) {
+    // 16x16x32 bf16 MFMA: lane (r, g) holds row r, 8 consecutive k; A and B are the same
+    // register (G = Z Z^T), so one 16-B load feeds both operands.  64 B per row per load.
+    constexpr int U = 8;
+    for (int64_t base = (int64_t)wave * 32; base < nel; base += 128 * U) {
+      bf16x8g v0[U], v1[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t e = base + (int64_t)u * 64 + 4 * g;
-      const bool ok = e < nel;
-      v0[u] = ok ? load_row4(j, r, B, e, p0, p1) : f32x4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (NB == 2) v1[u] = ok ? load_row4(j, r + 16, B, e, p0, p1) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+      for (int u = 0; u < U; ++u) {
+        const int64_t e = base + (int64_t)u * 128 + 8 * g;
+        const bool ok = e < nel;
+        v0[u] = ok ? load_row8_bf16(j, r, B, e, p0, p1) : bf16x8g{};
+        if constexpr (NB == 2) v1[u] = ok ? load_row8_bf16(j, r + 16, B, e, p0, p1) : bf16x8g{};
+      }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        acc00 = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[u][q], v0[u][q], acc00, 0, 0, 0);
+      for (int u = 0; u < U; ++u) {
+        acc00 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v0[u], v0[u], acc00, 0, 0, 0);
         if constexpr (NB == 2) {
-          acc01 = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[u][q], v1[u][q], acc01, 0, 0, 0);
-          acc11 = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[u][q], v1[u][q], acc11, 0, 0, 0);
+          acc01 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v0[u], v1[u], acc01, 0, 0, 0);
+          acc11 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v1[u], v1[u], acc11, 0, 0, 0);
+        }
+      }
+    }
+  } else {
+    // fp32: 16x16x4 f32 MFMA, lane (r, g) holds row r, 4 consecutive elements per load
+    constexpr int U = 4;
+    for (int64_t base = (int64_t)wave * 16; base < nel; base += 64 * U) {
+      f32x4 v0[U], v1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t e = base + (int64_t)u * 64 + 4 * g;
+        const bool ok = e < nel;
+        v0[u] = ok ? load_row4_f32(j, r, B, e, p0, p1) : f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (NB == 2) v1[u] = ok ? load_row4_f32(j, r + 16, B, e, p0, p1) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          acc00 = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[u][qq], v0[u][qq], acc00, 0, 0, 0);
+          if constexpr (NB == 2) {
+            acc01 = __builtin_amdgcn_mfma_f32_16x16x4f32(v0[u][qq], v1[u][qq], acc01, 0, 0, 0);
+            acc11 = __builtin_amdgcn_mfma_f32_16x16x4f32(v1[u][qq], v1[u][qq], acc11, 0, 0, 0);
+          }
         }
       }
     }
   }
-  // reduce the 4 waves' accumulators in a fixed order; C layout: col = l&15, row = 4*(l>>4)+i
   __shared__ float red[4][3][256];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    red[wave][0][lane * 4 + i] = acc00[i];
-    red[wave][1][lane * 4 + i] = acc01[i];
-    red[wave][2][lane * 4 + i] = acc11[i];
-  }
-  __syncthreads();
-  float* out = slabs + (int64_t)slab * 1024;
-  for (int idx = threadIdx.x; idx < 1024; idx += 256) {
-    const int row = idx >> 5, col = idx & 31;
-    const int I = row >> 4, J = col >> 4;
-    float v = 0.f;
-    if (!(I == 1 && J == 0)) {
-      const int t = (I == 0 && J == 0) ? 0 : ((I == 0) ? 1 : 2);
-      const int rr = row & 15, cc = col & 15;
-      const int l = cc + 16 * (rr >> 2);
-      const int i = rr & 3;
-      v = red[0][t][l * 4 + i] + red[1][t][l * 4 + i] + red[2][t][l * 4 + i] + red[3][t][l * 4 + i];
-    } else {
-      // lower-left block = transpose of the upper-right block
-      const int rr = col & 15, cc = row & 15;  // element (row, col) = G01[col-?]: G10[r][c] = G01[c][r]
-      const int l = cc + 16 * (rr >> 2);
-      const int i = rr & 3;
-      v = red[0][1][l * 4 + i] + red[1][1][l * 4 + i] + red[2][1][l * 4 + i] + red[3][1][l * 4 + i];
-    }
-    out[idx] = v;
-  }
+  gram_store_slab(red, acc00, acc01, acc11, slabs + (int64_t)slab * 1024);
 }
 
 // One block per pair: Gs = sum of the student job's slabs, Gt likewise, L1-normalise rows,
 // loss = ||Gt - Gs||_F^2 (/ B^2).  256 threads; B <= 32.
-__global__ __launch_bounds__(256) void spkd_finalize_kernel(const clskd_gram_job* __restrict__ jobs,
-                                                            const int32_t* __restrict__ pairs, int B,
+__global__ __launch_bounds__(256) void spkd_finalize_kernel(const SpkdPairsArg pa, int B,
                                                             int batchmean,
                                                             const float* __restrict__ slabs,
                                                             float* grams_s, float* grams_t,
                                                             float* losses) {
-  const int pr = blockIdx.x;
-  const clskd_gram_job js = jobs[pairs[2 * pr]];
-  const clskd_gram_job jt = jobs[pairs[2 * pr + 1]];
+  const int lp = blockIdx.x;
+  const int pr = pa.pair0 + lp;
+  const int s_first = pa.s_first[lp], s_n = pa.s_n[lp];
+  const int t_first = pa.t_first[lp], t_n = pa.t_n[lp];
   __shared__ double Gs[32 * 32], Gt[32 * 32];
   __shared__ double rs[32], rt[32];
   __shared__ double red[256];
@@ -121,8 +168,8 @@ __global__ __launch_bounds__(256) void spkd_finalize_kernel(const clskd_gram_job
   for (int idx = tid; idx < B * B; idx += 256) {
     const int i = idx / B, k = idx % B;
     double s = 0.0, t = 0.0;
-    for (int q = 0; q < js.nslab; ++q) s += (double)slabs[(int64_t)(js.first_slab + q) * 1024 + i * 32 + k];
-    for (int q = 0; q < jt.nslab; ++q) t += (double)slabs[(int64_t)(jt.first_slab + q) * 1024 + i * 32 + k];
+    for (int q = 0; q < s_n; ++q) s += (double)slabs[(int64_t)(s_first + q) * 1024 + i * 32 + k];
+    for (int q = 0; q < t_n; ++q) t += (double)slabs[(int64_t)(t_first + q) * 1024 + i * 32 + k];
     Gs[idx] = s;
     Gt[idx] = t;
   }
@@ -273,31 +320,79 @@ __global__ void sum_f32_kernel(const float* a, int n, float scale, float* out) {
 
 using namespace clskd;
 
-extern "C" int clskd_gram_partial(const clskd_gram_job* jobs_dev, int32_t njobs, int32_t total_slabs,
-                                  const int32_t* slab_job_dev, int32_t B, float* slabs,
-                                  void* stream) {
-  CLSKD_CHECK_ARG(jobs_dev && slab_job_dev && slabs, "gram_partial: null pointer");
-  CLSKD_CHECK_SHAPE(B >= 1 && B <= 32, "gram_partial: batch %d must be in [1, 32]", B);
-  CLSKD_CHECK_SHAPE(njobs >= 1 && total_slabs >= 1, "gram_partial: empty job list");
-  hipStream_t st = as_stream(stream);
-  if (B <= 16)
-    hipLaunchKernelGGL(gram_partial_kernel<1>, dim3(total_slabs), dim3(256), 0, st, jobs_dev,
-                       slab_job_dev, B, slabs);
-  else
-    hipLaunchKernelGGL(gram_partial_kernel<2>, dim3(total_slabs), dim3(256), 0, st, jobs_dev,
-                       slab_job_dev, B, slabs);
-  CLSKD_LAUNCH_CHECK("gram_partial");
+static int validate_gram_jobs(const clskd_gram_job* jobs, int32_t njobs, int32_t B,
+                              int32_t* total) {
+  CLSKD_CHECK_ARG(jobs, "gram: null job array");
+  CLSKD_CHECK_SHAPE(B >= 1 && B <= 32, "gram: batch %d must be in [1, 32]", B);
+  CLSKD_CHECK_SHAPE(njobs >= 1, "gram: empty job list");
+  int32_t next = 0;
+  for (int k = 0; k < njobs; ++k) {
+    const clskd_gram_job& j = jobs[k];
+    CLSKD_CHECK_ARG(j.ptr, "gram: job %d has a null tensor", k);
+    CLSKD_CHECK_SHAPE(j.dtype == CLSKD_F32 || j.dtype == CLSKD_BF16, "gram: job %d dtype", k);
+    const int g = j.dtype == CLSKD_BF16 ? 8 : 4;
+    CLSKD_CHECK_SHAPE(j.Cs > 0 && j.Cs % g == 0 && j.c0 % g == 0 && j.Ctot % g == 0 &&
+                          j.sB % g == 0 && j.P > 0 && j.chunk > 0,
+                      "gram: job %d geometry (Cs %d, c0 %d, Ctot %d) needs multiples of %d", k,
+                      j.Cs, j.c0, j.Ctot, g);
+    CLSKD_CHECK_SHAPE(j.first_slab == next && j.nslab == (int32_t)((j.P + j.chunk - 1) / j.chunk),
+                      "gram: job %d slab range [%d, +%d) is not contiguous", k, j.first_slab,
+                      j.nslab);
+    next += j.nslab;
+  }
+  *total = next;
   return CLSKD_OK;
 }
 
-extern "C" int clskd_spkd_finalize(const clskd_gram_job* jobs_dev, const int32_t* pairs_dev,
+extern "C" int clskd_gram_partial(const clskd_gram_job* jobs, int32_t njobs, int32_t B,
+                                  float* slabs, void* stream) {
+  int32_t total = 0;
+  const int rc = validate_gram_jobs(jobs, njobs, B, &total);
+  if (rc != CLSKD_OK) return rc;
+  CLSKD_CHECK_ARG(slabs, "gram_partial: null slab buffer");
+  hipStream_t st = as_stream(stream);
+  for (int k0 = 0; k0 < njobs; k0 += CLSKD_GRAM_MAX_JOBS) {
+    GramJobsArg a;
+    a.n = njobs - k0 < CLSKD_GRAM_MAX_JOBS ? njobs - k0 : CLSKD_GRAM_MAX_JOBS;
+    for (int k = 0; k < a.n; ++k) a.j[k] = jobs[k0 + k];
+    for (int k = a.n; k < CLSKD_GRAM_MAX_JOBS; ++k) a.j[k] = jobs[k0];
+    a.slab0 = a.j[0].first_slab;
+    const int nb = a.j[a.n - 1].first_slab + a.j[a.n - 1].nslab - a.slab0;
+    if (B <= 16)
+      hipLaunchKernelGGL(gram_partial_kernel<1>, dim3(nb), dim3(256), 0, st, a, B, slabs);
+    else
+      hipLaunchKernelGGL(gram_partial_kernel<2>, dim3(nb), dim3(256), 0, st, a, B, slabs);
+    CLSKD_LAUNCH_CHECK("gram_partial");
+  }
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_spkd_finalize(const clskd_gram_job* jobs, int32_t njobs, const int32_t* pairs,
                                    int32_t npairs, int32_t B, int32_t batchmean, const float* slabs,
                                    float* grams_s, float* grams_t, float* losses, void* stream) {
-  CLSKD_CHECK_ARG(jobs_dev && pairs_dev && slabs && losses, "spkd_finalize: null pointer");
-  CLSKD_CHECK_SHAPE(B >= 1 && B <= 32 && npairs >= 1, "spkd_finalize: shape");
-  hipLaunchKernelGGL(spkd_finalize_kernel, dim3(npairs), dim3(256), 0, as_stream(stream), jobs_dev,
-                     pairs_dev, B, batchmean, slabs, grams_s, grams_t, losses);
-  CLSKD_LAUNCH_CHECK("spkd_finalize");
+  int32_t total = 0;
+  const int rc = validate_gram_jobs(jobs, njobs, B, &total);
+  if (rc != CLSKD_OK) return rc;
+  CLSKD_CHECK_ARG(pairs && slabs && losses, "spkd_finalize: null pointer");
+  CLSKD_CHECK_SHAPE(npairs >= 1, "spkd_finalize: no pairs");
+  hipStream_t st = as_stream(stream);
+  for (int p0 = 0; p0 < npairs; p0 += CLSKD_SPKD_MAX_PAIRS) {
+    SpkdPairsArg a;
+    const int n = npairs - p0 < CLSKD_SPKD_MAX_PAIRS ? npairs - p0 : CLSKD_SPKD_MAX_PAIRS;
+    for (int k = 0; k < CLSKD_SPKD_MAX_PAIRS; ++k) {
+      const int s = k < n ? pairs[2 * (p0 + k)] : 0, t = k < n ? pairs[2 * (p0 + k) + 1] : 0;
+      CLSKD_CHECK_SHAPE(s >= 0 && s < njobs && t >= 0 && t < njobs,
+                        "spkd_finalize: pair %d names a job outside [0, %d)", p0 + k, njobs);
+      a.s_first[k] = jobs[s].first_slab;
+      a.s_n[k] = jobs[s].nslab;
+      a.t_first[k] = jobs[t].first_slab;
+      a.t_n[k] = jobs[t].nslab;
+    }
+    a.pair0 = p0;
+    hipLaunchKernelGGL(spkd_finalize_kernel, dim3(n), dim3(256), 0, st, a, B, batchmean, slabs,
+                       grams_s, grams_t, losses);
+    CLSKD_LAUNCH_CHECK("spkd_finalize");
+  }
   return CLSKD_OK;
 }
 

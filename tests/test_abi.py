@@ -84,3 +84,23 @@ def test_synthetic_data_recipe():
     a2, _ = synthetic_pairs(2, 16000, seed=3)
     assert a.shape == (2, 16000) and np.array_equal(a, a2)
     assert np.abs(a).max() <= 1.0 and np.abs(b).max() < 1.0
+
+
+def test_gram_job_validation_without_gpu():
+    """clskd_gram_partial / clskd_spkd_finalize take HOST job arrays (kernel arguments) and
+    validate them before any launch: bad geometry, non-contiguous slab ranges and pair indices
+    are reported, not executed."""
+    lib = _lib.load(require_gpu=False)
+    J = _lib.GramJob
+    fake = 1 << 20  # never dereferenced: validation fails first
+    good = J(fake, 64, 100, 8, 0, 8, 10, 0, 10, _lib.F32, 0)
+    bad_gap = (J * 2)(good, J(fake, 64, 100, 8, 0, 8, 10, 11, 10, _lib.F32, 0))
+    assert lib.clskd_gram_partial(bad_gap, 2, 4, fake, None) == -1
+    assert b"not contiguous" in lib.clskd_last_error()
+    bad_cs = (J * 1)(J(fake, 64, 100, 6, 0, 6, 10, 0, 10, _lib.F32, 0))
+    assert lib.clskd_gram_partial(bad_cs, 1, 4, fake, None) == -1
+    assert lib.clskd_gram_partial((J * 1)(good), 1, 33, fake, None) == -1  # B > 32
+    pairs = (ctypes.c_int32 * 2)(0, 5)
+    assert lib.clskd_spkd_finalize((J * 1)(good), 1, pairs, 1, 4, 1, fake, None, None, fake,
+                                   None) == -1
+    assert b"outside" in lib.clskd_last_error()

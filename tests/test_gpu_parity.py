@@ -317,3 +317,56 @@ def test_clskd_step_mixed_precision():
           " ".join(f"{v:.1e}" for v in rel), "total", out["loss"].item(), ref["loss"].item())
     assert rel.max() <= 2e-2, rel
     assert abs(out["loss"].item() - ref["loss"].item()) <= 2e-3 * ref["loss"].item()
+
+
+def test_step_graph_matches_eager():
+    """clskd.graph.StepGraph (hipGraph capture of the whole step, two streams) replays bitwise
+    what the eager step computes: loss, SPKD terms, student waveform and BN running statistics,
+    over two different batches; a changed student parameter triggers a re-capture."""
+    from clskd.data import synthetic_pairs
+    from clskd.graph import StepGraph
+    batches = []
+    for seed in (11, 12, 13):
+        n, c = synthetic_pairs(4, 32000, seed=seed)
+        batches.append((torch.from_numpy(n).to(DEV), torch.from_numpy(c).to(DEV)))
+    kd_e, kd_g = _kd().set_precision("mixed"), _kd().set_precision("mixed")
+    ref = []
+    for X, y in batches[:2]:
+        o = kd_e.training_step((X, y), 0, return_parts=True)
+        ref.append((o["loss"].item(), o["spkd"].clone(), o["student_wav"].clone()))
+    g = StepGraph(kd_g, *batches[0])
+    for (X, y), (l, sp, wav) in zip(batches[:2], ref):
+        assert g(X, y).item() == l
+        assert torch.equal(g.out["spkd"], sp)
+        assert torch.equal(g.out["student_wav"], wav)
+    for (k, a), b in zip(kd_e.state_dict().items(), kd_g.state_dict().values()):
+        assert torch.equal(a, b), k
+    with torch.no_grad():
+        for kd in (kd_e, kd_g):
+            kd.student.encoder[0][0].real_conv.weight.mul_(1.01)
+    X, y = batches[2]
+    l3 = kd_e.training_step((X, y), 0).item()
+    assert g(X, y).item() == l3 and g.captures == 2
+
+
+def test_step_graph_redraws_abf_each_replay():
+    """abf_reinit='step': the ABF re-initialisation (kaiming_uniform, framework.py:194-195) is
+    recorded into the graph and re-drawn on every replay (graph-safe Philox offsets): SPKD
+    ReviewKD terms change between replays of the same batch while the student waveform and the
+    clstm terms (no ABF on their path) do not."""
+    from clskd.data import synthetic_pairs
+    from clskd.distill import KnowledgeDistillation
+    from clskd.graph import StepGraph
+    n, c = synthetic_pairs(4, 32000, seed=21)
+    X, y = torch.from_numpy(n).to(DEV), torch.from_numpy(c).to(DEV)
+    kd = KnowledgeDistillation(_models("teacher").train(), _models("student").train(),
+                               abf_reinit="step", precision="mixed").to(DEV)
+    g = StepGraph(kd, X, y)
+    outs = []
+    for _ in range(2):
+        g(X, y)
+        outs.append({k: g.out[k].clone() for k in ("spkd", "student_wav", "loss")})
+    assert torch.isfinite(outs[0]["loss"]) and torch.isfinite(outs[1]["loss"])
+    assert torch.equal(outs[0]["student_wav"], outs[1]["student_wav"])
+    assert torch.equal(outs[0]["spkd"][12:], outs[1]["spkd"][12:])  # clstm real / imag
+    assert not torch.equal(outs[0]["spkd"][:12], outs[1]["spkd"][:12])
