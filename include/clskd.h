@@ -95,9 +95,25 @@ typedef struct {
   double* stats;     /* optional fused BatchNorm statistics: per M-block (128 output rows) fp64
                         partials stats[blockIdx.x][N][2] = {sum, sumsq} of the biased outputs,
                         consumed by clskd_bn_finalize (nblk = number of M-blocks) */
+  int32_t kvec;      /* channel-run granule of the K table: every aligned group of kvec k's is
+                        kvec contiguous channels of one tap and segment (1, 2, 4 or 8; 0 = 8 for
+                        bf16 segments, 4 if vec4, else 1).  Sets the direct-conv load width. */
+  int32_t wlayout;   /* CLSKD_WLAYOUT_NK: weight [N][K] -> implicit-GEMM MFMA engines.
+                        CLSKD_WLAYOUT_DIRECT: weight k-major [K][NP] fp32, or [K/2][NP][2] bf16
+                        (pairs of consecutive k), NP = clskd_conv_direct_np(N), zero columns for
+                        n >= N -> direct-convolution kernel (narrow GEMMs: N <= 16, or K <= 64
+                        with N <= 64; see clskd_conv_direct_ok). */
 } clskd_conv_desc;
 
+#define CLSKD_WLAYOUT_NK 0
+#define CLSKD_WLAYOUT_DIRECT 1
+
 int clskd_conv2d_fwd(const clskd_conv_desc* d, void* stream);
+/* Direct-path helpers: padded output width NP of the direct layout, and whether an (N, K)
+ * GEMM is served by the direct kernel (returns 1) — hosts pack CLSKD_WLAYOUT_DIRECT weights
+ * exactly when this is 1. */
+int clskd_conv_direct_np(int32_t N);
+int clskd_conv_direct_ok(int32_t N, int32_t K);
 
 /* ------------------------------------------------------------------------------------------
  * BatchNorm2d (train or eval) + optional PReLU over a BFTC tensor of `rows` x C.
@@ -141,6 +157,9 @@ int clskd_complex_combine(const float* rr, const float* ii, const float* ir, con
  * STFT helpers.
  * clskd_frame_pad: xp[b][j] = x[b][j - pad] with zero (mode 0) or reflect (mode 1) padding,
  *                  j in [0, Lp); x is [B][L] with row stride ldx.
+ * clskd_spec_bftc: encoder input of DCCRN.py:165-170 (real = spec[:, 1:257], imag =
+ *                  spec[:, 258:514] stacked as channels) in BFTC: out[b][f][t][0] =
+ *                  spec[b][t][re0+f], out[b][f][t][1] = spec[b][t][im0+f], f < F.
  * clskd_mask_e:    DCCRN masking_mode 'E' (DCCRN.py:207-226) from spec [B][T][ldspec] (real
  *                  bins 0..256 at 0.., imag at 257..) and the last decoder output
  *                  mask[B][256][Tm][2] read at time t+1; writes est [B][T][ldest] (real at 0..,
@@ -151,6 +170,8 @@ int clskd_complex_combine(const float* rr, const float* ii, const float* ir, con
  * -------------------------------------------------------------------------------------- */
 int clskd_frame_pad(const float* x, int64_t ldx, int32_t B, int32_t L, int32_t pad, int32_t Lp,
                     int32_t mode, float* xp, void* stream);
+int clskd_spec_bftc(const float* spec, int32_t B, int32_t T, int32_t ld, int32_t re0, int32_t im0,
+                    int32_t F, float* out, void* stream);
 int clskd_mask_e(const float* spec, int32_t ldspec, const float* mask, int32_t Tm, int32_t B,
                  int32_t T, float* est, int32_t ldest, float* mask_r, float* mask_i,
                  void* stream);

@@ -13,6 +13,7 @@ LIB_PATH = os.path.join(_HERE, "libclskd_hip.so")
 
 MAX_SEGS = 4
 F32, BF16 = 0, 1
+WLAYOUT_NK, WLAYOUT_DIRECT = 0, 1
 
 
 class Seg(C.Structure):
@@ -32,7 +33,8 @@ class ConvDesc(C.Structure):
                 ("bias", C.c_void_p), ("out", C.c_void_p), ("oB", C.c_int64), ("oF", C.c_int64),
                 ("oT", C.c_int64), ("oNhi", C.c_int64), ("oNlo", C.c_int64), ("nlo", C.c_int32),
                 ("of_mul", C.c_int32), ("of_add", C.c_int32), ("compute", C.c_int32),
-                ("in_dtype", C.c_int32), ("out_dtype", C.c_int32), ("stats", C.c_void_p)]
+                ("in_dtype", C.c_int32), ("out_dtype", C.c_int32), ("stats", C.c_void_p),
+                ("kvec", C.c_int32), ("wlayout", C.c_int32)]
 
 
 class GramJob(C.Structure):
@@ -51,6 +53,8 @@ SIGNATURES = {
     "clskd_last_error": (C.c_char_p, []),
     "clskd_version": (_i32, []),
     "clskd_conv2d_fwd": (_i32, [C.POINTER(ConvDesc), _p]),
+    "clskd_conv_direct_np": (_i32, [_i32]),
+    "clskd_conv_direct_ok": (_i32, [_i32, _i32]),
     "clskd_bn_partial_blocks": (_i32, [_i64, _i32]),
     "clskd_bn_stats_partial": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p]),
     "clskd_bn_finalize": (_i32, [_p, _i32, _i64, _i32, _p, _p, _f32, _p, _p, _f32, _i32, _p, _p,
@@ -61,6 +65,7 @@ SIGNATURES = {
                                     _i64, _i64, _p]),
     "clskd_complex_combine": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p]),
     "clskd_frame_pad": (_i32, [_p, _i64, _i32, _i32, _i32, _i32, _i32, _p, _p]),
+    "clskd_spec_bftc": (_i32, [_p, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p]),
     "clskd_mask_e": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p]),
     "clskd_ola": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p]),
     "clskd_abf_fuse": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _i32, _p]),

@@ -126,14 +126,18 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     main = torch.cuda.current_stream(dev)
     side = _side_stream(dev)
     side.wait_stream(main)  # spec ready; previous step's work on main is done before reuse
+    buf = torch.empty(16, dtype=torch.float32, device=dev)  # [sc, mag, spkd x 14]
     with torch.cuda.stream(side):
+        # everything that depends on the student alone runs beside the teacher forward:
+        # student forward, ReviewKD fusions on its taps (distill.py:92-96; tap contract
+        # SURVEY.md §8 a11) and the MRSTFT base loss on (student wav, clean) (distill.py:100-101)
         sf = student.run(X, train=student.training, bn_updates=2 if student.training else 0,
                          spec=s_spec, want_masks=False)
+        s_enc = review_encoder.forward_bftc(sf["enc"])
+        s_dec = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5])
+        stft_loss(sf["out_wav"], y, out2=buf[0:2])
     tf = teacher.run(X, train=teacher.training, bn_updates=1, spec=spec, want_masks=False)
     main.wait_stream(side)
-    # ReviewKD on the student taps (distill.py:92-96); tap contract SURVEY.md §8 a11
-    s_enc = review_encoder.forward_bftc(sf["enc"])
-    s_dec = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5])
     t_dec = [tf["dec_in"]] + tf["dec"][:5]
     pairs = [(_gram_bftc(a), _gram_bftc(b)) for a, b in zip(s_enc, tf["enc"])]
     pairs += [(_gram_bftc(a), _gram_bftc(b)) for a, b in zip(s_dec, t_dec)]
@@ -141,10 +145,8 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     Cht = tf["dec_in"].shape[-1] // 2
     pairs += [(_gram_bftc(sf["dec_in"], 0, Chs), _gram_bftc(tf["dec_in"], 0, Cht)),
               (_gram_bftc(sf["dec_in"], Chs, Chs), _gram_bftc(tf["dec_in"], Cht, Cht))]
-    buf = torch.empty(2 + len(pairs), dtype=torch.float32, device=dev)  # [sc, mag, spkd...]
+    assert len(pairs) == 14
     ops.spkd_losses(pairs, B, batchmean=True, out=buf[2:])
-    # MRSTFT base loss on (student wav, clean) (distill.py:100-101) -> buf[0:2]
-    stft_loss(sf["out_wav"], y, out2=buf[0:2])
     total = torch.empty((), dtype=torch.float32, device=dev)
     ops.sum_f32(buf[1:], total)
     return dict(loss=total, base=buf[1], sc=buf[0], spkd=buf[2:], enc=buf[2:8], dec=buf[8:14],

@@ -367,8 +367,10 @@ class DCCRN(nn.Module):
             Co = kn[i + 1]
             Fo = F // 2
             if i == 0:
-                segs = [Seg(spec, 1, SegGeom(1, T * 514, 1, 514, 256, T)),
-                        Seg(spec, 258, SegGeom(1, T * 514, 1, 514, 256, T))]
+                # real = spec[:, 1:257], imag = spec[:, 258:514] (DCCRN.py:165-170) as the two
+                # channels of a BFTC input: same K order (tap, re, im) as the packed weights
+                spec_b = ops.spec_bftc(spec, 1, 258, 256, torch.empty(B, 256, T, 2, **f32))
+                segs = [seg_bftc(spec_b)]
             else:
                 segs = [seg_bftc(enc[-1])]
             wp, bias = self._enc_w(i, self._cmp(segs, 10 * kn[i]))

@@ -4,6 +4,8 @@ torch is plumbing here (device memory, streams); every arithmetic op runs in a H
 the library.  Tensors are BFTC ([batch][freq][time][channel]) unless noted.
 """
 import ctypes as C
+import os
+from collections import OrderedDict
 from dataclasses import dataclass
 from functools import lru_cache
 
@@ -15,6 +17,7 @@ from ._lib import check, ptr
 
 BK = 16
 ZERO_DF = -32768
+_NO_DIRECT = os.environ.get("CLSKD_NO_DIRECT", "") == "1"  # host switch: MFMA engines only
 
 
 def lib():
@@ -32,11 +35,17 @@ class KernelTimer:
         cls.active, cls.records = True, []
 
     @classmethod
+    def per_launch(cls):
+        """Per-launch records (name, (M, N, K, in_dtype), us, TFLOP/s) — call after a sync."""
+        return [(n, shp, e0.elapsed_time(e1) * 1e3, fl / (e0.elapsed_time(e1) * 1e-3) / 1e12)
+                for n, fl, e0, e1, shp in cls.records]
+
+    @classmethod
     def stop(cls):
         cls.active = False
         torch.cuda.synchronize()
         out = {}
-        for name, flops, e0, e1 in cls.records:
+        for name, flops, e0, e1, _shape in cls.records:
             ms = e0.elapsed_time(e1)
             agg = out.setdefault(name, [0, 0.0, 0.0])
             agg[0] += 1
@@ -46,7 +55,52 @@ class KernelTimer:
         return out  # name -> [launches, total_ms, total_flops]
 
 
-def conv_kernel_name(N, vec4, bf16=False):
+@lru_cache(maxsize=4096)
+def _direct_policy(N, K):
+    return bool(_lib.load(require_gpu=False).clskd_conv_direct_ok(N, K))
+
+
+def direct_ok(N, K):
+    """Whether an (N, K) GEMM runs on the direct-convolution kernel (the library's policy,
+    clskd_conv_direct_ok; CLSKD_NO_DIRECT=1 routes everything to the MFMA engines)."""
+    return not _NO_DIRECT and _direct_policy(N, K)
+
+
+def direct_np(N):
+    return int(_lib.load(require_gpu=False).clskd_conv_direct_np(N))
+
+
+_DIRECT_W = OrderedDict()
+
+
+def direct_weight(wpacked):
+    """[N][Kp] packed weight -> the direct kernel's k-major layout (CLSKD_WLAYOUT_DIRECT):
+    fp32 [Kp][NP]; bf16 [Kp/2][NP][2].  Cached per packed tensor (pointer + version; the cache
+    holds the source alive so a pointer is never reused while its entry exists)."""
+    key = (wpacked.data_ptr(), wpacked._version, tuple(wpacked.shape), wpacked.dtype)
+    capturing = torch.cuda.is_current_stream_capturing()
+    ent = None if capturing else _DIRECT_W.get(key)
+    if ent is not None:
+        _DIRECT_W.move_to_end(key)
+        return ent[1]
+    N, Kp = wpacked.shape
+    NP = direct_np(N)
+    if wpacked.dtype == torch.bfloat16:
+        wd = wpacked.new_zeros(Kp // 2, NP, 2)
+        wd[:, :N, :] = wpacked.view(N, Kp // 2, 2).permute(1, 0, 2)
+    else:
+        wd = wpacked.new_zeros(Kp, NP)
+        wd[:, :N] = wpacked.t()
+    if not capturing:
+        _DIRECT_W[key] = (wpacked, wd)
+        while len(_DIRECT_W) > 512:
+            _DIRECT_W.popitem(last=False)
+    return wd
+
+
+def conv_kernel_name(N, vec4, bf16=False, K=None):
+    if K is not None and direct_ok(N, K):
+        return f"conv_direct<{'bf16' if bf16 else 'f32'}>"
     bn = 32 if N <= 32 else (64 if N <= 64 else 128)
     if bf16:
         return f"conv_igemm_bf16<{bn}>"
@@ -186,6 +240,16 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
     for s in segs:
         if seg_addr(s) % 16 != 0:
             vec4 = False
+    # channel-run granule of the K table (direct-conv load width): 8 bf16 / 4 / 2 / 1 fp32
+    if bf16:
+        kvec = 8
+    elif vec4:
+        kvec = 4
+    elif all(g.C % 2 == 0 and g.sB % 2 == 0 and g.sF % 2 == 0 and g.sT % 2 == 0 for g in geoms) \
+            and all(seg_addr(s) % 8 == 0 for s in segs):
+        kvec = 2
+    else:
+        kvec = 1
     if bf16 and not all(g.C % 8 == 0 and g.sB % 8 == 0 and g.sF % 8 == 0 and g.sT % 8 == 0
                         for g in geoms):
         raise RuntimeError("bf16 conv segments need channel runs of 8 and strides % 8")
@@ -199,7 +263,12 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
     for i in range(len(segs), _lib.MAX_SEGS):
         d.seg[i] = d.seg[0]
     d.ktab, d.kseg, d.vec4 = kt.data_ptr(), ks.data_ptr(), int(vec4)
-    d.weight = wpacked.data_ptr()
+    if direct_ok(N, Kp):
+        wd = direct_weight(wpacked)
+        d.weight, d.wlayout = wd.data_ptr(), _lib.WLAYOUT_DIRECT
+    else:
+        wd = None
+        d.weight, d.wlayout = wpacked.data_ptr(), _lib.WLAYOUT_NK
     d.bias = bias.data_ptr() if bias is not None else None
     d.out = out.data_ptr() + out.element_size() * out_offset
     d.oB, d.oF, d.oT, d.oNhi, d.oNlo = omap.oB, omap.oF, omap.oT, omap.oNhi, omap.oNlo
@@ -213,13 +282,15 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
         d.stats = stats.data_ptr() + 8 * stats_offset
     else:
         d.stats = None
+    d.kvec = kvec
     if KernelTimer.active and not torch.cuda.is_current_stream_capturing():
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
         check(lib().clskd_conv2d_fwd(C.byref(d), _stream()), "conv2d")
         e1.record()
-        KernelTimer.records.append((conv_kernel_name(N, vec4, bf16), 2.0 * B * Fo * To * N * K, e0, e1))
+        KernelTimer.records.append((conv_kernel_name(N, vec4, bf16, Kp), 2.0 * B * Fo * To * N * K, e0, e1,
+                                    (B * Fo * To, N, K, "bf16" if bf16 else "f32")))
     else:
         check(lib().clskd_conv2d_fwd(C.byref(d), _stream()), "conv2d")
     return out
@@ -283,6 +354,13 @@ def frame_pad(x, pad, Lp, mode, out):
     B, L = x.shape
     check(lib().clskd_frame_pad(ptr(x), x.stride(0), B, L, pad, Lp, mode, ptr(out), _stream()),
           "frame_pad")
+    return out
+
+
+def spec_bftc(spec, re0, im0, F, out):
+    """Frame-major spectrum [B][T][ld] -> BFTC [B][F][T][2] (re at re0+f, im at im0+f)."""
+    B, T, ld = spec.shape
+    check(lib().clskd_spec_bftc(ptr(spec), B, T, ld, re0, im0, F, ptr(out), _stream()), "spec_bftc")
     return out
 
 

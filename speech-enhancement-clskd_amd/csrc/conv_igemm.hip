@@ -254,6 +254,8 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
 
 int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st);
 
+int launch_conv_direct(const clskd_conv_desc& d, hipStream_t st);
+
 }  // namespace clskd
 
 using namespace clskd;
@@ -291,6 +293,16 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
   CLSKD_CHECK_SHAPE(M < (int64_t)INT32_MAX * 64, "conv2d: too many rows");
   hipStream_t st = as_stream(stream);
+  CLSKD_CHECK_SHAPE(d.kvec == 0 || d.kvec == 1 || d.kvec == 2 || d.kvec == 4 || d.kvec == 8,
+                    "conv2d: kvec=%d", d.kvec);
+  CLSKD_CHECK_ARG(d.wlayout == CLSKD_WLAYOUT_NK || d.wlayout == CLSKD_WLAYOUT_DIRECT,
+                  "conv2d: wlayout=%d", d.wlayout);
+  if (d.wlayout == CLSKD_WLAYOUT_DIRECT) {
+    const int rc = launch_conv_direct(d, st);
+    if (rc != CLSKD_OK) return rc;
+    CLSKD_LAUNCH_CHECK("conv2d_direct");
+    return CLSKD_OK;
+  }
   if (d.compute == CLSKD_BF16) {
     const int rc = launch_conv_bf16(d, st);
     if (rc != CLSKD_OK) return rc;

@@ -403,6 +403,32 @@ inline unsigned grid_for(int64_t n, int block = 256, int64_t cap = 8192) {
   return (unsigned)g;
 }
 
+
+// Frame-major spectrum -> BFTC encoder input: out[b][f][t][0|1] = spec[b][t][re0|im0 + f].
+// 64 frames x 32 bins per block through LDS: reads are 128-B bin runs of a frame, writes are
+// 512-B (64 frames x re/im) runs of a bin, both coalesced.
+__global__ __launch_bounds__(256) void spec_bftc_kernel(const float* __restrict__ spec, int T,
+                                                        int ld, int re0, int im0, int F,
+                                                        float* __restrict__ out) {
+  __shared__ float tile[2][64][33];
+  const int b = blockIdx.z, f0 = blockIdx.y * 32, t0 = blockIdx.x * 64;
+  const float* sp = spec + (int64_t)b * T * ld;
+  for (int i = threadIdx.x; i < 64 * 32; i += 256) {
+    const int tt = i >> 5, ff = i & 31;
+    const int t = t0 + tt, f = f0 + ff;
+    const bool ok = t < T && f < F;
+    tile[0][tt][ff] = ok ? sp[(int64_t)t * ld + re0 + f] : 0.f;
+    tile[1][tt][ff] = ok ? sp[(int64_t)t * ld + im0 + f] : 0.f;
+  }
+  __syncthreads();
+  float* op = out + (int64_t)b * F * T * 2;
+  for (int i = threadIdx.x; i < 32 * 128; i += 256) {
+    const int ff = i >> 7, r = i & 127, tt = r >> 1, c = r & 1;
+    const int t = t0 + tt, f = f0 + ff;
+    if (t < T && f < F) op[((int64_t)f * T + t) * 2 + c] = tile[c][tt][ff];
+  }
+}
+
 }  // namespace clskd
 
 using namespace clskd;
@@ -488,6 +514,18 @@ extern "C" int clskd_frame_pad(const float* x, int64_t ldx, int32_t B, int32_t L
   hipLaunchKernelGGL(frame_pad_kernel, dim3(grid_for((int64_t)B * Lp)), dim3(256), 0,
                      as_stream(stream), x, ldx, B, L, pad, Lp, mode, xp);
   CLSKD_LAUNCH_CHECK("frame_pad");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_spec_bftc(const float* spec, int32_t B, int32_t T, int32_t ld, int32_t re0,
+                               int32_t im0, int32_t F, float* out, void* stream) {
+  CLSKD_CHECK_ARG(spec && out, "spec_bftc: null pointer");
+  CLSKD_CHECK_SHAPE(B > 0 && T > 0 && F > 0 && re0 >= 0 && im0 >= 0 && re0 + F <= ld &&
+                        im0 + F <= ld,
+                    "spec_bftc: bins [%d,+%d) / [%d,+%d) outside a row of %d", re0, F, im0, F, ld);
+  hipLaunchKernelGGL(spec_bftc_kernel, dim3((unsigned)cdiv(T, 64), (unsigned)cdiv(F, 32), B),
+                     dim3(256), 0, as_stream(stream), spec, T, ld, re0, im0, F, out);
+  CLSKD_LAUNCH_CHECK("spec_bftc");
   return CLSKD_OK;
 }
 

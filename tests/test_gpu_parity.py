@@ -78,6 +78,56 @@ def test_conv_engine_against_torch():
     np.testing.assert_allclose(_np(out3.permute(0, 3, 1, 2)), ref3.numpy(), rtol=1e-5, atol=1e-5)
 
 
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("C1,C2,N", [(2, 0, 8), (2, 0, 16), (8, 8, 2), (16, 16, 2), (6, 0, 4),
+                                     (6, 2, 3), (3, 0, 1), (1, 0, 16)])
+def test_conv_direct_against_torch_and_engine(dt, C1, C2, N):
+    """Direct-convolution kernel (narrow N / short K): 2-segment 5x2 stride-(2,1) conv with fused
+    BN statistics against torch (fp64 on the same bf16-rounded operands for bf16) and against the
+    MFMA engines on the same descriptor (CLSKD_WLAYOUT_NK).  Tolerance: 1e-5 relative (fp32
+    accumulation orders differ)."""
+    from clskd import ops
+    if dt == "bf16" and (C1 % 8 or C2 % 8):
+        pytest.skip("bf16 segments need channel runs of 8")
+    g = torch.Generator().manual_seed(C1 * 100 + C2 * 10 + N)
+    B, F, T = 3, 33, 29
+    tdt = torch.bfloat16 if dt == "bf16" else torch.float32
+    segs_h = [torch.randn(B, F, T, C1, generator=g).to(tdt)]
+    if C2:
+        segs_h.append(torch.randn(B, F, T, C2, generator=g).to(tdt))
+    Cin = C1 + C2
+    w = (torch.randn(N, Cin, 5, 2, generator=g) * 0.2)
+    bias = torch.randn(N, generator=g)
+    taps = [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)]
+    Fo = (F + 4 - 5) // 2 + 1
+    To = T
+    wk = w.permute(0, 2, 3, 1).reshape(N, 10, Cin)
+    wp = ops.pack_weight(wk.to(DEV), 10 * Cin, "bf16" if dt == "bf16" else "fp32")
+    wq = wp[:, :10 * Cin].float().cpu().reshape(N, 5, 2, Cin).permute(0, 3, 1, 2).double()
+    xin = torch.cat([x.double() for x in segs_h], 3).permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv2d(torch.nn.functional.pad(xin, (1, 0, 2, 2)), wq, bias.double(),
+                                     stride=(2, 1))[..., :To]
+    segs = [ops.seg_bftc(x.to(DEV)) for x in segs_h]
+    res = {}
+    for route in ("direct", "engine"):
+        ops._NO_DIRECT = route == "engine"
+        try:
+            assert ops.direct_ok(N, wp.shape[1]) == (route == "direct")
+            out = torch.empty(B, Fo, To, N, device=DEV, dtype=torch.float32)
+            nblk = ops.conv_mblocks(B, Fo, To)
+            st = torch.empty(nblk * N * 2, device=DEV, dtype=torch.float64)
+            ops.conv(segs, taps, B, Fo, To, N, wp, bias.to(DEV), out, ops.OutMap(Fo * To * N, To * N, N),
+                     stride_f=2, stats=st)
+            res[route] = (out.permute(0, 3, 1, 2).double().cpu(), st.view(nblk, N, 2).sum(0).cpu())
+        finally:
+            ops._NO_DIRECT = False
+    for route, (o, st) in res.items():
+        np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=1e-5, atol=1e-5, err_msg=route)
+        np.testing.assert_allclose(st[:, 0].numpy(), ref.sum((0, 2, 3)).numpy(), rtol=1e-5, atol=1e-3)
+        np.testing.assert_allclose(st[:, 1].numpy(), (ref ** 2).sum((0, 2, 3)).numpy(), rtol=1e-5)
+    np.testing.assert_allclose(res["direct"][0].numpy(), res["engine"][0].numpy(), rtol=1e-5, atol=1e-5)
+
 def test_stft_istft_golden():
     st = golden("stft.npz")
     m = _models("student")
