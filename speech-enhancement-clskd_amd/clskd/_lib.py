@@ -57,6 +57,7 @@ SIGNATURES = {
     "clskd_conv_direct_ok": (_i32, [_i32, _i32]),
     "clskd_bn_partial_blocks": (_i32, [_i64, _i32]),
     "clskd_bn_stats_partial": (_i32, [_p, _i64, _i32, _p, _i32, _i32, _p]),
+    "clskd_bn_compact": (_i32, [_p, _i32, _i32, _i32, _p, _p]),
     "clskd_bn_finalize": (_i32, [_p, _i32, _i64, _i32, _p, _p, _f32, _p, _p, _f32, _i32, _p, _p,
                                  _p, _p, _p]),
     "clskd_bn_eval_coeffs": (_i32, [_p, _p, _p, _p, _f32, _i32, _p, _p, _p]),

@@ -117,8 +117,6 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     X = X.contiguous()
     y = y.float().reshape(X.shape[0], -1).contiguous()
     B = X.shape[0]
-    if reinit is not None:
-        reinit()
     dev = X.device
     spec = teacher.spectrum(X)
     # both ConvSTFTs are the fixed (win 400, hop 100, fft 512) kernel of the same window type
@@ -133,6 +131,8 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
         # SURVEY.md §8 a11) and the MRSTFT base loss on (student wav, clean) (distill.py:100-101)
         sf = student.run(X, train=student.training, bn_updates=2 if student.training else 0,
                          spec=s_spec, want_masks=False)
+        if reinit is not None:  # fresh ABF modules (distill.py:92-96): only ReviewKD reads them
+            reinit()
         s_enc = review_encoder.forward_bftc(sf["enc"])
         s_dec = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5])
         stft_loss(sf["out_wav"], y, out2=buf[0:2])

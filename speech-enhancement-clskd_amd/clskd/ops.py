@@ -318,6 +318,12 @@ def batch_norm_bftc(x, y, gamma, beta, running_mean, running_var, train, momentu
             nblk = L.clskd_bn_partial_blocks(rows, Cn)
             part = torch.empty(nblk * Cn * 2, device=dev, dtype=torch.float64)
             check(L.clskd_bn_stats_partial(ptr(x), rows, Cn, ptr(part), nblk, _dt(x), st), "bn_stats")
+        if nblk > 256:  # two-level: coalesced group sums across the chip, then the finalize
+            grp = 64
+            ng = -(-nblk // grp)
+            part2 = torch.empty(ng * Cn * 2, device=dev, dtype=torch.float64)
+            check(L.clskd_bn_compact(ptr(part), nblk, Cn, grp, ptr(part2), st), "bn_compact")
+            part, nblk = part2, ng
         mean_o = var_o = None
         if stats_out is not None:
             mean_o, var_o = stats_out

@@ -429,6 +429,34 @@ __global__ __launch_bounds__(256) void spec_bftc_kernel(const float* __restrict_
   }
 }
 
+
+// Level-2 reduction of BatchNorm partials: out[g][c] = sum_{r in [g*group, (g+1)*group)} in[r][c]
+// (fixed order).  Block = 64 channels x 4 row lanes; each lane sums group/4 rows with coalesced
+// 16-B {sum, sumsq} loads (consecutive lanes = consecutive channels).
+__global__ __launch_bounds__(256) void bn_compact_kernel(const double* __restrict__ in, int nblk,
+                                                         int C, int group,
+                                                         double* __restrict__ out) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const int g = blockIdx.x;
+  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int lane_r = threadIdx.x >> 6;
+  const int r0 = g * group, r1 = min(nblk, r0 + group);
+  d2 acc = {0.0, 0.0};
+  if (c < C) {
+#pragma unroll 4
+    for (int r = r0 + lane_r; r < r1; r += 4)
+      acc += *reinterpret_cast<const d2*>(in + ((int64_t)r * C + c) * 2);
+  }
+  __shared__ d2 red[4][64];
+  red[lane_r][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (lane_r == 0 && c < C) {
+    const int l = threadIdx.x & 63;
+    const d2 v = ((red[0][l] + red[1][l]) + red[2][l]) + red[3][l];
+    *reinterpret_cast<d2*>(out + ((int64_t)g * C + c) * 2) = v;
+  }
+}
+
 }  // namespace clskd
 
 using namespace clskd;
@@ -456,6 +484,18 @@ extern "C" int clskd_bn_stats_partial(const void* x, int64_t rows, int32_t C, do
     hipLaunchKernelGGL(bn_stats_partial_kernel<float>, dim3(nblk), dim3(256), 0, as_stream(stream),
                        (const float*)x, rows, C, rpb, partial);
   CLSKD_LAUNCH_CHECK("bn_stats_partial");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_bn_compact(const double* partial, int32_t nblk, int32_t C, int32_t group,
+                                double* out, void* stream) {
+  CLSKD_CHECK_ARG(partial && out, "bn_compact: null pointer");
+  CLSKD_CHECK_SHAPE(nblk > 0 && C > 0 && group >= 4, "bn_compact: shape");
+  CLSKD_CHECK_ARG(((uintptr_t)partial & 15) == 0 && ((uintptr_t)out & 15) == 0,
+                  "bn_compact: partials must be 16-byte aligned");
+  hipLaunchKernelGGL(bn_compact_kernel, dim3((unsigned)cdiv(nblk, group), (unsigned)cdiv(C, 64)),
+                     dim3(256), 0, as_stream(stream), partial, nblk, C, group, out);
+  CLSKD_LAUNCH_CHECK("bn_compact");
   return CLSKD_OK;
 }
 
