@@ -6,13 +6,15 @@
 // The K-table gather becomes a per-lane SOURCE address (the LDS destination of one wave
 // instruction is linear: 8 rows x 128 B); out-of-bounds taps read a zero page.
 //
-// Tile BM=128 x BN x BK=64, 256 threads = 4 waves, v_mfma_f32_32x32x16_bf16 (fp32 accumulate).
+// Tile BM=128 x BN x BK=64, 8 waves (4 for BN=32), v_mfma_f32_32x32x16_bf16 (fp32 accumulate).
 // Three LDS stages, two K-tiles in flight: per K-tile every wave waits on a COUNTED vmcnt (its
 // own DMAs for the tile it is about to read), then a raw s_barrier makes every wave's DMA
 // visible; no __syncthreads (which would drain vmcnt to 0).  LDS rows are 128 B with the 16-B
 // chunk XOR-swizzled by ((row>>1)&7): the DMA applies the inverse permutation on the source
 // address, the ds_read_b128 fragment reads apply it on the LDS address (same involution), so
 // every read lane group of 16 rows hits 16 distinct bank slots.  All LDS is one dynamic array.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace clskd {
@@ -70,19 +72,20 @@ struct ConvArgsV2 {
   clskd_conv_desc d;
 };
 
-template <int BN, typename OutT>
-__global__ __launch_bounds__(256) void conv_igemm_bf16_dma(const ConvArgsV2 args) {
+template <int BN, int NW, typename OutT>
+__global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 args) {
   using namespace v2;
   const clskd_conv_desc& d = args.d;
-  constexpr int WN = (BN >= 128) ? 2 : 1;
-  constexpr int WM = 4 / WN;
+  constexpr int NT = NW * 64;       // threads
+  constexpr int WN = (BN >= 128 || NW == 8) ? 2 : 1;
+  constexpr int WM = NW / WN;
   constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / WN / 32;
   constexpr int SB = stage_bytes(BN);
-  constexpr int NGA = BM / 8 / 4;   // A DMA instructions per wave per K-tile (4)
-  constexpr int NGB = BN / 8 / 4;   // B DMA instructions per wave per K-tile (>= 1)
+  constexpr int NGA = BM / 8 / NW;  // A DMA instructions per wave per K-tile
+  constexpr int NGB = (BN / 8 + NW - 1) / NW;  // B DMA instructions per wave per K-tile
   constexpr int NG = NGA + NGB;
-  static_assert(NGB >= 1, "BN >= 32");
+  static_assert(TM >= 1 && NGA >= 1 && NGB >= 1, "tile / wave split");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* stages = smem;
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16_dma(const ConvArgsV2 args
     const uint64_t pv = (uint64_t)(uintptr_t)g.ptr;
     segtab[tid] = make_int4((int)(unsigned)pv, (int)(unsigned)(pv >> 32), g.F, g.T);
   }
-  for (int q = tid; q < d.K / 8; q += 256) {
+  for (int q = tid; q < d.K / 8; q += NT) {
     const clskd_ktab_entry e = d.ktab[q * 8];
     const int s = d.kseg[q * 8];
     ctab[q] = make_int2(e.off, (int)(((unsigned)e.dF & 0xFFFFu) | (((unsigned)e.dT & 0xFFu) << 16) |
@@ -161,7 +164,9 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16_dma(const ConvArgsV2 args
     }
 #pragma unroll
     for (int i = 0; i < NGB; ++i) {
-      const int r = (wave + 4 * i) * 8 + prow;
+      // B rows beyond the tile (BN/8 not a multiple of NW) re-load row group 0: harmless dup
+      const int rg = (wave + NW * i) < BN / 8 ? (wave + NW * i) : 0;
+      const int r = rg * 8 + prow;
       const int c = ppos ^ swz(r);
       const int n = n0 + r;
       srcB[i] = n < d.N ? (uint64_t)(uintptr_t)(wgt + (int64_t)n * d.K + kt * BK + c * 8) : zero_addr;
@@ -171,7 +176,10 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16_dma(const ConvArgsV2 args
 #pragma unroll
     for (int i = 0; i < NGA; ++i) glds16((const void*)srcA[i], sl + (wave * NGA + i) * 1024);
 #pragma unroll
-    for (int i = 0; i < NGB; ++i) glds16((const void*)srcB[i], sl + BM * ROWB + (wave + 4 * i) * 1024);
+    for (int i = 0; i < NGB; ++i) {
+      const int rg = (wave + NW * i) < BN / 8 ? (wave + NW * i) : 0;
+      glds16((const void*)srcB[i], sl + BM * ROWB + rg * 1024);
+    }
   };
 
   // accumulators start at the bias (its loads are waited for here, once, before the pipeline)
@@ -252,7 +260,7 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16_dma(const ConvArgsV2 args
       }
     }
     __syncthreads();
-    for (int c = tid; c < BN; c += 256) {
+    for (int c = tid; c < BN; c += NT) {
       const int n = n0 + c;
       if (n >= d.N) continue;
       double S = 0.0, Q = 0.0;
@@ -284,7 +292,7 @@ __global__ __launch_bounds__(256) void conv_igemm_bf16_dma(const ConvArgsV2 args
   }
 }
 
-template <int BN, typename OutT>
+template <int BN, int NW, typename OutT>
 static int launch_v2(const clskd_conv_desc& d, hipStream_t st) {
   using namespace v2;
   const size_t lds = (size_t)STAGES * stage_bytes(BN) + BM * 16 + 4 * BM * 4 + BM * 8 + 64 +
@@ -293,7 +301,7 @@ static int launch_v2(const clskd_conv_desc& d, hipStream_t st) {
     set_error("conv2d(bf16): K=%d needs %zu B of LDS", d.K, lds);
     return CLSKD_E_SHAPE;
   }
-  auto kern = conv_igemm_bf16_dma<BN, OutT>;
+  auto kern = conv_igemm_bf16_dma<BN, NW, OutT>;
   static bool attr_set = false;  // per instantiation
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -301,16 +309,29 @@ static int launch_v2(const clskd_conv_desc& d, hipStream_t st) {
   }
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
   ConvArgsV2 a{d};
-  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, BM), (unsigned)cdiv(d.N, BN)), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, BM), (unsigned)cdiv(d.N, BN)), dim3(NW * 64), lds, st, a);
   return CLSKD_OK;
 }
 
-int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
+template <int NW>
+static int launch_nw(const clskd_conv_desc& d, hipStream_t st) {
   const bool f32out = d.out_dtype == CLSKD_F32;
-  if (d.N <= 32) return f32out ? launch_v2<32, float>(d, st) : launch_v2<32, __bf16>(d, st);
-  if (d.N <= 64) return f32out ? launch_v2<64, float>(d, st) : launch_v2<64, __bf16>(d, st);
-  if (d.N <= 128) return f32out ? launch_v2<128, float>(d, st) : launch_v2<128, __bf16>(d, st);
-  return f32out ? launch_v2<256, float>(d, st) : launch_v2<256, __bf16>(d, st);
+  if (d.N <= 32) return f32out ? launch_v2<32, 4, float>(d, st) : launch_v2<32, 4, __bf16>(d, st);
+  if (d.N <= 64) return f32out ? launch_v2<64, NW, float>(d, st) : launch_v2<64, NW, __bf16>(d, st);
+  if (d.N <= 128) return f32out ? launch_v2<128, NW, float>(d, st) : launch_v2<128, NW, __bf16>(d, st);
+  return f32out ? launch_v2<256, NW, float>(d, st) : launch_v2<256, NW, __bf16>(d, st);
+}
+
+// 8 waves (512 threads) per workgroup: twice the LDS-DMA issuers of a 4-wave tile — the
+// engine is bound by DMA issue/latency, not MFMA (tools/conv_micro.py: 13-25 % faster for
+// BN >= 64).  BN = 32 keeps 4 waves (four 32x32 MFMA tiles).  CLSKD_BF16_WAVES=4 selects the
+// 4-wave tiles everywhere (A/B measurements).
+int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
+  static const int nw = [] {
+    const char* e = getenv("CLSKD_BF16_WAVES");
+    return e && e[0] == '4' ? 4 : 8;
+  }();
+  return nw == 8 ? launch_nw<8>(d, st) : launch_nw<4>(d, st);
 }
 
 }  // namespace clskd
