@@ -7,9 +7,10 @@ A step = one KnowledgeDistillation.training_step (distill.py:72-148) over B=16 s
 4 s noisy/clean pairs per GPU: teacher + student DCCRN forwards (train-mode BN), ReviewKD
 fusions, 14 SPKD Gram losses and the MRSTFT base loss; frames = B * T with T = L/100 + 3 = 643.
 Each rank processes its own batch shard (weak scaling; forward+loss has no exchange step).
-By default the step is captured once as a hipGraph (clskd.graph.StepGraph) and replayed: every
-replay recomputes the full step (ABF re-draw, both forwards, Grams, MRSTFT) from the batch copied
-into its static input buffers; --no-graph launches every kernel from Python.
+The step runs on three HIP streams (teacher | student -> ReviewKD-decoder | ReviewKD-encoder ->
+MRSTFT), launched eagerly (the host enqueues ahead of the device); --graph replays a captured
+hipGraph of the same step instead (clskd.graph.StepGraph: every replay recomputes the step from
+the batch copied into its static inputs).
 Prints one JSON line on rank 0.
 """
 import argparse
@@ -88,9 +89,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--abf-reinit", default="step", choices=["step", "once"])
-    ap.add_argument("--no-graph", action="store_true",
-                    help="launch every kernel eagerly from Python instead of replaying the "
-                         "captured hipGraph of the step")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the captured hipGraph of the step (clskd.graph.StepGraph) instead "
+                         "of launching the three-stream schedule eagerly; ROCm's graph executor "
+                         "does not keep the three streams concurrent, so eager is faster here")
     ap.add_argument("--precision", default="mixed", choices=["mixed", "fp32"],
                     help="mixed: teacher + ReviewKD GEMMs on bf16 MFMA operands (fp32 accumulate), "
                          "student fp32; fp32: every GEMM on exact-f32 MFMA")
@@ -115,7 +117,7 @@ def main():
         Ys.append(torch.from_numpy(clean).to(dev))
     T = cfg.n_frames(L)
 
-    if args.no_graph:
+    if (not args.graph):
         def step(i):
             return kd.training_step((Xs[i % NBATCH], Ys[i % NBATCH]), i)
     else:
@@ -131,14 +133,14 @@ def main():
 
     # ---- timed region: exactly K steps, barrier + sync on both sides --------------------
     cdist.barrier(dev)
-    if args.no_graph:
+    if (not args.graph):
         ops.KernelTimer.start()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(i)
     cdist.barrier(dev)
     el = time.perf_counter() - t0
-    if args.no_graph:
+    if (not args.graph):
         ktimes = ops.KernelTimer.stop()
         timing = "HIP events around every conv-engine launch inside the timed region"
     else:
@@ -192,7 +194,8 @@ def main():
                        "global_batch": world * B_PER_GPU, "per_gpu_batch": B_PER_GPU,
                        "clip_samples": L, "frames_per_clip": T, "parallelism": f"dp{world}",
                        "abf_reinit": args.abf_reinit, "loss": round(loss_v, 6),
-                       "launch": "eager" if args.no_graph else "hipGraph replay (clskd.graph.StepGraph)",
+                       "launch": ("eager, 3 HIP streams" if (not args.graph)
+                                  else "hipGraph replay (clskd.graph.StepGraph)"),
                        "precision": ("teacher+ReviewKD GEMMs bf16 MFMA operands / fp32 accumulate; "
                                      "student, STFT/iSTFT, LSTM recurrence, BN, losses fp32")
                        if args.precision == "mixed" else "fp32 MFMA everywhere"},

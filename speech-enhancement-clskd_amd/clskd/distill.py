@@ -29,10 +29,10 @@ from .model import DCCRN
 _SIDE = {}
 
 
-def _side_stream(dev):
-    """A second HIP stream per device: the student forward runs there, overlapping the teacher's
-    latency-bound LSTM recurrence and small kernels with the other model's GEMMs."""
-    key = torch.device(dev).index
+def _side_stream(dev, which=0):
+    """Extra HIP streams per device (which = 0, 1): the student chain runs beside the teacher,
+    overlapping the latency-bound LSTM recurrences and small kernels with the GEMMs."""
+    key = (torch.device(dev).index, which)
     if key not in _SIDE:
         _SIDE[key] = torch.cuda.Stream(device=dev)
     return _SIDE[key]
@@ -85,11 +85,15 @@ class KnowledgeDistillation(nn.Module):
     def configure_optimizers(self):
         return torch.optim.Adam(self.student.parameters(), lr=self.cfg.learning_rate)
 
-    def _reinit_abf(self):
+    def _reinit_abf(self, which=None):
+        """Re-draw the ABF weights (framework.py:194-195 / distill.py:92-96) of one ReviewKD
+        module (which = 'encoder' | 'decoder') or of both."""
         if self.abf_reinit != "step":
             return
+        mods = {"encoder": (self.review_encoder,), "decoder": (self.review_decoder,),
+                None: (self.review_encoder, self.review_decoder)}[which]
         with torch.no_grad():
-            for rk in (self.review_encoder, self.review_decoder):
+            for rk in mods:
                 for abf in rk.abfs:
                     nn.init.kaiming_uniform_(abf.conv1[0].weight, a=1)
                     nn.init.kaiming_uniform_(abf.conv2[0].weight, a=1)
@@ -122,22 +126,44 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     # both ConvSTFTs are the fixed (win 400, hop 100, fft 512) kernel of the same window type
     s_spec = spec if teacher.win_type == student.win_type else None
     main = torch.cuda.current_stream(dev)
-    side = _side_stream(dev)
-    side.wait_stream(main)  # spec ready; previous step's work on main is done before reuse
+    side = _side_stream(dev, 0)
+    side2 = _side_stream(dev, 1)
+    # spec ready; the previous step's work (joined into main) is done before buffers are reused
+    side.wait_stream(main)
+    side2.wait_stream(main)
     buf = torch.empty(16, dtype=torch.float32, device=dev)  # [sc, mag, spkd x 14]
+    # Everything that depends on the student alone runs beside the teacher forward (main):
+    #   side : student forward -> decoder-ABF re-draw -> ReviewKD decoder fusions
+    #   side2: encoder-ABF re-draw -> (student encoder done) ReviewKD encoder fusions ->
+    #          (student done) MRSTFT base loss on (student wav, clean) (distill.py:100-101)
+    # ReviewKD: distill.py:92-96, tap contract SURVEY.md §8 a11.
+    held = {}
+    if reinit is not None:  # fresh ABF modules (distill.py:92-96): only ReviewKD reads them
+        with torch.cuda.stream(side2):
+            reinit("encoder")
+
+    def fork_review_encoder(enc):
+        ev = torch.cuda.Event()
+        ev.record(side)
+        with torch.cuda.stream(side2):
+            side2.wait_event(ev)
+            held["s_enc"] = review_encoder.forward_bftc(enc)
+
     with torch.cuda.stream(side):
-        # everything that depends on the student alone runs beside the teacher forward:
-        # student forward, ReviewKD fusions on its taps (distill.py:92-96; tap contract
-        # SURVEY.md §8 a11) and the MRSTFT base loss on (student wav, clean) (distill.py:100-101)
         sf = student.run(X, train=student.training, bn_updates=2 if student.training else 0,
-                         spec=s_spec, want_masks=False)
-        if reinit is not None:  # fresh ABF modules (distill.py:92-96): only ReviewKD reads them
-            reinit()
-        s_enc = review_encoder.forward_bftc(sf["enc"])
+                         spec=s_spec, want_masks=False, on_encoder=fork_review_encoder)
+        student_done = torch.cuda.Event()
+        student_done.record(side)
+        if reinit is not None:
+            reinit("decoder")
         s_dec = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5])
+    with torch.cuda.stream(side2):
+        side2.wait_event(student_done)
         stft_loss(sf["out_wav"], y, out2=buf[0:2])
+    s_enc = held["s_enc"]
     tf = teacher.run(X, train=teacher.training, bn_updates=1, spec=spec, want_masks=False)
     main.wait_stream(side)
+    main.wait_stream(side2)
     t_dec = [tf["dec_in"]] + tf["dec"][:5]
     pairs = [(_gram_bftc(a), _gram_bftc(b)) for a, b in zip(s_enc, tf["enc"])]
     pairs += [(_gram_bftc(a), _gram_bftc(b)) for a, b in zip(s_dec, t_dec)]

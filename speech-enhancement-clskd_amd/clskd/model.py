@@ -343,8 +343,10 @@ class DCCRN(nn.Module):
                  OutMap(T * 514, 0, 514))
         return spec
 
-    def run(self, x, train=True, bn_updates=1, spec=None, want_masks=True):
-        """Full forward on the HIP device.  Returns a dict of BFTC buffers and NCHW views."""
+    def run(self, x, train=True, bn_updates=1, spec=None, want_masks=True, on_encoder=None):
+        """Full forward on the HIP device.  Returns a dict of BFTC buffers and NCHW views.
+        on_encoder(enc): called (on the launching stream) right after the encoder, so a caller can
+        fork work that only needs the encoder taps before the LSTM and decoder are enqueued."""
         if not x.is_cuda:
             raise RuntimeError("clskd.DCCRN.forward needs inputs on the HIP device")
         x = x.float()
@@ -386,6 +388,8 @@ class DCCRN(nn.Module):
                                 partial=(part, nmb) if train else None)
             enc.append(raw)
             F = Fo
+        if on_encoder is not None:
+            on_encoder(enc)
         # ---------------- complex LSTM (DCCRN.py:178-199, tools_for_model.py:159-174)
         C6 = kn[-1]
         Ch = C6 // 2

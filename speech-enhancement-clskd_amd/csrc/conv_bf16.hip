@@ -29,7 +29,6 @@ namespace v2 {
 constexpr int BM = 128;
 constexpr int BK = 64;
 constexpr int ROWB = 128;  // bytes per LDS row (64 bf16)
-constexpr int STAGES = 3;
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
@@ -72,7 +71,7 @@ struct ConvArgsV2 {
   clskd_conv_desc d;
 };
 
-template <int BN, int NW, typename OutT>
+template <int BN, int NW, int NS, typename OutT>
 __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 args) {
   using namespace v2;
   const clskd_conv_desc& d = args.d;
@@ -89,7 +88,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* stages = smem;
-  int* rowinfo = reinterpret_cast<int*>(smem + STAGES * SB);        // [BM][4]: fi0, ti0, valid, -
+  int* rowinfo = reinterpret_cast<int*>(smem + NS * SB);        // [BM][4]: fi0, ti0, valid, -
   int* rowbase = rowinfo + BM * 4;                                   // [4 seg][BM] element offsets
   int64_t* out_row = reinterpret_cast<int64_t*>(rowbase + 4 * BM);   // [BM]
   int4* segtab = reinterpret_cast<int4*>(out_row + BM);              // [4]: ptr lo, ptr hi, F, T
@@ -197,11 +196,17 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  issue(0, 0);
-  if (nk > 1) issue(1, 1);
+  // prologue: NS-1 K-tiles in flight
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) issue(t, t);
 
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) {
+    // wait for this wave's DMAs of tile kt; the (up to NS-2) younger tiles stay in flight
+    const int ahead = min(NS - 2, nk - 1 - kt);
+    if (ahead >= 2) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NG) : "memory");
+    } else if (ahead == 1) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -209,8 +214,8 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % STAGES);
-    const unsigned char* sa = stages + (kt % STAGES) * SB;
+    if (kt + NS - 1 < nk) issue(kt + NS - 1, (kt + NS - 1) % NS);
+    const unsigned char* sa = stages + (kt % NS) * SB;
     const unsigned char* sb = sa + BM * ROWB;
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
@@ -292,16 +297,16 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
   }
 }
 
-template <int BN, int NW, typename OutT>
+template <int BN, int NW, int S, typename OutT>
 static int launch_v2(const clskd_conv_desc& d, hipStream_t st) {
   using namespace v2;
-  const size_t lds = (size_t)STAGES * stage_bytes(BN) + BM * 16 + 4 * BM * 4 + BM * 8 + 64 +
+  const size_t lds = (size_t)S * stage_bytes(BN) + BM * 16 + 4 * BM * 4 + BM * 8 + 64 +
                      (size_t)(d.K / 8) * 8;
   if (lds > 160 * 1024) {
     set_error("conv2d(bf16): K=%d needs %zu B of LDS", d.K, lds);
     return CLSKD_E_SHAPE;
   }
-  auto kern = conv_igemm_bf16_dma<BN, NW, OutT>;
+  auto kern = conv_igemm_bf16_dma<BN, NW, S, OutT>;
   static bool attr_set = false;  // per instantiation
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -313,13 +318,14 @@ static int launch_v2(const clskd_conv_desc& d, hipStream_t st) {
   return CLSKD_OK;
 }
 
-template <int NW>
+template <int NW, int S>
 static int launch_nw(const clskd_conv_desc& d, hipStream_t st) {
   const bool f32out = d.out_dtype == CLSKD_F32;
-  if (d.N <= 32) return f32out ? launch_v2<32, 4, float>(d, st) : launch_v2<32, 4, __bf16>(d, st);
-  if (d.N <= 64) return f32out ? launch_v2<64, NW, float>(d, st) : launch_v2<64, NW, __bf16>(d, st);
-  if (d.N <= 128) return f32out ? launch_v2<128, NW, float>(d, st) : launch_v2<128, NW, __bf16>(d, st);
-  return f32out ? launch_v2<256, NW, float>(d, st) : launch_v2<256, NW, __bf16>(d, st);
+  if (d.N <= 32) return f32out ? launch_v2<32, 4, S, float>(d, st) : launch_v2<32, 4, S, __bf16>(d, st);
+  if (d.N <= 64) return f32out ? launch_v2<64, NW, S, float>(d, st) : launch_v2<64, NW, S, __bf16>(d, st);
+  if (d.N <= 128) return f32out ? launch_v2<128, NW, S, float>(d, st) : launch_v2<128, NW, S, __bf16>(d, st);
+  // BN = 256: 48 KB per stage, three stages fill the 160 KB LDS
+  return f32out ? launch_v2<256, NW, 3, float>(d, st) : launch_v2<256, NW, 3, __bf16>(d, st);
 }
 
 // 8 waves (512 threads) per workgroup: twice the LDS-DMA issuers of a 4-wave tile — the
@@ -331,7 +337,12 @@ int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
     const char* e = getenv("CLSKD_BF16_WAVES");
     return e && e[0] == '4' ? 4 : 8;
   }();
-  return nw == 8 ? launch_nw<8>(d, st) : launch_nw<4>(d, st);
+  static const int stages = [] {  // experiment knob: CLSKD_BF16_STAGES=3|4
+    const char* e = getenv("CLSKD_BF16_STAGES");
+    return e && e[0] == '4' ? 4 : 3;
+  }();
+  if (stages == 4) return nw == 8 ? launch_nw<8, 4>(d, st) : launch_nw<4, 4>(d, st);
+  return nw == 8 ? launch_nw<8, 3>(d, st) : launch_nw<4, 3>(d, st);
 }
 
 }  // namespace clskd
