@@ -34,6 +34,7 @@ PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (f32-in MF
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
 B_PER_GPU = 16
 NBATCH = 4
+TRAFFIC_FILE = "r1_pmc_traffic.json"  # written by tools/pmc_traffic.py
 L = 64000
 
 
@@ -157,21 +158,33 @@ def main():
 
     if rank == 0:
         frames = world * B_PER_GPU * T * args.steps
-        # dominant kernel = conv engine variant with the largest total time
+        # dominant kernel = conv kernel instance with the largest total time
         name, (n_l, ms, flops) = max(ktimes.items(), key=lambda kv: kv[1][1])
         conv_total_ms = sum(v[1] for v in ktimes.values())
         conv_total_fl = sum(v[2] for v in ktimes.values())
         avg_ms = ms / n_l
         achieved = flops / n_l / (avg_ms * 1e-3) / 1e12
-        peak = PEAK_BF16_MFMA_TFLOPS if "bf16" in name else PEAK_F32_MFMA_TFLOPS
+        peak = PEAK_BF16_MFMA_TFLOPS if name.startswith("conv_igemm_bf16") else PEAK_F32_MFMA_TFLOPS
+        traffic, traffic_src = None, None
+        tpath = os.path.join(REPO, "profiles", TRAFFIC_FILE)
+        if os.path.exists(tpath):
+            tk = json.load(open(tpath))["kernels"].get(name)
+            if tk is not None:
+                traffic = round(tk["hbm_bytes_per_launch"])
+                traffic_src = f"profiles/{TRAFFIC_FILE} (PMC FETCH_SIZE x2 + WRITE_SIZE, per launch)"
         roof = dict(bound="mfma", kernel=name, achieved=round(achieved, 2),
                     peak=peak, unit="TFLOP/s",
-                    frac=round(achieved / peak, 4), traffic=None,
-                    launches_per_step=n_l // args.steps, timing=timing, avg_launch_us=round(avg_ms * 1e3, 2),
+                    frac=round(achieved / peak, 4), traffic=traffic, traffic_source=traffic_src,
+                    launches_per_step=n_l // args.steps, timing=timing,
+                    avg_launch_us=round(avg_ms * 1e3, 2),
                     algorithmic_gflop_per_launch=round(flops / n_l / 1e9, 3),
-                    conv_engine_all_variants=dict(
+                    conv_all_kernels=dict(
                         ms_per_step=round(conv_total_ms / args.steps, 3),
-                        tflops=round(conv_total_fl / (conv_total_ms * 1e-3) / 1e12, 2)))
+                        tflops=round(conv_total_fl / (conv_total_ms * 1e-3) / 1e12, 2),
+                        per_kernel={k: dict(launches_per_step=v[0] // args.steps,
+                                            avg_us=round(v[1] / v[0] * 1e3, 1),
+                                            tflops=round(v[2] / (v[1] * 1e-3) / 1e12, 1))
+                                    for k, v in sorted(ktimes.items(), key=lambda kv: -kv[1][1])}))
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_seconds)

@@ -98,13 +98,22 @@ def direct_weight(wpacked):
     return wd
 
 
-def conv_kernel_name(N, vec4, bf16=False, K=None):
+_BF16_WAVES = 4 if os.environ.get("CLSKD_BF16_WAVES", "") == "4" else 8
+
+
+def conv_kernel_name(N, vec4, bf16=False, K=None, out_bf16=False, kvec=None):
+    """Canonical name of the kernel instance a conv launch runs (the template arguments rocprof
+    shows): engine, tile width, waves / load width, output storage."""
+    out = "bf16" if out_bf16 else "float"
     if K is not None and direct_ok(N, K):
-        return f"conv_direct<{'bf16' if bf16 else 'f32'}>"
-    bn = 32 if N <= 32 else (64 if N <= 64 else 128)
+        npad = direct_np(N)
+        return f"conv_direct_kernel<{npad},{kvec or (8 if bf16 else 4)},{'bf16' if bf16 else 'float'},{out}>"
     if bf16:
-        return f"conv_igemm_bf16<{bn}>"
-    return f"conv_igemm_f32<{bn},{'true' if vec4 else 'false'}>"
+        bn = 32 if N <= 32 else 64 if N <= 64 else 128 if N <= 128 else 256
+        nw = 4 if bn == 32 else _BF16_WAVES
+        return f"conv_igemm_bf16_dma<{bn},{nw},3,{out}>"
+    bn = 32 if N <= 32 else (64 if N <= 64 else 128)
+    return f"conv_igemm_f32<{bn},{'true' if vec4 else 'false'},{out}>"
 
 
 def _stream():
@@ -289,7 +298,7 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
         e0.record()
         check(lib().clskd_conv2d_fwd(C.byref(d), _stream()), "conv2d")
         e1.record()
-        KernelTimer.records.append((conv_kernel_name(N, vec4, bf16, Kp), 2.0 * B * Fo * To * N * K, e0, e1,
+        KernelTimer.records.append((conv_kernel_name(N, vec4, bf16, Kp, out.dtype == torch.bfloat16, kvec), 2.0 * B * Fo * To * N * K, e0, e1,
                                     (B * Fo * To, N, K, "bf16" if bf16 else "f32")))
     else:
         check(lib().clskd_conv2d_fwd(C.byref(d), _stream()), "conv2d")

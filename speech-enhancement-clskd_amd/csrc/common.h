@@ -57,6 +57,15 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// XCD-aware tile order: the hardware places workgroup i on XCD i % 8.  Give every XCD one
+// contiguous run of M-tiles (a bijection on [0, nb)), so neighbouring tiles — which read
+// overlapping input rows through the conv taps — share that XCD's L2 instead of each of the
+// eight L2s fetching the same rows.
+__device__ __forceinline__ int xcd_tile(int bid, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = bid & 7, j = bid >> 3;
+  return x * q + (x < r ? x : r) + j;
+}
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 }  // namespace clskd

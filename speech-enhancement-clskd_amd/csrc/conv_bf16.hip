@@ -71,7 +71,7 @@ struct ConvArgsV2 {
   clskd_conv_desc d;
 };
 
-template <int BN, int NW, int NS, typename OutT>
+template <int BN, int NW, int NS, typename OutT, int DBG = 0>
 __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 args) {
   using namespace v2;
   const clskd_conv_desc& d = args.d;
@@ -99,7 +99,8 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
-  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t m0 = (int64_t)tile * BM;
   const int n0 = blockIdx.y * BN;
   const int nk = d.K / BK;
   const int64_t FoTo = (int64_t)d.Fo * d.To;
@@ -141,24 +142,41 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
 
   const uint64_t zero_addr = (uint64_t)(uintptr_t)g_zero_page;
   const unsigned stage_lds0 = __builtin_amdgcn_readfirstlane(lds_addr(stages));
+  // Loop-invariant geometry of this lane's A rows (one per DMA group i): the per-K-tile source
+  // address then costs ONE LDS read (the K-chunk entry) plus ALU — the issue step is no longer
+  // a chain of dependent LDS round trips sitting between the barrier and the MFMAs.
+  int a_fi0[NGA], a_ti0[NGA], a_c[NGA];
+  bool a_valid[NGA];
+  int a_rb[NGA][4];
+#pragma unroll
+  for (int i = 0; i < NGA; ++i) {
+    const int r = (wave * NGA + i) * 8 + prow;
+    a_c[i] = ppos ^ swz(r);
+    const int4 ri = reinterpret_cast<const int4*>(rowinfo)[r];
+    a_fi0[i] = ri.x;
+    a_ti0[i] = ri.y;
+    a_valid[i] = ri.z != 0;
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) a_rb[i][sg] = rowbase[sg * BM + r];
+  }
+  const uint64_t sp0 = (uint64_t)(uintptr_t)d.seg[0].ptr, sp1 = (uint64_t)(uintptr_t)d.seg[1].ptr;
+  const uint64_t sp2 = (uint64_t)(uintptr_t)d.seg[2].ptr, sp3 = (uint64_t)(uintptr_t)d.seg[3].ptr;
   auto issue = [&](int kt, int stage) {
-    // phase 1: every source address of this K-tile (LDS table reads only)
     uint64_t srcA[NGA], srcB[NGB];
 #pragma unroll
     for (int i = 0; i < NGA; ++i) {
-      const int r = (wave * NGA + i) * 8 + prow;
-      const int c = ppos ^ swz(r);
-      const int2 ce = ctab[kt * 8 + c];
-      const int s = (int)((unsigned)ce.y >> 24);
+      const int2 ce = ctab[kt * 8 + a_c[i]];
+      const int sg = (int)((unsigned)ce.y >> 24);
       const int dF = (int)(short)(ce.y & 0xFFFF);
       const int dT = (int)(signed char)((ce.y >> 16) & 0xFF);
-      const int4 ri = reinterpret_cast<const int4*>(rowinfo)[r];
-      const int4 sg = segtab[s];
-      const int fi = ri.x + dF;
-      const int ti = ri.y + dT;
-      const bool ok = ri.z && (unsigned)fi < (unsigned)sg.z && (unsigned)ti < (unsigned)sg.w;
-      const uint64_t base = ((uint64_t)(unsigned)sg.y << 32) | (uint64_t)(unsigned)sg.x;
-      const int64_t eoff = (int64_t)rowbase[s * BM + r] + ce.x;
+      const int fi = a_fi0[i] + dF;
+      const int ti = a_ti0[i] + dT;
+      const int Fb = sel4(sg, d.seg[0].F, d.seg[1].F, d.seg[2].F, d.seg[3].F);
+      const int Tb = sel4(sg, d.seg[0].T, d.seg[1].T, d.seg[2].T, d.seg[3].T);
+      const bool ok = a_valid[i] && (unsigned)fi < (unsigned)Fb && (unsigned)ti < (unsigned)Tb;
+      const uint64_t base = sel4(sg, sp0, sp1, sp2, sp3);
+      const int rb = sel4(sg, a_rb[i][0], a_rb[i][1], a_rb[i][2], a_rb[i][3]);
+      const int64_t eoff = (int64_t)rb + ce.x;
       srcA[i] = ok ? base + (uint64_t)(eoff * 2) : zero_addr;
     }
 #pragma unroll
@@ -170,7 +188,8 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
       const int n = n0 + r;
       srcB[i] = n < d.N ? (uint64_t)(uintptr_t)(wgt + (int64_t)n * d.K + kt * BK + c * 8) : zero_addr;
     }
-    // phase 2: the DMAs, back to back
+    if constexpr (DBG == 1) return;  // timing experiment: no operand traffic
+    // the DMAs, back to back
     const unsigned sl = stage_lds0 + stage * SB;
 #pragma unroll
     for (int i = 0; i < NGA; ++i) glds16((const void*)srcA[i], sl + (wave * NGA + i) * 1024);
@@ -231,11 +250,18 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
         const int row = wn * (BN / WN) + j * 32 + l32;
         bfr[j] = *reinterpret_cast<const bf16x8*>(sb + row * ROWB + ((c ^ swz(row)) << 4));
       }
+      if constexpr (DBG != 2) {  // DBG 2: timing experiment without the MFMAs
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j][0] += (float)af[i][0] * (float)bfr[j][0];
+      }
     }
   }
 
@@ -274,8 +300,8 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
         S += red[(w * BN + c) * 2];
         Q += red[(w * BN + c) * 2 + 1];
       }
-      d.stats[((int64_t)blockIdx.x * d.N + n) * 2] = S;
-      d.stats[((int64_t)blockIdx.x * d.N + n) * 2 + 1] = Q;
+      d.stats[((int64_t)tile * d.N + n) * 2] = S;
+      d.stats[((int64_t)tile * d.N + n) * 2 + 1] = Q;
     }
   }
 
@@ -297,7 +323,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
   }
 }
 
-template <int BN, int NW, int S, typename OutT>
+template <int BN, int NW, int S, typename OutT, int DBG = 0>
 static int launch_v2(const clskd_conv_desc& d, hipStream_t st) {
   using namespace v2;
   const size_t lds = (size_t)S * stage_bytes(BN) + BM * 16 + 4 * BM * 4 + BM * 8 + 64 +
@@ -306,7 +332,7 @@ static int launch_v2(const clskd_conv_desc& d, hipStream_t st) {
     set_error("conv2d(bf16): K=%d needs %zu B of LDS", d.K, lds);
     return CLSKD_E_SHAPE;
   }
-  auto kern = conv_igemm_bf16_dma<BN, NW, S, OutT>;
+  auto kern = conv_igemm_bf16_dma<BN, NW, S, OutT, DBG>;
   static bool attr_set = false;  // per instantiation
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -341,6 +367,14 @@ int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
     const char* e = getenv("CLSKD_BF16_STAGES");
     return e && e[0] == '4' ? 4 : 3;
   }();
+  static const int dbg = [] {  // timing experiments only: 1 = no DMA, 2 = no MFMA (wrong results)
+    const char* e = getenv("CLSKD_BF16_DEBUG_MODE");
+    return e ? atoi(e) : 0;
+  }();
+  if (dbg == 1 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 8, 3, __bf16, 1>(d, st);
+  if (dbg == 2 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 8, 3, __bf16, 2>(d, st);
+  if (dbg == 1 && d.out_dtype == CLSKD_BF16 && d.N <= 32) return launch_v2<32, 4, 3, __bf16, 1>(d, st);
+  if (dbg == 2 && d.out_dtype == CLSKD_BF16 && d.N <= 32) return launch_v2<32, 4, 3, __bf16, 2>(d, st);
   if (stages == 4) return nw == 8 ? launch_nw<8, 4>(d, st) : launch_nw<4, 4>(d, st);
   return nw == 8 ? launch_nw<8, 3>(d, st) : launch_nw<4, 3>(d, st);
 }

@@ -6,7 +6,7 @@
 //
 // Same descriptor, K table, output map and fused-BN-statistics protocol as the engines
 // (include/clskd.h): one thread per output row (b, fo, to), 128 rows per block, so the
-// statistics partials stats[blockIdx.x][N][2] line up with conv_mblocks().  The K loop is
+// statistics partials stats[tile][N][2] line up with conv_mblocks().  The K loop is
 // uniform across the block: the K table (one entry per channel run of kvec) is staged in LDS,
 // the packed weights are read with scalar loads (constant address space) and enter the VALU as
 // SGPR operands — v_fma_f32 for fp32 runs, v_dot2c_f32_bf16 (bf16 pairs, fp32 accumulate) for
@@ -77,7 +77,8 @@ __global__ __launch_bounds__(128) void conv_direct_kernel(const DirectArgs args)
   __syncthreads();
 
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
-  const int64_t m = (int64_t)blockIdx.x * 128 + tid;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t m = (int64_t)tile * 128 + tid;
   const bool valid = m < M;
   const int64_t FoTo = (int64_t)d.Fo * d.To;
   const int64_t mm = valid ? m : 0;
@@ -193,14 +194,14 @@ __global__ __launch_bounds__(128) void conv_direct_kernel(const DirectArgs args)
         S += v;
         Q = fma(v, v, Q);
       }
-      d.stats[((int64_t)blockIdx.x * d.N + n) * 2] = S;
-      d.stats[((int64_t)blockIdx.x * d.N + n) * 2 + 1] = Q;
+      d.stats[((int64_t)tile * d.N + n) * 2] = S;
+      d.stats[((int64_t)tile * d.N + n) * 2 + 1] = Q;
     }
   }
   if (rows_contig) {
     // output rows m0 .. m0+127 are one contiguous run of 128*NP elements: 16-B chunks
     constexpr int CH = 16 / sizeof(OutT);  // elements per chunk
-    const int64_t m0 = (int64_t)blockIdx.x * 128;
+    const int64_t m0 = (int64_t)tile * 128;
     const int rows = (int)min((int64_t)128, M - m0);
     OutT* dst = reinterpret_cast<OutT*>(d.out) + m0 * NP;
     typedef typename VecOf<OutT, CH>::T V;

@@ -45,7 +45,8 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
-  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t m0 = (int64_t)tile * BM;
   const int n0 = blockIdx.y * BN;
   const int nk = d.K / BK;  // host pads K to a multiple of BK
   const int64_t FoTo = (int64_t)d.Fo * d.To;
@@ -231,8 +232,8 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
       const double S = red[c * 2] + red[(BN + c) * 2] + red[(2 * BN + c) * 2] + red[(3 * BN + c) * 2];
       const double Q = red[c * 2 + 1] + red[(BN + c) * 2 + 1] + red[(2 * BN + c) * 2 + 1] +
                        red[(3 * BN + c) * 2 + 1];
-      d.stats[((int64_t)blockIdx.x * d.N + n) * 2] = S;
-      d.stats[((int64_t)blockIdx.x * d.N + n) * 2 + 1] = Q;
+      d.stats[((int64_t)tile * d.N + n) * 2] = S;
+      d.stats[((int64_t)tile * d.N + n) * 2 + 1] = Q;
     }
   }
 
