@@ -26,11 +26,16 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 __device__ __attribute__((aligned(64))) unsigned char g_zero_page[64];
 
 namespace v2 {
-constexpr int BM = 128;
-constexpr int BK = 64;
-constexpr int ROWB = 128;  // bytes per LDS row (64 bf16)
-
-__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+// Tile geometry: BM output rows x BK reduction columns per stage; LDS rows of BK bf16
+// (ROWB = 2*BK bytes = CPR 16-B chunks); one DMA wave instruction fills RPD = 64/CPR rows.
+// The 16-B chunk index is XOR-swizzled so the 16 rows a ds_read_b128 cycle serves hit 16
+// distinct bank slots: 128-B rows pair up per 256-B bank line -> swizzle by (row>>1)&7;
+// 64-B rows come four per line -> (row>>2)&3.
+template <int BK>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (BK == 64) return (row >> 1) & 7;
+  else return (row >> 2) & 3;
+}
 
 template <typename T>
 __device__ __forceinline__ T sel4(int s, T a0, T a1, T a2, T a3) {
@@ -44,7 +49,7 @@ __device__ __forceinline__ void store_out<float>(float* p, float v) { *p = v; }
 template <>
 __device__ __forceinline__ void store_out<__bf16>(__bf16* p, float v) { *p = (__bf16)v; }
 
-__host__ __device__ constexpr int stage_bytes(int BN) { return BM * ROWB + BN * ROWB; }
+__host__ __device__ constexpr int stage_bytes(int BM, int BK, int BN) { return (BM + BN) * BK * 2; }
 
 // One 1-KiB LDS-DMA wave instruction: lane l copies 16 B from gsrc to lds_base + 16*l.
 // Inline asm (cdna_hip_programming.md §5.7): hipcc neither tracks nor waits for it, so the
@@ -71,20 +76,24 @@ struct ConvArgsV2 {
   clskd_conv_desc d;
 };
 
-template <int BN, int NW, int NS, typename OutT, int DBG = 0>
+template <int BM, int BK, int BN, int NW, int NS, typename OutT, int DBG = 0>
 __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 args) {
   using namespace v2;
   const clskd_conv_desc& d = args.d;
   constexpr int NT = NW * 64;       // threads
-  constexpr int WN = (BN >= 128 || NW == 8) ? 2 : 1;
+  constexpr int ROWB = BK * 2;      // bytes per LDS row
+  constexpr int CPR = ROWB / 16;    // 16-B chunks per row
+  constexpr int RPD = 64 / CPR;     // rows per 1-KiB DMA wave instruction
+  constexpr int WN = BM == 256 ? (BN >= 256 ? 4 : 2) : ((BN >= 128 || NW == 8) ? 2 : 1);
   constexpr int WM = NW / WN;
   constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / WN / 32;
-  constexpr int SB = stage_bytes(BN);
-  constexpr int NGA = BM / 8 / NW;  // A DMA instructions per wave per K-tile
-  constexpr int NGB = (BN / 8 + NW - 1) / NW;  // B DMA instructions per wave per K-tile
+  constexpr int SB = stage_bytes(BM, BK, BN);
+  constexpr int NGA = BM / RPD / NW;  // A DMA instructions per wave per K-tile
+  constexpr int NGB = (BN / RPD + NW - 1) / NW;  // B DMA instructions per wave per K-tile
   constexpr int NG = NGA + NGB;
-  static_assert(TM >= 1 && NGA >= 1 && NGB >= 1, "tile / wave split");
+  static_assert(TM >= 1 && TN >= 1 && NGA >= 1 && NGB >= 1 && WM * WN == NW, "tile / wave split");
+  static_assert(BM / WM <= 128 && 128 % (BM / WM) == 0, "a wave's rows stay inside one 128-row half");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* stages = smem;
@@ -137,8 +146,8 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
   __syncthreads();
 
   const unsigned short* wgt = reinterpret_cast<const unsigned short*>(d.weight);
-  const int prow = lane >> 3;  // row within an 8-row DMA group
-  const int ppos = lane & 7;   // 16-B chunk position within the LDS row
+  const int prow = lane / CPR;  // row within an RPD-row DMA group
+  const int ppos = lane % CPR;  // 16-B chunk position within the LDS row
 
   const uint64_t zero_addr = (uint64_t)(uintptr_t)g_zero_page;
   const unsigned stage_lds0 = __builtin_amdgcn_readfirstlane(lds_addr(stages));
@@ -150,8 +159,8 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
   int a_rb[NGA][4];
 #pragma unroll
   for (int i = 0; i < NGA; ++i) {
-    const int r = (wave * NGA + i) * 8 + prow;
-    a_c[i] = ppos ^ swz(r);
+    const int r = (wave * NGA + i) * RPD + prow;
+    a_c[i] = ppos ^ swz<BK>(r);
     const int4 ri = reinterpret_cast<const int4*>(rowinfo)[r];
     a_fi0[i] = ri.x;
     a_ti0[i] = ri.y;
@@ -165,7 +174,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
     uint64_t srcA[NGA], srcB[NGB];
 #pragma unroll
     for (int i = 0; i < NGA; ++i) {
-      const int2 ce = ctab[kt * 8 + a_c[i]];
+      const int2 ce = ctab[kt * CPR + a_c[i]];
       const int sg = (int)((unsigned)ce.y >> 24);
       const int dF = (int)(short)(ce.y & 0xFFFF);
       const int dT = (int)(signed char)((ce.y >> 16) & 0xFF);
@@ -182,9 +191,9 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
 #pragma unroll
     for (int i = 0; i < NGB; ++i) {
       // B rows beyond the tile (BN/8 not a multiple of NW) re-load row group 0: harmless dup
-      const int rg = (wave + NW * i) < BN / 8 ? (wave + NW * i) : 0;
-      const int r = rg * 8 + prow;
-      const int c = ppos ^ swz(r);
+      const int rg = (wave + NW * i) < BN / RPD ? (wave + NW * i) : 0;
+      const int r = rg * RPD + prow;
+      const int c = ppos ^ swz<BK>(r);
       const int n = n0 + r;
       srcB[i] = n < d.N ? (uint64_t)(uintptr_t)(wgt + (int64_t)n * d.K + kt * BK + c * 8) : zero_addr;
     }
@@ -195,7 +204,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
     for (int i = 0; i < NGA; ++i) glds16((const void*)srcA[i], sl + (wave * NGA + i) * 1024);
 #pragma unroll
     for (int i = 0; i < NGB; ++i) {
-      const int rg = (wave + NW * i) < BN / 8 ? (wave + NW * i) : 0;
+      const int rg = (wave + NW * i) < BN / RPD ? (wave + NW * i) : 0;
       glds16((const void*)srcB[i], sl + BM * ROWB + rg * 1024);
     }
   };
@@ -243,12 +252,12 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * (BM / WM) + i * 32 + l32;
-        af[i] = *reinterpret_cast<const bf16x8*>(sa + row * ROWB + ((c ^ swz(row)) << 4));
+        af[i] = *reinterpret_cast<const bf16x8*>(sa + row * ROWB + ((c ^ swz<BK>(row)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * (BN / WN) + j * 32 + l32;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(sb + row * ROWB + ((c ^ swz(row)) << 4));
+        bfr[j] = *reinterpret_cast<const bf16x8*>(sb + row * ROWB + ((c ^ swz<BK>(row)) << 4));
       }
       if constexpr (DBG != 2) {  // DBG 2: timing experiment without the MFMAs
 #pragma unroll
@@ -265,7 +274,9 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
     }
   }
 
-  if (d.stats) {  // fused BatchNorm statistics of this block's valid rows
+  if (d.stats) {  // fused BatchNorm statistics: one fp64 partial per 128 output rows
+    constexpr int HALVES = BM / 128;     // 128-row halves of this tile (host contract)
+    constexpr int WPH = WM / HALVES;     // waves (along M) per half
     __syncthreads();  // all DMAs retired (vmcnt(0) on the last K-tile); stage LDS is free
     double* red = reinterpret_cast<double*>(smem);  // [WM][BN][2]
 #pragma unroll
@@ -291,17 +302,20 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
       }
     }
     __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
+    const int64_t nblk128 = (M + 127) / 128;
+    for (int idx = tid; idx < HALVES * BN; idx += NT) {
+      const int hv = idx / BN, c = idx % BN;
       const int n = n0 + c;
-      if (n >= d.N) continue;
+      const int64_t blk = (int64_t)tile * HALVES + hv;
+      if (n >= d.N || blk >= nblk128) continue;
       double S = 0.0, Q = 0.0;
 #pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        S += red[(w * BN + c) * 2];
-        Q += red[(w * BN + c) * 2 + 1];
+      for (int w = 0; w < WPH; ++w) {
+        S += red[((hv * WPH + w) * BN + c) * 2];
+        Q += red[((hv * WPH + w) * BN + c) * 2 + 1];
       }
-      d.stats[((int64_t)tile * d.N + n) * 2] = S;
-      d.stats[((int64_t)tile * d.N + n) * 2 + 1] = Q;
+      d.stats[(blk * d.N + n) * 2] = S;
+      d.stats[(blk * d.N + n) * 2 + 1] = Q;
     }
   }
 
@@ -323,16 +337,16 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
   }
 }
 
-template <int BN, int NW, int S, typename OutT, int DBG = 0>
+template <int BM, int BK, int BN, int NW, int S, typename OutT, int DBG = 0>
 static int launch_v2(const clskd_conv_desc& d, hipStream_t st) {
   using namespace v2;
-  const size_t lds = (size_t)S * stage_bytes(BN) + BM * 16 + 4 * BM * 4 + BM * 8 + 64 +
+  const size_t lds = (size_t)S * stage_bytes(BM, BK, BN) + BM * 16 + 4 * BM * 4 + BM * 8 + 64 +
                      (size_t)(d.K / 8) * 8;
   if (lds > 160 * 1024) {
     set_error("conv2d(bf16): K=%d needs %zu B of LDS", d.K, lds);
     return CLSKD_E_SHAPE;
   }
-  auto kern = conv_igemm_bf16_dma<BN, NW, S, OutT, DBG>;
+  auto kern = conv_igemm_bf16_dma<BM, BK, BN, NW, S, OutT, DBG>;
   static bool attr_set = false;  // per instantiation
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -347,11 +361,19 @@ static int launch_v2(const clskd_conv_desc& d, hipStream_t st) {
 template <int NW, int S>
 static int launch_nw(const clskd_conv_desc& d, hipStream_t st) {
   const bool f32out = d.out_dtype == CLSKD_F32;
-  if (d.N <= 32) return f32out ? launch_v2<32, 4, S, float>(d, st) : launch_v2<32, 4, S, __bf16>(d, st);
-  if (d.N <= 64) return f32out ? launch_v2<64, NW, S, float>(d, st) : launch_v2<64, NW, S, __bf16>(d, st);
-  if (d.N <= 128) return f32out ? launch_v2<128, NW, S, float>(d, st) : launch_v2<128, NW, S, __bf16>(d, st);
+  if (d.N <= 32) return f32out ? launch_v2<128, 64, 32, 4, S, float>(d, st) : launch_v2<128, 64, 32, 4, S, __bf16>(d, st);
+  if (d.N <= 64) return f32out ? launch_v2<128, 64, 64, NW, S, float>(d, st) : launch_v2<128, 64, 64, NW, S, __bf16>(d, st);
+  if (d.N <= 128) return f32out ? launch_v2<128, 64, 128, NW, S, float>(d, st) : launch_v2<128, 64, 128, NW, S, __bf16>(d, st);
   // BN = 256: 48 KB per stage, three stages fill the 160 KB LDS
-  return f32out ? launch_v2<256, NW, 3, float>(d, st) : launch_v2<256, NW, 3, __bf16>(d, st);
+  return f32out ? launch_v2<128, 64, 256, NW, 3, float>(d, st) : launch_v2<128, 64, 256, NW, 3, __bf16>(d, st);
+}
+
+// 256-row tiles, BK = 32, 16 waves: a third fewer staged bytes per FLOP than 128 x 256 x 64
+static int launch_big(const clskd_conv_desc& d, hipStream_t st) {
+  const bool f32out = d.out_dtype == CLSKD_F32;
+  if (d.N <= 64) return f32out ? launch_v2<256, 32, 64, 16, 3, float>(d, st) : launch_v2<256, 32, 64, 16, 3, __bf16>(d, st);
+  if (d.N <= 128) return f32out ? launch_v2<256, 32, 128, 16, 3, float>(d, st) : launch_v2<256, 32, 128, 16, 3, __bf16>(d, st);
+  return f32out ? launch_v2<256, 32, 256, 16, 3, float>(d, st) : launch_v2<256, 32, 256, 16, 3, __bf16>(d, st);
 }
 
 // 8 waves (512 threads) per workgroup: twice the LDS-DMA issuers of a 4-wave tile — the
@@ -371,10 +393,27 @@ int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
     const char* e = getenv("CLSKD_BF16_DEBUG_MODE");
     return e ? atoi(e) : 0;
   }();
-  if (dbg == 1 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 8, 3, __bf16, 1>(d, st);
-  if (dbg == 2 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 8, 3, __bf16, 2>(d, st);
-  if (dbg == 1 && d.out_dtype == CLSKD_BF16 && d.N <= 32) return launch_v2<32, 4, 3, __bf16, 1>(d, st);
-  if (dbg == 2 && d.out_dtype == CLSKD_BF16 && d.N <= 32) return launch_v2<32, 4, 3, __bf16, 2>(d, st);
+  static const int tilecfg = [] {  // A/B knob: CLSKD_BF16_TILE=128|256 forces one row-tile height
+    const char* e = getenv("CLSKD_BF16_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  if (dbg == 1 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<128, 64, 256, 8, 3, __bf16, 1>(d, st);
+  if (dbg == 2 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<128, 64, 256, 8, 3, __bf16, 2>(d, st);
+  if (d.N > 32 && d.K % 32 == 0 && tilecfg != 128) {
+    // 256-row tiles stage a third fewer bytes per FLOP (measured 1.1-1.25x faster per tile
+    // worth of work) but halve the workgroup count: pick them unless the tail rounds eat the
+    // gain — a 256-row tile costs ~1.6 rounds-equivalents of a 128-row tile, one workgroup per
+    // CU either way.
+    static const int ncu = [] {
+      int v = 256;
+      (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, 0);
+      return v > 0 ? v : 256;
+    }();
+    const int64_t M = (int64_t)d.B * d.Fo * d.To;
+    const int64_t ny = cdiv(d.N, d.N <= 64 ? 64 : d.N <= 128 ? 128 : 256);
+    const int64_t r256 = cdiv(cdiv(M, 256) * ny, ncu), r128 = cdiv(cdiv(M, 128) * ny, ncu);
+    if (tilecfg == 256 || 16 * r256 < 10 * r128) return launch_big(d, st);
+  }
   if (stages == 4) return nw == 8 ? launch_nw<8, 4>(d, st) : launch_nw<4, 4>(d, st);
   return nw == 8 ? launch_nw<8, 3>(d, st) : launch_nw<4, 3>(d, st);
 }

@@ -128,6 +128,43 @@ def test_conv_direct_against_torch_and_engine(dt, C1, C2, N):
         np.testing.assert_allclose(st[:, 1].numpy(), (ref ** 2).sum((0, 2, 3)).numpy(), rtol=1e-5)
     np.testing.assert_allclose(res["direct"][0].numpy(), res["engine"][0].numpy(), rtol=1e-5, atol=1e-5)
 
+
+@pytest.mark.parametrize("N", [45, 64, 100, 256, 300])
+@pytest.mark.parametrize("out_bf16", [False, True])
+def test_conv_bf16_engine_against_torch(N, out_bf16):
+    """bf16 LDS-DMA MFMA engine (every tile configuration the dispatcher picks for these N):
+    2-segment 5x2 stride-(2,1) conv with fused BN statistics, M not a tile multiple, vs torch in
+    fp64 on the same bf16 operands.  Tolerance: outputs 1e-4 relative (fp32 accumulation;
+    bf16 output storage adds its own rounding: 8e-3), statistics 1e-5 relative."""
+    from clskd import ops
+    g = torch.Generator().manual_seed(N)
+    B, F, T, C1, C2 = 3, 34, 61, 64, 32
+    segs_h = [torch.randn(B, F, T, C1, generator=g).to(torch.bfloat16),
+              torch.randn(B, F, T, C2, generator=g).to(torch.bfloat16)]
+    Cin = C1 + C2
+    w = torch.randn(N, Cin, 5, 2, generator=g) * 0.05
+    bias = torch.randn(N, generator=g)
+    taps = [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)]
+    Fo, To = (F + 4 - 5) // 2 + 1, T
+    wp = ops.pack_weight(w.permute(0, 2, 3, 1).reshape(N, 10, Cin).to(DEV), 10 * Cin, "bf16")
+    assert not ops.direct_ok(N, wp.shape[1])
+    wq = wp[:, :10 * Cin].float().cpu().reshape(N, 5, 2, Cin).permute(0, 3, 1, 2).double()
+    xin = torch.cat([x.double() for x in segs_h], 3).permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv2d(torch.nn.functional.pad(xin, (1, 0, 2, 2)), wq, bias.double(),
+                                     stride=(2, 1))[..., :To]
+    out = torch.empty(B, Fo, To, N, device=DEV, dtype=torch.bfloat16 if out_bf16 else torch.float32)
+    nblk = ops.conv_mblocks(B, Fo, To)
+    st = torch.full((nblk * N * 2,), float("nan"), device=DEV, dtype=torch.float64)
+    ops.conv([ops.seg_bftc(x.to(DEV)) for x in segs_h], taps, B, Fo, To, N, wp, bias.to(DEV), out,
+             ops.OutMap(Fo * To * N, To * N, N), stride_f=2, stats=st)
+    o = out.permute(0, 3, 1, 2).double().cpu()
+    tol = 8e-3 if out_bf16 else 1e-4
+    np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=tol, atol=tol)
+    stc = st.view(nblk, N, 2).cpu()
+    assert torch.isfinite(stc).all(), "every 128-row partial must be written"
+    np.testing.assert_allclose(stc[:, :, 0].sum(0).numpy(), ref.sum((0, 2, 3)).numpy(), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(stc[:, :, 1].sum(0).numpy(), (ref ** 2).sum((0, 2, 3)).numpy(), rtol=1e-5)
+
 def test_stft_istft_golden():
     st = golden("stft.npz")
     m = _models("student")
