@@ -103,6 +103,15 @@ typedef struct {
                         (pairs of consecutive k), NP = clskd_conv_direct_np(N), zero columns for
                         n >= N -> direct-convolution kernel (narrow GEMMs: N <= 16, or K <= 64
                         with N <= 64; see clskd_conv_direct_ok). */
+  /* Optional K-table structure (ntaps = 0: not provided).  When given, K is ordered (tap,
+     segment, channel) with ctot = sum(seg_c) channels per tap and tap t's displacement
+     (tap_df[t], tap_dt[t]); this lets small-N bf16 launches run the halo-tiled kernel (input
+     tile staged once per channel chunk and reused across taps, weights resident in LDS). */
+  int32_t ntaps;
+  int32_t ctot;
+  int32_t seg_c[CLSKD_MAX_SEGS];
+  int16_t tap_df[16];
+  int16_t tap_dt[16];
 } clskd_conv_desc;
 
 #define CLSKD_WLAYOUT_NK 0

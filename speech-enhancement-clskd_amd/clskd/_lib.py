@@ -34,7 +34,9 @@ class ConvDesc(C.Structure):
                 ("oT", C.c_int64), ("oNhi", C.c_int64), ("oNlo", C.c_int64), ("nlo", C.c_int32),
                 ("of_mul", C.c_int32), ("of_add", C.c_int32), ("compute", C.c_int32),
                 ("in_dtype", C.c_int32), ("out_dtype", C.c_int32), ("stats", C.c_void_p),
-                ("kvec", C.c_int32), ("wlayout", C.c_int32)]
+                ("kvec", C.c_int32), ("wlayout", C.c_int32), ("ntaps", C.c_int32),
+                ("ctot", C.c_int32), ("seg_c", C.c_int32 * MAX_SEGS), ("tap_df", C.c_int16 * 16),
+                ("tap_dt", C.c_int16 * 16)]
 
 
 class GramJob(C.Structure):

@@ -292,6 +292,13 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
     else:
         d.stats = None
     d.kvec = kvec
+    if len(taps) <= 16:  # K-table structure (tap, segment, channel) for the halo-tiled kernel
+        d.ntaps = len(taps)
+        d.ctot = sum(g.C for g in geoms)
+        for i, g in enumerate(geoms):
+            d.seg_c[i] = g.C
+        for i, (dF, dT) in enumerate(taps):
+            d.tap_df[i], d.tap_dt[i] = dF, dT
     if KernelTimer.active and not torch.cuda.is_current_stream_capturing():
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)

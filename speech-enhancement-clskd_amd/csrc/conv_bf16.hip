@@ -380,7 +380,18 @@ static int launch_big(const clskd_conv_desc& d, hipStream_t st) {
 // engine is bound by DMA issue/latency, not MFMA (tools/conv_micro.py: 13-25 % faster for
 // BN >= 64).  BN = 32 keeps 4 waves (four 32x32 MFMA tiles).  CLSKD_BF16_WAVES=4 selects the
 // 4-wave tiles everywhere (A/B measurements).
+int launch_conv_halo(const clskd_conv_desc& d, hipStream_t st, bool* launched);
+
 int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
+  static const bool no_halo = [] {  // A/B switch: CLSKD_NO_HALO=1 keeps narrow layers on the engine
+    const char* e = getenv("CLSKD_NO_HALO");
+    return e && e[0] == '1';
+  }();
+  if (!no_halo) {
+    bool launched = false;
+    const int rc = launch_conv_halo(d, st, &launched);
+    if (rc != CLSKD_OK || launched) return rc;
+  }
   static const int nw = [] {
     const char* e = getenv("CLSKD_BF16_WAVES");
     return e && e[0] == '4' ? 4 : 8;

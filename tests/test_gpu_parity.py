@@ -165,6 +165,61 @@ def test_conv_bf16_engine_against_torch(N, out_bf16):
     np.testing.assert_allclose(stc[:, :, 0].sum(0).numpy(), ref.sum((0, 2, 3)).numpy(), rtol=1e-5, atol=1e-3)
     np.testing.assert_allclose(stc[:, :, 1].sum(0).numpy(), (ref ** 2).sum((0, 2, 3)).numpy(), rtol=1e-5)
 
+
+HALO_CASES = {
+    # name: (segment channels, N, taps, stride_f, Fi, Fo, of_mul, of_add, out_bf16)
+    "abf3x3_n32": ((64,), 32, [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], 1, 24, 24, 1, 0, True),
+    "abf3x3_n64": ((64,), 64, [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], 1, 24, 24, 1, 0, True),
+    "enc5x2_s2": ((32,), 64, [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)], 2, 48, 24, 1, 0, True),
+    "dec_parity1": ((32, 32), 32, [(dF, -kt) for dF in (1, 0) for kt in (0, 1)], 1, 24, 24, 2, 1, False),
+}
+
+
+@pytest.mark.parametrize("case", sorted(HALO_CASES))
+def test_conv_halo_kernel_against_torch(case):
+    """Halo-tiled narrow bf16 conv (weights resident in LDS, input halo reused across taps):
+    shapes the dispatcher routes there (N <= 64, channel runs of 32) incl. two segments, stride-2
+    F and an interleaved (polyphase) output map, fused BN statistics; vs torch fp64 on the same
+    bf16 operands.  Tolerance 1e-4 relative (fp32 out) / 8e-3 (bf16 out); stats 1e-5."""
+    from clskd import ops
+    segc, N, taps, sf, Fi, Fo, of_mul, of_add, out_bf16 = HALO_CASES[case]
+    g = torch.Generator().manual_seed(len(case) * 7 + N)
+    B, T = 3, 100
+    segs_h = [torch.randn(B, Fi, T, c, generator=g).to(torch.bfloat16) for c in segc]
+    Cin = sum(segc)
+    K = len(taps) * Cin
+    w = torch.randn(N, len(taps), Cin, generator=g) * 0.05
+    bias = torch.randn(N, generator=g)
+    wp = ops.pack_weight(w.to(DEV), K, "bf16")
+    assert not ops.direct_ok(N, wp.shape[1])
+    wq = wp[:, :K].float().cpu().double().view(N, len(taps), Cin)
+    x = torch.cat([s.double() for s in segs_h], 3)  # [B, Fi, T, Cin]
+    ref = bias.double().view(1, 1, 1, N).expand(B, Fo, T, N).clone()
+    for ti, (dF, dT) in enumerate(taps):
+        fi = torch.arange(Fo) * sf + dF
+        tt = torch.arange(T) + dT
+        vf = (fi >= 0) & (fi < Fi)
+        vt = (tt >= 0) & (tt < T)
+        sub = torch.zeros(B, Fo, T, Cin, dtype=torch.float64)
+        sub[:, vf.nonzero()[:, 0][:, None], vt.nonzero()[:, 0][None, :]] = \
+            x[:, fi[vf][:, None], tt[vt][None, :]]
+        ref += torch.einsum("bftc,nc->bftn", sub, wq[:, ti])
+    Fout = Fo * of_mul
+    out = torch.zeros(B, Fout, T, N, device=DEV, dtype=torch.bfloat16 if out_bf16 else torch.float32)
+    nblk = ops.conv_mblocks(B, Fo, T)
+    st = torch.full((nblk * N * 2,), float("nan"), device=DEV, dtype=torch.float64)
+    ops.conv([ops.seg_bftc(s.to(DEV)) for s in segs_h], taps, B, Fo, T, N, wp, bias.to(DEV), out,
+             ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add), stride_f=sf, stats=st)
+    o = out.double().cpu()[:, of_add::of_mul]
+    tol = 8e-3 if out_bf16 else 1e-4
+    np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=tol, atol=tol)
+    if of_mul > 1:  # the other parity's rows are untouched
+        assert torch.all(out.double().cpu()[:, (of_add + 1) % of_mul::of_mul] == 0)
+    stc = st.view(nblk, N, 2).cpu()
+    assert torch.isfinite(stc).all(), "every statistics slot must be written"
+    np.testing.assert_allclose(stc[:, :, 0].sum(0).numpy(), ref.sum((0, 1, 2)).numpy(), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(stc[:, :, 1].sum(0).numpy(), (ref ** 2).sum((0, 1, 2)).numpy(), rtol=1e-5)
+
 def test_stft_istft_golden():
     st = golden("stft.npz")
     m = _models("student")
