@@ -118,6 +118,10 @@ typedef struct {
 #define CLSKD_WLAYOUT_DIRECT 1
 
 int clskd_conv2d_fwd(const clskd_conv_desc* d, void* stream);
+/* Instance name ("kernel<template args>", as rocprofv3 reports it) of the kernel the calling
+ * thread's last successful clskd_conv2d_fwd launched — the dispatch policy (direct / halo /
+ * 128- or 256-row bf16 engine / fp32 engine) is the library's, so hosts label timings with it. */
+const char* clskd_conv_last_kernel(void);
 /* Direct-path helpers: padded output width NP of the direct layout, and whether an (N, K)
  * GEMM is served by the direct kernel (returns 1) — hosts pack CLSKD_WLAYOUT_DIRECT weights
  * exactly when this is 1. */
@@ -203,6 +207,33 @@ int clskd_abf_fuse(const void* x, const void* res, int32_t B, int32_t F, int32_t
                    int32_t dtype, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Uniform weight re-draw (replaces the per-step ABF rebuild of framework.py:194-195 —
+ * nn.init.kaiming_uniform_(w, a=1) on conv1/conv2 and Conv2d.reset_parameters on att_conv —
+ * and the repacking of the drawn weights).  Job k draws numel values U(-bound, bound) into
+ * param (contiguous fp32, layout [N][Cin][ntap]) and, when packed != NULL, the same values into
+ * the packed conv operand packed[n][tap*Cin + c] (row pitch Kp, storage packed_dtype; padding
+ * columns untouched).  Philox4x32-10 keyed by `seed`; the draw counter state[0] (device
+ * uint64[2] = {counter, ticket}, zeroed once by the caller; one state per concurrently running
+ * stream) is read by the kernel and advanced by its last workgroup, so graph replays re-draw.
+ * Job arrays are host memory passed as kernel arguments.  Distribution matches the reference;
+ * the random stream is this library's own (the reference draws from torch's generator).
+ * -------------------------------------------------------------------------------------- */
+#define CLSKD_DRAW_MAX_JOBS 32
+
+typedef struct {
+  float* param;
+  void* packed;
+  int64_t numel;
+  int32_t Cin, ntap, Kp;
+  int32_t packed_dtype;
+  float bound;
+  int32_t stream_id; /* distinct per job within a launch (decorrelates the Philox counters) */
+} clskd_draw_job;
+
+int clskd_uniform_redraw(const clskd_draw_job* jobs, int32_t njobs, uint64_t seed,
+                         uint64_t* state, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * SPKD / Gram (framework.py:150-172; replaces SPKDLoss.forward / get_similarity_matrix, the
  * per-tap torch.mm(z, z.t()) of framework.py:156-160, for every tap of a step at once).
  * A gram job views a tap as z_b = x[b][p][c0 .. c0+Cs) for p < P positions with position
@@ -215,6 +246,10 @@ int clskd_abf_fuse(const void* x, const void* res, int32_t B, int32_t F, int32_t
  *                     sum the slabs in order (fp64), L1-normalise rows (normalize(G, p=1) — the
  *                     reference passes 1 as p), loss = ||Gt-Gs||_F^2 (/B^2 if batchmean);
  *                     writes losses[i] and, if non-null, grams_s/grams_t[i][B][B].
+ * clskd_spkd_finalize_ranges: the same finalize over slab ranges given directly (pair i: the
+ *                     s_nslab[i] slabs at s_slabs[i], device pointers into any slab buffers),
+ *                     so a step can run its Gram launches on several streams — each as soon
+ *                     as its features exist — and finalize once after joining them.
  * -------------------------------------------------------------------------------------- */
 #define CLSKD_GRAM_MAX_JOBS 32   /* jobs per kernel launch (the library splits larger lists) */
 #define CLSKD_SPKD_MAX_PAIRS 64  /* pairs per finalize launch (likewise) */
@@ -236,6 +271,10 @@ int clskd_gram_partial(const clskd_gram_job* jobs, int32_t njobs, int32_t B, flo
 int clskd_spkd_finalize(const clskd_gram_job* jobs, int32_t njobs, const int32_t* pairs,
                         int32_t npairs, int32_t B, int32_t batchmean, const float* slabs,
                         float* grams_s, float* grams_t, float* losses, void* stream);
+int clskd_spkd_finalize_ranges(const float* const* s_slabs, const int32_t* s_nslab,
+                               const float* const* t_slabs, const int32_t* t_nslab,
+                               int32_t npairs, int32_t B, int32_t batchmean, float* grams_s,
+                               float* grams_t, float* losses, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Losses.

@@ -46,13 +46,21 @@ class GramJob(C.Structure):
                 ("reserved", C.c_int32)]
 
 
+class DrawJob(C.Structure):
+    _fields_ = [("param", C.c_void_p), ("packed", C.c_void_p), ("numel", C.c_int64),
+                ("Cin", C.c_int32), ("ntap", C.c_int32), ("Kp", C.c_int32),
+                ("packed_dtype", C.c_int32), ("bound", C.c_float), ("stream_id", C.c_int32)]
+
+
 assert C.sizeof(KtabEntry) == 8
+assert C.sizeof(DrawJob) == 48
 assert C.sizeof(GramJob) == 56
 
 _p, _i32, _i64, _f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float
 
 SIGNATURES = {
     "clskd_last_error": (C.c_char_p, []),
+    "clskd_conv_last_kernel": (C.c_char_p, []),
     "clskd_version": (_i32, []),
     "clskd_conv2d_fwd": (_i32, [C.POINTER(ConvDesc), _p]),
     "clskd_conv_direct_np": (_i32, [_i32]),
@@ -74,6 +82,10 @@ SIGNATURES = {
     "clskd_abf_fuse": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _i32, _p]),
     "clskd_gram_partial": (_i32, [_p, _i32, _i32, _p, _p]),
     "clskd_spkd_finalize": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
+    "clskd_uniform_redraw": (_i32, [_p, _i32, C.c_uint64, _p, _p]),
+    "clskd_spkd_finalize_ranges": (_i32, [C.POINTER(C.c_void_p), C.POINTER(C.c_int32),
+                                          C.POINTER(C.c_void_p), C.POINTER(C.c_int32), _i32, _i32,
+                                          _i32, _p, _p, _p, _p]),
     "clskd_stft_mag_loss": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p]),
     "clskd_stft_loss_finalize": (_i32, [_p, _i64, _f32, _f32, _i32, _p, _p]),
     "clskd_sisnr_rows": (_i32, [_p, _p, _i32, _i32, _i64, _i64, _f32, _p, _p]),
@@ -92,11 +104,14 @@ def header_symbols():
 
 
 _LIB = None
+_GPU_OK = False
 
 
 def load(require_gpu=True):
     """Load the shared library.  Raises (never falls back) when missing."""
-    global _LIB
+    global _LIB, _GPU_OK
+    if _GPU_OK:  # launch fast path: library loaded and a HIP device already verified
+        return _LIB
     if _LIB is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"libclskd_hip.so not built at {LIB_PATH}; run __graft_entry__.build()")
@@ -106,8 +121,10 @@ def load(require_gpu=True):
             fn.restype = res
             fn.argtypes = args
         _LIB = lib
-    if require_gpu and not torch.cuda.is_available():
-        raise RuntimeError("clskd: no HIP device visible; the MI355X path has no CPU fallback")
+    if require_gpu:
+        if not torch.cuda.is_available():
+            raise RuntimeError("clskd: no HIP device visible; the MI355X path has no CPU fallback")
+        _GPU_OK = True
     return _LIB
 
 
@@ -117,9 +134,15 @@ def check(rc, what=""):
         raise RuntimeError(f"clskd {what} failed ({rc}): {msg}")
 
 
-def stream_ptr(device=None):
-    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+_raw_stream = torch._C._cuda_getCurrentRawStream
+_cur_dev = torch._C._cuda_getDevice
+
+
+def stream_ptr():
+    """hipStream_t (as an int) of torch's current stream on the current device."""
+    return _raw_stream(_cur_dev())
 
 
 def ptr(t):
-    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+    """Device address of a tensor for a c_void_p argument (None -> NULL)."""
+    return t.data_ptr() if t is not None else None

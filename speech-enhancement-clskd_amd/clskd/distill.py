@@ -17,24 +17,42 @@ Deliberate equivalences (documented in DESIGN.md):
     modules are built once (``abf_reinit='once'``) or re-drawn every step on the device
     (``abf_reinit='step'``, kaiming_uniform(a=1) like framework.py:194-195).
 """
+import os
+
 import torch
 import torch.nn as nn
 
 from . import config as cfg
-from . import ops
+from . import _lib, ops
 from .framework import MultiResolutionSTFTLoss, SPKDLoss, build_review_kd
 from .model import DCCRN
 
 
 _SIDE = {}
+_MARKS = None  # diagnostics (tools/stream_marks.py): list collecting (label, event) per step
+
+
+def _mark(label, stream):
+    if _MARKS is not None:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream)
+        _MARKS.append((label, ev))
+
+
+_PRIO = os.environ.get("CLSKD_STREAM_PRIO", "none")
 
 
 def _side_stream(dev, which=0):
-    """Extra HIP streams per device (which = 0, 1): the student chain runs beside the teacher,
-    overlapping the latency-bound LSTM recurrences and small kernels with the GEMMs."""
+    """Extra HIP streams per device.  which = 0, 1: the student chain and the ReviewKD-encoder /
+    MRSTFT chain run beside the teacher, overlapping the latency-bound LSTM recurrences and small
+    kernels with the GEMMs.  which = 2: the teacher's stream (the step's critical path when the
+    three share the CUs).  CLSKD_STREAM_PRIO=teacher creates it at high priority; measured on
+    MI355X that is 0.5-1 % slower than equal priorities (the default), since the side chains'
+    small kernels then queue behind the teacher's large GEMMs."""
     key = (torch.device(dev).index, which)
     if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(device=dev)
+        prio = -1 if (which == 2 and _PRIO == "teacher") else 0
+        _SIDE[key] = torch.cuda.Stream(device=dev, priority=prio)
     return _SIDE[key]
 
 
@@ -62,6 +80,11 @@ class KnowledgeDistillation(nn.Module):
         self.review_encoder = build_review_kd(None, "encoder")
         self.review_decoder = build_review_kd(None, "decoder")
         self.last = None
+        # ABF re-draw: Philox keys from torch's CPU generator (torch.manual_seed reproducible)
+        k = torch.randint(0, 2 ** 62, (2,), dtype=torch.int64)
+        self._draw_seed = {"encoder": int(k[0]), "decoder": int(k[1])}
+        self._draw_state = {}
+        self._draw_jobs = {}
         self.set_precision(precision)
 
     def set_precision(self, precision):
@@ -87,18 +110,36 @@ class KnowledgeDistillation(nn.Module):
 
     def _reinit_abf(self, which=None):
         """Re-draw the ABF weights (framework.py:194-195 / distill.py:92-96) of one ReviewKD
-        module (which = 'encoder' | 'decoder') or of both."""
+        module (which = 'encoder' | 'decoder') or of both: one clskd_uniform_redraw launch per
+        module on the current stream (parameters and packed operands written together)."""
         if self.abf_reinit != "step":
             return
-        mods = {"encoder": (self.review_encoder,), "decoder": (self.review_decoder,),
-                None: (self.review_encoder, self.review_decoder)}[which]
-        with torch.no_grad():
-            for rk in mods:
-                for abf in rk.abfs:
-                    nn.init.kaiming_uniform_(abf.conv1[0].weight, a=1)
-                    nn.init.kaiming_uniform_(abf.conv2[0].weight, a=1)
-                    if abf.att_conv is not None:
-                        abf.att_conv[0].reset_parameters()
+        names = ("encoder", "decoder") if which is None else (which,)
+        for name in names:
+            rk = self.review_encoder if name == "encoder" else self.review_decoder
+            jobs = [j for abf in rk.abfs for j in abf.redraw_jobs()]
+            dev = jobs[0][0].device
+            st = self._draw_state.get((name, dev))
+            if st is None:  # {draw counter, ticket} per module: the two modules draw on
+                st = torch.zeros(2, dtype=torch.int64, device=dev)  # different streams
+                self._draw_state[(name, dev)] = st
+            key = tuple((w.data_ptr(), wp.data_ptr() if wp is not None else 0) for w, wp, *_ in jobs)
+            arr = self._draw_jobs.get((name, key))
+            if arr is None:
+                arr = (_lib.DrawJob * len(jobs))()
+                for i, (w, wp, cin, ntap, bound) in enumerate(jobs):
+                    assert w.dtype == torch.float32 and w.is_contiguous()
+                    if wp is not None:
+                        assert wp.is_contiguous() and wp.shape[0] == w.shape[0]
+                    arr[i] = _lib.DrawJob(w.data_ptr(), wp.data_ptr() if wp is not None else None,
+                                          w.numel(), cin, ntap, wp.shape[1] if wp is not None else 0,
+                                          ops._dt(wp) if wp is not None else 0, bound, i)
+                self._draw_jobs = {k: v for k, v in self._draw_jobs.items() if k[0] != name}
+                self._draw_jobs[(name, key)] = arr
+            ops.check(ops.lib().clskd_uniform_redraw(arr, len(jobs), self._draw_seed[name],
+                                                     st.data_ptr(), ops._stream()), "uniform_redraw")
+            for abf in rk.abfs:
+                abf.after_redraw()
 
     def training_step(self, batch, batch_idx=0, return_parts=False):
         X, y = batch
@@ -122,6 +163,7 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     y = y.float().reshape(X.shape[0], -1).contiguous()
     B = X.shape[0]
     dev = X.device
+    _mark("start", torch.cuda.current_stream(dev))
     spec = teacher.spectrum(X)
     # both ConvSTFTs are the fixed (win 400, hop 100, fft 512) kernel of the same window type
     s_spec = spec if teacher.win_type == student.win_type else None
@@ -142,42 +184,65 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
         with torch.cuda.stream(side2):
             reinit("encoder")
 
+    # SPKD Gram partials run on the stream that produced their features, as soon as those
+    # exist (side2: ReviewKD-encoder maps, side: ReviewKD-decoder maps + student dec_in halves,
+    # main: teacher taps); one finalize on main after the join (framework.py:150-172).
     def fork_review_encoder(enc):
         ev = torch.cuda.Event()
         ev.record(side)
         with torch.cuda.stream(side2):
             side2.wait_event(ev)
-            held["s_enc"] = review_encoder.forward_bftc(enc)
+            _mark("side2: student encoder ready", side2)
+            s_enc = review_encoder.forward_bftc(enc)
+            _mark("side2: review encoder done", side2)
+            held["s_enc"] = s_enc
+            held["g_enc"] = ops.GramSlabs([_gram_bftc(a) for a in s_enc], B)
+            _mark("side2: enc grams done", side2)
 
     with torch.cuda.stream(side):
         sf = student.run(X, train=student.training, bn_updates=2 if student.training else 0,
                          spec=s_spec, want_masks=False, on_encoder=fork_review_encoder)
         student_done = torch.cuda.Event()
         student_done.record(side)
+        _mark("side: student done", side)
         if reinit is not None:
             reinit("decoder")
         s_dec = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5])
+        Chs = sf["dec_in"].shape[-1] // 2
+        g_dec = ops.GramSlabs([_gram_bftc(a) for a in s_dec] +
+                              [_gram_bftc(sf["dec_in"], 0, Chs), _gram_bftc(sf["dec_in"], Chs, Chs)],
+                              B)
+        _mark("side: review decoder + grams done", side)
     with torch.cuda.stream(side2):
         side2.wait_event(student_done)
         stft_loss(sf["out_wav"], y, out2=buf[0:2])
-    s_enc = held["s_enc"]
-    tf = teacher.run(X, train=teacher.training, bn_updates=1, spec=spec, want_masks=False)
+        _mark("side2: mrstft done", side2)
+    s_enc, g_enc = held["s_enc"], held["g_enc"]
+    tstream = _side_stream(dev, 2)
+    tstream.wait_stream(main)
+    with torch.cuda.stream(tstream):
+        tf = teacher.run(X, train=teacher.training, bn_updates=1, spec=spec, want_masks=False)
+        _mark("teacher: done", tstream)
+        t_dec = [tf["dec_in"]] + tf["dec"][:5]
+        Cht = tf["dec_in"].shape[-1] // 2
+        g_t = ops.GramSlabs([_gram_bftc(a) for a in tf["enc"]] + [_gram_bftc(a) for a in t_dec] +
+                            [_gram_bftc(tf["dec_in"], 0, Cht), _gram_bftc(tf["dec_in"], Cht, Cht)],
+                            B)
+        _mark("teacher: grams done", tstream)
+    main.wait_stream(tstream)
     main.wait_stream(side)
     main.wait_stream(side2)
-    t_dec = [tf["dec_in"]] + tf["dec"][:5]
-    pairs = [(_gram_bftc(a), _gram_bftc(b)) for a, b in zip(s_enc, tf["enc"])]
-    pairs += [(_gram_bftc(a), _gram_bftc(b)) for a, b in zip(s_dec, t_dec)]
-    Chs = sf["dec_in"].shape[-1] // 2
-    Cht = tf["dec_in"].shape[-1] // 2
-    pairs += [(_gram_bftc(sf["dec_in"], 0, Chs), _gram_bftc(tf["dec_in"], 0, Cht)),
-              (_gram_bftc(sf["dec_in"], Chs, Chs), _gram_bftc(tf["dec_in"], Cht, Cht))]
-    assert len(pairs) == 14
-    ops.spkd_losses(pairs, B, batchmean=True, out=buf[2:])
+    _mark("main: joined", main)
+    s_refs = g_enc.refs + g_dec.refs
+    assert len(s_refs) == 14 and len(g_t.refs) == 14
+    ops.spkd_finalize(s_refs, g_t.refs, B, batchmean=True, out=buf[2:])
     total = torch.empty((), dtype=torch.float32, device=dev)
     ops.sum_f32(buf[1:], total)
+    _mark("main: end", main)
     return dict(loss=total, base=buf[1], sc=buf[0], spkd=buf[2:], enc=buf[2:8], dec=buf[8:14],
                 clstm_real=buf[14], clstm_img=buf[15], student_wav=sf["out_wav"],
-                teacher_wav=tf["out_wav"], s_enc=s_enc, s_dec=s_dec, t=tf, s=sf)
+                teacher_wav=tf["out_wav"], s_enc=s_enc, s_dec=s_dec, t=tf, s=sf,
+                gram_slabs=(g_enc, g_dec, g_t))
 
 
 class SPKDDistillation(nn.Module):

@@ -182,10 +182,46 @@ class ABF(nn.Module):
     def act_dtype(self):
         return torch.bfloat16 if self.compute == "bf16" else torch.float32
 
-    def _weights(self, in_dtype):
+    def _params(self):
         ps = [self.conv1[0].weight, self.conv2[0].weight]
         if self.att_conv is not None:
             ps += [self.att_conv[0].weight, self.att_conv[0].bias]
+        return ps
+
+    def redraw_jobs(self):
+        """Draw jobs (clskd_uniform_redraw) re-initialising this ABF like framework.py:179-195:
+        conv1/conv2 kaiming_uniform(a=1) -> U(+-sqrt(3/fan_in)); att_conv default Conv2d init ->
+        weight and bias U(+-1/sqrt(fan_in)).  Targets the packed operands of the current
+        weight cache as well, so no repack follows the draw."""
+        ent = self._wcache.get("w")
+        w1p = w2p = None
+        if ent is not None:
+            w1p, w2p, _ = ent[1]
+        jobs = []
+        for w, wp in ((self.conv1[0].weight, w1p), (self.conv2[0].weight, w2p)):
+            N, Cin, kh, kw = w.shape
+            jobs.append((w, wp, Cin, kh * kw, math.sqrt(3.0 / (Cin * kh * kw))))
+        if self.att_conv is not None:
+            aw, ab = self.att_conv[0].weight, self.att_conv[0].bias
+            fan_in = aw.shape[1] * aw.shape[2] * aw.shape[3]
+            jobs.append((aw, None, aw.shape[1], aw.shape[2] * aw.shape[3], 1.0 / math.sqrt(fan_in)))
+            jobs.append((ab, None, 1, 1, 1.0 / math.sqrt(fan_in)))
+        return jobs
+
+    def after_redraw(self):
+        """The parameters were rewritten in place by a kernel: advance their version counters
+        (autograd / cache bookkeeping) and mark the packed operands (written by the same
+        kernel) current."""
+        ps = self._params()
+        torch.autograd.graph.increment_version(ps)
+        ent = self._wcache.get("w")
+        if ent is not None:
+            w1p, w2p, _ = ent[1]
+            torch.autograd.graph.increment_version([w1p, w2p])  # invalidates derived layouts
+            self._wcache["w"] = (_pv(*ps) + ent[0][-2:], ent[1])
+
+    def _weights(self, in_dtype):
+        ps = self._params()
         ver = _pv(*ps) + (self.compute, in_dtype)
         ent = self._wcache.get("w")
         if ent is None or ent[0] != ver:

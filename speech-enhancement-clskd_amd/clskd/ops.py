@@ -29,10 +29,15 @@ class KernelTimer:
     Enabled by bench.py over its timed region; records (kernel variant, flops, start, end)."""
     active = False
     records = []
+    only = None  # optional kernel-instance name: time just that kernel's launches
 
     @classmethod
-    def start(cls):
-        cls.active, cls.records = True, []
+    def start(cls, only=None):
+        cls.active, cls.records, cls.only = True, [], only
+
+    @classmethod
+    def wants(cls, name):
+        return cls.only is None or name == cls.only
 
     @classmethod
     def per_launch(cls):
@@ -98,26 +103,7 @@ def direct_weight(wpacked):
     return wd
 
 
-_BF16_WAVES = 4 if os.environ.get("CLSKD_BF16_WAVES", "") == "4" else 8
-
-
-def conv_kernel_name(N, vec4, bf16=False, K=None, out_bf16=False, kvec=None):
-    """Canonical name of the kernel instance a conv launch runs (the template arguments rocprof
-    shows): engine, tile width, waves / load width, output storage."""
-    out = "bf16" if out_bf16 else "float"
-    if K is not None and direct_ok(N, K):
-        npad = direct_np(N)
-        return f"conv_direct_kernel<{npad},{kvec or (8 if bf16 else 4)},{'bf16' if bf16 else 'float'},{out}>"
-    if bf16:
-        bn = 32 if N <= 32 else 64 if N <= 64 else 128 if N <= 128 else 256
-        nw = 4 if bn == 32 else _BF16_WAVES
-        return f"conv_igemm_bf16_dma<{bn},{nw},3,{out}>"
-    bn = 32 if N <= 32 else (64 if N <= 64 else 128)
-    return f"conv_igemm_f32<{bn},{'true' if vec4 else 'false'},{out}>"
-
-
-def _stream():
-    return _lib.stream_ptr()
+_stream = _lib.stream_ptr
 
 
 # ------------------------------------------------------------------------------------------
@@ -232,18 +218,21 @@ def conv_mblocks(B, Fo, To):
     return -(-(B * Fo * To) // 128)
 
 
-def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, stride_f=1,
-         stride_t=1, stats=None, stats_offset=0):
-    """out[b, fo*of_mul+of_add, to, n] = bias[n] + sum_k A[(b,fo,to),k] W[n,k].
-    bf16 segments run the LDS-DMA bf16-MFMA engine (weights packed bf16, K % 64); fp32 segments
-    the fp32-MFMA engine (weights fp32, K % 16).  `out` may be fp32 or bf16 storage."""
-    dev = out.device
-    geoms = tuple(s.geom for s in segs)
+class _ConvPlan:
+    """Launch descriptor of one conv signature, built once; per call only the pointers change."""
+    __slots__ = ("desc", "segs", "nseg", "direct", "name", "flops", "shape", "nstats", "osize")
+
+
+_CONV_PLANS = {}
+
+
+def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, stride_f, stride_t,
+               stats):
     in_dt = {_dt(s.tensor) for s in segs}
     assert len(in_dt) == 1, "all segments of one conv share a storage type"
     in_dt = in_dt.pop()
     bf16 = in_dt == _lib.BF16
-    kt, ks, K, Kp, vec4 = _ktab(geoms, tuple(taps), dev.index or 0, BK_BF16 if bf16 else BK)
+    kt, ks, K, Kp, vec4 = _ktab(geoms, taps, out.device.index or 0, BK_BF16 if bf16 else BK)
     assert wpacked.shape == (N, Kp) and wpacked.is_contiguous(), (wpacked.shape, N, Kp)
     assert wpacked.dtype == (torch.bfloat16 if bf16 else torch.float32), wpacked.dtype
     for s in segs:
@@ -266,31 +255,19 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
     d.B, d.Fo, d.To, d.N, d.K = B, Fo, To, N, Kp
     d.stride_f, d.stride_t = stride_f, stride_t
     d.nseg = len(segs)
-    for i, s in enumerate(segs):
-        g = s.geom
-        d.seg[i] = _lib.Seg(seg_addr(s), g.sB, g.sF, g.sT, g.F, g.T)
+    for i, g in enumerate(geoms):
+        d.seg[i] = _lib.Seg(0, g.sB, g.sF, g.sT, g.F, g.T)
     for i in range(len(segs), _lib.MAX_SEGS):
         d.seg[i] = d.seg[0]
     d.ktab, d.kseg, d.vec4 = kt.data_ptr(), ks.data_ptr(), int(vec4)
-    if direct_ok(N, Kp):
-        wd = direct_weight(wpacked)
-        d.weight, d.wlayout = wd.data_ptr(), _lib.WLAYOUT_DIRECT
-    else:
-        wd = None
-        d.weight, d.wlayout = wpacked.data_ptr(), _lib.WLAYOUT_NK
-    d.bias = bias.data_ptr() if bias is not None else None
-    d.out = out.data_ptr() + out.element_size() * out_offset
+    direct = direct_ok(N, Kp)
+    d.wlayout = _lib.WLAYOUT_DIRECT if direct else _lib.WLAYOUT_NK
     d.oB, d.oF, d.oT, d.oNhi, d.oNlo = omap.oB, omap.oF, omap.oT, omap.oNhi, omap.oNlo
     d.nlo = min(omap.nlo, 1 << 30)
     d.of_mul, d.of_add = omap.of_mul, omap.of_add
     d.compute = _lib.BF16 if bf16 else _lib.F32
     d.in_dtype = in_dt
     d.out_dtype = _dt(out)
-    if stats is not None:
-        assert stats.dtype == torch.float64 and stats.numel() >= stats_offset + conv_mblocks(B, Fo, To) * N * 2
-        d.stats = stats.data_ptr() + 8 * stats_offset
-    else:
-        d.stats = None
     d.kvec = kvec
     if len(taps) <= 16:  # K-table structure (tap, segment, channel) for the halo-tiled kernel
         d.ntaps = len(taps)
@@ -299,17 +276,74 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
             d.seg_c[i] = g.C
         for i, (dF, dT) in enumerate(taps):
             d.tap_df[i], d.tap_dt[i] = dF, dT
-    if KernelTimer.active and not torch.cuda.is_current_stream_capturing():
+    pl = _ConvPlan()
+    pl.desc, pl.nseg, pl.direct = d, len(segs), direct
+    pl.segs = [d.seg[i] for i in range(_lib.MAX_SEGS)]  # views into d (patched per call)
+    pl.name = None  # kernel instance the library dispatches to (read after the first launch)
+    pl.flops = 2.0 * B * Fo * To * N * K
+    pl.shape = (B * Fo * To, N, K, "bf16" if bf16 else "f32")
+    pl.nstats = conv_mblocks(B, Fo, To) * N * 2
+    pl.osize = out.element_size()
+    _CONV_PLANS[key] = pl
+    return pl
+
+
+def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, stride_f=1,
+         stride_t=1, stats=None, stats_offset=0):
+    """out[b, fo*of_mul+of_add, to, n] = bias[n] + sum_k A[(b,fo,to),k] W[n,k].
+    bf16 segments run the LDS-DMA bf16-MFMA engine (weights packed bf16, K % 64); fp32 segments
+    the fp32-MFMA engine (weights fp32, K % 16).  `out` may be fp32 or bf16 storage.
+    The descriptor of each launch signature (geometry, taps, output map, dtypes, pointer
+    alignment class) is built once (_conv_plan); a call patches only the pointers."""
+    addrs = [s.tensor.data_ptr() + s.tensor.element_size() * s.offset for s in segs]
+    taps = tuple(taps)
+    geoms = tuple(s.geom for s in segs)
+    key = (geoms, taps, B, Fo, To, N, wpacked.shape, wpacked.dtype, omap, stride_f, stride_t,
+           out.dtype, out.device.index, stats is None, bias is None,
+           tuple(a % 16 for a in addrs), tuple(s.tensor.dtype for s in segs))
+    pl = _CONV_PLANS.get(key)
+    if pl is None:
+        pl = _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, stride_f,
+                        stride_t, stats)
+    if not wpacked.is_contiguous():
+        raise RuntimeError("conv: packed weight must be contiguous")
+    d = pl.desc
+    sg = pl.segs
+    for i, a in enumerate(addrs):
+        sg[i].ptr = a
+    for i in range(pl.nseg, _lib.MAX_SEGS):
+        sg[i].ptr = addrs[0]
+    d.weight = direct_weight(wpacked).data_ptr() if pl.direct else wpacked.data_ptr()
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.out = out.data_ptr() + pl.osize * out_offset
+    if stats is not None:
+        if stats.dtype != torch.float64 or stats.numel() < stats_offset + pl.nstats:
+            raise RuntimeError("conv: fused statistics buffer must be float64 with room for "
+                               "2 x N x mblocks partials")
+        d.stats = stats.data_ptr() + 8 * stats_offset
+    else:
+        d.stats = None
+    L = lib()
+    if KernelTimer.active and not torch.cuda.is_current_stream_capturing() \
+            and KernelTimer.wants(pl.name):
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
-        check(lib().clskd_conv2d_fwd(C.byref(d), _stream()), "conv2d")
+        check(L.clskd_conv2d_fwd(d, _stream()), "conv2d")
         e1.record()
-        KernelTimer.records.append((conv_kernel_name(N, vec4, bf16, Kp, out.dtype == torch.bfloat16, kvec), 2.0 * B * Fo * To * N * K, e0, e1,
-                                    (B * Fo * To, N, K, "bf16" if bf16 else "f32")))
+        if pl.name is None:
+            pl.name = L.clskd_conv_last_kernel().decode()
+        KernelTimer.records.append((pl.name, pl.flops, e0, e1, pl.shape))
     else:
-        check(lib().clskd_conv2d_fwd(C.byref(d), _stream()), "conv2d")
+        check(L.clskd_conv2d_fwd(d, _stream()), "conv2d")
+        if pl.name is None:
+            pl.name = L.clskd_conv_last_kernel().decode()
     return out
+
+
+def conv_kernel_of_last_launch():
+    """Kernel instance (rocprof name, 'base<args>') of this thread's last conv launch."""
+    return lib().clskd_conv_last_kernel().decode()
 
 
 # ------------------------------------------------------------------------------------------
@@ -324,8 +358,9 @@ def batch_norm_bftc(x, y, gamma, beta, running_mean, running_var, train, momentu
     Cn = x.shape[-1]
     rows = x.numel() // Cn
     dev = x.device
-    scale = torch.empty(Cn, device=dev, dtype=torch.float32)
-    shift = torch.empty(Cn, device=dev, dtype=torch.float32)
+    coef = torch.empty(2 * Cn, device=dev, dtype=torch.float32)  # [scale | shift]
+    scale = coef.data_ptr()
+    shift = scale + 4 * Cn
     st = _stream()
     if train:
         if partial is not None:
@@ -347,13 +382,13 @@ def batch_norm_bftc(x, y, gamma, beta, running_mean, running_var, train, momentu
         check(L.clskd_bn_finalize(ptr(part), nblk, rows, Cn, ptr(gamma), ptr(beta), eps,
                                   ptr(running_mean) if upd else None,
                                   ptr(running_var) if upd else None, momentum, n_updates,
-                                  ptr(scale), ptr(shift), ptr(mean_o), ptr(var_o), st),
+                                  scale, shift, ptr(mean_o), ptr(var_o), st),
               "bn_finalize")
     else:
         check(L.clskd_bn_eval_coeffs(ptr(running_mean), ptr(running_var), ptr(gamma), ptr(beta),
-                                     eps, Cn, ptr(scale), ptr(shift), st), "bn_eval")
+                                     eps, Cn, scale, shift, st), "bn_eval")
     assert x.dtype == y.dtype
-    check(L.clskd_bn_apply(ptr(x), ptr(y), rows, Cn, ptr(scale), ptr(shift), ptr(alpha), _dt(x), st),
+    check(L.clskd_bn_apply(ptr(x), ptr(y), rows, Cn, scale, shift, ptr(alpha), _dt(x), st),
           "bn_apply")
     return y
 
@@ -447,38 +482,63 @@ def gram_view(t):
     return GramView(tc, 0, n, n // g, g, 0, g)
 
 
+class GramSlabs:
+    """Gram partials of some views, launched on the current stream into a slab buffer of their
+    own (clskd_gram_partial).  `refs[i]` = (device address of view i's first slab, slab count)
+    for clskd_spkd_finalize_ranges; the object owns the buffer (keep it until the finalize ran)."""
+
+    def __init__(self, views, B, chunk_elems=16384):
+        dev = views[0].tensor.device
+        jobs = (_lib.GramJob * len(views))()
+        first = 0
+        spans = []
+        for j, v in enumerate(views):
+            chunk = max(1, chunk_elems // v.Cs)
+            ns = -(-v.P // chunk)
+            dt = _dt(v.tensor)
+            assert v.Cs % (8 if dt == _lib.BF16 else 4) == 0
+            jobs[j] = _lib.GramJob(v.tensor.data_ptr() + v.tensor.element_size() * v.offset, v.sB,
+                                   v.P, v.Ctot, v.c0, v.Cs, chunk, first, ns, dt, 0)
+            spans.append((first, ns))
+            first += ns
+        self.slabs = torch.empty(first * 1024, dtype=torch.float32, device=dev)
+        base = self.slabs.data_ptr()
+        self.refs = [(base + 4096 * f, n) for f, n in spans]
+        # job table is a host array passed as kernel arguments (no upload, capturable)
+        check(lib().clskd_gram_partial(jobs, len(views), B, base, _stream()), "gram_partial")
+
+
+def spkd_finalize(s_refs, t_refs, B, batchmean=True, out=None, return_grams=False, device=None):
+    """Per pair i: Gs from the slabs s_refs[i], Gt from t_refs[i] (GramSlabs.refs entries, any
+    streams — the caller orders them before this launch); row-L1-normalise, ||Gt - Gs||^2."""
+    n = len(s_refs)
+    assert len(t_refs) == n and n >= 1
+    losses = out if out is not None else torch.empty(n, dtype=torch.float32, device=device)
+    assert losses.is_contiguous() and losses.numel() == n
+    gs = gt = None
+    if return_grams:
+        gs = torch.empty(n, B, B, dtype=torch.float32, device=losses.device)
+        gt = torch.empty_like(gs)
+    sp = (C.c_void_p * n)(*[r[0] for r in s_refs])
+    tp = (C.c_void_p * n)(*[r[0] for r in t_refs])
+    sn = (C.c_int32 * n)(*[r[1] for r in s_refs])
+    tn = (C.c_int32 * n)(*[r[1] for r in t_refs])
+    check(lib().clskd_spkd_finalize_ranges(sp, sn, tp, tn, n, B, int(batchmean), ptr(gs), ptr(gt),
+                                           ptr(losses), _stream()), "spkd_finalize")
+    if return_grams:
+        return losses, gs, gt
+    return losses
+
+
 def spkd_losses(pairs_views, B, batchmean=True, return_grams=False, chunk_elems=16384, out=None):
     """pairs_views: list of (student GramView, teacher GramView).  One gram launch for every
     view, one finalize launch for every pair.  Returns losses [npairs] (and grams)."""
     views = [v for pr in pairs_views for v in pr]
-    dev = views[0].tensor.device
-    jobs = (_lib.GramJob * len(views))()
-    first = 0
-    for j, v in enumerate(views):
-        chunk = max(1, chunk_elems // v.Cs)
-        ns = -(-v.P // chunk)
-        dt = _dt(v.tensor)
-        assert v.Cs % (8 if dt == _lib.BF16 else 4) == 0
-        jobs[j] = _lib.GramJob(v.tensor.data_ptr() + v.tensor.element_size() * v.offset, v.sB, v.P,
-                               v.Ctot, v.c0, v.Cs, chunk, first, ns, dt, 0)
-        first += ns
-    pairs = (C.c_int32 * (2 * len(pairs_views)))(*range(2 * len(pairs_views)))
-    slabs = torch.empty(first * 1024, dtype=torch.float32, device=dev)
-    losses = out if out is not None else torch.empty(len(pairs_views), dtype=torch.float32, device=dev)
-    assert losses.is_contiguous() and losses.numel() == len(pairs_views)
-    gs = gt = None
-    if return_grams:
-        gs = torch.empty(len(pairs_views), B, B, dtype=torch.float32, device=dev)
-        gt = torch.empty_like(gs)
-    L = lib()
-    st = _stream()
-    # job / pair tables are host arrays passed as kernel arguments (no upload, capturable)
-    check(L.clskd_gram_partial(jobs, len(views), B, ptr(slabs), st), "gram_partial")
-    check(L.clskd_spkd_finalize(jobs, len(views), pairs, len(pairs_views), B, int(batchmean),
-                                ptr(slabs), ptr(gs), ptr(gt), ptr(losses), st), "spkd_finalize")
-    if return_grams:
-        return losses, gs, gt
-    return losses
+    g = GramSlabs(views, B, chunk_elems)
+    r = spkd_finalize(g.refs[0::2], g.refs[1::2], B, batchmean, out, return_grams,
+                      device=views[0].tensor.device)
+    del g  # slab buffer returns to the allocator after both launches are enqueued (same stream)
+    return r
 
 
 # ------------------------------------------------------------------------------------------

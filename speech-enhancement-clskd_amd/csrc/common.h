@@ -11,6 +11,12 @@ namespace clskd {
 
 // ---- host-side error plumbing (thread-local message; no exceptions across the C ABI) ----------
 void set_error(const char* fmt, ...);
+// Instance name of the kernel the calling thread's last conv launch ran ("base<arg,...>", the
+// template arguments rocprof shows); read back through clskd_conv_last_kernel().
+void note_kernel(const char* fmt, ...);
+template <typename T> inline const char* type_name();
+template <> inline const char* type_name<float>() { return "float"; }
+template <> inline const char* type_name<__bf16>() { return "bf16"; }
 
 #define CLSKD_CHECK_ARG(cond, ...)                 \
   do {                                             \

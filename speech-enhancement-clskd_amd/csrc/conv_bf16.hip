@@ -355,6 +355,7 @@ static int launch_v2(const clskd_conv_desc& d, hipStream_t st) {
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
   ConvArgsV2 a{d};
   hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, BM), (unsigned)cdiv(d.N, BN)), dim3(NW * 64), lds, st, a);
+  note_kernel("conv_igemm_bf16_dma<%d,%d,%d,%d,%d,%s,%d>", BM, BK, BN, NW, S, type_name<OutT>(), DBG);
   return CLSKD_OK;
 }
 

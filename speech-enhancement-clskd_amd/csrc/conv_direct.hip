@@ -270,6 +270,8 @@ static void launch_np(const clskd_conv_desc& d, hipStream_t st) {
   else
     hipLaunchKernelGGL((conv_direct_kernel<NP, G, InT, float>), dim3((unsigned)cdiv(M, 128)),
                        dim3(128), lds, st, a);
+  note_kernel("conv_direct_kernel<%d,%d,%s,%s>", NP, G, type_name<InT>(),
+              d.out_dtype == CLSKD_BF16 ? "bf16" : "float");
 }
 
 template <int G, typename InT>

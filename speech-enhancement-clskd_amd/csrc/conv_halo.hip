@@ -448,6 +448,7 @@ int launch_conv_halo(const clskd_conv_desc& d, hipStream_t st, bool* launched) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,      \
                               160 * 1024);                                                     \
     hipLaunchKernelGGL(k, dim3(grid), dim3(512), lds, st, a);                                  \
+    note_kernel("conv_halo_kernel<%d,%s,%d>", BN_, type_name<O_>(), NT_);                      \
   } while (0)
 #define HALO_NT(NT_)                                                                           \
   do {                                                                                         \

@@ -313,7 +313,11 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
   ConvArgs a{d};
   const unsigned gx = (unsigned)cdiv(M, BM);
 #define LAUNCH(BN_, V_, O_)                                                                  \
-  hipLaunchKernelGGL((conv_igemm_f32<BN_, V_, O_>), dim3(gx, (unsigned)cdiv(d.N, BN_)), dim3(256), 0, st, a)
+  do {                                                                                       \
+    hipLaunchKernelGGL((conv_igemm_f32<BN_, V_, O_>), dim3(gx, (unsigned)cdiv(d.N, BN_)),     \
+                       dim3(256), 0, st, a);                                                 \
+    note_kernel("conv_igemm_f32<%d,%s,%s>", BN_, (V_) ? "true" : "false", type_name<O_>()); \
+  } while (0)
 #define LAUNCH_O(BN_, V_) \
   do { if (d.out_dtype == CLSKD_BF16) LAUNCH(BN_, V_, __bf16); else LAUNCH(BN_, V_, float); } while (0)
   if (d.N <= 32) {

@@ -7,6 +7,8 @@
 // v_mfma_f32_16x16x4_f32 operand layout (lane l: row l&15, 4 consecutive elements at 4*(l>>4));
 // A and B operands are the same register, so one load feeds both.  Partial 32x32 slabs are
 // summed in a fixed order by the finalize kernel: bitwise reproducible, no atomics.
+#include <vector>
+
 #include "common.h"
 
 namespace clskd {
@@ -21,9 +23,12 @@ struct GramJobsArg {
   int32_t slab0;  // absolute slab index of blockIdx.x == 0
 };
 
+// Per pair: the student / teacher job's first slab (any slab buffer: gram launches of one step
+// may run on different streams into different buffers) and slab count.
 struct SpkdPairsArg {
-  int32_t s_first[CLSKD_SPKD_MAX_PAIRS], s_n[CLSKD_SPKD_MAX_PAIRS];
-  int32_t t_first[CLSKD_SPKD_MAX_PAIRS], t_n[CLSKD_SPKD_MAX_PAIRS];
+  const float* s_ptr[CLSKD_SPKD_MAX_PAIRS];
+  const float* t_ptr[CLSKD_SPKD_MAX_PAIRS];
+  int32_t s_n[CLSKD_SPKD_MAX_PAIRS], t_n[CLSKD_SPKD_MAX_PAIRS];
   int32_t pair0;  // absolute pair index of blockIdx.x == 0
 };
 
@@ -151,27 +156,56 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const GramJobsArg job
 }
 
 // One block per pair: Gs = sum of the student job's slabs, Gt likewise, L1-normalise rows,
-// loss = ||Gt - Gs||_F^2 (/ B^2).  256 threads; B <= 32.
-__global__ __launch_bounds__(256) void spkd_finalize_kernel(const SpkdPairsArg pa, int B,
-                                                            int batchmean,
-                                                            const float* __restrict__ slabs,
-                                                            float* grams_s, float* grams_t,
-                                                            float* losses) {
+// loss = ||Gt - Gs||_F^2 (/ B^2).  1024 threads: the B*B Gram entries x NPH slab phases, each
+// thread summing every NPH-th slab with four independent fp64 accumulators (many loads in
+// flight), then the phases combined in a fixed order: bitwise reproducible.  B <= 32.
+constexpr int FIN_THREADS = 1024;
+
+__device__ __forceinline__ double sum_slabs(const float* __restrict__ base, int n, int e, int ph,
+                                            int nph) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int q = ph;
+  for (; q + 3 * nph < n; q += 4 * nph) {
+    a0 += (double)base[(int64_t)q * 1024 + e];
+    a1 += (double)base[(int64_t)(q + nph) * 1024 + e];
+    a2 += (double)base[(int64_t)(q + 2 * nph) * 1024 + e];
+    a3 += (double)base[(int64_t)(q + 3 * nph) * 1024 + e];
+  }
+  for (; q < n; q += nph) a0 += (double)base[(int64_t)q * 1024 + e];
+  return (a0 + a1) + (a2 + a3);
+}
+
+__global__ __launch_bounds__(FIN_THREADS) void spkd_finalize_kernel(const SpkdPairsArg pa, int B,
+                                                                    int batchmean,
+                                                                    float* grams_s, float* grams_t,
+                                                                    float* losses) {
   const int lp = blockIdx.x;
   const int pr = pa.pair0 + lp;
-  const int s_first = pa.s_first[lp], s_n = pa.s_n[lp];
-  const int t_first = pa.t_first[lp], t_n = pa.t_n[lp];
+  __shared__ double Ps[FIN_THREADS], Pt[FIN_THREADS];
   __shared__ double Gs[32 * 32], Gt[32 * 32];
   __shared__ double rs[32], rt[32];
-  __shared__ double red[256];
+  __shared__ double red[FIN_THREADS / 64];
   const int tid = threadIdx.x;
-  for (int idx = tid; idx < B * B; idx += 256) {
-    const int i = idx / B, k = idx % B;
-    double s = 0.0, t = 0.0;
-    for (int q = 0; q < s_n; ++q) s += (double)slabs[(int64_t)(s_first + q) * 1024 + i * 32 + k];
-    for (int q = 0; q < t_n; ++q) t += (double)slabs[(int64_t)(t_first + q) * 1024 + i * 32 + k];
-    Gs[idx] = s;
-    Gt[idx] = t;
+  const int E = B * B;
+  const int nph = FIN_THREADS / E;  // >= 1 for B <= 32
+  const int e = tid % E, ph = tid / E;
+  double s = 0.0, t = 0.0;
+  if (ph < nph) {
+    const int slot = (e / B) * 32 + (e % B);  // slab layout [32][32]
+    s = sum_slabs(pa.s_ptr[lp], pa.s_n[lp], slot, ph, nph);
+    t = sum_slabs(pa.t_ptr[lp], pa.t_n[lp], slot, ph, nph);
+  }
+  Ps[tid] = s;
+  Pt[tid] = t;
+  __syncthreads();
+  if (tid < E) {
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < nph; ++k) {
+      a += Ps[k * E + tid];
+      b += Pt[k * E + tid];
+    }
+    Gs[tid] = a;
+    Gt[tid] = b;
   }
   __syncthreads();
   if (tid < B) {
@@ -185,22 +219,24 @@ __global__ __launch_bounds__(256) void spkd_finalize_kernel(const SpkdPairsArg p
   }
   __syncthreads();
   double acc = 0.0;
-  for (int idx = tid; idx < B * B; idx += 256) {
-    const int i = idx / B;
-    const float gs = (float)(Gs[idx] / rs[i]);
-    const float gt = (float)(Gt[idx] / rt[i]);
-    if (grams_s) grams_s[(int64_t)pr * B * B + idx] = gs;
-    if (grams_t) grams_t[(int64_t)pr * B * B + idx] = gt;
+  if (tid < E) {
+    const int i = tid / B;
+    const float gs = (float)(Gs[tid] / rs[i]);
+    const float gt = (float)(Gt[tid] / rt[i]);
+    if (grams_s) grams_s[(int64_t)pr * E + tid] = gs;
+    if (grams_t) grams_t[(int64_t)pr * E + tid] = gt;
     const double dlt = (double)gt - (double)gs;
-    acc += dlt * dlt;
+    acc = dlt * dlt;
   }
-  red[tid] = acc;
+  // fixed-order block reduction: wave sums by DPP-free shuffles, then the 16 wave partials
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+  if ((tid & 63) == 0) red[tid >> 6] = acc;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) red[tid] += red[tid + o];
-    __syncthreads();
+  if (tid == 0) {
+    double tot = 0.0;
+    for (int w = 0; w < FIN_THREADS / 64; ++w) tot += red[w];
+    losses[pr] = (float)(batchmean ? tot / ((double)B * B) : tot);
   }
-  if (tid == 0) losses[pr] = (float)(batchmean ? red[0] / ((double)B * B) : red[0]);
 }
 
 // MRSTFT partials: per block {sum (Y-X)^2, sum Y^2, sum |log Y - log X|} over its elements.
@@ -367,6 +403,28 @@ extern "C" int clskd_gram_partial(const clskd_gram_job* jobs, int32_t njobs, int
   return CLSKD_OK;
 }
 
+static int launch_spkd_finalize(const float* const* s_ptr, const int32_t* s_n,
+                                const float* const* t_ptr, const int32_t* t_n, int32_t npairs,
+                                int32_t B, int32_t batchmean, float* grams_s, float* grams_t,
+                                float* losses, hipStream_t st) {
+  for (int p0 = 0; p0 < npairs; p0 += CLSKD_SPKD_MAX_PAIRS) {
+    SpkdPairsArg a;
+    const int n = npairs - p0 < CLSKD_SPKD_MAX_PAIRS ? npairs - p0 : CLSKD_SPKD_MAX_PAIRS;
+    for (int k = 0; k < CLSKD_SPKD_MAX_PAIRS; ++k) {
+      const int q = k < n ? p0 + k : p0;
+      a.s_ptr[k] = s_ptr[q];
+      a.t_ptr[k] = t_ptr[q];
+      a.s_n[k] = s_n[q];
+      a.t_n[k] = t_n[q];
+    }
+    a.pair0 = p0;
+    hipLaunchKernelGGL(spkd_finalize_kernel, dim3(n), dim3(FIN_THREADS), 0, st, a, B, batchmean,
+                       grams_s, grams_t, losses);
+    CLSKD_LAUNCH_CHECK("spkd_finalize");
+  }
+  return CLSKD_OK;
+}
+
 extern "C" int clskd_spkd_finalize(const clskd_gram_job* jobs, int32_t njobs, const int32_t* pairs,
                                    int32_t npairs, int32_t B, int32_t batchmean, const float* slabs,
                                    float* grams_s, float* grams_t, float* losses, void* stream) {
@@ -375,25 +433,35 @@ extern "C" int clskd_spkd_finalize(const clskd_gram_job* jobs, int32_t njobs, co
   if (rc != CLSKD_OK) return rc;
   CLSKD_CHECK_ARG(pairs && slabs && losses, "spkd_finalize: null pointer");
   CLSKD_CHECK_SHAPE(npairs >= 1, "spkd_finalize: no pairs");
-  hipStream_t st = as_stream(stream);
-  for (int p0 = 0; p0 < npairs; p0 += CLSKD_SPKD_MAX_PAIRS) {
-    SpkdPairsArg a;
-    const int n = npairs - p0 < CLSKD_SPKD_MAX_PAIRS ? npairs - p0 : CLSKD_SPKD_MAX_PAIRS;
-    for (int k = 0; k < CLSKD_SPKD_MAX_PAIRS; ++k) {
-      const int s = k < n ? pairs[2 * (p0 + k)] : 0, t = k < n ? pairs[2 * (p0 + k) + 1] : 0;
-      CLSKD_CHECK_SHAPE(s >= 0 && s < njobs && t >= 0 && t < njobs,
-                        "spkd_finalize: pair %d names a job outside [0, %d)", p0 + k, njobs);
-      a.s_first[k] = jobs[s].first_slab;
-      a.s_n[k] = jobs[s].nslab;
-      a.t_first[k] = jobs[t].first_slab;
-      a.t_n[k] = jobs[t].nslab;
-    }
-    a.pair0 = p0;
-    hipLaunchKernelGGL(spkd_finalize_kernel, dim3(n), dim3(256), 0, st, a, B, batchmean, slabs,
-                       grams_s, grams_t, losses);
-    CLSKD_LAUNCH_CHECK("spkd_finalize");
+  std::vector<const float*> sp(npairs), tp(npairs);
+  std::vector<int32_t> sn(npairs), tn(npairs);
+  for (int i = 0; i < npairs; ++i) {
+    const int s = pairs[2 * i], t = pairs[2 * i + 1];
+    CLSKD_CHECK_SHAPE(s >= 0 && s < njobs && t >= 0 && t < njobs,
+                      "spkd_finalize: pair %d names a job outside [0, %d)", i, njobs);
+    sp[i] = slabs + (int64_t)jobs[s].first_slab * 1024;
+    tp[i] = slabs + (int64_t)jobs[t].first_slab * 1024;
+    sn[i] = jobs[s].nslab;
+    tn[i] = jobs[t].nslab;
   }
-  return CLSKD_OK;
+  return launch_spkd_finalize(sp.data(), sn.data(), tp.data(), tn.data(), npairs, B, batchmean,
+                              grams_s, grams_t, losses, as_stream(stream));
+}
+
+extern "C" int clskd_spkd_finalize_ranges(const float* const* s_slabs, const int32_t* s_nslab,
+                                          const float* const* t_slabs, const int32_t* t_nslab,
+                                          int32_t npairs, int32_t B, int32_t batchmean,
+                                          float* grams_s, float* grams_t, float* losses,
+                                          void* stream) {
+  CLSKD_CHECK_ARG(s_slabs && s_nslab && t_slabs && t_nslab && losses,
+                  "spkd_finalize_ranges: null pointer");
+  CLSKD_CHECK_SHAPE(B >= 1 && B <= 32, "spkd_finalize_ranges: batch %d must be in [1, 32]", B);
+  CLSKD_CHECK_SHAPE(npairs >= 1, "spkd_finalize_ranges: no pairs");
+  for (int i = 0; i < npairs; ++i)
+    CLSKD_CHECK_ARG(s_slabs[i] && t_slabs[i] && s_nslab[i] >= 1 && t_nslab[i] >= 1,
+                    "spkd_finalize_ranges: pair %d has an empty slab range", i);
+  return launch_spkd_finalize(s_slabs, s_nslab, t_slabs, t_nslab, npairs, B, batchmean, grams_s,
+                              grams_t, losses, as_stream(stream));
 }
 
 extern "C" int clskd_stft_mag_loss(const float* X, const float* Y, int64_t rows, int32_t ld,

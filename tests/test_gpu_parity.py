@@ -512,3 +512,46 @@ def test_step_graph_redraws_abf_each_replay():
     assert torch.equal(outs[0]["student_wav"], outs[1]["student_wav"])
     assert torch.equal(outs[0]["spkd"][12:], outs[1]["spkd"][12:])  # clstm real / imag
     assert not torch.equal(outs[0]["spkd"][:12], outs[1]["spkd"][:12])
+
+
+def test_abf_redraw_kernel():
+    """clskd_uniform_redraw (the per-step ABF rebuild, framework.py:179-195): every ABF weight
+    lies in its kaiming-uniform bound and is spread like U(-b, b); the packed MFMA operands hold
+    exactly the drawn parameters (bf16 RNE / fp32) so no repack is needed; two draws differ;
+    the draw counter advances in device memory (one launch per ReviewKD module)."""
+    import math
+    from clskd import ops
+    from clskd.distill import KnowledgeDistillation
+    from clskd.data import synthetic_pairs
+    n, c = synthetic_pairs(2, 16000, seed=5)
+    X, y = torch.from_numpy(n).to(DEV), torch.from_numpy(c).to(DEV)
+    kd = KnowledgeDistillation(_models("teacher").train(), _models("student").train(),
+                               abf_reinit="step", precision="mixed").to(DEV)
+    kd.training_step((X, y))  # builds the packed operands; the next draws target them
+    kd._reinit_abf(None)
+    torch.cuda.synchronize()
+    snap = {}
+    for name, rk in (("encoder", kd.review_encoder), ("decoder", kd.review_decoder)):
+        assert int(kd._draw_state[(name, X.device)][0]) == 2
+        for i, abf in enumerate(rk.abfs):
+            for j, (w, wp, cin, ntap, bound) in enumerate(abf.redraw_jobs()):
+                v = w.detach().float().reshape(-1)
+                assert float(v.abs().max()) <= bound * (1 + 1e-6)
+                if v.numel() >= 4096:  # uniform: mean ~ 0, var ~ b^2 / 3
+                    assert abs(float(v.mean())) < 0.05 * bound
+                    assert abs(float(v.var()) / (bound * bound / 3) - 1) < 0.05
+                if wp is not None:
+                    ref = ops.pack_weight(w.detach().reshape(w.shape[0], w.shape[1], ntap)
+                                          .permute(0, 2, 1), cin * ntap,
+                                          "bf16" if wp.dtype == torch.bfloat16 else "fp32")
+                    assert torch.equal(ref, wp), (name, i, j)
+                snap[(name, i, j)] = v.clone()
+    # the caches see the draw as current: a forward uses the drawn weights without repacking
+    w1p_before = kd.review_decoder.abfs[0]._wcache["w"][1][0]
+    kd.training_step((X, y))
+    assert kd.review_decoder.abfs[0]._wcache["w"][1][0] is w1p_before
+    for name, rk in (("encoder", kd.review_encoder), ("decoder", kd.review_decoder)):
+        for i, abf in enumerate(rk.abfs):
+            for j, (w, *_r) in enumerate(abf.redraw_jobs()):
+                assert not torch.equal(snap[(name, i, j)], w.detach().float().reshape(-1))
+    assert math.isfinite(float(kd.last["loss"]))

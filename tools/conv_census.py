@@ -20,19 +20,20 @@ def main():
     for _ in range(2):
         kd.training_step((X, y))
     torch.cuda.synchronize()
-    # serialise the two streams so per-launch times are not inflated by overlap
+    # serialise the three streams so per-launch times are not inflated by overlap
     import clskd.distill as D
-    D._SIDE[0] = torch.cuda.current_stream(dev)
+    for which in (0, 1):
+        D._SIDE[(dev.index, which)] = torch.cuda.current_stream(dev)
     ops.KernelTimer.start()
     kd.training_step((X, y))
     torch.cuda.synchronize()
     recs = ops.KernelTimer.per_launch()
     ops.KernelTimer.stop()
     tot = 0.0
-    print(f"{'kernel':28s} {'M':>9s} {'N':>5s} {'K':>6s} {'dt':>5s} {'us':>8s} {'TF/s':>7s}")
+    print(f"{'kernel':46s} {'M':>9s} {'N':>5s} {'K':>6s} {'dt':>5s} {'us':>8s} {'TF/s':>7s}")
     for name, (M, N, K, dt), us, tf in recs:
         tot += us
-        print(f"{name:28s} {M:9d} {N:5d} {K:6d} {dt:>5s} {us:8.1f} {tf:7.1f}")
+        print(f"{name:46s} {M:9d} {N:5d} {K:6d} {dt:>5s} {us:8.1f} {tf:7.1f}")
     print(f"total {tot / 1e3:.3f} ms over {len(recs)} launches")
 
 
