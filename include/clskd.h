@@ -201,10 +201,13 @@ int clskd_ola(const float* frames, const float* window, int32_t B, int32_t T, in
  * ReviewKD ABF attention fusion (framework.py:209-217), mid = 64 channels:
  *   y_up = nearest-interpolate(res [B][Fr][Tr][64] -> (F, T))
  *   z = sigmoid(W[2][128] . [x; y_up] + b);  out = x*z0 + y_up*z1
+ * x_scale/x_shift (optional, 64 fp32 each, both or neither): x := x*x_scale + x_shift on load
+ *   — the ABF's conv1 BatchNorm (framework.py:181) folded into the fuse, x = raw conv1 output.
  * -------------------------------------------------------------------------------------- */
 int clskd_abf_fuse(const void* x, const void* res, int32_t B, int32_t F, int32_t T,
-                   int32_t Fr, int32_t Tr, const float* w, const float* b, void* out,
-                   int32_t dtype, void* stream);
+                   int32_t Fr, int32_t Tr, const float* w, const float* b,
+                   const float* x_scale, const float* x_shift, void* out, int32_t dtype,
+                   void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Uniform weight re-draw (replaces the per-step ABF rebuild of framework.py:194-195 —

@@ -79,7 +79,8 @@ SIGNATURES = {
     "clskd_spec_bftc": (_i32, [_p, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p]),
     "clskd_mask_e": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p]),
     "clskd_ola": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p]),
-    "clskd_abf_fuse": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _i32, _p]),
+    "clskd_abf_fuse": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _i32,
+                              _p]),
     "clskd_gram_partial": (_i32, [_p, _i32, _i32, _p, _p]),
     "clskd_spkd_finalize": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
     "clskd_uniform_redraw": (_i32, [_p, _i32, C.c_uint64, _p, _p]),

@@ -255,16 +255,22 @@ class ABF(nn.Module):
         ops.conv([seg_bftc(x)], [(0, 0)], B, Fn, Tn, mid, w1p, None, x1,
                  OutMap(Fn * Tn * mid, Tn * mid, mid), stats=part)
         bn = self.conv1[1]
-        ops.batch_norm_bftc(x1, x1, bn.weight, bn.bias, bn.running_mean, bn.running_var, train,
-                            bn.momentum, bn.eps, 1, partial=(part, nmb) if train else None)
         if self.att_conv is not None:
             if shape != Fn:  # the reference's torch.cat would fail as well (framework.py:213-216)
                 raise ValueError(f"ABF fuse: residual upsampled to F={shape} but x has F={Fn}")
+            # conv1's BatchNorm is applied by the fuse kernel as it loads x1 (no extra pass)
+            coef = ops.batch_norm_bftc(x1, None, bn.weight, bn.bias, bn.running_mean,
+                                       bn.running_var, train, bn.momentum, bn.eps, 1,
+                                       partial=(part, nmb) if train else None)
             if y.dtype != x1.dtype:  # user-supplied residual of another storage type
                 y = y.to(x1.dtype).contiguous()
             xf = torch.empty_like(x1)
-            ops.abf_fuse(x1, y, att[0], att[1], xf)
+            ops.abf_fuse(x1, y, att[0], att[1], xf, x_coef=coef)
             x1 = xf
+        else:
+            ops.batch_norm_bftc(x1, x1, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                train, bn.momentum, bn.eps, 1,
+                                partial=(part, nmb) if train else None)
         if Tn != out_shape and Fn != out_shape:
             raise NotImplementedError(
                 f"ABF output interpolation to ({out_shape}, {Tn}) from F={Fn} is not on the CLSKD path")

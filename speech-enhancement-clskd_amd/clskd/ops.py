@@ -353,9 +353,13 @@ def batch_norm_bftc(x, y, gamma, beta, running_mean, running_var, train, momentu
                     eps=1e-5, n_updates=1, alpha=None, stats_out=None, partial=None):
     """nn.BatchNorm2d over a BFTC tensor (channels last), then optional PReLU (single alpha).
     train: batch statistics (biased var), running stats updated n_updates times (if given).
-    partial=(tensor, nblk): statistics already produced by the conv epilogue (fused)."""
+    partial=(tensor, nblk): statistics already produced by the conv epilogue (fused).
+    y=None: compute the coefficients only and return the [scale | shift] fp32 tensor (for a
+    consumer kernel that applies them on load)."""
     L = lib()
     Cn = x.shape[-1]
+    if Cn > 4096:
+        raise RuntimeError("batch_norm_bftc: more than 4096 channels")
     rows = x.numel() // Cn
     dev = x.device
     coef = torch.empty(2 * Cn, device=dev, dtype=torch.float32)  # [scale | shift]
@@ -387,6 +391,8 @@ def batch_norm_bftc(x, y, gamma, beta, running_mean, running_var, train, momentu
     else:
         check(L.clskd_bn_eval_coeffs(ptr(running_mean), ptr(running_var), ptr(gamma), ptr(beta),
                                      eps, Cn, scale, shift, st), "bn_eval")
+    if y is None:
+        return coef
     assert x.dtype == y.dtype
     check(L.clskd_bn_apply(ptr(x), ptr(y), rows, Cn, scale, shift, ptr(alpha), _dt(x), st),
           "bn_apply")
@@ -434,13 +440,20 @@ def ola_hop(frames, window, hop, out_len, trim, clamp, wav):
                           ptr(wav), _stream()), "ola")
 
 
-def abf_fuse(x, res, w, b, out):
+def abf_fuse(x, res, w, b, out, x_coef=None):
+    """x_coef: optional [scale | shift] (64 + 64 fp32) applied to x on load — the conv1
+    BatchNorm of the ABF folded into the fuse (x is then the raw conv1 output)."""
     B, F, T, Cm = x.shape
     _, Fr, Tr, Cr = res.shape
     assert Cm == 64 and Cr == 64, "ABF fuse is built for mid_channel = 64 (framework.py:235)"
     assert x.dtype == res.dtype == out.dtype
-    check(lib().clskd_abf_fuse(ptr(x), ptr(res), B, F, T, Fr, Tr, ptr(w), ptr(b), ptr(out),
-                               _dt(x), _stream()), "abf_fuse")
+    sc = sh = None
+    if x_coef is not None:
+        assert x_coef.dtype == torch.float32 and x_coef.numel() == 2 * Cm
+        sc = x_coef.data_ptr()
+        sh = sc + 4 * Cm
+    check(lib().clskd_abf_fuse(ptr(x), ptr(res), B, F, T, Fr, Tr, ptr(w), ptr(b), sc, sh,
+                               ptr(out), _dt(x), _stream()), "abf_fuse")
     return out
 
 

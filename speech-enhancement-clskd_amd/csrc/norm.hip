@@ -87,6 +87,36 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const T* __restri
   }
 }
 
+// scale/shift (and batch mean/var, running stats) of one channel from its totals.
+__device__ __forceinline__ void bn_channel_coeffs(int c, double S, double Q, int64_t rows,
+                                                  const float* gamma, const float* beta, float eps,
+                                                  float* running_mean, float* running_var,
+                                                  float momentum, int n_updates, float* scale,
+                                                  float* shift, float* mean_out, float* var_out) {
+  const double n = (double)rows;
+  const double mean = S / n;
+  double var = Q / n - mean * mean;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f;
+  const float bb = beta ? beta[c] : 0.f;
+  const float sc = invstd * g;
+  scale[c] = sc;
+  shift[c] = bb - (float)mean * sc;
+  if (mean_out) mean_out[c] = (float)mean;
+  if (var_out) var_out[c] = (float)var;
+  if (running_mean && running_var) {
+    const float unb = (float)(rows > 1 ? var * n / (n - 1.0) : var);
+    float rm = running_mean[c], rv = running_var[c];
+    for (int u = 0; u < n_updates; ++u) {
+      rm = (1.f - momentum) * rm + momentum * (float)mean;
+      rv = (1.f - momentum) * rv + momentum * unb;
+    }
+    running_mean[c] = rm;
+    running_var[c] = rv;
+  }
+}
+
 // one block per channel: sum partials in a fixed order, then scale/shift & running stats.
 __global__ __launch_bounds__(256) void bn_finalize_kernel(
     const double* __restrict__ partial, int nblk, int64_t rows, int C, const float* gamma,
@@ -110,30 +140,9 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
     }
     __syncthreads();
   }
-  if (tid == 0) {
-    const double n = (double)rows;
-    const double mean = rs[0] / n;
-    double var = rq[0] / n - mean * mean;
-    if (var < 0) var = 0;
-    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-    const float g = gamma ? gamma[c] : 1.f;
-    const float bb = beta ? beta[c] : 0.f;
-    const float sc = invstd * g;
-    scale[c] = sc;
-    shift[c] = bb - (float)mean * sc;
-    if (mean_out) mean_out[c] = (float)mean;
-    if (var_out) var_out[c] = (float)var;
-    if (running_mean && running_var) {
-      const float unb = (float)(rows > 1 ? var * n / (n - 1.0) : var);
-      float rm = running_mean[c], rv = running_var[c];
-      for (int u = 0; u < n_updates; ++u) {
-        rm = (1.f - momentum) * rm + momentum * (float)mean;
-        rv = (1.f - momentum) * rv + momentum * unb;
-      }
-      running_mean[c] = rm;
-      running_var[c] = rv;
-    }
-  }
+  if (tid == 0)
+    bn_channel_coeffs(c, rs[0], rq[0], rows, gamma, beta, eps, running_mean, running_var,
+                      momentum, n_updates, scale, shift, mean_out, var_out);
 }
 
 __global__ void bn_eval_coeffs_kernel(const float* rm, const float* rv, const float* gamma,
@@ -345,10 +354,21 @@ __global__ __launch_bounds__(256) void abf_fuse_kernel(const DT* __restrict__ x,
                                                        int F, int T, int Fr, int Tr,
                                                        const float* __restrict__ w,
                                                        const float* __restrict__ bias,
+                                                       const float* __restrict__ xs,
+                                                       const float* __restrict__ xh,
                                                        DT* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int sub = lane & 15;  // channel quad
   const int c = sub * 4;
+  // optional per-channel affine on x (the ABF conv1 BatchNorm, applied on load)
+  f32x4 sx = {1.f, 1.f, 1.f, 1.f}, hx = {0.f, 0.f, 0.f, 0.f};
+  if (xs) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sx[j] = xs[c + j];
+      hx[j] = xh[c + j];
+    }
+  }
   f32x4 w0x, w0y, w1x, w1y;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -368,7 +388,9 @@ __global__ __launch_bounds__(256) void abf_fuse_kernel(const DT* __restrict__ x,
     const int b = (int)(bf / F);
     const int fr = nearest_src(f, Fr, F);
     const int tr = nearest_src(t, Tr, T);
-    const f32x4 xv = load4<DT>(x + p * 64 + c);
+    f32x4 xv = load4<DT>(x + p * 64 + c);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[j] = fmaf(xv[j], sx[j], hx[j]);
     const f32x4 yv = load4<DT>(res + (((int64_t)b * Fr + fr) * Tr + tr) * 64 + c);
     float d0 = 0.f, d1 = 0.f;
 #pragma unroll
@@ -603,20 +625,23 @@ extern "C" int clskd_complex_combine(const float* rr, const float* ii, const flo
 }
 
 extern "C" int clskd_abf_fuse(const void* x, const void* res, int32_t B, int32_t F, int32_t T,
-                              int32_t Fr, int32_t Tr, const float* w, const float* b, void* out,
+                              int32_t Fr, int32_t Tr, const float* w, const float* b,
+                              const float* x_scale, const float* x_shift, void* out,
                               int32_t dtype, void* stream) {
   CLSKD_CHECK_ARG(x && res && w && b && out, "abf_fuse: null pointer");
+  CLSKD_CHECK_ARG((x_scale == nullptr) == (x_shift == nullptr),
+                  "abf_fuse: x_scale and x_shift go together");
   CLSKD_CHECK_SHAPE(B > 0 && F > 0 && T > 0 && Fr > 0 && Tr > 0, "abf_fuse: shape");
   CLSKD_CHECK_ARG(dtype == CLSKD_F32 || dtype == CLSKD_BF16, "abf_fuse: dtype");
   const int64_t npix = (int64_t)B * F * T;
   if (dtype == CLSKD_BF16)
     hipLaunchKernelGGL(abf_fuse_kernel<__bf16>, dim3(grid_for(npix * 16)), dim3(256), 0,
                        as_stream(stream), (const __bf16*)x, (const __bf16*)res, B, F, T, Fr, Tr, w, b,
-                       (__bf16*)out);
+                       x_scale, x_shift, (__bf16*)out);
   else
     hipLaunchKernelGGL(abf_fuse_kernel<float>, dim3(grid_for(npix * 16)), dim3(256), 0,
                        as_stream(stream), (const float*)x, (const float*)res, B, F, T, Fr, Tr, w, b,
-                       (float*)out);
+                       x_scale, x_shift, (float*)out);
   CLSKD_LAUNCH_CHECK("abf_fuse");
   return CLSKD_OK;
 }

@@ -64,15 +64,17 @@ __global__ __launch_bounds__(DRAW_THREADS) void uniform_redraw_kernel(const Draw
         reinterpret_cast<float*>(j.packed)[o] = v;
     }
   }
-  // the last workgroup to finish advances the draw counter (every block has read it by then)
+  // The last workgroup to arrive advances the draw counter.  Every block's read of state[0]
+  // has returned before its ticket (its stores consumed the value), so no fence is needed —
+  // and none is wanted: an agent-scope fence on gfx950 writes back and invalidates the XCD's
+  // whole L2 (buffer_wbl2 / buffer_inv sc1), evicting the concurrent streams' working sets.
+  // The next launch sees the new counter across the kernel boundary.
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
     const unsigned long long t = atomicAdd(&state[1], 1ull);
     if (t == gridDim.x - 1) {
       state[0] = draw + 1;
       state[1] = 0;
-      __threadfence();
     }
   }
 }

@@ -1,0 +1,10 @@
+#!/bin/bash
+# GPU parity tests + default bench line + steady-state kernel table (one gpurun call).
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/q
+mkdir -p $O
+timeout -k 10 500 python -m pytest $R/tests -m gpu -x -q > $O/gt.log 2>&1
+timeout -k 10 200 python $R/bench.py --no-cpu-baseline > $O/b.log 2>&1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/tr -o run -- python3 $R/bench.py --steps 4 --warmup 2 --no-cpu-baseline > $O/tr.log 2>&1
