@@ -37,27 +37,30 @@ __device__ __forceinline__ float tanh_fast(float x) {
   return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * 2.8853900817779268f));
 }
 
-// Thread layout (8H threads): thread = (hidden unit u = tid / 8, k-slice ks = tid % 8).  The
-// thread keeps the four gate rows (i, f, g, o) of unit u restricted to its slice
-// k in [ks*H/8, (ks+1)*H/8) in VGPRs, reads only that slice of h from LDS (H/8 floats —
-// the LDS read traffic per step is 1/4 of a two-threads-per-row layout, which was LDS-bandwidth
-// bound), and the 8 slices of a unit are adjacent lanes: three xor-shuffle adds give every lane
-// of the group the four pre-activations.  Lanes 0..3 of the group each apply one gate's
-// activation, lane 0 gathers them and updates the cell — no LDS round trip between the matvec
-// and the cell.  h goes to an LDS history ring, flushed to `out` every CH steps with coalesced
-// workgroup stores; the step barrier waits for LDS only.  Packed FMAs (v_pk_fma_f32).
-template <int H, int DBG = 0>
-__global__ __launch_bounds__(8 * H) void lstm_recurrent_kernel(
+// Thread layout (NKS*H threads): thread = (hidden unit u = tid / NKS, k-slice ks = tid % NKS).
+// The thread keeps the four gate rows (i, f, g, o) of unit u restricted to its slice
+// k in [ks*KW, (ks+1)*KW), KW = H/NKS, in VGPRs and reads that slice of h from LDS; the NKS
+// slices of a unit are adjacent lanes, reduced with log2(NKS) DPP adds.  Few, fat threads: the
+// per-step VALU work besides the FMAs (reductions, gate selects, activations) is paid once per
+// thread, so NKS = 2 (H = 128: 4 waves, one per SIMD, 256 weights per lane) issues ~2x fewer
+// instructions per SIMD per step than an 8-slice layout.  Gates: NKS >= 4 -> lane ks < 4 applies
+// gate ks; NKS = 2 -> lane 0 applies i and g, lane 1 f and o.  Lane 0 of the group updates the
+// cell.  h goes to an LDS history ring, flushed to `out` every CH steps with coalesced
+// workgroup stores; the step barrier waits for LDS only.  The projected inputs are prefetched
+// two steps ahead (named registers, loop unrolled by two).  Packed FMAs (v_pk_fma_f32).
+template <int H, int NKS, int DBG = 0>
+__global__ __launch_bounds__(NKS * H) void lstm_recurrent_kernel(
     const float* __restrict__ gx, int64_t gx_ws, int64_t gx_seq, int64_t gx_t,
     const float* __restrict__ whh, int T, float* __restrict__ out, int64_t o_ws, int64_t o_seq,
     int64_t o_t) {
-  constexpr int G = 4 * H;   // gate rows
-  constexpr int KW = H / 8;  // k-slice width
-  static_assert(KW % 2 == 0, "H >= 16");
+  constexpr int G = 4 * H;     // gate rows
+  constexpr int KW = H / NKS;  // k-slice width
+  constexpr int NT = NKS * H;  // threads
+  static_assert(NKS == 2 || NKS == 4 || NKS == 8, "k-slices");
+  static_assert(KW % 4 == 0, "k-slice of whole float4s");
   const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int u = tid >> 3;
-  const int ks = tid & 7;
+  const int u = tid / NKS;
+  const int ks = tid % NKS;
   const int ws = blockIdx.y;
   const int seq = blockIdx.x;
   constexpr int CH = 32;
@@ -73,65 +76,98 @@ __global__ __launch_bounds__(8 * H) void lstm_recurrent_kernel(
   }
   if (tid < H) hist[2 * CH - 1][tid] = 0.f;  // h(-1) = 0
   float cstate = 0.f;  // meaningful in lane ks == 0 of each unit group
-  // gx of this unit: lane ks < 4 fetches gate ks's projected input
-  const float* gp = gx + ws * gx_ws + seq * gx_seq + (ks & 3) * H + u;
+  // this lane's gates: NKS >= 4 -> gate ks & 3 (lanes >= 4 duplicate); NKS = 2 -> gates ks, ks+2
+  const int ga = NKS >= 4 ? (ks & 3) : ks;
+  const float* gp = gx + ws * gx_ws + seq * gx_seq + u;
   float* op = out + ws * o_ws + seq * o_seq;
-  float gnext = DBG == 1 ? 0.1f : gp[0];
+  auto load_g = [&](int t, float& g0, float& g1) {
+    const float* q = gp + (int64_t)min(t, T - 1) * gx_t;
+    g0 = DBG == 1 ? 0.1f : q[ga * H];
+    if constexpr (NKS == 2) g1 = DBG == 1 ? 0.1f : q[(ga + 2) * H];
+  };
+  float ga0 = 0.f, ga1 = 0.f, gb0 = 0.f, gb1 = 0.f;
+  load_g(0, ga0, ga1);
+  load_g(1, gb0, gb1);
   __syncthreads();
 
-  for (int t = 0; t < T; ++t) {
-    const float gcur = gnext;
-    if (DBG != 1 && t + 1 < T) gnext = gp[(int64_t)(t + 1) * gx_t];
+  auto step = [&](int t, float g0, float g1) {
     const float* hp = hist[(t + 2 * CH - 1) % (2 * CH)] + ks * KW;
-    f32x2l acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-    if constexpr (KW % 4 == 0) {
+    f32x4 hv[KW / 4];
 #pragma unroll
-      for (int j = 0; j < KW; j += 4) {
-        const f32x4 hv = *reinterpret_cast<const f32x4*>(hp + j);
-        const f32x2l h01 = {hv[0], hv[1]}, h23 = {hv[2], hv[3]};
+    for (int j = 0; j < KW / 4; ++j) hv[j] = reinterpret_cast<const f32x4*>(hp)[j];
+    f32x2l acc[4][2] = {};
 #pragma unroll
-        for (int gt = 0; gt < 4; ++gt) {
-          acc[gt] = __builtin_elementwise_fma(w[gt][j / 2], h01, acc[gt]);
-          acc[gt] = __builtin_elementwise_fma(w[gt][j / 2 + 1], h23, acc[gt]);
-        }
+    for (int j = 0; j < KW / 4; ++j) {
+      const f32x2l h01 = {hv[j][0], hv[j][1]}, h23 = {hv[j][2], hv[j][3]};
+#pragma unroll
+      for (int gt = 0; gt < 4; ++gt) {
+        acc[gt][j & 1] = __builtin_elementwise_fma(w[gt][2 * j], h01, acc[gt][j & 1]);
+        acc[gt][j & 1] = __builtin_elementwise_fma(w[gt][2 * j + 1], h23, acc[gt][j & 1]);
       }
-    } else {  // H = 16: 2-wide slices
-      const f32x2l h01 = *reinterpret_cast<const f32x2l*>(hp);
-#pragma unroll
-      for (int gt = 0; gt < 4; ++gt) acc[gt] = __builtin_elementwise_fma(w[gt][0], h01, acc[gt]);
     }
     float pre[4];
 #pragma unroll
-    for (int gt = 0; gt < 4; ++gt) {  // 8-lane group sum: xor 1, xor 2, half-row mirror
-      float v = acc[gt][0] + acc[gt][1];
+    for (int gt = 0; gt < 4; ++gt) {  // NKS-lane group sum
+      const f32x2l a2 = acc[gt][0] + acc[gt][1];
+      float v = a2[0] + a2[1];
       v += dpp<DPP_XOR1>(v);
-      v += dpp<DPP_XOR2>(v);
-      v += dpp<DPP_HALF_MIRROR>(v);
+      if constexpr (NKS >= 4) v += dpp<DPP_XOR2>(v);
+      if constexpr (NKS == 8) v += dpp<DPP_HALF_MIRROR>(v);
       pre[gt] = v;
     }
-    // lane ks (< 4) of the group: activation of gate ks (i, f, g, o = sig, sig, tanh, sig)
-    const int gsel = ks & 3;
-    const float pg = (gsel == 0 ? pre[0] : gsel == 1 ? pre[1] : gsel == 2 ? pre[2] : pre[3]) + gcur;
-    const float act = gsel == 2 ? tanh_fast(pg) : sigm_fast(pg);
-    const float fg = dpp<DPP_BCAST1>(act);
-    const float gg = dpp<DPP_BCAST2>(act);
-    const float og = dpp<DPP_BCAST3>(act);
+    float ig, fg, gg, og;
+    if constexpr (NKS >= 4) {
+      // lane ks (< 4): activation of gate ks (i, f, g, o = sig, sig, tanh, sig), branch-free
+      const float p01 = (ga & 1) ? pre[1] : pre[0];
+      const float p23 = (ga & 1) ? pre[3] : pre[2];
+      const float pg = ((ga & 2) ? p23 : p01) + g0;
+      const float k = ga == 2 ? 2.f : 1.f;
+      const float act = fmaf(k, sigm_fast(k * pg), ga == 2 ? -1.f : 0.f);
+      ig = act;
+      fg = dpp<DPP_BCAST1>(act);
+      gg = dpp<DPP_BCAST2>(act);
+      og = dpp<DPP_BCAST3>(act);
+    } else {
+      // lane 0: i (sig) and g (tanh); lane 1: f (sig) and o (sig)
+      const float pa = (ks ? pre[1] : pre[0]) + g0;
+      const float pb = (ks ? pre[3] : pre[2]) + g1;
+      const float a0 = sigm_fast(pa);
+      const float kb = ks ? 1.f : 2.f;
+      const float a1 = fmaf(kb, sigm_fast(kb * pb), ks ? 0.f : -1.f);
+      ig = a0;
+      gg = a1;
+      fg = dpp<DPP_BCAST1>(a0);  // quad_perm [1,1,1,1]: lane 0 of the pair reads lane 1
+      og = dpp<DPP_BCAST1>(a1);
+      if constexpr (true) {      // pairs (2,3) of a quad take lane 3
+        const float fg3 = dpp<DPP_BCAST3>(a0), og3 = dpp<DPP_BCAST3>(a1);
+        const bool hi = (tid & 2) != 0;
+        fg = hi ? fg3 : fg;
+        og = hi ? og3 : og;
+      }
+    }
     if (ks == 0) {
-      cstate = fg * cstate + act * gg;
+      cstate = fg * cstate + ig * gg;
       hist[t % (2 * CH)][u] = og * tanh_fast(cstate);
     }
     // Only LDS is exchanged between waves: wait for LDS alone (__syncthreads() would also be
-    // a release fence draining vmcnt, i.e. the prefetched gx load, on every step).
+    // a release fence draining vmcnt, i.e. the prefetched gx loads, on every step).
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if ((t + 1) % CH == 0 || t == T - 1) {  // uniform: flush steps t0 .. t
-      const int t0 = t - (t % CH);
-      const int n = (t - t0 + 1) * H;
-      for (int i = tid; i < n; i += 8 * H) {
-        const int r = t0 + i / H, c = i % H;
+      const int tf0 = t - (t % CH);
+      const int n = (t - tf0 + 1) * H;
+      for (int k = tid; k < n; k += NT) {
+        const int r = tf0 + k / H, c = k % H;
         op[(int64_t)r * o_t + c] = hist[r % (2 * CH)][c];
       }
     }
+  };
+
+  for (int t = 0; t < T; t += 2) {
+    step(t, ga0, ga1);
+    load_g(t + 2, ga0, ga1);
+    if (t + 1 < T) step(t + 1, gb0, gb1);
+    load_g(t + 3, gb0, gb1);
   }
 }
 
@@ -148,31 +184,45 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
   CLSKD_CHECK_ARG(((uintptr_t)whh & 15) == 0, "lstm: whh must be 16-byte aligned");
   dim3 grid(nseq, nws);
   hipStream_t st = as_stream(stream);
+  // k-slices per unit (measured on MI355X, tools/lstm_micro.py): H = 128 -> 4 (662 ns/step vs
+  // 772 with 8 — twice the reduction work — and 953 with 2, whose 256 weights per lane spill
+  // to AGPRs); H = 32 -> 8 (281 ns/step vs 297 / 312 with 4 / 2: a latency-bound chain, more
+  // waves hide more of it).  A/B knobs CLSKD_LSTM_NKS (H=128) and CLSKD_LSTM_NKS32 (H=32).
+  static const int nks128 = [] {
+    const char* e = getenv("CLSKD_LSTM_NKS");
+    const int v = e ? atoi(e) : 4;
+    return (v == 2 || v == 8) ? v : 4;
+  }();
+  static const int nks32 = [] {
+    const char* e = getenv("CLSKD_LSTM_NKS32");
+    const int v = e ? atoi(e) : 8;
+    return (v == 2 || v == 4) ? v : 8;
+  }();
+#define LSTM_LAUNCH(H_, NKS_) \
+  hipLaunchKernelGGL((lstm_recurrent_kernel<H_, NKS_>), grid, dim3(NKS_ * H_), 0, st, gx, gx_ws, \
+                     gx_seq, gx_t, whh, T, out, o_ws, o_seq, o_t)
   switch (H) {
     case 16:
-      hipLaunchKernelGGL(lstm_recurrent_kernel<16>, grid, dim3(128), 0, st, gx, gx_ws, gx_seq, gx_t, whh,
-                         T, out, o_ws, o_seq, o_t);
+      LSTM_LAUNCH(16, 4);
       break;
     case 32:
-      hipLaunchKernelGGL(lstm_recurrent_kernel<32>, grid, dim3(256), 0, st, gx, gx_ws, gx_seq, gx_t, whh,
-                         T, out, o_ws, o_seq, o_t);
+      if (nks32 == 4) LSTM_LAUNCH(32, 4);
+      else if (nks32 == 2) LSTM_LAUNCH(32, 2);
+      else LSTM_LAUNCH(32, 8);
       break;
     case 64:
-      hipLaunchKernelGGL(lstm_recurrent_kernel<64>, grid, dim3(512), 0, st, gx, gx_ws, gx_seq, gx_t, whh,
-                         T, out, o_ws, o_seq, o_t);
+      LSTM_LAUNCH(64, 4);
       break;
     case 128:
-      if (getenv("CLSKD_LSTM_DEBUG") && getenv("CLSKD_LSTM_DEBUG")[0] == '1')  // timing experiment
-        hipLaunchKernelGGL((lstm_recurrent_kernel<128, 1>), grid, dim3(1024), 0, st, gx, gx_ws, gx_seq,
-                           gx_t, whh, T, out, o_ws, o_seq, o_t);
-      else
-        hipLaunchKernelGGL(lstm_recurrent_kernel<128>, grid, dim3(1024), 0, st, gx, gx_ws, gx_seq, gx_t,
-                           whh, T, out, o_ws, o_seq, o_t);
+      if (nks128 == 8) LSTM_LAUNCH(128, 8);
+      else if (nks128 == 4) LSTM_LAUNCH(128, 4);
+      else LSTM_LAUNCH(128, 2);
       break;
     default:
       set_error("lstm: hidden size %d not built (16, 32, 64, 128)", H);
       return CLSKD_E_SHAPE;
   }
+#undef LSTM_LAUNCH
   CLSKD_LAUNCH_CHECK("lstm_recurrent");
   return CLSKD_OK;
 }
