@@ -253,10 +253,13 @@ static size_t direct_lds(const clskd_conv_desc& d, int NP, int G) {
 }
 
 // Direct path policy (measured on MI355X against the MFMA engines, tools/conv_census.py):
-// it wins for the 2-channel output layers (2-3x) and short-K narrow layers; with N >= 32, or
-// N = 16 with long K, the MFMA engines are faster.  K <= 1024 bounds the LDS K table (16 KB).
+// it wins for the 2-channel output layers (2-3x), short-K narrow layers and the 2-channel-input
+// first encoder layer (K = 20 -> 32, N = 32: the fp32 engine's scalar gather path takes 135 us
+// there); with N >= 32 and real K, or N = 16 with long K, the MFMA engines are faster.
+// K <= 1024 bounds the LDS K table (16 KB).
 bool conv_direct_ok(int N, int K) {
-  return N >= 1 && K >= 1 && K <= 1024 && (N <= 4 || (N <= 16 && K <= 128));
+  return N >= 1 && K >= 1 && K <= 1024 &&
+         (N <= 4 || (N <= 16 && K <= 128) || (N <= 32 && K <= 32));
 }
 
 template <int NP, int G, typename InT>

@@ -11,11 +11,12 @@
 // operands as 8 contiguous floats (two ds_read_b128): step s uses k = 8*(lane>>5) + s.
 // LDS rows are 64 B; 16-B chunks are XOR-swizzled by ((row>>2)&3) so the ds_read_b128 lane
 // groups hit 16 distinct bank slots.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace clskd {
 
-constexpr int BM = 128;
 constexpr int BK = 16;
 
 struct ConvArgs {
@@ -27,16 +28,22 @@ __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >>
 // select the per-segment value without runtime-indexed arrays (which would go to scratch)
 template <typename T>
 __device__ __forceinline__ T sel4(int s, T a0, T a1, T a2, T a3) {
-  return s == 0 ? a0 : (s == 1 ? a1 : (s == 2 ? a2 : a3));
+  // two levels of value selects (v_cndmask): an if-else chain compiles to exec-mask branches
+  const T lo = (s & 1) ? a1 : a0;
+  const T hi = (s & 1) ? a3 : a2;
+  return (s & 2) ? hi : lo;
 }
 
 template <typename OutT>
 __device__ __forceinline__ void store_val(OutT* p, float v) { *p = (OutT)v; }
 
-template <int BN, bool VEC4, typename OutT>
-__global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
+template <int BN, bool VEC4, typename OutT, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void conv_igemm_f32(const ConvArgs args) {
   const clskd_conv_desc& d = args.d;
   constexpr int NT = BN / 32;
+  constexpr int BM = 32 * NW;        // rows per tile: 32 per wave
+  constexpr int NTH = NW * 64;       // threads
+  constexpr int RSTEP = NTH / 4;     // A-gather row stride between a thread's two rows
   __shared__ __attribute__((aligned(16))) float As[2][BM * BK];
   __shared__ __attribute__((aligned(16))) float Bs[2][BN * BK];
   __shared__ int64_t out_row[BM];
@@ -51,58 +58,95 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
   const int nk = d.K / BK;  // host pads K to a multiple of BK
   const int64_t FoTo = (int64_t)d.Fo * d.To;
 
-  // ---- per-block output row offsets ----
+  // ---- per-block tables: output row offsets; (VEC4) per-row gather bases per segment and the
+  //      K-chunk table (one int2 per 4 k: element offset, dF | dT | segment) in LDS, so a
+  //      gathered float4 costs one LDS read and a few selects instead of 64-bit index math ----
+  __shared__ int rowinfo[BM][4];     // fi0, ti0, valid
+  __shared__ int rowbase[4][BM];     // element offset of (b, fi0, ti0) in segment s
   if (tid < BM) {
     int64_t m = m0 + tid;
     int64_t off = -1;
-    if (m < M) {
-      int64_t b = m / FoTo;
-      int64_t r = m - b * FoTo;
-      int fo = (int)(r / d.To);
-      int to = (int)(r - (int64_t)fo * d.To);
-      off = b * d.oB + (int64_t)(fo * d.of_mul + d.of_add) * d.oF + (int64_t)to * d.oT;
-    }
+    const bool valid = m < M;
+    const int64_t mm = valid ? m : 0;
+    const int64_t b = mm / FoTo;
+    const int64_t r = mm - b * FoTo;
+    const int fo = (int)(r / d.To);
+    const int to = (int)(r - (int64_t)fo * d.To);
+    if (valid) off = b * d.oB + (int64_t)(fo * d.of_mul + d.of_add) * d.oF + (int64_t)to * d.oT;
     out_row[tid] = off;
+    if constexpr (VEC4) {
+      const int fi0 = fo * d.stride_f, ti0 = to * d.stride_t;
+      rowinfo[tid][0] = fi0;
+      rowinfo[tid][1] = ti0;
+      rowinfo[tid][2] = valid ? 1 : 0;
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg)
+        rowbase[sg][tid] = (int)(b * d.seg[sg].sB + (int64_t)fi0 * d.seg[sg].sF + (int64_t)ti0 * d.seg[sg].sT);
+    }
+  }
+  extern __shared__ int2 ctab[];  // VEC4: [K/4] chunk entries (dynamic LDS)
+  if constexpr (VEC4) {
+    for (int q = tid; q < d.K / 4; q += NTH) {
+      const clskd_ktab_entry e = d.ktab[q * 4];
+      const int sg = d.kseg[q * 4];
+      ctab[q] = make_int2(e.off, (int)(((unsigned)e.dF & 0xFFFFu) | (((unsigned)e.dT & 0xFFu) << 16) |
+                                       ((unsigned)sg << 24)));
+    }
+    __syncthreads();
   }
 
-  // ---- A-gather rows owned by this thread: rows (tid>>2) and (tid>>2)+64, k-quad (tid&3) ----
+  // ---- A-gather rows owned by this thread: rows (tid>>2) and (tid>>2)+RSTEP, k-quad (tid&3) --
   const int kq = tid & 3;
   bool rvalid[2];
   int rb[2], rfi[2], rti[2];
+  int a_rb[2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    int64_t m = m0 + (tid >> 2) + 64 * i;
-    rvalid[i] = m < M;
-    int64_t mm = rvalid[i] ? m : 0;
-    int64_t b = mm / FoTo;
-    int64_t r = mm - b * FoTo;
-    int fo = (int)(r / d.To);
-    int to = (int)(r - (int64_t)fo * d.To);
-    rb[i] = (int)b;
-    rfi[i] = fo * d.stride_f;
-    rti[i] = to * d.stride_t;
+    const int row = (tid >> 2) + RSTEP * i;
+    if constexpr (VEC4) {
+      rfi[i] = rowinfo[row][0];
+      rti[i] = rowinfo[row][1];
+      rvalid[i] = rowinfo[row][2] != 0;
+      rb[i] = 0;
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) a_rb[i][sg] = rowbase[sg][row];
+    } else {
+      int64_t m = m0 + row;
+      rvalid[i] = m < M;
+      int64_t mm = rvalid[i] ? m : 0;
+      int64_t b = mm / FoTo;
+      int64_t r = mm - b * FoTo;
+      int fo = (int)(r / d.To);
+      int to = (int)(r - (int64_t)fo * d.To);
+      rb[i] = (int)b;
+      rfi[i] = fo * d.stride_f;
+      rti[i] = to * d.stride_t;
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) a_rb[i][sg] = 0;
+    }
   }
+  const float* sp0 = d.seg[0].ptr;
+  const float* sp1 = d.seg[1].ptr;
+  const float* sp2 = d.seg[2].ptr;
+  const float* sp3 = d.seg[3].ptr;
 
   auto load_a = [&](int kt, f32x4 (&ra)[2]) {
     if constexpr (VEC4) {
-      const int k = kt * BK + kq * 4;
-      const clskd_ktab_entry e = d.ktab[k];
-      const int s = d.kseg[k];
-      const float* sp = sel4(s, d.seg[0].ptr, d.seg[1].ptr, d.seg[2].ptr, d.seg[3].ptr);
-      const int64_t sB = sel4(s, d.seg[0].sB, d.seg[1].sB, d.seg[2].sB, d.seg[3].sB);
-      const int64_t sF = sel4(s, d.seg[0].sF, d.seg[1].sF, d.seg[2].sF, d.seg[3].sF);
-      const int64_t sT = sel4(s, d.seg[0].sT, d.seg[1].sT, d.seg[2].sT, d.seg[3].sT);
-      const int Fb = sel4(s, d.seg[0].F, d.seg[1].F, d.seg[2].F, d.seg[3].F);
-      const int Tb = sel4(s, d.seg[0].T, d.seg[1].T, d.seg[2].T, d.seg[3].T);
+      const int2 ce = ctab[kt * (BK / 4) + kq];
+      const int sg = (int)((unsigned)ce.y >> 24);
+      const int dF = (int)(short)(ce.y & 0xFFFF);
+      const int dT = (int)(signed char)((ce.y >> 16) & 0xFF);
+      const float* sp = sel4(sg, sp0, sp1, sp2, sp3);
+      const int Fb = sel4(sg, d.seg[0].F, d.seg[1].F, d.seg[2].F, d.seg[3].F);
+      const int Tb = sel4(sg, d.seg[0].T, d.seg[1].T, d.seg[2].T, d.seg[3].T);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int fi = rfi[i] + e.dF;
-        const int ti = rti[i] + e.dT;
+        const int fi = rfi[i] + dF;
+        const int ti = rti[i] + dT;
+        const int rbase = sel4(sg, a_rb[i][0], a_rb[i][1], a_rb[i][2], a_rb[i][3]);
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (rvalid[i] && fi >= 0 && fi < Fb && ti >= 0 && ti < Tb) {
-          const float* p = sp + (int64_t)rb[i] * sB + (int64_t)rfi[i] * sF + (int64_t)rti[i] * sT + e.off;
-          v = *reinterpret_cast<const f32x4*>(p);
-        }
+        if (rvalid[i] && (unsigned)fi < (unsigned)Fb && (unsigned)ti < (unsigned)Tb)
+          v = *reinterpret_cast<const f32x4*>(sp + (int64_t)(rbase + ce.x));
         ra[i] = v;
       }
     } else {
@@ -131,11 +175,11 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
     }
   };
 
-  constexpr int NBL = (BN * 4 + 255) / 256;  // float4 B loads per thread
+  constexpr int NBL = (BN * 4 + NTH - 1) / NTH;  // float4 B loads per thread
   auto load_b = [&](int kt, f32x4 (&rbv)[NBL]) {
 #pragma unroll
     for (int i = 0; i < NBL; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NTH * i;
       const int n = n0 + (idx >> 2);
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if ((idx >> 2) < BN && n < d.N)
@@ -148,12 +192,12 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
   auto store_tiles = [&](int buf, const f32x4 (&ra)[2], const f32x4 (&rbv)[NBL]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int row = (tid >> 2) + 64 * i;
+      const int row = (tid >> 2) + RSTEP * i;
       *reinterpret_cast<f32x4*>(&As[buf][row * BK + swz(row, kq) * 4]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < NBL; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NTH * i;
       const int row = idx >> 2;
       if (row < BN) *reinterpret_cast<f32x4*>(&Bs[buf][row * BK + swz(row, idx & 3) * 4]) = rbv[i];
     }
@@ -203,8 +247,11 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
   }
 
   if (d.stats) {  // fused BatchNorm statistics (fp32 per lane, fp64 across lanes/waves)
+    // one partial per 128-row block (the fused-statistics contract): waves 4h..4h+3 of a
+    // 256-row tile form block 2*tile + h
     __syncthreads();
-    double* red = reinterpret_cast<double*>(&As[0][0]);  // [4 waves][BN][2]
+    double* red = reinterpret_cast<double*>(&As[0][0]);  // [NW waves][BN][2]
+    static_assert(NW * BN * 2 * 8 <= 2 * BM * BK * 4, "stats scratch fits in As");
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int col = t * 32 + (lane & 31);
@@ -226,14 +273,19 @@ __global__ __launch_bounds__(256) void conv_igemm_f32(const ConvArgs args) {
       }
     }
     __syncthreads();
-    for (int c = tid; c < BN; c += 256) {
+    const int64_t nblk128 = (M + 127) / 128;
+    for (int q = tid; q < BN * (NW / 4); q += NTH) {
+      const int c = q % BN, hb = q / BN;
       const int n = n0 + c;
-      if (n >= d.N) continue;
-      const double S = red[c * 2] + red[(BN + c) * 2] + red[(2 * BN + c) * 2] + red[(3 * BN + c) * 2];
-      const double Q = red[c * 2 + 1] + red[(BN + c) * 2 + 1] + red[(2 * BN + c) * 2 + 1] +
-                       red[(3 * BN + c) * 2 + 1];
-      d.stats[((int64_t)tile * d.N + n) * 2] = S;
-      d.stats[((int64_t)tile * d.N + n) * 2 + 1] = Q;
+      const int64_t blk = (int64_t)tile * (NW / 4) + hb;
+      if (n >= d.N || blk >= nblk128) continue;
+      const int w0 = 4 * hb;
+      const double S = red[(w0 * BN + c) * 2] + red[((w0 + 1) * BN + c) * 2] +
+                       red[((w0 + 2) * BN + c) * 2] + red[((w0 + 3) * BN + c) * 2];
+      const double Q = red[(w0 * BN + c) * 2 + 1] + red[((w0 + 1) * BN + c) * 2 + 1] +
+                       red[((w0 + 2) * BN + c) * 2 + 1] + red[((w0 + 3) * BN + c) * 2 + 1];
+      d.stats[(blk * d.N + n) * 2] = S;
+      d.stats[(blk * d.N + n) * 2 + 1] = Q;
     }
   }
 
@@ -311,15 +363,26 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
     return CLSKD_OK;
   }
   ConvArgs a{d};
-  const unsigned gx = (unsigned)cdiv(M, BM);
-#define LAUNCH(BN_, V_, O_)                                                                  \
+  const size_t ctab_bytes = (size_t)(d.K / 4) * 8;  // VEC4 K-chunk table (dynamic LDS)
+  CLSKD_CHECK_SHAPE(!d.vec4 || ctab_bytes <= 32 * 1024, "conv2d(f32): K=%d too long for the chunk table", d.K);
+  // 8-wave 256-row tiles (A/B knob CLSKD_F32_WAVES=4|8): half the B staging per FLOP and two
+  // waves per SIMD to hide the gather latency
+  static const int nw = [] {
+    const char* e = getenv("CLSKD_F32_WAVES");
+    return e && e[0] == '8' ? 8 : 4;
+  }();
+#define LAUNCH(BN_, V_, O_, NW_)                                                             \
   do {                                                                                       \
-    hipLaunchKernelGGL((conv_igemm_f32<BN_, V_, O_>), dim3(gx, (unsigned)cdiv(d.N, BN_)),     \
-                       dim3(256), 0, st, a);                                                 \
-    note_kernel("conv_igemm_f32<%d,%s,%s>", BN_, (V_) ? "true" : "false", type_name<O_>()); \
+    hipLaunchKernelGGL((conv_igemm_f32<BN_, V_, O_, NW_>),                                    \
+                       dim3((unsigned)cdiv(M, 32 * NW_), (unsigned)cdiv(d.N, BN_)),           \
+                       dim3(NW_ * 64), (V_) ? ctab_bytes : 0, st, a);                        \
+    note_kernel("conv_igemm_f32<%d,%s,%s,%d>", BN_, (V_) ? "true" : "false",                  \
+                type_name<O_>(), NW_);                                                       \
   } while (0)
+#define LAUNCH_NW(BN_, V_, O_) \
+  do { if (nw == 8) LAUNCH(BN_, V_, O_, 8); else LAUNCH(BN_, V_, O_, 4); } while (0)
 #define LAUNCH_O(BN_, V_) \
-  do { if (d.out_dtype == CLSKD_BF16) LAUNCH(BN_, V_, __bf16); else LAUNCH(BN_, V_, float); } while (0)
+  do { if (d.out_dtype == CLSKD_BF16) LAUNCH_NW(BN_, V_, __bf16); else LAUNCH_NW(BN_, V_, float); } while (0)
   if (d.N <= 32) {
     if (d.vec4) LAUNCH_O(32, true); else LAUNCH_O(32, false);
   } else if (d.N <= 64) {
@@ -328,6 +391,7 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
     if (d.vec4) LAUNCH_O(128, true); else LAUNCH_O(128, false);
   }
 #undef LAUNCH_O
+#undef LAUNCH_NW
 #undef LAUNCH
   CLSKD_LAUNCH_CHECK("conv2d");
   return CLSKD_OK;

@@ -81,7 +81,7 @@ def test_conv_engine_against_torch():
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("C1,C2,N", [(2, 0, 8), (2, 0, 16), (8, 8, 2), (16, 16, 2), (6, 0, 4),
-                                     (6, 2, 3), (3, 0, 1), (1, 0, 16)])
+                                     (6, 2, 3), (3, 0, 1), (1, 0, 16), (2, 0, 32), (3, 0, 32)])
 def test_conv_direct_against_torch_and_engine(dt, C1, C2, N):
     """Direct-convolution kernel (narrow N / short K): 2-segment 5x2 stride-(2,1) conv with fused
     BN statistics against torch (fp64 on the same bf16-rounded operands for bf16) and against the
