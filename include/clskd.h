@@ -267,6 +267,12 @@ typedef struct {
   int32_t nslab;
   int32_t dtype;      /* CLSKD_F32 (Cs % 4 == 0) or CLSKD_BF16 (Cs % 8 == 0) storage */
   int32_t reserved;
+  /* optional per-channel affine applied to every loaded element before the product (NULL =
+   * none): z = x*scale[ch] + shift[ch], ch in [0, Ctot), rounded to the storage type — a
+   * BatchNorm whose apply pass is folded into the Gram (bitwise the same as clskd_bn_apply
+   * followed by a plain gram).  Ctot <= 1024 when given. */
+  const float* scale;
+  const float* shift;
 } clskd_gram_job;
 
 int clskd_gram_partial(const clskd_gram_job* jobs, int32_t njobs, int32_t B, float* slabs,

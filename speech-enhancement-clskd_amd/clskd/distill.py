@@ -57,9 +57,12 @@ def _side_stream(dev, which=0):
 
 
 def _gram_bftc(t, c0=0, Cs=None):
+    affine = None
+    if isinstance(t, ops.DeferredBN):  # BatchNorm folded into the Gram's loads
+        t, affine = t.raw, t.coef
     B, Fn, Tn, Ct = t.shape
     Cs = Ct if Cs is None else Cs
-    return ops.GramView(t, 0, Fn * Tn * Ct, Fn * Tn, Ct, c0, Cs)
+    return ops.GramView(t, 0, Fn * Tn * Ct, Fn * Tn, Ct, c0, Cs, affine)
 
 
 class KnowledgeDistillation(nn.Module):
@@ -193,7 +196,7 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
         with torch.cuda.stream(side2):
             side2.wait_event(ev)
             _mark("side2: student encoder ready", side2)
-            s_enc = review_encoder.forward_bftc(enc)
+            s_enc = review_encoder.forward_bftc(enc, defer_bn=True)
             _mark("side2: review encoder done", side2)
             held["s_enc"] = s_enc
             held["g_enc"] = ops.GramSlabs([_gram_bftc(a) for a in s_enc], B)
@@ -207,7 +210,7 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
         _mark("side: student done", side)
         if reinit is not None:
             reinit("decoder")
-        s_dec = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5])
+        s_dec = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5], defer_bn=True)
         Chs = sf["dec_in"].shape[-1] // 2
         g_dec = ops.GramSlabs([_gram_bftc(a) for a in s_dec] +
                               [_gram_bftc(sf["dec_in"], 0, Chs), _gram_bftc(sf["dec_in"], Chs, Chs)],
@@ -241,7 +244,8 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     _mark("main: end", main)
     return dict(loss=total, base=buf[1], sc=buf[0], spkd=buf[2:], enc=buf[2:8], dec=buf[8:14],
                 clstm_real=buf[14], clstm_img=buf[15], student_wav=sf["out_wav"],
-                teacher_wav=tf["out_wav"], s_enc=s_enc, s_dec=s_dec, t=tf, s=sf,
+                teacher_wav=tf["out_wav"], s_enc=ops.MaterializingList(s_enc),
+                s_dec=ops.MaterializingList(s_dec), t=tf, s=sf,
                 gram_slabs=(g_enc, g_dec, g_t))
 
 

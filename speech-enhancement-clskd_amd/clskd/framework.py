@@ -240,8 +240,10 @@ class ABF(nn.Module):
             self._wcache["w"] = ent
         return ent[1]
 
-    def forward_bftc(self, x, y=None, shape=None, out_shape=None, train=None):
-        """x: BFTC [B][F][T][Cin]; y: BFTC residual [B][Fr][Tr][mid].  Returns (out, x_fused) BFTC."""
+    def forward_bftc(self, x, y=None, shape=None, out_shape=None, train=None, defer_bn=False):
+        """x: BFTC [B][F][T][Cin]; y: BFTC residual [B][Fr][Tr][mid].  Returns (out, x_fused) BFTC.
+        defer_bn: conv2's BatchNorm is left unapplied — out is an ops.DeferredBN (raw output +
+        coefficients) for a consumer that folds the affine into its loads (the SPKD Gram)."""
         train = self.training if train is None else train
         B, Fn, Tn, Cin = x.shape
         w1p, w2p, att = self._weights(x.dtype)
@@ -280,6 +282,11 @@ class ABF(nn.Module):
         ops.conv([seg_bftc(x1)], [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], B, Fn,
                  Tn, Cout, w2p, None, out, OutMap(Fn * Tn * Cout, Tn * Cout, Cout), stats=part2)
         bn = self.conv2[1]
+        if defer_bn:
+            coef = ops.batch_norm_bftc(out, None, bn.weight, bn.bias, bn.running_mean,
+                                       bn.running_var, train, bn.momentum, bn.eps, 1,
+                                       partial=(part2, nmb) if train else None)
+            return ops.DeferredBN(out, coef), x1
         ops.batch_norm_bftc(out, out, bn.weight, bn.bias, bn.running_mean, bn.running_var, train,
                             bn.momentum, bn.eps, 1, partial=(part2, nmb) if train else None)
         return out, x1
@@ -310,15 +317,17 @@ class ReviewKD(nn.Module):
             abf.compute = compute
         return self
 
-    def forward_bftc(self, feats):
-        """feats: BFTC student features in the reference's list order.  Returns BFTC outputs."""
+    def forward_bftc(self, feats, defer_bn=False):
+        """feats: BFTC student features in the reference's list order.  Returns BFTC outputs
+        (ops.DeferredBN entries when defer_bn: the ABF output BatchNorms left for the consumer)."""
         xs = feats[::-1] if self.ft_type == "encoder" else list(feats)
         results = []
-        out, res = self.abfs[0].forward_bftc(xs[0], out_shape=self.out_shapes[0])
+        out, res = self.abfs[0].forward_bftc(xs[0], out_shape=self.out_shapes[0],
+                                             defer_bn=defer_bn)
         results.append(out)
         for feature, abf, shape, out_shape in zip(xs[1:], self.abfs[1:], self.shapes[1:],
                                                   self.out_shapes[1:]):
-            out, res = abf.forward_bftc(feature, res, shape, out_shape)
+            out, res = abf.forward_bftc(feature, res, shape, out_shape, defer_bn=defer_bn)
             if self.ft_type == "encoder":
                 results.insert(0, out)
             else:

@@ -469,6 +469,47 @@ class GramView:
     Ctot: int
     c0: int
     Cs: int
+    affine: torch.Tensor = None  # optional [scale | shift] (2 x Ctot fp32) applied on load
+
+
+class DeferredBN:
+    """A BFTC conv output whose BatchNorm apply is deferred: raw tensor + [scale | shift]
+    coefficients.  A Gram over it folds the affine into its loads (GramView.affine);
+    materialize() runs clskd_bn_apply once (on the current stream) for anyone who wants the
+    normalised tensor itself."""
+
+    def __init__(self, raw, coef):
+        self.raw, self.coef = raw, coef
+        self._y = None
+
+    @property
+    def shape(self):
+        return self.raw.shape
+
+    def materialize(self):
+        if self._y is None:
+            x = self.raw
+            Cn = x.shape[-1]
+            y = torch.empty_like(x)
+            sc = self.coef.data_ptr()
+            check(lib().clskd_bn_apply(ptr(x), ptr(y), x.numel() // Cn, Cn, sc, sc + 4 * Cn, None,
+                                       _dt(x), _stream()), "bn_apply")
+            self._y = y
+        return self._y
+
+
+class MaterializingList(list):
+    """List of tensors / DeferredBN entries that hands out materialised tensors."""
+
+    def __getitem__(self, i):
+        v = super().__getitem__(i)
+        if isinstance(i, slice):
+            return [x.materialize() if isinstance(x, DeferredBN) else x for x in v]
+        return v.materialize() if isinstance(v, DeferredBN) else v
+
+    def __iter__(self):
+        for i in range(len(self)):
+            yield self[i]
 
 
 def gram_view(t):
@@ -510,8 +551,13 @@ class GramSlabs:
             ns = -(-v.P // chunk)
             dt = _dt(v.tensor)
             assert v.Cs % (8 if dt == _lib.BF16 else 4) == 0
+            sc = sh = None
+            if v.affine is not None:
+                assert v.affine.dtype == torch.float32 and v.affine.numel() == 2 * v.Ctot
+                sc = v.affine.data_ptr()
+                sh = sc + 4 * v.Ctot
             jobs[j] = _lib.GramJob(v.tensor.data_ptr() + v.tensor.element_size() * v.offset, v.sB,
-                                   v.P, v.Ctot, v.c0, v.Cs, chunk, first, ns, dt, 0)
+                                   v.P, v.Ctot, v.c0, v.Cs, chunk, first, ns, dt, 0, sc, sh)
             spans.append((first, ns))
             first += ns
         self.slabs = torch.empty(first * 1024, dtype=torch.float32, device=dev)

@@ -32,30 +32,57 @@ struct SpkdPairsArg {
   int32_t pair0;  // absolute pair index of blockIdx.x == 0
 };
 
+// Optional folded BatchNorm (job.scale/shift): the job's per-channel affine, staged in LDS by
+// the workgroup (aff[0][ch] = scale, aff[1][ch] = shift, ch in [0, Ctot)).
+constexpr int GRAM_AFF_MAX = 1024;
+
+template <bool AFF>
 __device__ __forceinline__ f32x4 load_row4_f32(const clskd_gram_job& j, int b, int B, int64_t e,
-                                               int64_t p0, int64_t p1) {
+                                               int64_t p0, int64_t p1,
+                                               const float (*aff)[GRAM_AFF_MAX]) {
   // 4 fp32 elements at slab-relative element e (Cs % 4 == 0, e % 4 == 0)
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
   if (b < B) {
     const int64_t p = p0 + e / j.Cs;
     const int c = (int)(e % j.Cs);
-    if (p < p1)
+    if (p < p1) {
       v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(j.ptr) +
                                           (int64_t)b * j.sB + p * j.Ctot + j.c0 + c);
+      if constexpr (AFF) {
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(&aff[0][j.c0 + c]);
+        const f32x4 sh = *reinterpret_cast<const f32x4*>(&aff[1][j.c0 + c]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = fmaf(v[i], sc[i], sh[i]);
+      }
+    }
   }
   return v;
 }
 
+template <bool AFF>
 __device__ __forceinline__ bf16x8g load_row8_bf16(const clskd_gram_job& j, int b, int B, int64_t e,
-                                                  int64_t p0, int64_t p1) {
+                                                  int64_t p0, int64_t p1,
+                                                  const float (*aff)[GRAM_AFF_MAX]) {
   // 8 bf16 elements (one 16-B load) at slab-relative element e (Cs % 8 == 0, e % 8 == 0)
   bf16x8g v = {};
   if (b < B) {
     const int64_t p = p0 + e / j.Cs;
     const int c = (int)(e % j.Cs);
-    if (p < p1)
+    if (p < p1) {
       v = *reinterpret_cast<const bf16x8g*>(reinterpret_cast<const __bf16*>(j.ptr) +
                                             (int64_t)b * j.sB + p * j.Ctot + j.c0 + c);
+      if constexpr (AFF) {  // the same fmaf + RNE rounding as clskd_bn_apply
+        const f32x4 s0 = *reinterpret_cast<const f32x4*>(&aff[0][j.c0 + c]);
+        const f32x4 s1 = *reinterpret_cast<const f32x4*>(&aff[0][j.c0 + c + 4]);
+        const f32x4 h0 = *reinterpret_cast<const f32x4*>(&aff[1][j.c0 + c]);
+        const f32x4 h1 = *reinterpret_cast<const f32x4*>(&aff[1][j.c0 + c + 4]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = (__bf16)fmaf((float)v[i], s0[i], h0[i]);
+          v[i + 4] = (__bf16)fmaf((float)v[i + 4], s1[i], h1[i]);
+        }
+      }
+    }
   }
   return v;
 }
@@ -86,24 +113,15 @@ __device__ __forceinline__ void gram_store_slab(float (*red)[3][256], const f32x
   }
 }
 
-template <int NB>  // row blocks of 16: B <= 16*NB
-__global__ __launch_bounds__(256) void gram_partial_kernel(const GramJobsArg jobs, int B,
-                                                           float* __restrict__ slabs) {
-  const int slab = jobs.slab0 + blockIdx.x;
-  // uniform scan of the (<= 32) kernel-argument jobs for the one owning this slab
-  int q = 0;
-  for (int k = 1; k < jobs.n; ++k)
-    if (slab >= jobs.j[k].first_slab) q = k;
-  const clskd_gram_job j = jobs.j[q];
-  const int si = slab - j.first_slab;
-  const int64_t p0 = (int64_t)si * j.chunk;
-  const int64_t p1 = min(j.P, p0 + j.chunk);
-  const int64_t nel = (p1 - p0) * j.Cs;  // elements per row in this slab
+template <int NB, bool AFF>
+__device__ __forceinline__ void gram_accumulate(const clskd_gram_job& j, int B, int64_t nel,
+                                                int64_t p0, int64_t p1,
+                                                const float (*aff)[GRAM_AFF_MAX], f32x4& acc00,
+                                                f32x4& acc01, f32x4& acc11) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int r = lane & 15;
   const int g = lane >> 4;
-  f32x4 acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
   if (j.dtype == CLSKD_BF16) {
     // 16x16x32 bf16 MFMA: lane (r, g) holds row r, 8 consecutive k; A and B are the same
     // register (G = Z Z^T), so one 16-B load feeds both operands.  64 B per row per load.
@@ -114,8 +132,8 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const GramJobsArg job
       for (int u = 0; u < U; ++u) {
         const int64_t e = base + (int64_t)u * 128 + 8 * g;
         const bool ok = e < nel;
-        v0[u] = ok ? load_row8_bf16(j, r, B, e, p0, p1) : bf16x8g{};
-        if constexpr (NB == 2) v1[u] = ok ? load_row8_bf16(j, r + 16, B, e, p0, p1) : bf16x8g{};
+        v0[u] = ok ? load_row8_bf16<AFF>(j, r, B, e, p0, p1, aff) : bf16x8g{};
+        if constexpr (NB == 2) v1[u] = ok ? load_row8_bf16<AFF>(j, r + 16, B, e, p0, p1, aff) : bf16x8g{};
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -135,8 +153,8 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const GramJobsArg job
       for (int u = 0; u < U; ++u) {
         const int64_t e = base + (int64_t)u * 64 + 4 * g;
         const bool ok = e < nel;
-        v0[u] = ok ? load_row4_f32(j, r, B, e, p0, p1) : f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (NB == 2) v1[u] = ok ? load_row4_f32(j, r + 16, B, e, p0, p1) : f32x4{0.f, 0.f, 0.f, 0.f};
+        v0[u] = ok ? load_row4_f32<AFF>(j, r, B, e, p0, p1, aff) : f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (NB == 2) v1[u] = ok ? load_row4_f32<AFF>(j, r + 16, B, e, p0, p1, aff) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -150,6 +168,33 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const GramJobsArg job
         }
       }
     }
+  }
+}
+
+template <int NB>  // row blocks of 16: B <= 16*NB
+__global__ __launch_bounds__(256) void gram_partial_kernel(const GramJobsArg jobs, int B,
+                                                           float* __restrict__ slabs) {
+  const int slab = jobs.slab0 + blockIdx.x;
+  // uniform scan of the (<= 32) kernel-argument jobs for the one owning this slab
+  int q = 0;
+  for (int k = 1; k < jobs.n; ++k)
+    if (slab >= jobs.j[k].first_slab) q = k;
+  const clskd_gram_job j = jobs.j[q];
+  const int si = slab - j.first_slab;
+  const int64_t p0 = (int64_t)si * j.chunk;
+  const int64_t p1 = min(j.P, p0 + j.chunk);
+  const int64_t nel = (p1 - p0) * j.Cs;  // elements per row in this slab
+  f32x4 acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
+  __shared__ __attribute__((aligned(16))) float aff[2][GRAM_AFF_MAX];
+  if (j.scale) {  // uniform per workgroup
+    for (int c = threadIdx.x; c < j.Ctot; c += 256) {
+      aff[0][c] = j.scale[c];
+      aff[1][c] = j.shift[c];
+    }
+    __syncthreads();
+    gram_accumulate<NB, true>(j, B, nel, p0, p1, aff, acc00, acc01, acc11);
+  } else {
+    gram_accumulate<NB, false>(j, B, nel, p0, p1, aff, acc00, acc01, acc11);
   }
   __shared__ float red[4][3][256];
   gram_store_slab(red, acc00, acc01, acc11, slabs + (int64_t)slab * 1024);
@@ -371,6 +416,10 @@ static int validate_gram_jobs(const clskd_gram_job* jobs, int32_t njobs, int32_t
                           j.sB % g == 0 && j.P > 0 && j.chunk > 0,
                       "gram: job %d geometry (Cs %d, c0 %d, Ctot %d) needs multiples of %d", k,
                       j.Cs, j.c0, j.Ctot, g);
+    CLSKD_CHECK_ARG((j.scale == nullptr) == (j.shift == nullptr),
+                    "gram: job %d scale and shift go together", k);
+    CLSKD_CHECK_SHAPE(!j.scale || j.Ctot <= GRAM_AFF_MAX, "gram: job %d folded affine needs Ctot <= %d",
+                      k, GRAM_AFF_MAX);
     CLSKD_CHECK_SHAPE(j.first_slab == next && j.nslab == (int32_t)((j.P + j.chunk - 1) / j.chunk),
                       "gram: job %d slab range [%d, +%d) is not contiguous", k, j.first_slab,
                       j.nslab);

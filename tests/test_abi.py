@@ -24,12 +24,32 @@ def test_library_exports_every_header_symbol():
     assert isinstance(lib.clskd_last_error(), bytes)
 
 
-def test_struct_layouts_match_header():
-    # clskd_seg: ptr + 3 int64 + 2 int32 = 40 B; desc must be 8-aligned
-    assert ctypes.sizeof(_lib.Seg) == 40
-    assert ctypes.sizeof(_lib.KtabEntry) == 8
-    assert ctypes.sizeof(_lib.GramJob) == 56
-    assert ctypes.sizeof(_lib.ConvDesc) % 8 == 0
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors have the C compiler's layout of include/clskd.h (sizeof and the
+    offset of each struct's last field, from a probe compiled with gcc)."""
+    import subprocess
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    probe = tmp_path / "probe.c"
+    probe.write_text("""
+#include <stdio.h>
+#include <stddef.h>
+#include "clskd.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(clskd_seg), sizeof(clskd_ktab_entry),
+         sizeof(clskd_gram_job), offsetof(clskd_gram_job, shift), sizeof(clskd_draw_job),
+         offsetof(clskd_draw_job, stream_id), sizeof(clskd_conv_desc),
+         offsetof(clskd_conv_desc, tap_dt));
+  return 0;
+}
+""")
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c99", "-I", inc, str(probe), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    want = [ctypes.sizeof(_lib.Seg), ctypes.sizeof(_lib.KtabEntry), ctypes.sizeof(_lib.GramJob),
+            _lib.GramJob.shift.offset, ctypes.sizeof(_lib.DrawJob), _lib.DrawJob.stream_id.offset,
+            ctypes.sizeof(_lib.ConvDesc), _lib.ConvDesc.tap_dt.offset]
+    assert got == want
 
 
 def test_error_path_reports_without_gpu():
