@@ -267,8 +267,15 @@ class DCCRN(nn.Module):
             wr, wi = cc.real_conv.weight, cc.imag_conv.weight  # [Ci/2, Co/2, 5, 2]
             top = torch.cat([wr, wi], 1)   # real input -> [real out | imag out]
             bot = torch.cat([-wi, wr], 1)  # imag input -> [real out | imag out]
-            w = torch.cat([top, bot], 0)   # [Ci, Co, 5, 2]
+            w = torch.cat([top, bot], 0)   # [Ci, Co, 5, 2], rows [out_re, skip_re, out_im, skip_im]
             Ci, Co = w.shape[:2]
+            # K order per tap: [out_t (re, im), skip (re, im)] — two contiguous segments (the
+            # decoder input and the skip tensor, each whole): fewer, wider gather runs, and
+            # 32-channel segments make narrow layers eligible for the halo kernel
+            h = Ci // 4
+            perm = torch.cat([torch.arange(0, h), torch.arange(2 * h, 3 * h),
+                              torch.arange(h, 2 * h), torch.arange(3 * h, 4 * h)]).to(w.device)
+            w = w[perm]
             taps = [(kf, kt) for kf, _ in self._DEC_TAPS[parity] for kt in (0, 1)]
             w = torch.stack([w[:, :, kf, kt] for kf, kt in taps], 0)  # [ntap, Ci, Co]
             w = w.permute(2, 0, 1)  # [Co, ntap, Ci]
@@ -438,9 +445,10 @@ class DCCRN(nn.Module):
             skip = enc[-1 - d]
             Cof = out_t.shape[-1]
             Csk = skip.shape[-1]
-            segs = [seg_bftc(out_t, 0, Cof // 2, out_t0, out_T), seg_bftc(skip, 0, Csk // 2),
-                    seg_bftc(out_t, Cof // 2, Cof // 2, out_t0, out_T),
-                    seg_bftc(skip, Csk // 2, Csk // 2)]
+            # complex_cat (DCCRN.py:203-204): real = [out_re, skip_re], imag = [out_im, skip_im];
+            # the packed weights take K per tap as [out_t (re|im), skip (re|im)] (_dec_w)
+            assert Cof == Csk, "DCCRN decoder: input and skip channel counts match"
+            segs = [seg_bftc(out_t, 0, Cof, out_t0, out_T), seg_bftc(skip, 0, Csk)]
             Co = self.decoder[d][0].out_channels * 2
             last = d == nl - 1
             raw = torch.empty(B, 2 * F, T + 1, Co, **(f32 if last else act))

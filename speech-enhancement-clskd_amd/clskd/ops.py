@@ -260,8 +260,6 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
     for i in range(len(segs), _lib.MAX_SEGS):
         d.seg[i] = d.seg[0]
     d.ktab, d.kseg, d.vec4 = kt.data_ptr(), ks.data_ptr(), int(vec4)
-    direct = direct_ok(N, Kp)
-    d.wlayout = _lib.WLAYOUT_DIRECT if direct else _lib.WLAYOUT_NK
     d.oB, d.oF, d.oT, d.oNhi, d.oNlo = omap.oB, omap.oF, omap.oT, omap.oNhi, omap.oNlo
     d.nlo = min(omap.nlo, 1 << 30)
     d.of_mul, d.of_add = omap.of_mul, omap.of_add
@@ -276,6 +274,8 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
             d.seg_c[i] = g.C
         for i, (dF, dT) in enumerate(taps):
             d.tap_df[i], d.tap_dt[i] = dF, dT
+    direct = direct_ok(N, Kp)
+    d.wlayout = _lib.WLAYOUT_DIRECT if direct else _lib.WLAYOUT_NK
     pl = _ConvPlan()
     pl.desc, pl.nseg, pl.direct = d, len(segs), direct
     pl.segs = [d.seg[i] for i in range(_lib.MAX_SEGS)]  # views into d (patched per call)

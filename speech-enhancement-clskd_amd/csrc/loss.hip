@@ -322,16 +322,23 @@ __global__ __launch_bounds__(256) void stft_mag_loss_kernel(const float* __restr
 }
 
 // out[0] = factor_sc * sqrt(sum (Y-X)^2) / sqrt(sum Y^2) ; out[1] = factor_mag * sum|..| / count
-__global__ void stft_loss_finalize_kernel(const double* partial, int nblk, int64_t count,
-                                          float factor_sc, float factor_mag, int accumulate,
-                                          float* out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// 64 threads: lane l sums partials l, l+64, ... (fixed order), then a fixed xor-tree.
+__global__ __launch_bounds__(64) void stft_loss_finalize_kernel(const double* partial, int nblk,
+                                                               int64_t count, float factor_sc,
+                                                               float factor_mag, int accumulate,
+                                                               float* out) {
   double a = 0, b = 0, c = 0;
-  for (int i = 0; i < nblk; ++i) {
+  for (int i = threadIdx.x; i < nblk; i += 64) {
     a += partial[i * 3];
     b += partial[i * 3 + 1];
     c += partial[i * 3 + 2];
   }
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+    c += __shfl_xor(c, o, 64);
+  }
+  if (threadIdx.x != 0) return;
   const float sc = (float)(factor_sc * (sqrt(a) / sqrt(b)));
   const float mag = (float)(factor_mag * (c / (double)count));
   out[0] = accumulate ? out[0] + sc : sc;
