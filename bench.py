@@ -181,7 +181,8 @@ def main():
         conv_total_fl = sum(v[2] for v in census.values())
         avg_ms = ms / n_l
         achieved = flops / n_l / (avg_ms * 1e-3) / 1e12
-        peak = PEAK_BF16_MFMA_TFLOPS if name.startswith("conv_igemm_bf16") else PEAK_F32_MFMA_TFLOPS
+        bf16_ops = name.startswith("conv_igemm_bf16") or name.startswith("conv_halo_kernel")
+        peak = PEAK_BF16_MFMA_TFLOPS if bf16_ops else PEAK_F32_MFMA_TFLOPS
         traffic, traffic_src = None, None
         tpath = os.path.join(REPO, "profiles", TRAFFIC_FILE)
         if os.path.exists(tpath):

@@ -314,8 +314,8 @@ class DCCRN(nn.Module):
         return self._packed(("lstm", li, compute), ps, build)
 
     def _stft_w(self):
-        def build():
-            return self.stft.weight[:, 0, :].float().contiguous()  # [514, 400]
+        def build():  # [514, 400] -> K padded to the fp32 engine's multiple
+            return ops.pack_weight(self.stft.weight[:, 0, :].float().unsqueeze(1), 400)
         return self._packed(("stft",), (self.stft.weight,), build)
 
     def _istft_w(self):
