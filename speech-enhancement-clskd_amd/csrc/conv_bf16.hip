@@ -168,6 +168,8 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
 #pragma unroll
     for (int sg = 0; sg < 4; ++sg) a_rb[i][sg] = rowbase[sg * BM + r];
   }
+  // this wave's share of the B row groups: NGB, or NGB - 1 when the groups run out (uniform)
+  const bool fullB = (wave + NW * (NGB - 1)) < BN / RPD;
   const uint64_t sp0 = (uint64_t)(uintptr_t)d.seg[0].ptr, sp1 = (uint64_t)(uintptr_t)d.seg[1].ptr;
   const uint64_t sp2 = (uint64_t)(uintptr_t)d.seg[2].ptr, sp3 = (uint64_t)(uintptr_t)d.seg[3].ptr;
   auto issue = [&](int kt, int stage) {
@@ -190,7 +192,8 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
     }
 #pragma unroll
     for (int i = 0; i < NGB; ++i) {
-      // B rows beyond the tile (BN/8 not a multiple of NW) re-load row group 0: harmless dup
+      // B row groups are dealt round-robin over the waves; a wave past the last group in its
+      // final round issues nothing for it (fullB false): no duplicate DMA pieces
       const int rg = (wave + NW * i) < BN / RPD ? (wave + NW * i) : 0;
       const int r = rg * RPD + prow;
       const int c = ppos ^ swz<BK>(r);
@@ -204,8 +207,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
     for (int i = 0; i < NGA; ++i) glds16((const void*)srcA[i], sl + (wave * NGA + i) * 1024);
 #pragma unroll
     for (int i = 0; i < NGB; ++i) {
-      const int rg = (wave + NW * i) < BN / RPD ? (wave + NW * i) : 0;
-      glds16((const void*)srcB[i], sl + BM * ROWB + rg * 1024);
+      if (i < NGB - 1 || fullB) glds16((const void*)srcB[i], sl + BM * ROWB + (wave + NW * i) * 1024);
     }
   };
 
@@ -231,11 +233,14 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
 
   for (int kt = 0; kt < nk; ++kt) {
     // wait for this wave's DMAs of tile kt; the (up to NS-2) younger tiles stay in flight
+    // (per-wave piece count: NG, or NG - 1 for a wave without a B group in the last round)
     const int ahead = min(NS - 2, nk - 1 - kt);
     if (ahead >= 2) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NG) : "memory");
+      if (fullB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NG) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (NG - 1)) : "memory");
     } else if (ahead == 1) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
+      if (fullB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG - 1) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -320,6 +325,39 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
   }
 
   OutT* out = reinterpret_cast<OutT*>(d.out);
+  // Vectorised epilogue: each wave stages its (converted) sub-tile in the freed stage LDS and
+  // writes it back as 16-B row chunks — 4 dwordx4 stores per lane instead of 16 * TM * TN
+  // scalar stores (the store tail was 12-14 % of a 576-deep layer).  Needs a channel-contiguous,
+  // 16-B aligned output map; otherwise the scalar scatter below.
+  constexpr int CH = 16 / (int)sizeof(OutT);  // channels per 16-B chunk
+  constexpr int WR = BM / WM, WC = BN / WN;   // wave sub-tile
+  constexpr int WBYTES = WR * WC * (int)sizeof(OutT);
+  constexpr bool VEC_FITS = NW * WBYTES <= NS * SB && WC % CH == 0;
+  const bool vec = VEC_FITS && DBG != 3 && d.oNlo == 1 && d.nlo >= d.N && d.N % CH == 0 &&
+                   (((uintptr_t)d.out) & 15) == 0 && d.oB % CH == 0 && d.oF % CH == 0 &&
+                   d.oT % CH == 0;
+  if (vec) {
+    __syncthreads();  // every wave's last fragment reads and the statistics scratch are done
+    OutT* wt = reinterpret_cast<OutT*>(smem + wave * WBYTES);  // [WR][WC]
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          wt[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * WC + j * 32 + l32] = (OutT)acc[i][j][r];
+    constexpr int CPRW = WC / CH;  // 16-B chunks per sub-tile row
+#pragma unroll
+    for (int q0 = 0; q0 < WR * CPRW; q0 += 64) {
+      const int q = q0 + lane;
+      const int rr = q / CPRW, cc = q % CPRW;
+      const int64_t ro = out_row[wm * WR + rr];
+      const int n = n0 + wn * WC + cc * CH;
+      if (q < WR * CPRW && ro >= 0 && n < d.N)
+        *reinterpret_cast<uint4*>(out + ro + n) = *reinterpret_cast<const uint4*>(wt + rr * WC + cc * CH);
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * (BN / WN) + j * 32 + l32;
@@ -331,7 +369,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
       for (int r = 0; r < 16; ++r) {
         const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int64_t ro = out_row[row];
-        if (ro >= 0) store_out<OutT>(out + ro + coff, acc[i][j][r]);
+        if (DBG != 3 && ro >= 0) store_out<OutT>(out + ro + coff, acc[i][j][r]);
       }
     }
   }
@@ -411,6 +449,9 @@ int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
   }();
   if (dbg == 1 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<128, 64, 256, 8, 3, __bf16, 1>(d, st);
   if (dbg == 2 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<128, 64, 256, 8, 3, __bf16, 2>(d, st);
+  if (dbg == 1 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 3, __bf16, 1>(d, st);
+  if (dbg == 2 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 3, __bf16, 2>(d, st);
+  if (dbg == 3 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 3, __bf16, 3>(d, st);
   if (d.N > 32 && d.K % 32 == 0 && tilecfg != 128) {
     // 256-row tiles stage a third fewer bytes per FLOP (measured 1.1-1.25x faster per tile
     // worth of work) but halve the workgroup count: pick them unless the tail rounds eat the

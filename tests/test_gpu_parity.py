@@ -129,7 +129,7 @@ def test_conv_direct_against_torch_and_engine(dt, C1, C2, N):
     np.testing.assert_allclose(res["direct"][0].numpy(), res["engine"][0].numpy(), rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("N", [45, 64, 100, 256, 300])
+@pytest.mark.parametrize("N", [45, 64, 96, 100, 136, 256, 300])
 @pytest.mark.parametrize("out_bf16", [False, True])
 def test_conv_bf16_engine_against_torch(N, out_bf16):
     """bf16 LDS-DMA MFMA engine (every tile configuration the dispatcher picks for these N):

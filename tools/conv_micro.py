@@ -22,6 +22,7 @@ CFGS.update({
     "dec3": ("dec", 256, 128, 32),
     "dec5": ("dec", 64, 32, 128),
     "abf3": ("abf", 64, 256, 16),     # 3x3, 64 -> 256
+    "abf4": ("abf", 64, 128, 32),     # 3x3, 64 -> 128 (the 256x128-tile engine config)
     "abf5": ("abf", 64, 64, 64),
 })
 
