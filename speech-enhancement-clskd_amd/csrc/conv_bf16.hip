@@ -76,6 +76,22 @@ struct ConvArgsV2 {
   clskd_conv_desc d;
 };
 
+// Counted wait leaving `ahead` younger K-tiles of this wave's DMAs in flight (NG pieces per
+// tile, NG - 1 for a wave without a B group in the last round); vmcnt takes immediates only.
+template <int NG, int A>
+__device__ __forceinline__ void wait_tiles(int ahead, bool fullB) {
+  if constexpr (A <= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (ahead >= A) {
+      if (fullB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A * NG) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A * (NG - 1)) : "memory");
+    } else {
+      wait_tiles<NG, A - 1>(ahead, fullB);
+    }
+  }
+}
+
 template <int BM, int BK, int BN, int NW, int NS, typename OutT, int DBG = 0>
 __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 args) {
   using namespace v2;
@@ -235,15 +251,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
     // wait for this wave's DMAs of tile kt; the (up to NS-2) younger tiles stay in flight
     // (per-wave piece count: NG, or NG - 1 for a wave without a B group in the last round)
     const int ahead = min(NS - 2, nk - 1 - kt);
-    if (ahead >= 2) {
-      if (fullB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NG) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (NG - 1)) : "memory");
-    } else if (ahead == 1) {
-      if (fullB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG - 1) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    wait_tiles<NG, NS - 2>(ahead, fullB);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -408,12 +416,17 @@ static int launch_nw(const clskd_conv_desc& d, hipStream_t st) {
 }
 
 // 256-row tiles, BK = 32, 16 waves: a third fewer staged bytes per FLOP than 128 x 256 x 64
-static int launch_big(const clskd_conv_desc& d, hipStream_t st) {
+template <int S128, int S256>
+static int launch_big_s(const clskd_conv_desc& d, hipStream_t st) {
   const bool f32out = d.out_dtype == CLSKD_F32;
-  if (d.N <= 64) return f32out ? launch_v2<256, 32, 64, 16, 3, float>(d, st) : launch_v2<256, 32, 64, 16, 3, __bf16>(d, st);
-  if (d.N <= 128) return f32out ? launch_v2<256, 32, 128, 16, 3, float>(d, st) : launch_v2<256, 32, 128, 16, 3, __bf16>(d, st);
-  return f32out ? launch_v2<256, 32, 256, 16, 3, float>(d, st) : launch_v2<256, 32, 256, 16, 3, __bf16>(d, st);
+  if (d.N <= 64) return f32out ? launch_v2<256, 32, 64, 16, S128, float>(d, st) : launch_v2<256, 32, 64, 16, S128, __bf16>(d, st);
+  if (d.N <= 128) return f32out ? launch_v2<256, 32, 128, 16, S128, float>(d, st) : launch_v2<256, 32, 128, 16, S128, __bf16>(d, st);
+  return f32out ? launch_v2<256, 32, 256, 16, S256, float>(d, st) : launch_v2<256, 32, 256, 16, S256, __bf16>(d, st);
 }
+
+// Four stages for the 256-row tiles (three K-tiles in flight): 2-5 % over three on the
+// encoder/ABF layers; five or six measured no better (tools/conv_micro.py, CLSKD sweep).
+static int launch_big(const clskd_conv_desc& d, hipStream_t st) { return launch_big_s<4, 4>(d, st); }
 
 // 8 waves (512 threads) per workgroup: twice the LDS-DMA issuers of a 4-wave tile — the
 // engine is bound by DMA issue/latency, not MFMA (tools/conv_micro.py: 13-25 % faster for
