@@ -112,6 +112,10 @@ typedef struct {
   int32_t seg_c[CLSKD_MAX_SEGS];
   int16_t tap_df[16];
   int16_t tap_dt[16];
+  /* 1: out += result (read-modify-write, fp32 `out`, MFMA engines with wlayout NK and fp32
+     compute only) — lets several data-gradient contributions of one tensor sum in place. */
+  int32_t accumulate;
+  int32_t reserved_;
 } clskd_conv_desc;
 
 #define CLSKD_WLAYOUT_NK 0
@@ -307,6 +311,118 @@ int clskd_sum_f32(const float* a, int32_t n, float scale, float* out, void* stre
 
 /* small utilities */
 int clskd_zero_f64(double* p, int64_t n, void* stream);
+
+/* ==========================================================================================
+ * Backward pass of the CLSKD training step (config C3; SURVEY.md §8 f rank 1 — the student's
+ * gradients for distill.py's automatic optimisation: loss.backward() + Adam, distill.py:202-204).
+ * Gradients are fp32.  Every reduction has a fixed order (no float atomics): bitwise repeatable.
+ * ======================================================================================== */
+
+/* Weight gradient of a clskd_conv2d_fwd launch, through the SAME descriptor (segments = the
+ * forward's inputs, fp32 storage): dw[n][k] (+)= sum_rows dY(row, n) * A(row, k) over the
+ * padded K of the packed weight, dbias[n] (+)= sum_rows dY(row, n) (dbias may be NULL).  dY is
+ * read through the descriptor's output map (d->out is ignored; dy replaces it).  Replaces the
+ * autograd weight gradients of ComplexConv2d / ComplexConvTranspose2d (tools_for_model.py:
+ * 236-330), nn.LSTM W_ih / W_hh (with a time-shifted segment over the hidden history) and the
+ * NavieComplexLSTM Linear projections (tools_for_model.py:164-173).
+ * accumulate: bit 0 -> dw (+)=, bit 1 -> dbias (+)= (e.g. polyphase halves sharing one bias).
+ * `work` holds clskd_conv2d_wgrad_workspace(d) floats (split-M partials). */
+int64_t clskd_conv2d_wgrad_workspace(const clskd_conv_desc* d);
+int clskd_conv2d_wgrad(const clskd_conv_desc* d, const float* dy, float* dw, float* dbias,
+                       float* work, int64_t work_elems, int32_t accumulate, void* stream);
+
+/* out[i] (+)= sum_{j<J} sgn[i*J+j] * src[idx[i*J+j]] (idx < 0 skipped): maps packed-operand
+ * gradients back onto module parameters (complex [[Wr,-Wi],[Wi,Wr]] blocks, polyphase taps). */
+int clskd_index_gather(const float* src, const int32_t* idx, const float* sgn, int32_t J,
+                       int64_t n, float* out, int32_t accumulate, void* stream);
+
+/* torch.optim.Adam step (distill.py:202-204) over a flat parameter buffer: g *= grad_scale
+ * (e.g. 1/world for a summed all-reduce), L2 weight decay, bias corrections for `step` (1-based). */
+int clskd_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr,
+                    float beta1, float beta2, float eps, float weight_decay, int32_t step,
+                    float grad_scale, void* stream);
+int clskd_fill_f32(float* p, int64_t n, float value, void* stream);
+int clskd_axpy_f32(const float* x, float* y, int64_t n, float alpha, int32_t accumulate,
+                   void* stream);
+
+/* BatchNorm2d(train) + optional PReLU backward over a BFTC tensor x[rows][C] (the RAW conv
+ * output, storage `dtype`), given dy = dL/d(output).  scale/shift: the forward's coefficients
+ * (y_bn = x*scale + shift), mean/var: its batch statistics (biased var), gamma: BN weight.
+ * Writes dgamma/dbeta/dalpha (accumulate_params) and dx (accumulate_dx), fp32.
+ * `work`: clskd_bn_bwd_workspace(nblk, C) doubles, nblk = clskd_bn_bwd_blocks(rows, C). */
+int32_t clskd_bn_bwd_blocks(int64_t rows, int32_t C);
+int64_t clskd_bn_bwd_workspace(int32_t nblk, int32_t C);
+int clskd_bn_bwd(const void* x, const float* dy, int64_t rows, int32_t C, const float* scale,
+                 const float* shift, const float* mean, const float* var, float eps,
+                 const float* gamma, const float* alpha, double* work, int32_t nblk,
+                 float* dgamma, float* dbeta, float* dalpha, float* dx, int32_t accumulate_dx,
+                 int32_t accumulate_params, int32_t dtype, void* stream);
+
+/* ABF fusion backward (framework.py:209-219): from dout = dL/d(fused x), dx = dL/d(conv1 BN
+ * output) and dyup = dL/d(upsampled residual) (fp32 [B][F][T][64]); operands as clskd_abf_fuse.
+ * clskd_nearest_down_sum folds a gradient of a nearest upsampling (F.interpolate 'nearest',
+ * framework.py:213-222) back onto the source grid: out[b][fr][tr][c] (+)= sum of g over the
+ * destination pixels whose nearest source is (fr, tr). */
+int clskd_abf_fuse_bwd(const void* x1, const void* res, int32_t B, int32_t F, int32_t T,
+                       int32_t Fr, int32_t Tr, const float* w, const float* b,
+                       const float* x_scale, const float* x_shift, const float* dout, float* dx,
+                       float* dyup, int32_t dtype, void* stream);
+int clskd_nearest_down_sum(const float* g, int32_t B, int32_t F, int32_t T, int32_t Fr,
+                           int32_t Tr, int32_t C, float* out, int32_t accumulate, void* stream);
+
+/* Masking mode 'E' backward (DCCRN.py:207-226): d est [B][T][ldest] -> d mask [B][256][Tm][2]
+ * (time 0 of the decoder output gets zero).  ConviSTFT OLA + clamp backward (tools_for_model.py:
+ * 95-107, DCCRN.py:237): dwav -> dframes [B][T][win] (pre-clamp samples recomputed from frames).
+ * Framing pad backward (zero / reflect, as clskd_frame_pad): dxp [B][Lp] -> dx [B][L] (row ldx).
+ * STFT log-magnitude L1 backward (framework.py:58-68): dX = d(scale * sum|log|Y| - log|X||)/dX
+ * for raw spectra X, Y [rows][ld] (re at f, im at nbins+f).
+ * Complex-LSTM combine backward (tools_for_model.py:168-169): dh[2][2B][n] from dreal/dimag. */
+int clskd_mask_e_bwd(const float* spec, int32_t ldspec, const float* mask, int32_t Tm, int32_t B,
+                     int32_t T, const float* dest, int32_t ldest, float* dmask, void* stream);
+int clskd_ola_bwd(const float* frames, const float* window, const float* dwav, int32_t B,
+                  int32_t T, int32_t win, int32_t hop, int32_t out_len, int32_t trim,
+                  int32_t clamp, float* dframes, void* stream);
+int clskd_frame_pad_bwd(const float* dxp, int32_t B, int32_t L, int32_t pad, int32_t Lp,
+                        int32_t mode, float* dx, int64_t ldx, int32_t accumulate, void* stream);
+int clskd_stft_mag_loss_bwd(const float* X, const float* Y, int64_t rows, int32_t ld,
+                            int32_t nbins, float scale, float* dX, void* stream);
+int clskd_complex_combine_bwd(const float* dreal, const float* dimag, int32_t B, int64_t n,
+                              float* dh, void* stream);
+
+/* LSTM backward through time (nn.LSTM, tools_for_model.py:159-174).  pre: the forward's gate
+ * pre-activations [nws][nseq][T][4H] (strided like gx; rebuild them as gx + h_{t-1} W_hh^T with
+ * one accumulate conv over the saved h history), dh: dL/dh_t, whh [nws][4H][H].  Writes the
+ * gate pre-activation gradients dgates (strided like gx) — whose conv-engine wgrad / dgrad give
+ * dW_ih, db, dx and (over the shifted h history) dW_hh.  cbuf: nws*nseq*T*H floats (cell states). */
+int clskd_lstm_bwd(const float* pre, int64_t p_ws, int64_t p_seq, int64_t p_t, const float* dh,
+                   int64_t d_ws, int64_t d_seq, int64_t d_t, const float* whh, int32_t nws,
+                   int32_t nseq, int32_t T, int32_t H, float* cbuf, float* dgates, int64_t g_ws,
+                   int64_t g_seq, int64_t g_t, void* stream);
+
+/* SPKD backward (framework.py:150-172).  clskd_spkd_grad_ranges: per pair (slab ranges as in
+ * clskd_spkd_finalize_ranges) M = dG + dG^T [pair][B][B] where dG = d(scale * loss)/d(z z^T)
+ * through the row L1 normalisation.  clskd_gram_bwd: dz = M z for every job (student taps;
+ * optional folded BatchNorm affine as in the Gram), written fp32 with its own strides. */
+typedef struct {
+  const void* ptr;    /* z: as clskd_gram_job (element (b, p, c) at b*sB + p*Ctot + c0 + c) */
+  int64_t sB;
+  int64_t P;
+  int32_t Ctot, c0, Cs;
+  int32_t dtype;
+  const float* scale; /* optional affine on load (NULL = none), indexed by channel < Ctot */
+  const float* shift;
+  const float* coef;  /* device M [B][B] of this job's pair */
+  float* out;         /* dz (b, p, c) at out + b*o_sB + p*o_Ctot + o_c0 + c */
+  int64_t o_sB;
+  int32_t o_Ctot, o_c0;
+  int32_t accumulate;
+  int32_t reserved;
+} clskd_gram_bwd_job;
+
+int clskd_spkd_grad_ranges(const float* const* s_slabs, const int32_t* s_nslab,
+                           const float* const* t_slabs, const int32_t* t_nslab, int32_t npairs,
+                           int32_t B, int32_t batchmean, float scale, float* coef, void* stream);
+int clskd_gram_bwd(const clskd_gram_bwd_job* jobs, int32_t njobs, int32_t B, void* stream);
 
 #ifdef __cplusplus
 }

@@ -36,7 +36,7 @@ class ConvDesc(C.Structure):
                 ("in_dtype", C.c_int32), ("out_dtype", C.c_int32), ("stats", C.c_void_p),
                 ("kvec", C.c_int32), ("wlayout", C.c_int32), ("ntaps", C.c_int32),
                 ("ctot", C.c_int32), ("seg_c", C.c_int32 * MAX_SEGS), ("tap_df", C.c_int16 * 16),
-                ("tap_dt", C.c_int16 * 16)]
+                ("tap_dt", C.c_int16 * 16), ("accumulate", C.c_int32), ("reserved_", C.c_int32)]
 
 
 class GramJob(C.Structure):
@@ -50,6 +50,14 @@ class DrawJob(C.Structure):
     _fields_ = [("param", C.c_void_p), ("packed", C.c_void_p), ("numel", C.c_int64),
                 ("Cin", C.c_int32), ("ntap", C.c_int32), ("Kp", C.c_int32),
                 ("packed_dtype", C.c_int32), ("bound", C.c_float), ("stream_id", C.c_int32)]
+
+
+class GramBwdJob(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("sB", C.c_int64), ("P", C.c_int64), ("Ctot", C.c_int32),
+                ("c0", C.c_int32), ("Cs", C.c_int32), ("dtype", C.c_int32), ("scale", C.c_void_p),
+                ("shift", C.c_void_p), ("coef", C.c_void_p), ("out", C.c_void_p),
+                ("o_sB", C.c_int64), ("o_Ctot", C.c_int32), ("o_c0", C.c_int32),
+                ("accumulate", C.c_int32), ("reserved", C.c_int32)]
 
 
 assert C.sizeof(KtabEntry) == 8
@@ -92,6 +100,31 @@ SIGNATURES = {
     "clskd_sisnr_rows": (_i32, [_p, _p, _i32, _i32, _i64, _i64, _f32, _p, _p]),
     "clskd_sum_f32": (_i32, [_p, _i32, _f32, _p, _p]),
     "clskd_zero_f64": (_i32, [_p, _i64, _p]),
+    # backward (training step)
+    "clskd_conv2d_wgrad_workspace": (_i64, [C.POINTER(ConvDesc)]),
+    "clskd_conv2d_wgrad": (_i32, [C.POINTER(ConvDesc), _p, _p, _p, _p, _i64, _i32, _p]),
+    "clskd_index_gather": (_i32, [_p, _p, _p, _i32, _i64, _p, _i32, _p]),
+    "clskd_adam_step": (_i32, [_p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _f32, _p]),
+    "clskd_fill_f32": (_i32, [_p, _i64, _f32, _p]),
+    "clskd_axpy_f32": (_i32, [_p, _p, _i64, _f32, _i32, _p]),
+    "clskd_bn_bwd_blocks": (_i32, [_i64, _i32]),
+    "clskd_bn_bwd_workspace": (_i64, [_i32, _i32]),
+    "clskd_bn_bwd": (_i32, [_p, _p, _i64, _i32, _p, _p, _p, _p, _f32, _p, _p, _p, _i32, _p, _p,
+                            _p, _p, _i32, _i32, _i32, _p]),
+    "clskd_abf_fuse_bwd": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,
+                                  _p, _i32, _p]),
+    "clskd_nearest_down_sum": (_i32, [_p, _i32, _i32, _i32, _i32, _i32, _i32, _p, _i32, _p]),
+    "clskd_mask_e_bwd": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _i32, _p, _p]),
+    "clskd_ola_bwd": (_i32, [_p, _p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p]),
+    "clskd_frame_pad_bwd": (_i32, [_p, _i32, _i32, _i32, _i32, _i32, _p, _i64, _i32, _p]),
+    "clskd_stft_mag_loss_bwd": (_i32, [_p, _p, _i64, _i32, _i32, _f32, _p, _p]),
+    "clskd_complex_combine_bwd": (_i32, [_p, _p, _i32, _i64, _p, _p]),
+    "clskd_lstm_bwd": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _i64, _i64, _p, _i32, _i32, _i32,
+                              _i32, _p, _p, _i64, _i64, _i64, _p]),
+    "clskd_spkd_grad_ranges": (_i32, [C.POINTER(C.c_void_p), C.POINTER(C.c_int32),
+                                      C.POINTER(C.c_void_p), C.POINTER(C.c_int32), _i32, _i32,
+                                      _i32, _f32, _p, _p]),
+    "clskd_gram_bwd": (_i32, [_p, _i32, _i32, _p]),
 }
 
 

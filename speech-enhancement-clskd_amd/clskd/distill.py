@@ -144,8 +144,18 @@ class KnowledgeDistillation(nn.Module):
             for abf in rk.abfs:
                 abf.after_redraw()
 
+    def _wants_grad(self):
+        return torch.is_grad_enabled() and any(p.requires_grad for p in self.student.parameters())
+
     def training_step(self, batch, batch_idx=0, return_parts=False):
+        """distill.py:72-148.  Under autograd (grad enabled, trainable student) the returned loss
+        is connected to the student's parameters: loss.backward() runs the HIP backward
+        (clskd.backward) and accumulates into .grad, as Lightning's automatic optimisation
+        expects."""
         X, y = batch
+        if self._wants_grad() and not return_parts:
+            params = [p for p in self.student.parameters() if p.requires_grad]
+            return _CLSKDLoss.apply(self, X, y, *params)
         out = clskd_step(self.teacher, self.student, self.review_encoder, self.review_decoder,
                          self.stft_loss, X, y, reinit=self._reinit_abf)
         self.last = out
@@ -153,10 +163,36 @@ class KnowledgeDistillation(nn.Module):
             return out
         return out["loss"]
 
+    def forward_with_tape(self, X, y):
+        out = clskd_step(self.teacher, self.student, self.review_encoder, self.review_decoder,
+                         self.stft_loss, X, y, reinit=self._reinit_abf, tape=True)
+        self.last = out
+        return out
+
+    def backward_into(self, out, grads, accumulate=False, upstream=1.0):
+        """Student gradients of upstream * out['loss'] into `grads` (parameter -> fp32 tensor)."""
+        from .backward import clskd_backward
+        clskd_backward(out, self.student, self.review_encoder, self.review_decoder, grads,
+                       acc_params=accumulate, upstream=upstream)
+
+    def train_step(self, batch, flat, opt):
+        """One C3 training step without autograd bookkeeping: fwd+loss (tape) -> HIP backward
+        into the flat gradient buffer -> (multi-rank) one all-reduce -> one Adam launch.
+        flat: train.FlatParams(self.student); opt: train.FlatAdam(flat, ...)."""
+        from .train import allreduce_grads
+        X, y = batch
+        out = self.forward_with_tape(X, y)
+        self.backward_into(out, flat.grad_dict())
+        scale = allreduce_grads(flat)
+        opt.step(grad_scale=scale)
+        return out["loss"]
+
 
 @torch.no_grad()
-def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y, reinit=None):
-    """One CLSKD fwd+loss step (distill.py:72-148).  Returns a dict of device tensors."""
+def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y, reinit=None,
+               tape=False):
+    """One CLSKD fwd+loss step (distill.py:72-148).  Returns a dict of device tensors.
+    tape=True additionally records what clskd.backward.clskd_backward needs (result['tape'])."""
     if not (isinstance(teacher, DCCRN) and isinstance(student, DCCRN)):
         raise TypeError("clskd_step expects clskd.DCCRN teacher and student")
     X = X.float()
@@ -183,6 +219,7 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     #          (student done) MRSTFT base loss on (student wav, clean) (distill.py:100-101)
     # ReviewKD: distill.py:92-96, tap contract SURVEY.md §8 a11.
     held = {}
+    tapes = dict(s={}, re=[], rd=[], ms=[]) if tape else None
     if reinit is not None:  # fresh ABF modules (distill.py:92-96): only ReviewKD reads them
         with torch.cuda.stream(side2):
             reinit("encoder")
@@ -196,7 +233,8 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
         with torch.cuda.stream(side2):
             side2.wait_event(ev)
             _mark("side2: student encoder ready", side2)
-            s_enc = review_encoder.forward_bftc(enc, defer_bn=True)
+            s_enc = review_encoder.forward_bftc(enc, defer_bn=True,
+                                                tape=tapes["re"] if tapes else None)
             _mark("side2: review encoder done", side2)
             held["s_enc"] = s_enc
             held["g_enc"] = ops.GramSlabs([_gram_bftc(a) for a in s_enc], B)
@@ -204,13 +242,15 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
 
     with torch.cuda.stream(side):
         sf = student.run(X, train=student.training, bn_updates=2 if student.training else 0,
-                         spec=s_spec, want_masks=False, on_encoder=fork_review_encoder)
+                         spec=s_spec, want_masks=False, on_encoder=fork_review_encoder,
+                         tape=tapes["s"] if tapes else None)
         student_done = torch.cuda.Event()
         student_done.record(side)
         _mark("side: student done", side)
         if reinit is not None:
             reinit("decoder")
-        s_dec = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5], defer_bn=True)
+        s_dec = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5], defer_bn=True,
+                                            tape=tapes["rd"] if tapes else None)
         Chs = sf["dec_in"].shape[-1] // 2
         g_dec = ops.GramSlabs([_gram_bftc(a) for a in s_dec] +
                               [_gram_bftc(sf["dec_in"], 0, Chs), _gram_bftc(sf["dec_in"], Chs, Chs)],
@@ -218,7 +258,7 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
         _mark("side: review decoder + grams done", side)
     with torch.cuda.stream(side2):
         side2.wait_event(student_done)
-        stft_loss(sf["out_wav"], y, out2=buf[0:2])
+        stft_loss(sf["out_wav"], y, out2=buf[0:2], tape=tapes["ms"] if tapes else None)
         _mark("side2: mrstft done", side2)
     s_enc, g_enc = held["s_enc"], held["g_enc"]
     tstream = _side_stream(dev, 2)
@@ -246,7 +286,27 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
                 clstm_real=buf[14], clstm_img=buf[15], student_wav=sf["out_wav"],
                 teacher_wav=tf["out_wav"], s_enc=ops.MaterializingList(s_enc),
                 s_dec=ops.MaterializingList(s_dec), t=tf, s=sf,
-                gram_slabs=(g_enc, g_dec, g_t))
+                gram_slabs=(g_enc, g_dec, g_t), s_enc_list=s_enc, s_dec_list=s_dec, tape=tapes)
+
+
+class _CLSKDLoss(torch.autograd.Function):
+    """Connects the HIP fwd+loss step to autograd: forward = clskd_step(tape=True), backward =
+    clskd.backward over that tape, returning one gradient per student parameter."""
+
+    @staticmethod
+    def forward(ctx, kd, X, y, *params):
+        out = kd.forward_with_tape(X, y)
+        ctx.kd, ctx.out, ctx.params = kd, out, params
+        return out["loss"].clone()
+
+    @staticmethod
+    def backward(ctx, gout):
+        kd, out, params = ctx.kd, ctx.out, ctx.params
+        up = float(gout.reshape(()).item()) if gout is not None else 1.0
+        grads = {p: torch.empty_like(p, dtype=torch.float32) for p in params}
+        kd.backward_into(out, grads, accumulate=False, upstream=up)
+        ctx.out = None
+        return (None, None, None) + tuple(grads[p] for p in params)
 
 
 class SPKDDistillation(nn.Module):

@@ -89,13 +89,19 @@ class STFTLoss(nn.Module):
         self.register_buffer("window", getattr(torch, window)(win_length))
         self._plan = _StftPlan(fft_size, shift_size, win_length, self.window)
 
-    def accumulate(self, x, y, out2, factor_sc, factor_mag, accumulate):
+    def accumulate(self, x, y, out2, factor_sc, factor_mag, accumulate, tape=None):
         x = x.reshape(-1, x.shape[-1]).float().contiguous()
         y = y.reshape(-1, y.shape[-1]).float().contiguous()
         X = self._plan.spectrum(x)
         Y = self._plan.spectrum(y)
-        return ops.stft_mag_loss(X, Y, self.fft_size // 2 + 1, factor_sc, factor_mag, out2,
-                                 accumulate)
+        nb = self.fft_size // 2 + 1
+        if tape is not None:  # what backward.mrstft_backward needs
+            L = x.shape[1]
+            Lr = L + 2 * (self.fft_size // 2) + self._plan.KT * self._plan.hop
+            Lr += (-Lr) % 4
+            tape.append(dict(X=X, Y=Y, plan=self._plan, factor_mag=factor_mag,
+                             count=X.shape[0] * X.shape[1] * nb, L=L, Lr=Lr))
+        return ops.stft_mag_loss(X, Y, nb, factor_sc, factor_mag, out2, accumulate)
 
     def forward(self, x, y):
         out2 = self.accumulate(x, y, None, 1.0, 1.0, False)
@@ -116,10 +122,10 @@ class MultiResolutionSTFTLoss(nn.Module):
         self.factor_sc = factor_sc
         self.factor_mag = factor_mag
 
-    def forward(self, x, y, out2=None):
+    def forward(self, x, y, out2=None, tape=None):
         R = len(self.stft_losses)
         for r, f in enumerate(self.stft_losses):
-            out2 = f.accumulate(x, y, out2, self.factor_sc / R, self.factor_mag / R, r > 0)
+            out2 = f.accumulate(x, y, out2, self.factor_sc / R, self.factor_mag / R, r > 0, tape)
         return out2[0], out2[1]
 
 
@@ -240,11 +246,16 @@ class ABF(nn.Module):
             self._wcache["w"] = ent
         return ent[1]
 
-    def forward_bftc(self, x, y=None, shape=None, out_shape=None, train=None, defer_bn=False):
+    def forward_bftc(self, x, y=None, shape=None, out_shape=None, train=None, defer_bn=False,
+                     tape=None):
         """x: BFTC [B][F][T][Cin]; y: BFTC residual [B][Fr][Tr][mid].  Returns (out, x_fused) BFTC.
         defer_bn: conv2's BatchNorm is left unapplied — out is an ops.DeferredBN (raw output +
-        coefficients) for a consumer that folds the affine into its loads (the SPKD Gram)."""
+        coefficients) for a consumer that folds the affine into its loads (the SPKD Gram).
+        tape: a dict receiving what ABF.backward_bftc needs (raw conv outputs, BN coefficients and
+        batch statistics, the fused map and the residual)."""
         train = self.training if train is None else train
+        if tape is not None and not train:
+            raise ValueError("ABF tape (backward) needs train-mode BatchNorm")
         B, Fn, Tn, Cin = x.shape
         w1p, w2p, att = self._weights(x.dtype)
         mid = w1p.shape[0]
@@ -257,18 +268,33 @@ class ABF(nn.Module):
         ops.conv([seg_bftc(x)], [(0, 0)], B, Fn, Tn, mid, w1p, None, x1,
                  OutMap(Fn * Tn * mid, Tn * mid, mid), stats=part)
         bn = self.conv1[1]
+        mv1 = torch.empty(2, mid, device=dev, dtype=torch.float32) if tape is not None else None
+        so1 = (mv1[0], mv1[1]) if tape is not None else None
+        if tape is not None:
+            tape.update(x_in=x, x1=x1, mv1=mv1, res=y)
         if self.att_conv is not None:
             if shape != Fn:  # the reference's torch.cat would fail as well (framework.py:213-216)
                 raise ValueError(f"ABF fuse: residual upsampled to F={shape} but x has F={Fn}")
             # conv1's BatchNorm is applied by the fuse kernel as it loads x1 (no extra pass)
             coef = ops.batch_norm_bftc(x1, None, bn.weight, bn.bias, bn.running_mean,
                                        bn.running_var, train, bn.momentum, bn.eps, 1,
-                                       partial=(part, nmb) if train else None)
+                                       partial=(part, nmb) if train else None, stats_out=so1)
+            if tape is not None:
+                tape["coef1"] = coef
             if y.dtype != x1.dtype:  # user-supplied residual of another storage type
                 y = y.to(x1.dtype).contiguous()
             xf = torch.empty_like(x1)
             ops.abf_fuse(x1, y, att[0], att[1], xf, x_coef=coef)
+            if tape is not None:
+                tape["res"] = y
             x1 = xf
+        elif tape is not None:
+            x1n = torch.empty_like(x1)
+            _, coef = ops.batch_norm_bftc(x1, x1n, bn.weight, bn.bias, bn.running_mean,
+                                          bn.running_var, train, bn.momentum, bn.eps, 1,
+                                          partial=(part, nmb), stats_out=so1, return_coef=True)
+            tape["coef1"] = coef
+            x1 = x1n
         else:
             ops.batch_norm_bftc(x1, x1, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                 train, bn.momentum, bn.eps, 1,
@@ -282,6 +308,14 @@ class ABF(nn.Module):
         ops.conv([seg_bftc(x1)], [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], B, Fn,
                  Tn, Cout, w2p, None, out, OutMap(Fn * Tn * Cout, Tn * Cout, Cout), stats=part2)
         bn = self.conv2[1]
+        if tape is not None:
+            mv2 = torch.empty(2, Cout, device=dev, dtype=torch.float32)
+            coef = ops.batch_norm_bftc(out, None, bn.weight, bn.bias, bn.running_mean,
+                                       bn.running_var, train, bn.momentum, bn.eps, 1,
+                                       partial=(part2, nmb), stats_out=(mv2[0], mv2[1]))
+            tape.update(xf=x1, out_raw=out, coef2=coef, mv2=mv2)
+            d = ops.DeferredBN(out, coef)
+            return (d if defer_bn else d.materialize()), x1
         if defer_bn:
             coef = ops.batch_norm_bftc(out, None, bn.weight, bn.bias, bn.running_mean,
                                        bn.running_var, train, bn.momentum, bn.eps, 1,
@@ -317,17 +351,24 @@ class ReviewKD(nn.Module):
             abf.compute = compute
         return self
 
-    def forward_bftc(self, feats, defer_bn=False):
+    def forward_bftc(self, feats, defer_bn=False, tape=None):
         """feats: BFTC student features in the reference's list order.  Returns BFTC outputs
-        (ops.DeferredBN entries when defer_bn: the ABF output BatchNorms left for the consumer)."""
+        (ops.DeferredBN entries when defer_bn: the ABF output BatchNorms left for the consumer).
+        tape: a list receiving one ABF tape dict per level, in processing order."""
         xs = feats[::-1] if self.ft_type == "encoder" else list(feats)
         results = []
+        tp = {} if tape is not None else None
         out, res = self.abfs[0].forward_bftc(xs[0], out_shape=self.out_shapes[0],
-                                             defer_bn=defer_bn)
+                                             defer_bn=defer_bn, tape=tp)
+        if tape is not None:
+            tape.append(tp)
         results.append(out)
         for feature, abf, shape, out_shape in zip(xs[1:], self.abfs[1:], self.shapes[1:],
                                                   self.out_shapes[1:]):
-            out, res = abf.forward_bftc(feature, res, shape, out_shape, defer_bn=defer_bn)
+            tp = {} if tape is not None else None
+            out, res = abf.forward_bftc(feature, res, shape, out_shape, defer_bn=defer_bn, tape=tp)
+            if tape is not None:
+                tape.append(tp)
             if self.ft_type == "encoder":
                 results.insert(0, out)
             else:

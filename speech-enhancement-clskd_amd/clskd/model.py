@@ -350,10 +350,14 @@ class DCCRN(nn.Module):
                  OutMap(T * 514, 0, 514))
         return spec
 
-    def run(self, x, train=True, bn_updates=1, spec=None, want_masks=True, on_encoder=None):
+    def run(self, x, train=True, bn_updates=1, spec=None, want_masks=True, on_encoder=None,
+            tape=None):
         """Full forward on the HIP device.  Returns a dict of BFTC buffers and NCHW views.
         on_encoder(enc): called (on the launching stream) right after the encoder, so a caller can
-        fork work that only needs the encoder taps before the LSTM and decoder are enqueued."""
+        fork work that only needs the encoder taps before the LSTM and decoder are enqueued.
+        tape: a dict that receives what the backward pass (clskd.backward) needs — pre-BN conv
+        outputs kept beside the activations, BN coefficients and batch statistics, the LSTM gate
+        inputs and hidden histories, the iSTFT frames."""
         if not x.is_cuda:
             raise RuntimeError("clskd.DCCRN.forward needs inputs on the HIP device")
         x = x.float()
@@ -380,6 +384,8 @@ class DCCRN(nn.Module):
                 # channels of a BFTC input: same K order (tap, re, im) as the packed weights
                 spec_b = ops.spec_bftc(spec, 1, 258, 256, torch.empty(B, 256, T, 2, **f32))
                 segs = [seg_bftc(spec_b)]
+                if tape is not None:
+                    tape["spec_b"] = spec_b
             else:
                 segs = [seg_bftc(enc[-1])]
             wp, bias = self._enc_w(i, self._cmp(segs, 10 * kn[i]))
@@ -390,10 +396,21 @@ class DCCRN(nn.Module):
             ops.conv(segs, taps, B, Fo, T, Co, wp, bias, raw, OutMap(Fo * T * Co, T * Co, Co),
                      stride_f=2, stats=part)
             bn, pr = self.encoder[i][1], self.encoder[i][2]
-            ops.batch_norm_bftc(raw, raw, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                                train, bn.momentum, bn.eps, bn_updates, alpha=pr.weight,
-                                partial=(part, nmb) if train else None)
-            enc.append(raw)
+            if tape is not None:
+                post = torch.empty_like(raw)
+                mv = torch.empty(2, Co, **f32)
+                _, coef = ops.batch_norm_bftc(raw, post, bn.weight, bn.bias, bn.running_mean,
+                                              bn.running_var, train, bn.momentum, bn.eps,
+                                              bn_updates, alpha=pr.weight,
+                                              partial=(part, nmb) if train else None,
+                                              stats_out=(mv[0], mv[1]), return_coef=True)
+                tape.setdefault("enc_bn", []).append((raw, coef, mv))
+                enc.append(post)
+            else:
+                ops.batch_norm_bftc(raw, raw, bn.weight, bn.bias, bn.running_mean,
+                                    bn.running_var, train, bn.momentum, bn.eps, bn_updates,
+                                    alpha=pr.weight, partial=(part, nmb) if train else None)
+                enc.append(raw)
             F = Fo
         if on_encoder is not None:
             on_encoder(enc)
@@ -422,6 +439,8 @@ class DCCRN(nn.Module):
             hs = torch.empty(2, 2 * B, T, H, **f32)
             ops.lstm_recurrent(gx, 4 * H, T * 8 * H, 8 * H, whh, 2, 2 * B, T, H, hs,
                                2 * B * T * H, T * H, H)
+            if tape is not None:
+                tape.setdefault("lstm", []).append(dict(gx=gx, hs=hs, r_in=r_in))
             ro = torch.empty(B, T, H, **f32)
             io = torch.empty(B, T, H, **f32)
             ops.complex_combine(hs[0, :B], hs[1, B:], hs[0, B:], hs[1, :B], ro, io)
@@ -465,9 +484,23 @@ class DCCRN(nn.Module):
                          stats=part, stats_offset=parity * nmb * Co * 2)
             if has_bn:
                 bn, pr = self.decoder[d][1], self.decoder[d][2]
-                ops.batch_norm_bftc(raw, raw, bn.weight, bn.bias, bn.running_mean,
-                                    bn.running_var, train, bn.momentum, bn.eps, bn_updates,
-                                    alpha=pr.weight, partial=(part, 2 * nmb) if part is not None else None)
+                if tape is not None:
+                    post = torch.empty_like(raw)
+                    mv = torch.empty(2, Co, **f32)
+                    _, coef = ops.batch_norm_bftc(
+                        raw, post, bn.weight, bn.bias, bn.running_mean, bn.running_var, train,
+                        bn.momentum, bn.eps, bn_updates, alpha=pr.weight,
+                        partial=(part, 2 * nmb) if part is not None else None,
+                        stats_out=(mv[0], mv[1]), return_coef=True)
+                    tape.setdefault("dec_bn", []).append((raw, coef, mv))
+                    raw = post
+                else:
+                    ops.batch_norm_bftc(raw, raw, bn.weight, bn.bias, bn.running_mean,
+                                        bn.running_var, train, bn.momentum, bn.eps, bn_updates,
+                                        alpha=pr.weight,
+                                        partial=(part, 2 * nmb) if part is not None else None)
+            elif tape is not None:
+                tape.setdefault("dec_bn", []).append(None)
             dec.append(raw)
             out_t, out_t0, out_T = raw, 1, T
             F = 2 * F
@@ -486,6 +519,9 @@ class DCCRN(nn.Module):
         out_len = (T + 1) * 100 - 400
         wav = torch.empty(B, out_len, **f32)
         ops.ola_hop(frames, window, 100, out_len, 300, True, wav)
+        if tape is not None:
+            tape.update(spec=spec, est=est, frames=frames, window=window, out_len=out_len, T=T,
+                        B=B, train=train)
         nchw = lambda t: t.permute(0, 3, 1, 2)
         return dict(
             out_wav=wav,

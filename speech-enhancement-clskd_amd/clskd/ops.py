@@ -179,7 +179,9 @@ def pack_weight(w, K, compute="fp32"):
         w = torch.cat([w, w.new_zeros(N, Kp - K)], 1)
     if compute == "bf16":
         return w.to(torch.bfloat16).contiguous()
-    return w.contiguous()
+    # always a fresh, 16-B-aligned tensor: never a view aliasing the parameter storage (which
+    # may sit at any offset of a flat parameter buffer, clskd.train.FlatParams)
+    return w.clone(memory_format=torch.contiguous_format)
 
 
 def _dt(t):
@@ -227,7 +229,7 @@ _CONV_PLANS = {}
 
 
 def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, stride_f, stride_t,
-               stats):
+               stats, accumulate=False, mfma_only=False):
     in_dt = {_dt(s.tensor) for s in segs}
     assert len(in_dt) == 1, "all segments of one conv share a storage type"
     in_dt = in_dt.pop()
@@ -274,7 +276,8 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
             d.seg_c[i] = g.C
         for i, (dF, dT) in enumerate(taps):
             d.tap_df[i], d.tap_dt[i] = dF, dT
-    direct = direct_ok(N, Kp)
+    direct = direct_ok(N, Kp) and not (accumulate or mfma_only)
+    d.accumulate = int(bool(accumulate))
     d.wlayout = _lib.WLAYOUT_DIRECT if direct else _lib.WLAYOUT_NK
     pl = _ConvPlan()
     pl.desc, pl.nseg, pl.direct = d, len(segs), direct
@@ -289,22 +292,24 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
 
 
 def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, stride_f=1,
-         stride_t=1, stats=None, stats_offset=0):
+         stride_t=1, stats=None, stats_offset=0, accumulate=False, mfma_only=False):
     """out[b, fo*of_mul+of_add, to, n] = bias[n] + sum_k A[(b,fo,to),k] W[n,k].
     bf16 segments run the LDS-DMA bf16-MFMA engine (weights packed bf16, K % 64); fp32 segments
     the fp32-MFMA engine (weights fp32, K % 16).  `out` may be fp32 or bf16 storage.
     The descriptor of each launch signature (geometry, taps, output map, dtypes, pointer
-    alignment class) is built once (_conv_plan); a call patches only the pointers."""
+    alignment class) is built once (_conv_plan); a call patches only the pointers.
+    accumulate=True adds into `out` (fp32 engine; data-gradient sums); mfma_only skips the
+    direct-convolution kernel."""
     addrs = [s.tensor.data_ptr() + s.tensor.element_size() * s.offset for s in segs]
     taps = tuple(taps)
     geoms = tuple(s.geom for s in segs)
     key = (geoms, taps, B, Fo, To, N, wpacked.shape, wpacked.dtype, omap, stride_f, stride_t,
            out.dtype, out.device.index, stats is None, bias is None,
-           tuple(a % 16 for a in addrs), tuple(s.tensor.dtype for s in segs))
+           tuple(a % 16 for a in addrs), tuple(s.tensor.dtype for s in segs), accumulate, mfma_only)
     pl = _CONV_PLANS.get(key)
     if pl is None:
         pl = _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, stride_f,
-                        stride_t, stats)
+                        stride_t, stats, accumulate, mfma_only)
     if not wpacked.is_contiguous():
         raise RuntimeError("conv: packed weight must be contiguous")
     d = pl.desc
@@ -350,12 +355,14 @@ def conv_kernel_of_last_launch():
 # BatchNorm (+ PReLU)
 # ------------------------------------------------------------------------------------------
 def batch_norm_bftc(x, y, gamma, beta, running_mean, running_var, train, momentum=0.1,
-                    eps=1e-5, n_updates=1, alpha=None, stats_out=None, partial=None):
+                    eps=1e-5, n_updates=1, alpha=None, stats_out=None, partial=None,
+                    return_coef=False):
     """nn.BatchNorm2d over a BFTC tensor (channels last), then optional PReLU (single alpha).
     train: batch statistics (biased var), running stats updated n_updates times (if given).
     partial=(tensor, nblk): statistics already produced by the conv epilogue (fused).
     y=None: compute the coefficients only and return the [scale | shift] fp32 tensor (for a
-    consumer kernel that applies them on load)."""
+    consumer kernel that applies them on load).  return_coef: return (y, coef) (the backward
+    pass needs the forward's coefficients with stats_out's batch mean / var)."""
     L = lib()
     Cn = x.shape[-1]
     if Cn > 4096:
@@ -396,7 +403,7 @@ def batch_norm_bftc(x, y, gamma, beta, running_mean, running_var, train, momentu
     assert x.dtype == y.dtype
     check(L.clskd_bn_apply(ptr(x), ptr(y), rows, Cn, scale, shift, ptr(alpha), _dt(x), st),
           "bn_apply")
-    return y
+    return (y, coef) if return_coef else y
 
 
 # ------------------------------------------------------------------------------------------
@@ -638,3 +645,172 @@ def sum_f32(a, out, scale=1.0):
     """out[0] = scale * sum(a) for a contiguous (or 1-D strided-1) tensor a."""
     check(lib().clskd_sum_f32(ptr(a), a.numel(), scale, ptr(out), _stream()), "sum_f32")
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# backward (training step): weight gradients, data-gradient helpers, optimizer
+# ------------------------------------------------------------------------------------------
+_WGRAD_PLANS = {}
+
+
+def conv_wgrad(segs, taps, B, Fo, To, N, dy, omap, dw, dbias=None, dy_offset=0, stride_f=1,
+               stride_t=1, accumulate=False, accumulate_bias=None):
+    """Weight gradient of the conv launch conv(segs, taps, B, Fo, To, N, ..., omap): fp32
+    segments (the forward inputs), dy read through the forward's output map at dy + dy_offset.
+    dw: [N][Kp] fp32 (the packed-weight layout, Kp = K padded to 16); dbias: [N] or None.
+    accumulate adds into dw (and dbias, unless accumulate_bias says otherwise)."""
+    addrs = [seg_addr(sg) for sg in segs]
+    taps = tuple(taps)
+    geoms = tuple(sg.geom for sg in segs)
+    key = (geoms, taps, B, Fo, To, N, omap, stride_f, stride_t, dy.device.index,
+           tuple(a % 16 for a in addrs))
+    pl = _WGRAD_PLANS.get(key)
+    if pl is None:
+        assert all(sg.tensor.dtype == torch.float32 for sg in segs), "wgrad: fp32 segments"
+        kt, ks, K, Kp, vec4 = _ktab(geoms, taps, dy.device.index or 0, BK)
+        if any(a % 16 for a in addrs):
+            vec4 = False
+        d = _lib.ConvDesc()
+        d.B, d.Fo, d.To, d.N, d.K = B, Fo, To, N, Kp
+        d.stride_f, d.stride_t = stride_f, stride_t
+        d.nseg = len(segs)
+        for i, g in enumerate(geoms):
+            d.seg[i] = _lib.Seg(0, g.sB, g.sF, g.sT, g.F, g.T)
+        for i in range(len(segs), _lib.MAX_SEGS):
+            d.seg[i] = d.seg[0]
+        d.ktab, d.kseg, d.vec4 = kt.data_ptr(), ks.data_ptr(), int(vec4)
+        d.oB, d.oF, d.oT, d.oNhi, d.oNlo = omap.oB, omap.oF, omap.oT, omap.oNhi, omap.oNlo
+        d.nlo = min(omap.nlo, 1 << 30)
+        d.of_mul, d.of_add = omap.of_mul, omap.of_add
+        d.compute = d.in_dtype = d.out_dtype = _lib.F32
+        ws = int(lib().clskd_conv2d_wgrad_workspace(d))
+        pl = (d, Kp, ws)
+        _WGRAD_PLANS[key] = pl
+    d, Kp, ws = pl
+    assert dw.shape == (N, Kp) and dw.dtype == torch.float32 and dw.is_contiguous(), (dw.shape, N, Kp)
+    for i, a in enumerate(addrs):
+        d.seg[i].ptr = a
+    for i in range(len(segs), _lib.MAX_SEGS):
+        d.seg[i].ptr = addrs[0]
+    work = torch.empty(ws, dtype=torch.float32, device=dy.device)
+    acc_b = accumulate if accumulate_bias is None else accumulate_bias
+    check(lib().clskd_conv2d_wgrad(d, dy.data_ptr() + 4 * dy_offset, ptr(dw), ptr(dbias), ptr(work),
+                                   ws, int(bool(accumulate)) | (int(bool(acc_b)) << 1), _stream()),
+          "conv2d_wgrad")
+    return dw
+
+
+def bn_bwd(x, dy, scale, shift, mean, var, eps, gamma, alpha, dx, dgamma=None, dbeta=None,
+           dalpha=None, accumulate_dx=False, accumulate_params=False):
+    """BatchNorm2d(train) [+ PReLU] backward over BFTC x (raw conv output, fp32 or bf16)."""
+    L = lib()
+    Cn = x.shape[-1]
+    rows = x.numel() // Cn
+    nblk = int(L.clskd_bn_bwd_blocks(rows, Cn))
+    work = torch.empty(int(L.clskd_bn_bwd_workspace(nblk, Cn)), dtype=torch.float64, device=x.device)
+    check(L.clskd_bn_bwd(ptr(x), ptr(dy), rows, Cn, ptr(scale), ptr(shift), ptr(mean), ptr(var), eps,
+                         ptr(gamma), ptr(alpha), ptr(work), nblk, ptr(dgamma), ptr(dbeta),
+                         ptr(dalpha), ptr(dx), int(accumulate_dx), int(accumulate_params), _dt(x),
+                         _stream()), "bn_bwd")
+    return dx
+
+
+def abf_fuse_bwd(x1, res, w, b, x_coef, dout, dx, dyup):
+    B, F, T, Cm = x1.shape
+    _, Fr, Tr, _ = res.shape
+    sc = sh = None
+    if x_coef is not None:
+        sc = x_coef.data_ptr()
+        sh = sc + 4 * Cm
+    check(lib().clskd_abf_fuse_bwd(ptr(x1), ptr(res), B, F, T, Fr, Tr, ptr(w), ptr(b), sc, sh,
+                                   ptr(dout), ptr(dx), ptr(dyup), _dt(x1), _stream()), "abf_fuse_bwd")
+
+
+def nearest_down_sum(g, out, accumulate=False):
+    B, F, T, Cn = g.shape
+    _, Fr, Tr, _ = out.shape
+    check(lib().clskd_nearest_down_sum(ptr(g), B, F, T, Fr, Tr, Cn, ptr(out), int(accumulate),
+                                       _stream()), "nearest_down_sum")
+
+
+def mask_e_bwd(spec, mask, T, dest, dmask):
+    B = spec.shape[0]
+    check(lib().clskd_mask_e_bwd(ptr(spec), spec.shape[-1], ptr(mask), mask.shape[2], B, T,
+                                 ptr(dest), dest.shape[-1], ptr(dmask), _stream()), "mask_e_bwd")
+
+
+def ola_bwd(frames, window, dwav, hop, out_len, trim, clamp, dframes):
+    B, T, win = frames.shape
+    check(lib().clskd_ola_bwd(ptr(frames), ptr(window), ptr(dwav), B, T, win, hop, out_len, trim,
+                              int(clamp), ptr(dframes), _stream()), "ola_bwd")
+
+
+def frame_pad_bwd(dxp, L, pad, mode, dx, accumulate=False):
+    B, Lp = dxp.shape
+    check(lib().clskd_frame_pad_bwd(ptr(dxp), B, L, pad, Lp, mode, ptr(dx), dx.stride(0),
+                                    int(accumulate), _stream()), "frame_pad_bwd")
+
+
+def stft_mag_loss_bwd(X, Y, nbins, scale, dX):
+    rows = X.numel() // X.shape[-1]
+    check(lib().clskd_stft_mag_loss_bwd(ptr(X), ptr(Y), rows, X.shape[-1], nbins, scale, ptr(dX),
+                                        _stream()), "stft_mag_loss_bwd")
+
+
+def complex_combine_bwd(dre, dim, dh):
+    B = dre.shape[0]
+    check(lib().clskd_complex_combine_bwd(ptr(dre), ptr(dim), B, dre.numel() // B, ptr(dh),
+                                          _stream()), "complex_combine_bwd")
+
+
+def lstm_bwd(pre, p_strides, dh, d_strides, whh, nws, nseq, T, H, dgates, g_strides):
+    cbuf = torch.empty(nws * nseq * T * H, dtype=torch.float32, device=pre.device)
+    check(lib().clskd_lstm_bwd(ptr(pre), *p_strides, ptr(dh), *d_strides, ptr(whh), nws, nseq, T, H,
+                               ptr(cbuf), ptr(dgates), *g_strides, _stream()), "lstm_bwd")
+
+
+def spkd_grad(s_refs, t_refs, B, batchmean=True, scale=1.0, out=None, device=None):
+    """M = dG + dG^T per pair (clskd_spkd_grad_ranges) -> [npairs][B][B] fp32."""
+    n = len(s_refs)
+    coef = out if out is not None else torch.empty(n, B, B, dtype=torch.float32, device=device)
+    sp = (C.c_void_p * n)(*[r[0] for r in s_refs])
+    tp = (C.c_void_p * n)(*[r[0] for r in t_refs])
+    sn = (C.c_int32 * n)(*[r[1] for r in s_refs])
+    tn = (C.c_int32 * n)(*[r[1] for r in t_refs])
+    check(lib().clskd_spkd_grad_ranges(sp, sn, tp, tn, n, B, int(batchmean), scale, ptr(coef),
+                                       _stream()), "spkd_grad")
+    return coef
+
+
+def gram_bwd(items, B):
+    """items: list of (GramView z, coef [B][B] tensor, out tensor, o_sB, o_Ctot, o_c0,
+    accumulate): dz = M z written fp32 into out."""
+    jobs = (_lib.GramBwdJob * len(items))()
+    for i, (v, coef, out, o_sB, o_Ctot, o_c0, acc) in enumerate(items):
+        sc = sh = None
+        if v.affine is not None:
+            sc = v.affine.data_ptr()
+            sh = sc + 4 * v.Ctot
+        assert out.dtype == torch.float32 and coef.dtype == torch.float32
+        jobs[i] = _lib.GramBwdJob(v.tensor.data_ptr() + v.tensor.element_size() * v.offset, v.sB,
+                                  v.P, v.Ctot, v.c0, v.Cs, _dt(v.tensor), sc, sh, coef.data_ptr(),
+                                  out.data_ptr(), o_sB, o_Ctot, o_c0, int(acc), 0)
+    check(lib().clskd_gram_bwd(jobs, len(items), B, _stream()), "gram_bwd")
+
+
+def index_gather(src, idx, sgn, out, accumulate=False):
+    """out[i] (+)= sum_j sgn[i, j] * src.flat[idx[i, j]] (idx < 0 skipped)."""
+    n, J = idx.shape
+    assert out.numel() == n and out.is_contiguous()
+    check(lib().clskd_index_gather(ptr(src), ptr(idx), ptr(sgn), J, n, ptr(out), int(accumulate),
+                                   _stream()), "index_gather")
+
+
+def adam_step(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
+    check(lib().clskd_adam_step(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, beta1, beta2, eps,
+                                weight_decay, step, grad_scale, _stream()), "adam")
+
+
+def fill(t, value=0.0):
+    check(lib().clskd_fill_f32(ptr(t), t.numel(), value, _stream()), "fill")
+    return t

@@ -300,7 +300,13 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_f32(const ConvArgs args) {
     for (int r = 0; r < 16; ++r) {
       const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
       const int64_t ro = out_row[row];
-      if (ro >= 0) store_val<OutT>(outp + ro + coff, acc[t][r]);
+      if (ro >= 0) {
+        float v = acc[t][r];
+        if constexpr (sizeof(OutT) == 4) {
+          if (d.accumulate) v += outp[ro + coff];
+        }
+        store_val<OutT>(outp + ro + coff, v);
+      }
     }
   }
 }
@@ -350,6 +356,9 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
                     "conv2d: kvec=%d", d.kvec);
   CLSKD_CHECK_ARG(d.wlayout == CLSKD_WLAYOUT_NK || d.wlayout == CLSKD_WLAYOUT_DIRECT,
                   "conv2d: wlayout=%d", d.wlayout);
+  CLSKD_CHECK_ARG(!d.accumulate || (d.wlayout == CLSKD_WLAYOUT_NK && d.compute == CLSKD_F32 &&
+                                     d.out_dtype == CLSKD_F32),
+                  "conv2d: accumulate needs the fp32 engine (wlayout NK, fp32 compute and out)");
   if (d.wlayout == CLSKD_WLAYOUT_DIRECT) {
     const int rc = launch_conv_direct(d, st);
     if (rc != CLSKD_OK) return rc;

@@ -1,0 +1,323 @@
+// Backward-pass GEMMs and optimizer kernels (student training step, SURVEY.md §8 f rank 1).
+//
+// conv_wgrad_f32: the weight gradient of any launch of the implicit-GEMM conv engine, read
+// through the SAME descriptor as the forward launch (segments, K table, output map):
+//     dW[n][k] = sum_m dY(m, n) * A(m, k),   dbias[n] = sum_m dY(m, n)
+// where m runs over the forward's output rows (b, fo, to), A is the forward's K-table gather and
+// dY is addressed with the forward's output map.  This covers every trained GEMM of the student:
+// complex Conv2d, both polyphase halves of ComplexConvTranspose2d, the LSTM input projections
+// (and, with a time-shifted segment over the hidden history, the recurrent weights W_hh) and the
+// complex-LSTM Linear projections.
+//
+// Layout: the reduction runs over M (up to B*F*T ~ 1.3 M rows), so the grid splits M into S
+// row ranges; a workgroup owns a 64(n) x 64(k) tile of one range, staging 32 rows of dY and of
+// the gathered A per step in LDS and issuing v_mfma_f32_32x32x2_f32 with the ROW axis as the
+// MFMA reduction axis (A operand = dY^T, B operand = A).  Range partials go to a workspace
+// [S][N][Kp] and a second kernel sums them in a fixed order: deterministic, no float atomics.
+#include <algorithm>
+
+#include "common.h"
+
+namespace clskd {
+
+constexpr int WG_TN = 64;   // n per workgroup tile
+constexpr int WG_TK = 64;   // k per workgroup tile
+constexpr int WG_RB = 32;   // rows staged per step
+
+struct WgradArgs {
+  clskd_conv_desc d;
+  const float* dy;
+  float* work;      // [S][N][Kp] partial dW, then [S][N] partial dbias (if bias wanted)
+  int64_t rows_per_split;
+  int S;
+  int want_bias;
+};
+
+template <bool VEC4>
+__global__ __launch_bounds__(256) void conv_wgrad_f32(const WgradArgs a) {
+  const clskd_conv_desc& d = a.d;
+  __shared__ __attribute__((aligned(16))) float As[WG_RB][WG_TK + 4];
+  __shared__ __attribute__((aligned(16))) float Ds[WG_RB][WG_TN + 4];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int split = blockIdx.x;
+  const int n0 = blockIdx.y * WG_TN;
+  const int k0 = blockIdx.z * WG_TK;
+  const int64_t M = (int64_t)d.B * d.Fo * d.To;
+  const int64_t FoTo = (int64_t)d.Fo * d.To;
+  const int64_t r_begin = (int64_t)split * a.rows_per_split;
+  const int64_t r_end = min(M, r_begin + a.rows_per_split);
+  const bool ncontig = d.oNlo == 1 && d.nlo >= d.N;
+
+  // staging roles: row lr = tid >> 3 of the 32-row step, quads q0 = tid & 7 and q0 + 8
+  const int lr = tid >> 3;
+  const int q0 = tid & 7;
+  const int nsub = wave & 1, ksub = wave >> 1;
+  f32x16 acc = {};
+  float bacc = 0.f;  // dbias partial of column n0 + tid (tid < 64, k-tile 0 only)
+
+  for (int64_t rs = r_begin; rs < r_end; rs += WG_RB) {
+    const int64_t m = rs + lr;
+    const bool valid = m < r_end;
+    int64_t b = 0, fo = 0, to = 0;
+    if (valid) {
+      b = m / FoTo;
+      const int64_t r = m - b * FoTo;
+      fo = r / d.To;
+      to = r - fo * d.To;
+    }
+    // ---- gathered A: 16 consecutive k per thread as 2 x 4-k quads of the 64-k tile ----
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      const int kl = (q0 + 8 * qq) * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (valid) {
+        if constexpr (VEC4) {
+          const int k = k0 + kl;
+          if (k < d.K) {
+            const clskd_ktab_entry e = d.ktab[k];
+            const int s = d.kseg[k];
+            const clskd_seg& g = d.seg[s];
+            const int64_t fi = fo * d.stride_f + e.dF, ti = to * d.stride_t + e.dT;
+            if (fi >= 0 && fi < g.F && ti >= 0 && ti < g.T)
+              v = *reinterpret_cast<const f32x4*>(g.ptr + b * g.sB + fo * d.stride_f * g.sF +
+                                                  to * d.stride_t * g.sT + e.off);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int k = k0 + kl + j;
+            if (k < d.K) {
+              const clskd_ktab_entry e = d.ktab[k];
+              const int s = d.kseg[k];
+              const clskd_seg& g = d.seg[s];
+              const int64_t fi = fo * d.stride_f + e.dF, ti = to * d.stride_t + e.dT;
+              if (fi >= 0 && fi < g.F && ti >= 0 && ti < g.T)
+                v[j] = g.ptr[b * g.sB + fo * d.stride_f * g.sF + to * d.stride_t * g.sT + e.off];
+            }
+          }
+        }
+      }
+      *reinterpret_cast<f32x4*>(&As[lr][kl]) = v;
+    }
+    // ---- dY through the forward's output map ----
+    const int64_t orow = b * d.oB + (fo * d.of_mul + d.of_add) * d.oF + to * d.oT;
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      const int nl = (q0 + 8 * qq) * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (valid) {
+        if (ncontig && n0 + nl + 3 < d.N && ((orow + n0 + nl) & 3) == 0) {
+          v = *reinterpret_cast<const f32x4*>(a.dy + orow + n0 + nl);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int n = n0 + nl + j;
+            if (n < d.N) v[j] = a.dy[orow + (int64_t)(n / d.nlo) * d.oNhi + (int64_t)(n % d.nlo) * d.oNlo];
+          }
+        }
+      }
+      *reinterpret_cast<f32x4*>(&Ds[lr][nl]) = v;
+    }
+    __syncthreads();
+    // ---- 16 MFMAs (2 rows each) per wave: C[n][k] += dY^T[n][r] A[r][k] ----
+    const int cl = lane & 31, rh = lane >> 5;
+#pragma unroll
+    for (int s = 0; s < WG_RB / 2; ++s) {
+      const float av = Ds[2 * s + rh][nsub * 32 + cl];
+      const float bv = As[2 * s + rh][ksub * 32 + cl];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    }
+    if (a.want_bias && blockIdx.z == 0 && tid < WG_TN) {
+#pragma unroll 8
+      for (int r = 0; r < WG_RB; ++r) bacc += Ds[r][tid];
+    }
+    __syncthreads();
+  }
+  // ---- partial tile out: work[split][n][k] ----
+  const int Kp = d.K;
+  float* wp = a.work + (int64_t)split * d.N * Kp;
+  const int kc = k0 + ksub * 32 + (lane & 31);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int n = n0 + nsub * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (n < d.N && kc < Kp) wp[(int64_t)n * Kp + kc] = acc[r];
+  }
+  if (a.want_bias && blockIdx.z == 0 && tid < WG_TN && n0 + tid < d.N)
+    a.work[(int64_t)a.S * d.N * Kp + (int64_t)split * d.N + n0 + tid] = bacc;
+}
+
+// dw[i] (+)= sum_s work[s][i] in split order; i < total (N*Kp, then N bias entries)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ work, int S,
+                                                          int64_t per, float* __restrict__ dw,
+                                                          int accumulate) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < per;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int j = 0; j < S; ++j) s += work[(int64_t)j * per + i];
+    dw[i] = accumulate ? dw[i] + s : s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Gradient unpack: out[i] (+)= sum_{j<J} sgn[i*J+j] * src[idx[i*J+j]]  (idx < 0: skipped).
+// Maps a packed GEMM-operand gradient (e.g. [[Wr,-Wi],[Wi,Wr]] blocks, polyphase taps, padded
+// K) back onto the module's parameter layout; the host derives idx/sgn once per layer from
+// the packing transform.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void index_gather_kernel(const float* __restrict__ src,
+                                                           const int32_t* __restrict__ idx,
+                                                           const float* __restrict__ sgn, int J,
+                                                           int64_t n, float* __restrict__ out,
+                                                           int accumulate) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int j = 0; j < J; ++j) {
+      const int32_t q = idx[i * J + j];
+      if (q >= 0) s = fmaf(sgn[i * J + j], src[q], s);
+    }
+    out[i] = accumulate ? out[i] + s : s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Adam (torch.optim.Adam semantics, distill.py:202-204): L2 weight decay folded into g,
+// bias corrections from the step count, eps added to sqrt(v)/sqrt(bc2).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   int64_t n, float lr, float beta1, float beta2,
+                                                   float eps, float wd, float bc1, float bc2s,
+                                                   float gscale) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float gi = g[i] * gscale;
+    const float pi = p[i];
+    if (wd != 0.f) gi = fmaf(wd, pi, gi);
+    const float mi = beta1 * m[i] + (1.f - beta1) * gi;
+    const float vi = beta2 * v[i] + (1.f - beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    p[i] = pi - (lr / bc1) * (mi / denom);
+  }
+}
+
+__global__ void fill_f32_kernel(float* p, int64_t n, float v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+// y (+)= alpha * x
+__global__ void axpy_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
+                                float alpha, int accumulate) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = accumulate ? fmaf(alpha, x[i], y[i]) : alpha * x[i];
+}
+
+inline unsigned grid_for(int64_t n) { return (unsigned)std::min<int64_t>(cdiv(n, 256), 8192); }
+
+// splits of the row axis: ~2048 workgroups in flight, at least 256 rows per split
+inline void wgrad_plan(const clskd_conv_desc& d, int& S, int64_t& rps) {
+  const int64_t M = (int64_t)d.B * d.Fo * d.To;
+  const int64_t tiles = cdiv(d.N, WG_TN) * cdiv(d.K, WG_TK);
+  int64_t s = cdiv(2048, tiles);
+  s = std::max<int64_t>(1, std::min<int64_t>(s, cdiv(M, 256)));
+  rps = cdiv(cdiv(M, s), WG_RB) * WG_RB;
+  S = (int)cdiv(M, rps);
+}
+
+}  // namespace clskd
+
+using namespace clskd;
+
+extern "C" int64_t clskd_conv2d_wgrad_workspace(const clskd_conv_desc* dp) {
+  if (!dp) return -1;
+  int S;
+  int64_t rps;
+  wgrad_plan(*dp, S, rps);
+  return (int64_t)S * dp->N * dp->K + (int64_t)S * dp->N;
+}
+
+extern "C" int clskd_conv2d_wgrad(const clskd_conv_desc* dp, const float* dy, float* dw,
+                                  float* dbias, float* work, int64_t work_elems,
+                                  int32_t accumulate, void* stream) {
+  CLSKD_CHECK_ARG(dp && dy && dw && work, "conv2d_wgrad: null pointer");
+  const clskd_conv_desc& d = *dp;
+  CLSKD_CHECK_SHAPE(d.B > 0 && d.Fo > 0 && d.To > 0 && d.N > 0 && d.K > 0, "conv2d_wgrad: empty shape");
+  CLSKD_CHECK_ARG(d.in_dtype == CLSKD_F32, "conv2d_wgrad: fp32 segments only");
+  CLSKD_CHECK_SHAPE(d.nseg >= 1 && d.nseg <= CLSKD_MAX_SEGS && d.K % 4 == 0, "conv2d_wgrad: nseg/K");
+  int S;
+  int64_t rps;
+  wgrad_plan(d, S, rps);
+  const int64_t need = (int64_t)S * d.N * d.K + (int64_t)S * d.N;
+  CLSKD_CHECK_SHAPE(work_elems >= need, "conv2d_wgrad: workspace %lld < %lld", (long long)work_elems,
+                    (long long)need);
+  if (d.vec4) {
+    for (int s = 0; s < d.nseg; ++s)
+      CLSKD_CHECK_ARG(((uintptr_t)d.seg[s].ptr & 15) == 0 && d.seg[s].sB % 4 == 0 &&
+                          d.seg[s].sF % 4 == 0 && d.seg[s].sT % 4 == 0,
+                      "conv2d_wgrad: vec4 segment %d not 16-byte aligned", s);
+  }
+  WgradArgs a{d, dy, work, rps, S, dbias ? 1 : 0};
+  hipStream_t st = as_stream(stream);
+  dim3 grid(S, (unsigned)cdiv(d.N, WG_TN), (unsigned)cdiv(d.K, WG_TK));
+  if (d.vec4)
+    hipLaunchKernelGGL((conv_wgrad_f32<true>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_wgrad_f32<false>), grid, dim3(256), 0, st, a);
+  CLSKD_LAUNCH_CHECK("conv2d_wgrad");
+  const int64_t per = (int64_t)d.N * d.K;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(per)), dim3(256), 0, st, work, S, per, dw,
+                     accumulate & 1);
+  if (dbias)
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(d.N)), dim3(256), 0, st,
+                       work + (int64_t)S * per, S, (int64_t)d.N, dbias, (accumulate >> 1) & 1);
+  CLSKD_LAUNCH_CHECK("conv2d_wgrad_reduce");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_index_gather(const float* src, const int32_t* idx, const float* sgn, int32_t J,
+                                  int64_t n, float* out, int32_t accumulate, void* stream) {
+  CLSKD_CHECK_ARG(src && idx && sgn && out && J >= 1, "index_gather: bad argument");
+  if (n <= 0) return CLSKD_OK;
+  hipLaunchKernelGGL(index_gather_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), src,
+                     idx, sgn, J, n, out, accumulate);
+  CLSKD_LAUNCH_CHECK("index_gather");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr,
+                               float beta1, float beta2, float eps, float weight_decay,
+                               int32_t step, float grad_scale, void* stream) {
+  CLSKD_CHECK_ARG(p && g && m && v && step >= 1, "adam: bad argument");
+  if (n <= 0) return CLSKD_OK;
+  const float bc1 = 1.f - powf(beta1, (float)step);
+  const float bc2s = sqrtf(1.f - powf(beta2, (float)step));
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, g, m, v,
+                     n, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, grad_scale);
+  CLSKD_LAUNCH_CHECK("adam");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_fill_f32(float* p, int64_t n, float value, void* stream) {
+  CLSKD_CHECK_ARG(p || n == 0, "fill: null pointer");
+  if (n <= 0) return CLSKD_OK;
+  hipLaunchKernelGGL(fill_f32_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, n, value);
+  CLSKD_LAUNCH_CHECK("fill_f32");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_axpy_f32(const float* x, float* y, int64_t n, float alpha, int32_t accumulate,
+                              void* stream) {
+  CLSKD_CHECK_ARG((x && y) || n == 0, "axpy: null pointer");
+  if (n <= 0) return CLSKD_OK;
+  hipLaunchKernelGGL(axpy_f32_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, y, n,
+                     alpha, accumulate);
+  CLSKD_LAUNCH_CHECK("axpy_f32");
+  return CLSKD_OK;
+}

@@ -404,6 +404,159 @@ __global__ void sum_f32_kernel(const float* a, int n, float scale, float* out) {
   out[0] = (float)(s * scale);
 }
 
+
+// ------------------------------------------------------------------------------------------
+// SPKD backward (framework.py:150-172).  Per pair: recompute Gs / Gt from the slabs (same
+// fixed-order sums as the finalize), then with n = G / max(||G_i||_1, 1e-12) row-wise,
+//   dn = -2 * scale * inv * (n_t - n_s)         (inv = 1/B^2 for batchmean)
+//   dG_ij = dn_ij / s_i - sign(G_ij) * (sum_k dn_ik G_ik) / s_i^2   (s_i > 1e-12)
+// and M = dG + dG^T, so that dz = M z for G = z z^T.  M [pair][B][B] fp32.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(FIN_THREADS) void spkd_grad_kernel(const SpkdPairsArg pa, int B,
+                                                                int batchmean, float scale,
+                                                                float* __restrict__ mout) {
+  const int lp = blockIdx.x;
+  const int pr = pa.pair0 + lp;
+  __shared__ double Ps[FIN_THREADS], Pt[FIN_THREADS];
+  __shared__ double Gs[32 * 32], Gt[32 * 32], dG[32 * 32];
+  __shared__ double rs[32], rt[32], dot[32];
+  const int tid = threadIdx.x;
+  const int E = B * B;
+  const int nph = FIN_THREADS / E;
+  const int e = tid % E, ph = tid / E;
+  double sv = 0.0, tv = 0.0;
+  if (ph < nph) {
+    const int slot = (e / B) * 32 + (e % B);
+    sv = sum_slabs(pa.s_ptr[lp], pa.s_n[lp], slot, ph, nph);
+    tv = sum_slabs(pa.t_ptr[lp], pa.t_n[lp], slot, ph, nph);
+  }
+  Ps[tid] = sv;
+  Pt[tid] = tv;
+  __syncthreads();
+  if (tid < E) {
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < nph; ++k) {
+      a += Ps[k * E + tid];
+      b += Pt[k * E + tid];
+    }
+    Gs[tid] = a;
+    Gt[tid] = b;
+  }
+  __syncthreads();
+  if (tid < B) {
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < B; ++k) {
+      a += fabs(Gs[tid * B + k]);
+      b += fabs(Gt[tid * B + k]);
+    }
+    rs[tid] = a;
+    rt[tid] = b > 1e-12 ? b : 1e-12;
+  }
+  __syncthreads();
+  const double inv = batchmean ? 1.0 / ((double)B * B) : 1.0;
+  if (tid < E) {  // dn (kept in dG for now)
+    const int i = tid / B;
+    const double si = rs[i] > 1e-12 ? rs[i] : 1e-12;
+    const double ns = Gs[tid] / si, nt = Gt[tid] / rt[i];
+    dG[tid] = -2.0 * (double)scale * inv * (nt - ns);
+  }
+  __syncthreads();
+  if (tid < B) {
+    double a = 0.0;
+    for (int k = 0; k < B; ++k) a += dG[tid * B + k] * Gs[tid * B + k];
+    dot[tid] = a;
+  }
+  __syncthreads();
+  double g = 0.0;
+  if (tid < E) {
+    const int i = tid / B;
+    const double si = rs[i];
+    if (si > 1e-12) {
+      const double sg = Gs[tid] > 0 ? 1.0 : (Gs[tid] < 0 ? -1.0 : 0.0);
+      g = dG[tid] / si - sg * dot[i] / (si * si);
+    } else {
+      g = dG[tid] / 1e-12;
+    }
+  }
+  __syncthreads();
+  if (tid < E) dG[tid] = g;
+  __syncthreads();
+  if (tid < E) {
+    const int i = tid / B, j = tid % B;
+    mout[(int64_t)pr * E + tid] = (float)(dG[i * B + j] + dG[j * B + i]);
+  }
+}
+
+// dz[b] (+)= sum_j M[b][j] z_j over a job's elements; z read like the Gram (optional folded
+// affine), dz written fp32 at out + b*o_sB + p*o_Ctot + o_c0 + c.  One thread per (p, 4 ch).
+struct GramBwdJobsArg {
+  clskd_gram_bwd_job j[CLSKD_GRAM_MAX_JOBS];
+  int32_t blk0[CLSKD_GRAM_MAX_JOBS + 1];  // first block of each job
+  int32_t n;
+};
+
+template <int BMAX>
+__global__ __launch_bounds__(256) void gram_bwd_kernel(const GramBwdJobsArg a, int B) {
+  int q = 0;
+  for (int k = 1; k < a.n; ++k)
+    if ((int)blockIdx.x >= a.blk0[k]) q = k;
+  const clskd_gram_bwd_job& j = a.j[q];
+  __shared__ float Ms[BMAX * BMAX];
+  for (int i = threadIdx.x; i < B * B; i += 256) Ms[i] = j.coef[i];
+  __syncthreads();
+  const int CQ = j.Cs / 4;
+  const int64_t nq = j.P * CQ;
+  const int64_t qi = (int64_t)(blockIdx.x - a.blk0[q]) * 256 + threadIdx.x;
+  if (qi >= nq) return;
+  const int64_t p = qi / CQ;
+  const int c = (int)(qi - p * CQ) * 4;
+  f32x4 sc = {1.f, 1.f, 1.f, 1.f}, sh = {0.f, 0.f, 0.f, 0.f};
+  if (j.scale) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      sc[i] = j.scale[j.c0 + c + i];
+      sh[i] = j.shift[j.c0 + c + i];
+    }
+  }
+  f32x4 z[BMAX];
+#pragma unroll
+  for (int b = 0; b < BMAX; ++b) {
+    z[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (b < B) {
+      const int64_t off = (int64_t)b * j.sB + p * j.Ctot + j.c0 + c;
+      f32x4 v;
+      if (j.dtype == CLSKD_BF16) {
+        typedef __bf16 bf16x4g __attribute__((ext_vector_type(4)));
+        const bf16x4g w = *reinterpret_cast<const bf16x4g*>(reinterpret_cast<const __bf16*>(j.ptr) + off);
+        v = f32x4{(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
+        if (j.scale) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = (float)(__bf16)fmaf(v[i], sc[i], sh[i]);
+        }
+      } else {
+        v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(j.ptr) + off);
+        if (j.scale) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = fmaf(v[i], sc[i], sh[i]);
+        }
+      }
+      z[b] = v;
+    }
+  }
+  for (int b = 0; b < B; ++b) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < BMAX; ++k) {
+      if (k < B) {
+        const float m = Ms[b * B + k];
+        acc += m * z[k];
+      }
+    }
+    float* o = j.out + (int64_t)b * j.o_sB + p * j.o_Ctot + j.o_c0 + c;
+    if (j.accumulate) acc += *reinterpret_cast<const f32x4*>(o);
+    *reinterpret_cast<f32x4*>(o) = acc;
+  }
+}
 }  // namespace clskd
 
 using namespace clskd;
@@ -555,5 +708,65 @@ extern "C" int clskd_sum_f32(const float* a, int32_t n, float scale, float* out,
   CLSKD_CHECK_ARG(a && out && n >= 1, "sum_f32: bad args");
   hipLaunchKernelGGL(sum_f32_kernel, dim3(1), dim3(64), 0, as_stream(stream), a, n, scale, out);
   CLSKD_LAUNCH_CHECK("sum_f32");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_spkd_grad_ranges(const float* const* s_slabs, const int32_t* s_nslab,
+                                      const float* const* t_slabs, const int32_t* t_nslab,
+                                      int32_t npairs, int32_t B, int32_t batchmean, float scale,
+                                      float* coef, void* stream) {
+  CLSKD_CHECK_ARG(s_slabs && s_nslab && t_slabs && t_nslab && coef, "spkd_grad: null pointer");
+  CLSKD_CHECK_SHAPE(B >= 1 && B <= 32 && npairs >= 1, "spkd_grad: B=%d npairs=%d", B, npairs);
+  hipStream_t st = as_stream(stream);
+  for (int p0 = 0; p0 < npairs; p0 += CLSKD_SPKD_MAX_PAIRS) {
+    SpkdPairsArg a;
+    const int n = npairs - p0 < CLSKD_SPKD_MAX_PAIRS ? npairs - p0 : CLSKD_SPKD_MAX_PAIRS;
+    for (int k = 0; k < CLSKD_SPKD_MAX_PAIRS; ++k) {
+      const int q = k < n ? p0 + k : p0;
+      CLSKD_CHECK_ARG(s_slabs[q] && t_slabs[q] && s_nslab[q] >= 1 && t_nslab[q] >= 1,
+                      "spkd_grad: pair %d has an empty slab range", q);
+      a.s_ptr[k] = s_slabs[q];
+      a.t_ptr[k] = t_slabs[q];
+      a.s_n[k] = s_nslab[q];
+      a.t_n[k] = t_nslab[q];
+    }
+    a.pair0 = p0;
+    hipLaunchKernelGGL(spkd_grad_kernel, dim3(n), dim3(FIN_THREADS), 0, st, a, B, batchmean, scale,
+                       coef);
+    CLSKD_LAUNCH_CHECK("spkd_grad");
+  }
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_gram_bwd(const clskd_gram_bwd_job* jobs, int32_t njobs, int32_t B,
+                              void* stream) {
+  CLSKD_CHECK_ARG(jobs && njobs >= 1, "gram_bwd: no jobs");
+  CLSKD_CHECK_SHAPE(B >= 1 && B <= 32, "gram_bwd: batch %d must be in [1, 32]", B);
+  hipStream_t st = as_stream(stream);
+  for (int k0 = 0; k0 < njobs; k0 += CLSKD_GRAM_MAX_JOBS) {
+    GramBwdJobsArg a;
+    a.n = njobs - k0 < CLSKD_GRAM_MAX_JOBS ? njobs - k0 : CLSKD_GRAM_MAX_JOBS;
+    int32_t blk = 0;
+    for (int k = 0; k < a.n; ++k) {
+      const clskd_gram_bwd_job& j = jobs[k0 + k];
+      CLSKD_CHECK_ARG(j.ptr && j.out && j.coef && j.P >= 1 && j.Cs % 4 == 0 && j.o_c0 % 4 == 0 &&
+                          j.o_Ctot % 4 == 0 && j.o_sB % 4 == 0 &&
+                          (j.dtype == CLSKD_F32 || j.dtype == CLSKD_BF16),
+                      "gram_bwd: job %d malformed", k0 + k);
+      a.j[k] = j;
+      a.blk0[k] = blk;
+      blk += (int32_t)cdiv(j.P * (j.Cs / 4), 256);
+    }
+    for (int k = a.n; k < CLSKD_GRAM_MAX_JOBS; ++k) {
+      a.j[k] = jobs[k0];
+      a.blk0[k] = blk;
+    }
+    a.blk0[CLSKD_GRAM_MAX_JOBS] = blk;
+    if (B <= 16)
+      hipLaunchKernelGGL(gram_bwd_kernel<16>, dim3(blk), dim3(256), 0, st, a, B);
+    else
+      hipLaunchKernelGGL(gram_bwd_kernel<32>, dim3(blk), dim3(256), 0, st, a, B);
+    CLSKD_LAUNCH_CHECK("gram_bwd");
+  }
   return CLSKD_OK;
 }

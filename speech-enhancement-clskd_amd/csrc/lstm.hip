@@ -171,6 +171,93 @@ __global__ __launch_bounds__(NKS * H) void lstm_recurrent_kernel(
   }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Backward of the recurrence (BPTT) for one (weight set, sequence) per workgroup.
+// Inputs: pre[ws][seq][t][4H] = the gate PRE-activations of the forward (x W_ih^T + b + h_{t-1}
+// W_hh^T — the host rebuilds them with one conv-engine GEMM over the saved h history, so the
+// forward kernel stores nothing extra), dh[ws][seq][t][H] = dL/dh_t from the layer's outputs.
+// Phase 1 (lanes ks == 0, one unit each): the cell scan c_t = f c_{t-1} + i g into cbuf.
+// Phase 2 (t = T-1 .. 0): lane ks == 0 of unit u forms dh = dh_in + (W_hh^T da_{t+1})_u and the
+// gate gradients da (i, f, g, o pre-activation) of unit u, writes them to dgates and LDS; after
+// one barrier every thread (u, ks) multiplies its slice of W_hh's column u with da and the NKS
+// slices reduce by lane shuffles into (W_hh^T da_t)_u for step t-1.  da is double-buffered in
+// LDS, so one barrier per step suffices.
+// ------------------------------------------------------------------------------------------
+template <int H, int NKS>
+__global__ __launch_bounds__(NKS * H) void lstm_bwd_kernel(
+    const float* __restrict__ pre, int64_t p_ws, int64_t p_seq, int64_t p_t,
+    const float* __restrict__ dh, int64_t d_ws, int64_t d_seq, int64_t d_t,
+    const float* __restrict__ whh, int T, float* __restrict__ cbuf,
+    float* __restrict__ dg, int64_t g_ws, int64_t g_seq, int64_t g_t) {
+  constexpr int G = 4 * H;
+  constexpr int GW = G / NKS;  // gate rows per k-slice
+  const int tid = threadIdx.x;
+  const int u = tid / NKS;
+  const int ks = tid % NKS;
+  const int ws = blockIdx.y;
+  const int seq = blockIdx.x;
+  __shared__ float das[2][G];
+  // column u of W_hh restricted to gate rows [ks*GW, (ks+1)*GW)
+  float wc[GW];
+#pragma unroll
+  for (int j = 0; j < GW; ++j) wc[j] = whh[((int64_t)ws * G + ks * GW + j) * H + u];
+  const float* pp = pre + ws * p_ws + seq * p_seq + u;
+  const float* dp = dh + ws * d_ws + seq * d_seq + u;
+  float* cp = cbuf + ((int64_t)ws * gridDim.x + seq) * (int64_t)T * H + u;
+  float* gp = dg + ws * g_ws + seq * g_seq + u;
+  auto acts = [&](int t, float& ig, float& fg, float& gg, float& og) {
+    const float* q = pp + (int64_t)t * p_t;
+    ig = sigm_fast(q[0]);
+    fg = sigm_fast(q[H]);
+    gg = fmaf(2.f, sigm_fast(2.f * q[2 * H]), -1.f);
+    og = sigm_fast(q[3 * H]);
+  };
+  if (ks == 0) {
+    float c = 0.f;
+#pragma unroll 4
+    for (int t = 0; t < T; ++t) {
+      float ig, fg, gg, og;
+      acts(t, ig, fg, gg, og);
+      c = fg * c + ig * gg;
+      cp[(int64_t)t * H] = c;
+    }
+  }
+  float dc = 0.f, dhr = 0.f;
+  for (int t = T - 1; t >= 0; --t) {
+    const int buf = t & 1;
+    if (ks == 0) {
+      float ig, fg, gg, og;
+      acts(t, ig, fg, gg, og);
+      const float ct = cp[(int64_t)t * H];
+      const float cprev = t > 0 ? cp[(int64_t)(t - 1) * H] : 0.f;
+      const float tc = tanh_fast(ct);
+      const float dht = dp[(int64_t)t * d_t] + dhr;
+      dc = fmaf(dht * og, 1.f - tc * tc, dc);
+      const float a_i = dc * gg * ig * (1.f - ig);
+      const float a_f = dc * cprev * fg * (1.f - fg);
+      const float a_g = dc * ig * (1.f - gg * gg);
+      const float a_o = dht * tc * og * (1.f - og);
+      dc *= fg;
+      float* o = gp + (int64_t)t * g_t;
+      o[0] = a_i;
+      o[H] = a_f;
+      o[2 * H] = a_g;
+      o[3 * H] = a_o;
+      das[buf][u] = a_i;
+      das[buf][H + u] = a_f;
+      das[buf][2 * H + u] = a_g;
+      das[buf][3 * H + u] = a_o;
+    }
+    __syncthreads();
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < GW; ++j) s = fmaf(wc[j], das[buf][ks * GW + j], s);
+#pragma unroll
+    for (int o = 1; o < NKS; o <<= 1) s += __shfl_xor(s, o, 64);
+    dhr = s;
+  }
+}
 }  // namespace clskd
 
 using namespace clskd;
@@ -224,5 +311,31 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
   }
 #undef LSTM_LAUNCH
   CLSKD_LAUNCH_CHECK("lstm_recurrent");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_lstm_bwd(const float* pre, int64_t p_ws, int64_t p_seq, int64_t p_t,
+                              const float* dh, int64_t d_ws, int64_t d_seq, int64_t d_t,
+                              const float* whh, int32_t nws, int32_t nseq, int32_t T, int32_t H,
+                              float* cbuf, float* dgates, int64_t g_ws, int64_t g_seq,
+                              int64_t g_t, void* stream) {
+  CLSKD_CHECK_ARG(pre && dh && whh && cbuf && dgates, "lstm_bwd: null pointer");
+  CLSKD_CHECK_SHAPE(nws >= 1 && nseq >= 1 && T >= 1, "lstm_bwd: empty shape");
+  dim3 grid(nseq, nws);
+  hipStream_t st = as_stream(stream);
+#define LSTM_BWD(H_, NKS_)                                                                     \
+  hipLaunchKernelGGL((lstm_bwd_kernel<H_, NKS_>), grid, dim3(NKS_ * H_), 0, st, pre, p_ws, p_seq, \
+                     p_t, dh, d_ws, d_seq, d_t, whh, T, cbuf, dgates, g_ws, g_seq, g_t)
+  switch (H) {
+    case 16: LSTM_BWD(16, 8); break;
+    case 32: LSTM_BWD(32, 8); break;
+    case 64: LSTM_BWD(64, 8); break;
+    case 128: LSTM_BWD(128, 8); break;
+    default:
+      set_error("lstm_bwd: hidden size %d not built (16, 32, 64, 128)", H);
+      return CLSKD_E_SHAPE;
+  }
+#undef LSTM_BWD
+  CLSKD_LAUNCH_CHECK("lstm_bwd");
   return CLSKD_OK;
 }

@@ -1,0 +1,606 @@
+// Backward of the elementwise / normalisation ops of the CLSKD step (student side):
+// BatchNorm2d(train) + PReLU, ReviewKD ABF attention fusion and nearest upsampling, masking
+// mode 'E', ConviSTFT overlap-add + clamp, framing pads, the STFT log-magnitude L1 loss and the
+// complex-LSTM output combine.  HBM-bound passes; statistics reductions in fp64 with fixed
+// orders (no float atomics), so every gradient is bitwise repeatable.
+#include <algorithm>
+
+#include "common.h"
+
+namespace clskd {
+
+typedef __bf16 bf16x4b __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ f32x4 ld4(const T* p);
+template <>
+__device__ __forceinline__ f32x4 ld4<float>(const float* p) {
+  return *reinterpret_cast<const f32x4*>(p);
+}
+template <>
+__device__ __forceinline__ f32x4 ld4<__bf16>(const __bf16* p) {
+  const bf16x4b v = *reinterpret_cast<const bf16x4b*>(p);
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+
+// ------------------------------------------------------------------------------------------
+// BatchNorm (train) + optional PReLU backward.  Forward: y_bn = x*scale + shift (scale = gamma *
+// rstd, shift = beta - mean*scale), y = prelu(y_bn) when alpha != NULL.  Given dy = dL/dy:
+//   dz = alpha ? (y_bn > 0 ? dy : alpha*dy) : dy      (torch prelu backward)
+//   dbeta = sum dz, dgamma = sum dz*xhat, dalpha = sum_{y_bn<=0} y_bn*dy
+//   dx = k1*dz + k2*x + k3   with k1 = gamma*rstd, k2 = -gamma*rstd^2*dgamma/n,
+//                              k3 = -gamma*rstd*dbeta/n + gamma*rstd^2*mean*dgamma/n
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
+    const T* __restrict__ x, const float* __restrict__ dy, int64_t rows, int C, int64_t rpb,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ mean, const float* __restrict__ var, float eps,
+    const float* __restrict__ alpha, double* __restrict__ partial) {
+  const int CG = C >> 2;
+  const int RP = 256 / CG;
+  const int tid = threadIdx.x;
+  const int cg = tid % CG;
+  const int rl = tid / CG;
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = min(rows, r0 + rpb);
+  const float al = alpha ? alpha[0] : 1.f;
+  f32x4 sc, sh, mu, rs;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = (cg * 4 + j) % C;
+    sc[j] = scale[c];
+    sh[j] = shift[c];
+    mu[j] = mean[c];
+    rs[j] = (float)(1.0 / sqrt((double)var[c] + (double)eps));
+  }
+  double sb[4] = {0, 0, 0, 0}, sg[4] = {0, 0, 0, 0}, sa[4] = {0, 0, 0, 0};
+  if (rl < RP) {
+    for (int64_t r = r0 + rl; r < r1; r += RP) {
+      const f32x4 xv = ld4<T>(x + r * C + cg * 4);
+      const f32x4 gv = *reinterpret_cast<const f32x4*>(dy + r * C + cg * 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float yb = fmaf(xv[j], sc[j], sh[j]);
+        float dz = gv[j];
+        if (alpha) {
+          if (!(yb > 0.f)) {
+            sa[j] += (double)yb * (double)gv[j];
+            dz = al * gv[j];
+          }
+        }
+        const float xh = (xv[j] - mu[j]) * rs[j];
+        sb[j] += (double)dz;
+        sg[j] += (double)dz * (double)xh;
+      }
+    }
+  }
+  __shared__ double red[256][13];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    red[tid][j] = sb[j];
+    red[tid][4 + j] = sg[j];
+    red[tid][8 + j] = sa[j];
+  }
+  __syncthreads();
+  if (tid < CG) {
+    double B[4] = {0, 0, 0, 0}, G[4] = {0, 0, 0, 0}, A[4] = {0, 0, 0, 0};
+    for (int l = 0; l < RP; ++l) {
+      const int t = l * CG + tid;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        B[j] += red[t][j];
+        G[j] += red[t][4 + j];
+        A[j] += red[t][8 + j];
+      }
+    }
+    double* p = partial + ((int64_t)blockIdx.x * C + tid * 4) * 3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      p[3 * j] = B[j];
+      p[3 * j + 1] = G[j];
+      p[3 * j + 2] = A[j];
+    }
+  }
+}
+
+// one block per channel; writes dgamma/dbeta (accumulate optional), k[3][C], alpha_part[C]
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
+    const double* __restrict__ partial, int nblk, int64_t rows, int C, const float* gamma,
+    const float* mean, const float* var, float eps, float* dgamma, float* dbeta, float* k,
+    double* alpha_part, int accumulate) {
+  const int c = blockIdx.x;
+  const int tid = threadIdx.x;
+  double SB = 0, SG = 0, SA = 0;
+  for (int b = tid; b < nblk; b += 256) {
+    const double* p = partial + ((int64_t)b * C + c) * 3;
+    SB += p[0];
+    SG += p[1];
+    SA += p[2];
+  }
+  __shared__ double r0[256], r1[256], r2[256];
+  r0[tid] = SB;
+  r1[tid] = SG;
+  r2[tid] = SA;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      r0[tid] += r0[tid + o];
+      r1[tid] += r1[tid + o];
+      r2[tid] += r2[tid + o];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    SB = r0[0];
+    SG = r1[0];
+    const double n = (double)rows;
+    const double rs = 1.0 / sqrt((double)var[c] + (double)eps);
+    const double g = gamma ? (double)gamma[c] : 1.0;
+    k[c] = (float)(g * rs);
+    k[C + c] = (float)(-g * rs * rs * SG / n);
+    k[2 * C + c] = (float)(-g * rs * SB / n + g * rs * rs * (double)mean[c] * SG / n);
+    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)SG : (float)SG;
+    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)SB : (float)SB;
+    if (alpha_part) alpha_part[c] = r2[0];
+  }
+}
+
+// dalpha (+)= sum over channels of alpha_part (fixed order)
+__global__ void bn_bwd_alpha_kernel(const double* alpha_part, int C, float* dalpha, int accumulate) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    double s = 0;
+    for (int c = 0; c < C; ++c) s += alpha_part[c];
+    dalpha[0] = accumulate ? dalpha[0] + (float)s : (float)s;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const T* __restrict__ x, const float* __restrict__ dy, int64_t rows, int C,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ alpha, const float* __restrict__ k, float* __restrict__ dx,
+    int accumulate) {
+  const int64_t nq = rows * C / 4;
+  const float al = alpha ? alpha[0] : 1.f;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)((q * 4) % C);
+    const f32x4 xv = ld4<T>(x + q * 4);
+    const f32x4 gv = *reinterpret_cast<const f32x4*>(dy + q * 4);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + j;
+      float dz = gv[j];
+      if (alpha) {
+        const float yb = fmaf(xv[j], scale[c], shift[c]);
+        if (!(yb > 0.f)) dz = al * gv[j];
+      }
+      o[j] = fmaf(k[c], dz, fmaf(k[C + c], xv[j], k[2 * C + c]));
+    }
+    if (accumulate) o += *reinterpret_cast<const f32x4*>(dx + q * 4);
+    *reinterpret_cast<f32x4*>(dx + q * 4) = o;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// ABF fusion backward (framework.py:209-219), mid = 64.  Forward (abf_fuse_kernel): x = x1*xs +
+// xh, y = res[nearest(f), nearest(t)], z_k = sigmoid(w_k . [x; y] + b_k), out = x*z0 + y*z1.
+// Given dout: dx = dout*z0 + a0*w0x + a1*w1x, dy = dout*z1 + a0*w0y + a1*w1y with
+// a_k = (sum_c dout_c * {x,y}_c) * z_k (1 - z_k).  dx is w.r.t. the BN1 output x; dy is w.r.t.
+// the UPSAMPLED residual (reduce with clskd_nearest_down_sum).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int nearest_src_b(int dst, int in_size, int out_size) {
+  if (out_size == in_size) return dst;
+  if (out_size == 2 * in_size) return dst >> 1;
+  const float scale = (float)in_size / (float)out_size;
+  const int s = (int)floorf((float)dst * scale);
+  return s < in_size - 1 ? s : in_size - 1;
+}
+
+template <typename DT>
+__global__ __launch_bounds__(256) void abf_fuse_bwd_kernel(
+    const DT* __restrict__ x1, const DT* __restrict__ res, int B, int F, int T, int Fr, int Tr,
+    const float* __restrict__ w, const float* __restrict__ bias, const float* __restrict__ xs,
+    const float* __restrict__ xh, const float* __restrict__ dout, float* __restrict__ dx,
+    float* __restrict__ dyup) {
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & 15;
+  const int c = sub * 4;
+  f32x4 sx = {1.f, 1.f, 1.f, 1.f}, hx = {0.f, 0.f, 0.f, 0.f};
+  if (xs) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sx[j] = xs[c + j];
+      hx[j] = xh[c + j];
+    }
+  }
+  f32x4 w0x, w0y, w1x, w1y;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    w0x[j] = w[c + j];
+    w0y[j] = w[64 + c + j];
+    w1x[j] = w[128 + c + j];
+    w1y[j] = w[192 + c + j];
+  }
+  const float b0 = bias[0], b1 = bias[1];
+  const int64_t npix = (int64_t)B * F * T;
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int64_t nslots = ((int64_t)gridDim.x * blockDim.x) >> 4;
+  for (int64_t p = gw; p < npix; p += nslots) {
+    const int t = (int)(p % T);
+    const int64_t bf = p / T;
+    const int f = (int)(bf % F);
+    const int b = (int)(bf / F);
+    const int fr = nearest_src_b(f, Fr, F);
+    const int tr = nearest_src_b(t, Tr, T);
+    f32x4 xv = ld4<DT>(x1 + p * 64 + c);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[j] = fmaf(xv[j], sx[j], hx[j]);
+    const f32x4 yv = ld4<DT>(res + (((int64_t)b * Fr + fr) * Tr + tr) * 64 + c);
+    const f32x4 g = *reinterpret_cast<const f32x4*>(dout + p * 64 + c);
+    float d0 = 0.f, d1 = 0.f, e0 = 0.f, e1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      d0 += w0x[j] * xv[j] + w0y[j] * yv[j];
+      d1 += w1x[j] * xv[j] + w1y[j] * yv[j];
+      e0 += g[j] * xv[j];
+      e1 += g[j] * yv[j];
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      d0 += __shfl_xor(d0, o, 16);
+      d1 += __shfl_xor(d1, o, 16);
+      e0 += __shfl_xor(e0, o, 16);
+      e1 += __shfl_xor(e1, o, 16);
+    }
+    const float z0 = sigmoidf_(d0 + b0);
+    const float z1 = sigmoidf_(d1 + b1);
+    const float a0 = e0 * z0 * (1.f - z0);
+    const float a1 = e1 * z1 * (1.f - z1);
+    f32x4 ox, oy;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ox[j] = g[j] * z0 + a0 * w0x[j] + a1 * w1x[j];
+      oy[j] = g[j] * z1 + a0 * w0y[j] + a1 * w1y[j];
+    }
+    *reinterpret_cast<f32x4*>(dx + p * 64 + c) = ox;
+    *reinterpret_cast<f32x4*>(dyup + p * 64 + c) = oy;
+  }
+}
+
+// out[b][fr][tr][c] (+)= sum of g[b][f][t][c] over the (f, t) whose nearest source is (fr, tr)
+__device__ __forceinline__ int first_dst(int s, int in_size, int out_size) {
+  // smallest dst with nearest_src(dst) >= s (nearest_src is non-decreasing in dst)
+  int d0 = (int)((double)s * out_size / in_size) - 2;
+  if (d0 < 0) d0 = 0;
+  while (d0 < out_size && nearest_src_b(d0, in_size, out_size) < s) ++d0;
+  return d0;
+}
+
+__global__ __launch_bounds__(256) void nearest_down_sum_kernel(
+    const float* __restrict__ g, int B, int F, int T, int Fr, int Tr, int C,
+    float* __restrict__ out, int accumulate) {
+  const int CQ = C / 4;
+  const int64_t total = (int64_t)B * Fr * Tr * CQ;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int cq = (int)(i % CQ);
+    const int64_t pix = i / CQ;
+    const int tr = (int)(pix % Tr);
+    const int64_t bf = pix / Tr;
+    const int fr = (int)(bf % Fr);
+    const int b = (int)(bf / Fr);
+    const int fa = first_dst(fr, Fr, F), ta = first_dst(tr, Tr, T);
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int f = fa; f < F && nearest_src_b(f, Fr, F) == fr; ++f)
+      for (int t = ta; t < T && nearest_src_b(t, Tr, T) == tr; ++t)
+        s += *reinterpret_cast<const f32x4*>(g + ((((int64_t)b * F + f) * T + t) * C) + cq * 4);
+    float* op = out + pix * C + cq * 4;
+    if (accumulate) s += *reinterpret_cast<const f32x4*>(op);
+    *reinterpret_cast<f32x4*>(op) = s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// masking mode 'E' backward (DCCRN.py:207-226): d est (real at 0.., imag at 257..) -> d mask,
+// mask = last decoder output [B][256][Tm][2] read at time t+1 (time 0 gets no gradient).
+// A = tanh|M| * |S|, psi = angle(S) + atan2(mi, mr):
+//   dA = dre cos psi + dim sin psi,  dpsi = A (dim cos psi - dre sin psi)
+//   dmr = dA |S| (1 - tanh^2|M|) mr/|M| - dpsi mi/|M|^2,  dmi = ... mi/|M| + dpsi mr/|M|^2
+// (the atan2 of the 1/(|M|+1e-8)-scaled pair is scale invariant, so its derivative is atan2's).
+// ------------------------------------------------------------------------------------------
+__global__ void mask_e_bwd_kernel(const float* __restrict__ spec, int ldspec,
+                                  const float* __restrict__ mask, int Tm, int B, int T,
+                                  const float* __restrict__ dest, int ldest,
+                                  float* __restrict__ dmask) {
+  const int64_t total = (int64_t)B * 256 * Tm;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int tm = (int)(i % Tm);
+    const int64_t bf = i / Tm;
+    const int fm = (int)(bf % 256);
+    const int b = (int)(bf / 256);
+    float gr = 0.f, gi = 0.f;
+    if (tm >= 1 && tm - 1 < T) {
+      const int t = tm - 1, f = fm + 1;
+      const int64_t bt = (int64_t)b * T + t;
+      const float re = spec[bt * ldspec + f];
+      const float im = spec[bt * ldspec + 257 + f];
+      const float mags = sqrtf(re * re + im * im + 1e-8f);
+      const float phase = atan2f(im, re);
+      const float mr = mask[i * 2], mi = mask[i * 2 + 1];
+      const float m2 = mr * mr + mi * mi;
+      const float mm = sqrtf(m2);
+      const float rp = mr / (mm + 1e-8f);
+      const float ip = mi / (mm + 1e-8f);
+      const float th = tanhf(mm);
+      const float A = th * mags;
+      const float psi = phase + atan2f(ip, rp);
+      const float cp = cosf(psi), sp = sinf(psi);
+      const float dre = dest[bt * ldest + f], dim = dest[bt * ldest + 257 + f];
+      const float dA = dre * cp + dim * sp;
+      const float dpsi = A * (dim * cp - dre * sp);
+      if (mm > 0.f) {
+        const float dmm = dA * mags * (1.f - th * th);
+        gr = dmm * mr / mm - dpsi * mi / m2;
+        gi = dmm * mi / mm + dpsi * mr / m2;
+      }
+    }
+    dmask[i * 2] = gr;
+    dmask[i * 2 + 1] = gi;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// ConviSTFT overlap-add backward (tools_for_model.py:95-107 + clamp DCCRN.py:237):
+// dframes[b][t][o] = dwav[b][t*hop+o-trim] * [|pre| <= 1] / (sum window^2 + 1e-8), with the
+// pre-clamp sample recomputed from the frames (clamp passes the gradient for -1 <= pre <= 1).
+// ------------------------------------------------------------------------------------------
+__global__ void ola_bwd_kernel(const float* __restrict__ frames, const float* __restrict__ window,
+                               const float* __restrict__ dwav, int B, int T, int win, int hop,
+                               int out_len, int trim, int clamp, float* __restrict__ dframes) {
+  const int64_t total = (int64_t)B * T * win;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int o = (int)(i % win);
+    const int64_t bt = i / win;
+    const int t = (int)(bt % T);
+    const int b = (int)(bt / T);
+    const int p = t * hop + o;
+    const int n = p - trim;
+    float g = 0.f;
+    if (n >= 0 && n < out_len) {
+      int t_hi = p / hop;
+      if (t_hi > T - 1) t_hi = T - 1;
+      const int t_lo = p - win + 1 <= 0 ? 0 : (p - win + 1 + hop - 1) / hop;
+      float acc = 0.f, coff = 0.f;
+      for (int u = t_lo; u <= t_hi; ++u) {
+        const int q = p - u * hop;
+        acc += frames[((int64_t)b * T + u) * win + q];
+        const float w = window[q];
+        coff += w * w;
+      }
+      const float den = coff + 1e-8f;
+      const float v = acc / den;
+      const bool pass = !clamp || (v >= -1.f && v <= 1.f);
+      if (pass) g = dwav[(int64_t)b * out_len + n] / den;
+    }
+    dframes[i] = g;
+  }
+}
+
+// framing pad backward: dx[b][j] (+)= sum of dxp[b][i] over the padded positions i reading x[j]
+__global__ void frame_pad_bwd_kernel(const float* __restrict__ dxp, int B, int L, int pad, int Lp,
+                                     int mode, float* __restrict__ dx, int64_t ldx, int accumulate) {
+  const int64_t total = (int64_t)B * L;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(i / L);
+    const int j = (int)(i - (int64_t)b * L);
+    const float* row = dxp + (int64_t)b * Lp;
+    float s = 0.f;
+    if (j + pad < Lp) s = row[j + pad];
+    if (mode == 1) {
+      if (j >= 1 && j <= pad && pad - j < Lp) s += row[pad - j];  // src = -(j) reflected
+      const int src = 2 * (L - 1) - j;                           // src >= L reflected onto j
+      if (src >= L && src < L + pad && src + pad < Lp) s += row[src + pad];
+    }
+    float* o = dx + (int64_t)b * ldx + j;
+    *o = accumulate ? *o + s : s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// STFT log-magnitude L1 backward (framework.py:58-68, 85-101): loss = scale_sum * sum|log Y -
+// log X| with X = sqrt(max(re^2 + im^2, 1e-7)) of the estimate's spectrum.
+// dre = -scale * sign(log Y - log X) * re / X^2 (clamp passes for re^2+im^2 >= 1e-7), same for im.
+// ------------------------------------------------------------------------------------------
+__global__ void stft_mag_loss_bwd_kernel(const float* __restrict__ X, const float* __restrict__ Y,
+                                         int64_t rows, int ld, int nbins, float scale,
+                                         float* __restrict__ dX) {
+  const int64_t total = rows * ld;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int col = (int)(i % ld);
+    const int64_t r = i / ld;
+    float g = 0.f;
+    if (col < 2 * nbins) {
+      const int f = col < nbins ? col : col - nbins;
+      const float* xr = X + r * ld;
+      const float* yr = Y + r * ld;
+      const float xre = xr[f], xim = xr[nbins + f];
+      const float yre = yr[f], yim = yr[nbins + f];
+      const float px = xre * xre + xim * xim;
+      const float py = yre * yre + yim * yim;
+      const float mx = sqrtf(fmaxf(px, 1e-7f));
+      const float my = sqrtf(fmaxf(py, 1e-7f));
+      const float dlog = logf(my) - logf(mx);
+      const float sgn = dlog > 0.f ? 1.f : (dlog < 0.f ? -1.f : 0.f);
+      if (px >= 1e-7f) {
+        const float comp = col < nbins ? xre : xim;
+        g = -scale * sgn * comp / (mx * mx);
+      }
+    }
+    dX[i] = g;
+  }
+}
+
+// complex-LSTM combine backward: real = h[0][:B] - h[1][B:], imag = h[0][B:] + h[1][:B]
+// (tools_for_model.py:168-169) -> dh[ws][2B][n] from dreal/dimag [B][n]
+__global__ void complex_combine_bwd_kernel(const float* __restrict__ dre, const float* __restrict__ dim,
+                                           int B, int64_t n, float* __restrict__ dh) {
+  const int64_t total = (int64_t)B * n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float r = dre[i], m = dim[i];
+    const int64_t half = (int64_t)B * n;
+    dh[i] = r;                  // ws 0 (real_lstm), real input
+    dh[half + i] = m;           // ws 0, imag input
+    dh[2 * half + i] = m;       // ws 1 (imag_lstm), real input
+    dh[3 * half + i] = -r;      // ws 1, imag input
+  }
+}
+
+inline unsigned grid_of(int64_t n, int64_t cap = 8192) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n, 256), cap));
+}
+
+}  // namespace clskd
+
+using namespace clskd;
+
+extern "C" int32_t clskd_bn_bwd_blocks(int64_t rows, int32_t C) {
+  (void)C;
+  return (int32_t)std::max<int64_t>(1, std::min<int64_t>(1024, cdiv(rows, 512)));
+}
+
+extern "C" int clskd_bn_bwd(const void* x, const float* dy, int64_t rows, int32_t C,
+                            const float* scale, const float* shift, const float* mean,
+                            const float* var, float eps, const float* gamma, const float* alpha,
+                            double* work, int32_t nblk, float* dgamma, float* dbeta,
+                            float* dalpha, float* dx, int32_t accumulate_dx,
+                            int32_t accumulate_params, int32_t dtype, void* stream) {
+  CLSKD_CHECK_ARG(x && dy && scale && shift && mean && var && work && dx, "bn_bwd: null pointer");
+  CLSKD_CHECK_SHAPE(rows > 0 && C >= 4 && C % 4 == 0 && C <= 1024 && nblk >= 1,
+                    "bn_bwd: rows=%lld C=%d nblk=%d", (long long)rows, C, nblk);
+  CLSKD_CHECK_ARG(dtype == CLSKD_F32 || dtype == CLSKD_BF16, "bn_bwd: dtype");
+  hipStream_t st = as_stream(stream);
+  // work layout: partial[nblk][C][3] | k[3C] (as floats) | alpha_part[C]
+  double* partial = work;
+  float* k = reinterpret_cast<float*>(work + (int64_t)nblk * C * 3);
+  double* apart = work + (int64_t)nblk * C * 3 + cdiv(3 * C, 2);
+  const int64_t rpb = cdiv(rows, nblk);
+  if (dtype == CLSKD_BF16)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<__bf16>, dim3(nblk), dim3(256), 0, st,
+                       (const __bf16*)x, dy, rows, C, rpb, scale, shift, mean, var, eps, alpha, partial);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3(nblk), dim3(256), 0, st, (const float*)x,
+                       dy, rows, C, rpb, scale, shift, mean, var, eps, alpha, partial);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, nblk, rows, C,
+                     gamma, mean, var, eps, dgamma, dbeta, k, alpha ? apart : nullptr,
+                     accumulate_params);
+  if (alpha && dalpha)
+    hipLaunchKernelGGL(bn_bwd_alpha_kernel, dim3(1), dim3(64), 0, st, apart, C, dalpha,
+                       accumulate_params);
+  const int64_t nq = rows * C / 4;
+  if (dtype == CLSKD_BF16)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<__bf16>, dim3(grid_of(nq)), dim3(256), 0, st,
+                       (const __bf16*)x, dy, rows, C, scale, shift, alpha, k, dx, accumulate_dx);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(grid_of(nq)), dim3(256), 0, st,
+                       (const float*)x, dy, rows, C, scale, shift, alpha, k, dx, accumulate_dx);
+  CLSKD_LAUNCH_CHECK("bn_bwd");
+  return CLSKD_OK;
+}
+
+extern "C" int64_t clskd_bn_bwd_workspace(int32_t nblk, int32_t C) {
+  return (int64_t)nblk * C * 3 + cdiv(3 * C, 2) + C;  // doubles
+}
+
+extern "C" int clskd_abf_fuse_bwd(const void* x1, const void* res, int32_t B, int32_t F, int32_t T,
+                                  int32_t Fr, int32_t Tr, const float* w, const float* b,
+                                  const float* x_scale, const float* x_shift, const float* dout,
+                                  float* dx, float* dyup, int32_t dtype, void* stream) {
+  CLSKD_CHECK_ARG(x1 && res && w && b && dout && dx && dyup, "abf_fuse_bwd: null pointer");
+  CLSKD_CHECK_ARG((x_scale == nullptr) == (x_shift == nullptr), "abf_fuse_bwd: scale/shift pair");
+  const int64_t npix = (int64_t)B * F * T;
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(npix * 16, 256), 16384);
+  if (dtype == CLSKD_BF16)
+    hipLaunchKernelGGL(abf_fuse_bwd_kernel<__bf16>, dim3(grid), dim3(256), 0, as_stream(stream),
+                       (const __bf16*)x1, (const __bf16*)res, B, F, T, Fr, Tr, w, b, x_scale,
+                       x_shift, dout, dx, dyup);
+  else
+    hipLaunchKernelGGL(abf_fuse_bwd_kernel<float>, dim3(grid), dim3(256), 0, as_stream(stream),
+                       (const float*)x1, (const float*)res, B, F, T, Fr, Tr, w, b, x_scale,
+                       x_shift, dout, dx, dyup);
+  CLSKD_LAUNCH_CHECK("abf_fuse_bwd");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_nearest_down_sum(const float* g, int32_t B, int32_t F, int32_t T, int32_t Fr,
+                                      int32_t Tr, int32_t C, float* out, int32_t accumulate,
+                                      void* stream) {
+  CLSKD_CHECK_ARG(g && out, "nearest_down_sum: null pointer");
+  CLSKD_CHECK_SHAPE(C % 4 == 0 && F >= Fr && T >= Tr, "nearest_down_sum: shape");
+  const int64_t total = (int64_t)B * Fr * Tr * (C / 4);
+  hipLaunchKernelGGL(nearest_down_sum_kernel, dim3(grid_of(total)), dim3(256), 0, as_stream(stream),
+                     g, B, F, T, Fr, Tr, C, out, accumulate);
+  CLSKD_LAUNCH_CHECK("nearest_down_sum");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_mask_e_bwd(const float* spec, int32_t ldspec, const float* mask, int32_t Tm,
+                                int32_t B, int32_t T, const float* dest, int32_t ldest,
+                                float* dmask, void* stream) {
+  CLSKD_CHECK_ARG(spec && mask && dest && dmask, "mask_e_bwd: null pointer");
+  CLSKD_CHECK_SHAPE(Tm >= T + 1, "mask_e_bwd: Tm=%d < T+1", Tm);
+  const int64_t total = (int64_t)B * 256 * Tm;
+  hipLaunchKernelGGL(mask_e_bwd_kernel, dim3(grid_of(total)), dim3(256), 0, as_stream(stream), spec,
+                     ldspec, mask, Tm, B, T, dest, ldest, dmask);
+  CLSKD_LAUNCH_CHECK("mask_e_bwd");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_ola_bwd(const float* frames, const float* window, const float* dwav, int32_t B,
+                             int32_t T, int32_t win, int32_t hop, int32_t out_len, int32_t trim,
+                             int32_t clamp, float* dframes, void* stream) {
+  CLSKD_CHECK_ARG(frames && window && dwav && dframes, "ola_bwd: null pointer");
+  const int64_t total = (int64_t)B * T * win;
+  hipLaunchKernelGGL(ola_bwd_kernel, dim3(grid_of(total)), dim3(256), 0, as_stream(stream), frames,
+                     window, dwav, B, T, win, hop, out_len, trim, clamp, dframes);
+  CLSKD_LAUNCH_CHECK("ola_bwd");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_frame_pad_bwd(const float* dxp, int32_t B, int32_t L, int32_t pad, int32_t Lp,
+                                   int32_t mode, float* dx, int64_t ldx, int32_t accumulate,
+                                   void* stream) {
+  CLSKD_CHECK_ARG(dxp && dx, "frame_pad_bwd: null pointer");
+  CLSKD_CHECK_SHAPE(mode == 0 || (mode == 1 && pad < L), "frame_pad_bwd: reflect pad %d >= L %d", pad, L);
+  const int64_t total = (int64_t)B * L;
+  hipLaunchKernelGGL(frame_pad_bwd_kernel, dim3(grid_of(total)), dim3(256), 0, as_stream(stream), dxp,
+                     B, L, pad, Lp, mode, dx, ldx, accumulate);
+  CLSKD_LAUNCH_CHECK("frame_pad_bwd");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_stft_mag_loss_bwd(const float* X, const float* Y, int64_t rows, int32_t ld,
+                                       int32_t nbins, float scale, float* dX, void* stream) {
+  CLSKD_CHECK_ARG(X && Y && dX, "stft_mag_loss_bwd: null pointer");
+  CLSKD_CHECK_SHAPE(ld >= 2 * nbins, "stft_mag_loss_bwd: ld");
+  hipLaunchKernelGGL(stft_mag_loss_bwd_kernel, dim3(grid_of(rows * ld)), dim3(256), 0,
+                     as_stream(stream), X, Y, rows, ld, nbins, scale, dX);
+  CLSKD_LAUNCH_CHECK("stft_mag_loss_bwd");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_complex_combine_bwd(const float* dreal, const float* dimag, int32_t B,
+                                         int64_t n, float* dh, void* stream) {
+  CLSKD_CHECK_ARG(dreal && dimag && dh, "complex_combine_bwd: null pointer");
+  hipLaunchKernelGGL(complex_combine_bwd_kernel, dim3(grid_of((int64_t)B * n)), dim3(256), 0,
+                     as_stream(stream), dreal, dimag, B, n, dh);
+  CLSKD_LAUNCH_CHECK("complex_combine_bwd");
+  return CLSKD_OK;
+}

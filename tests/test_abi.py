@@ -35,10 +35,11 @@ def test_struct_layouts_match_header(tmp_path):
 #include <stddef.h>
 #include "clskd.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(clskd_seg), sizeof(clskd_ktab_entry),
-         sizeof(clskd_gram_job), offsetof(clskd_gram_job, shift), sizeof(clskd_draw_job),
-         offsetof(clskd_draw_job, stream_id), sizeof(clskd_conv_desc),
-         offsetof(clskd_conv_desc, tap_dt));
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(clskd_seg),
+         sizeof(clskd_ktab_entry), sizeof(clskd_gram_job), offsetof(clskd_gram_job, shift),
+         sizeof(clskd_draw_job), offsetof(clskd_draw_job, stream_id), sizeof(clskd_conv_desc),
+         offsetof(clskd_conv_desc, tap_dt), offsetof(clskd_conv_desc, accumulate),
+         sizeof(clskd_gram_bwd_job), offsetof(clskd_gram_bwd_job, accumulate));
   return 0;
 }
 """)
@@ -48,7 +49,9 @@ int main(void) {
                                           check=True).stdout.split()]
     want = [ctypes.sizeof(_lib.Seg), ctypes.sizeof(_lib.KtabEntry), ctypes.sizeof(_lib.GramJob),
             _lib.GramJob.shift.offset, ctypes.sizeof(_lib.DrawJob), _lib.DrawJob.stream_id.offset,
-            ctypes.sizeof(_lib.ConvDesc), _lib.ConvDesc.tap_dt.offset]
+            ctypes.sizeof(_lib.ConvDesc), _lib.ConvDesc.tap_dt.offset,
+            _lib.ConvDesc.accumulate.offset, ctypes.sizeof(_lib.GramBwdJob),
+            _lib.GramBwdJob.accumulate.offset]
     assert got == want
 
 

@@ -1,0 +1,243 @@
+"""GPU parity of the CLSKD training step's backward pass (config C3, SURVEY.md §8 f rank 1):
+the HIP gradients (clskd.backward) against the CPU oracle's autograd (oracle/ref_cpu.py, the
+fp32 PyTorch restatement of the reference pinned by tests/golden), plus the primitives
+(wgrad / accumulate conv, LSTM BPTT, Adam) against torch.
+
+Tolerance: relative L2 error ||g - g_ref|| / ||g_ref|| <= 2e-3 per parameter (fp32 on both
+sides, different summation orders; BatchNorm backward over small batches amplifies rounding).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from clskd import config as cfg
+from clskd.weights import ABF_SEED, STUDENT_SEED, TEACHER_SEED, apply_recipe
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+torch.set_num_threads(min(16, os.cpu_count() or 1))
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64).ravel()
+    b = np.asarray(b, np.float64).ravel()
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy()
+
+
+def test_conv_wgrad_and_accumulate_against_torch():
+    """wgrad through a forward descriptor (2 segments, 3x3, stride 2 in freq, N not a tile
+    multiple) and an accumulating data-gradient launch, against torch autograd."""
+    from clskd import ops
+    g = torch.Generator().manual_seed(1)
+    B, F, T, C1, C2, N = 2, 10, 23, 8, 4, 40
+    a = torch.randn(B, F, T, C1, generator=g)
+    b = torch.randn(B, F, T, C2, generator=g)
+    w = (torch.randn(N, C1 + C2, 3, 3, generator=g) * 0.1).requires_grad_()
+    bias = torch.randn(N, generator=g).requires_grad_()
+    x = torch.cat([a, b], 3).permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv2d(x, w, bias, stride=(2, 1), padding=1)
+    dy = torch.randn(ref.shape, generator=g)
+    ref.backward(dy)
+    Fo = ref.shape[2]
+    taps = [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)]
+    dyd = dy.permute(0, 2, 3, 1).contiguous().to(DEV)
+    segs = [ops.seg_bftc(a.to(DEV)), ops.seg_bftc(b.to(DEV))]
+    Kp = -(-9 * (C1 + C2) // 16) * 16
+    dw = torch.empty(N, Kp, device=DEV)
+    db = torch.empty(N, device=DEV)
+    ops.conv_wgrad(segs, taps, B, Fo, T, N, dyd, ops.OutMap(Fo * T * N, T * N, N), dw, db, stride_f=2)
+    got = dw[:, :9 * (C1 + C2)].reshape(N, 3, 3, C1 + C2).permute(0, 3, 1, 2)
+    assert _rel(_np(got), w.grad.numpy()) < 1e-5
+    assert _rel(_np(db), bias.grad.numpy()) < 1e-5
+    # accumulate: out = prior + conv
+    out = torch.randn(B, Fo, T, N, generator=g).to(DEV)
+    prior = out.clone()
+    wp = ops.pack_weight(w.detach().permute(0, 2, 3, 1).reshape(N, 9, C1 + C2).to(DEV), 9 * (C1 + C2))
+    ops.conv(segs, taps, B, Fo, T, N, wp, None, out, ops.OutMap(Fo * T * N, T * N, N),
+             stride_f=2, accumulate=True)
+    plain = torch.nn.functional.conv2d(x, w.detach(), None, stride=(2, 1), padding=1)
+    np.testing.assert_allclose(_np(out - prior), plain.permute(0, 2, 3, 1).numpy(), rtol=1e-5,
+                               atol=1e-5)
+
+
+@pytest.mark.parametrize("H", [32, 128])
+def test_lstm_bwd_against_torch(H):
+    """BPTT kernel: gate gradients for given dh, pre-activations rebuilt from the h history."""
+    from clskd import ops
+    g = torch.Generator().manual_seed(2)
+    nseq, T = 3, 57
+    lstm = torch.nn.LSTM(16, H)
+    for p in lstm.parameters():
+        torch.nn.init.uniform_(p, -0.3, 0.3, generator=g)
+    x = torch.randn(T, nseq, 16, generator=g)
+    out, _ = lstm(x)
+    dh = torch.randn(out.shape, generator=g)
+    whh_t = lstm.weight_hh_l0.detach()
+    gx = (x @ lstm.weight_ih_l0.t() + lstm.bias_ih_l0 + lstm.bias_hh_l0).detach().requires_grad_()
+    # full BPTT reference: d loss / d gx == d loss / d (gate pre-activations)
+    h = torch.zeros(nseq, H)
+    c = torch.zeros(nseq, H)
+    hs, pres = [], []
+    for t in range(T):
+        pre_t = gx[t] + h @ whh_t.t()
+        pres.append(pre_t.detach())
+        gi, gf, gg, go = pre_t.chunk(4, 1)
+        c = torch.sigmoid(gf) * c + torch.sigmoid(gi) * torch.tanh(gg)
+        h = torch.sigmoid(go) * torch.tanh(c)
+        hs.append(h)
+    (torch.stack(hs) * dh).sum().backward()
+    pre = torch.stack(pres)  # [T, nseq, 4H]
+    # HIP: layouts [ws=1][seq][T][4H]
+    pre_d = pre.permute(1, 0, 2).contiguous().to(DEV)
+    dh_d = dh.permute(1, 0, 2).contiguous().to(DEV)
+    whh = lstm.weight_hh_l0.detach().contiguous().to(DEV)
+    dg = torch.empty_like(pre_d)
+    st = (0, T * 4 * H, 4 * H)
+    ops.lstm_bwd(pre_d, st, dh_d, (0, T * H, H), whh, 1, nseq, T, H, dg, st)
+    ref = gx.grad.permute(1, 0, 2).numpy()
+    assert _rel(_np(dg), ref) < 1e-4
+
+
+def test_adam_kernel_matches_torch():
+    from clskd import ops
+    g = torch.Generator().manual_seed(3)
+    p0 = torch.randn(1000, generator=g)
+    ref = p0.clone().requires_grad_()
+    opt = torch.optim.Adam([ref], lr=6e-4, weight_decay=0.01)
+    p = p0.clone().to(DEV)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    for step in range(1, 4):
+        grad = torch.randn(1000, generator=g)
+        ref.grad = grad.clone()
+        opt.step()
+        ops.adam_step(p, grad.to(DEV), m, v, 6e-4, 0.9, 0.999, 1e-8, 0.01, step)
+    np.testing.assert_allclose(_np(p), ref.detach().numpy(), rtol=1e-6, atol=1e-7)
+
+
+# ------------------------------------------------------------------------------------------
+# the whole CLSKD step against the oracle's autograd
+# ------------------------------------------------------------------------------------------
+def _kd(precision="fp32"):
+    from clskd.distill import KnowledgeDistillation
+    from clskd.model import DCCRN
+    t = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.TEACHER), TEACHER_SEED)
+    s = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.STUDENT), STUDENT_SEED)
+    kd = KnowledgeDistillation(t.train(), s.train(), precision=precision).to(DEV)
+    apply_recipe(kd.review_encoder, ABF_SEED, "encoder.")
+    apply_recipe(kd.review_decoder, ABF_SEED, "decoder.")
+    return kd
+
+
+def _oracle_grads(noisy, clean):
+    from oracle import ref_cpu as R
+    from clskd.weights import recipe_state_dict
+    pt = R.to_torch_params(recipe_state_dict(cfg.dccrn_param_shapes(**cfg.TEACHER), TEACHER_SEED))
+    ps = R.to_torch_params(recipe_state_dict(cfg.dccrn_param_shapes(**cfg.STUDENT), STUDENT_SEED))
+    shapes = {**cfg.review_param_shapes("encoder"), **cfg.review_param_shapes("decoder")}
+    pa = R.to_torch_params(recipe_state_dict(shapes, ABF_SEED))
+    for k, v in ps.items():
+        if v.is_floating_point() and not k.endswith(("running_mean", "running_var")):
+            v.requires_grad_()
+    # the oracle's explicit LSTM restatement (R.lstm) is differentiable w.r.t. the weight dict
+    ref = R.clskd_step(pt, ps, pa, torch.from_numpy(noisy), torch.from_numpy(clean), lstm_fn=R.lstm)
+    taps = ref["s_taps"]
+    for t in list(taps["encoder"]) + list(taps["decoder"]) + [ref["student_wav"]]:
+        t.retain_grad()
+    ref["total"].backward()
+    return ps, ref
+
+
+def _compare(kd, ps, grads, tol):
+    """Relative L2 error per parameter.  Conv biases feeding a train-mode BatchNorm have an
+    analytically zero gradient (BN removes the per-channel mean); both sides then hold rounding
+    noise, so those are checked as ~0 against the layer's weight-gradient norm instead."""
+    bad, rows = [], []
+    for name, p in kd.student.named_parameters():
+        if name not in ps or ps[name].grad is None:
+            continue
+        got, ref = _np(grads[p]), ps[name].grad.numpy()
+        pre_bn = name.endswith("_conv.bias") and not name.startswith("decoder.5.")
+        if pre_bn:
+            wref = np.linalg.norm(ps[name.replace(".bias", ".weight")].grad.numpy())
+            e = max(np.linalg.norm(got), np.linalg.norm(ref)) / wref
+            rows.append(f"{name:40s} {e:.2e} (|g| / |dW|, analytically 0)")
+            ok = e <= 1e-3
+        else:
+            e = _rel(got, ref)
+            rows.append(f"{name:40s} {e:.2e}")
+            ok = e <= tol
+        if not ok:
+            bad.append(name)
+    return bad, "\n".join(rows)
+
+
+def test_clskd_backward_against_oracle():
+    """Every student parameter gradient of the CLSKD loss (MRSTFT base + 14 SPKD terms through
+    both ReviewKD fusions), plus the tap / waveform gradients, against the oracle's autograd."""
+    from clskd.data import synthetic_pairs
+    noisy, clean = synthetic_pairs(2, 8000, seed=21)
+    ps, ref = _oracle_grads(noisy, clean)
+    kd = _kd()
+    out = kd.forward_with_tape(torch.from_numpy(noisy).to(DEV), torch.from_numpy(clean).to(DEV))
+    assert abs(out["loss"].item() - ref["total"].item()) <= 1e-4 * abs(ref["total"].item())
+    grads = {p: torch.empty_like(p) for p in kd.student.parameters()}
+    from clskd.backward import clskd_backward
+    g = clskd_backward(out, kd.student, kd.review_encoder, kd.review_decoder, grads)
+    torch.cuda.synchronize()
+    taps = ref["s_taps"]
+    errs = {"wav": _rel(_np(g["wav"]), ref["student_wav"].grad.numpy())}
+    for i, t in enumerate(taps["encoder"]):
+        errs[f"enc{i}"] = _rel(_np(g["enc"][i].permute(0, 3, 1, 2)), t.grad.numpy())
+    for k in range(5):
+        errs[f"dec{k}"] = _rel(_np(g["dec"][k].permute(0, 3, 1, 2)), taps["decoder"][k + 1].grad.numpy())
+    bad, table = _compare(kd, ps, grads, 2e-3)
+    msg = "\n".join(f"{k:8s} {v:.2e}" for k, v in errs.items()) + "\n" + table
+    print(msg)
+    assert all(v <= 2e-3 for v in errs.values()), msg
+    assert not bad, f"parameters over tolerance: {bad}\n{msg}"
+
+
+def test_autograd_dropin_and_train_step():
+    """loss.backward() through KnowledgeDistillation.training_step gives the explicit backward's
+    gradients; FlatParams + FlatAdam step matches torch.optim.Adam on those gradients; the HIP
+    backward is bitwise repeatable."""
+    from clskd.data import synthetic_pairs
+    from clskd.train import FlatAdam, FlatParams
+    noisy, clean = synthetic_pairs(2, 8000, seed=22)
+    X, y = torch.from_numpy(noisy).to(DEV), torch.from_numpy(clean).to(DEV)
+    kd = _kd()
+    loss = kd.training_step((X, y), 0)
+    assert loss.requires_grad
+    loss.backward()
+    g_auto = {n: p.grad.clone() for n, p in kd.student.named_parameters()}
+    grads = {p: torch.empty_like(p) for p in kd.student.parameters()}
+    kd.backward_into(kd.forward_with_tape(X, y), grads)
+    grads2 = {p: torch.empty_like(p) for p in kd.student.parameters()}
+    kd.backward_into(kd.forward_with_tape(X, y), grads2)
+    for n, p in kd.student.named_parameters():
+        assert torch.equal(grads[p], grads2[p]), n
+        assert torch.equal(g_auto[n], grads[p]), n
+    # one Adam step through the flat buffers vs torch.optim.Adam on the same gradients
+    ref_params = {n: p.detach().clone().requires_grad_() for n, p in kd.student.named_parameters()}
+    for n, p in kd.student.named_parameters():
+        ref_params[n].grad = grads[p].clone()
+    torch.optim.Adam(list(ref_params.values()), lr=cfg.learning_rate).step()
+    kd.student.zero_grad(set_to_none=True)
+    flat = FlatParams(kd.student)
+    opt = FlatAdam(flat, lr=cfg.learning_rate)
+    for p in flat.params:
+        flat.gviews[p].copy_(grads[p])
+    opt.step()
+    for n, p in kd.student.named_parameters():
+        np.testing.assert_allclose(_np(p), _np(ref_params[n]), rtol=1e-6, atol=1e-7, err_msg=n)
+    # the packed-weight caches see the update: the next forward uses the new weights
+    l2 = kd.training_step((X, y), 0, return_parts=True)["loss"].item()
+    assert l2 != loss.item()

@@ -4,7 +4,7 @@ set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/q
 mkdir -p $O
-timeout -k 10 500 python -m pytest $R/tests -m gpu -x -q > $O/gt.log 2>&1
+timeout -k 10 500 python -u -m pytest $R/tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gt.log 2>&1
 timeout -k 10 200 python $R/bench.py --no-cpu-baseline > $O/b.log 2>&1
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/tr -o run -- python3 $R/bench.py --steps 4 --warmup 2 --no-cpu-baseline > $O/tr.log 2>&1
