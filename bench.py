@@ -30,6 +30,7 @@ import torch  # noqa: E402
 from clskd import config as cfg  # noqa: E402
 
 METRIC = "frames/sec/GPU DCCRN-CLSKD fwd+loss @16k 4s; SI-SNR parity ±0.01 dB"
+METRIC_TRAIN = "frames/sec/GPU DCCRN-CLSKD training step (fwd+loss+bwd+Adam) @16k 4s"
 PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (f32-in MFMA), dense
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
 B_PER_GPU = 16
@@ -94,6 +95,10 @@ def main():
                     help="replay the captured hipGraph of the step (clskd.graph.StepGraph) instead "
                          "of launching the three-stream schedule eagerly; ROCm's graph executor "
                          "does not keep the three streams concurrent, so eager is faster here")
+    ap.add_argument("--train", action="store_true",
+                    help="config C3: the full training step — fwd+loss, HIP backward into the flat "
+                         "student gradient, one RCCL all-reduce (N > 1), one Adam launch "
+                         "(KnowledgeDistillation.train_step); reported under its own metric")
     ap.add_argument("--precision", default="mixed", choices=["mixed", "fp32"],
                     help="mixed: teacher + ReviewKD GEMMs on bf16 MFMA operands (fp32 accumulate), "
                          "student fp32; fp32: every GEMM on exact-f32 MFMA")
@@ -118,7 +123,14 @@ def main():
         Ys.append(torch.from_numpy(clean).to(dev))
     T = cfg.n_frames(L)
 
-    if (not args.graph):
+    if args.train:
+        from clskd.train import FlatAdam, FlatParams
+        flat = FlatParams(kd.student)
+        opt = FlatAdam(flat, lr=cfg.learning_rate)
+
+        def step(i):
+            return kd.train_step((Xs[i % NBATCH], Ys[i % NBATCH]), flat, opt)
+    elif (not args.graph):
         def step(i):
             return kd.training_step((Xs[i % NBATCH], Ys[i % NBATCH]), i)
     else:
@@ -207,10 +219,15 @@ def main():
                                             tflops=round(v[2] / (v[1] * 1e-3) / 1e12, 1))
                                     for k, v in sorted(census.items(), key=lambda kv: -kv[1][1])}))
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not args.train:
             cpu = cpu_baseline(args.cpu_seconds)
+        workload = ("C2: DCCRN-CLSKD fwd+loss (teacher 3.67M + student 0.23M params, ReviewKD "
+                    "enc+dec, 14 SPKD Grams, MRSTFT)")
+        if args.train:
+            workload = ("C3: DCCRN-CLSKD training step = C2 fwd+loss + HIP backward to the 231,565 "
+                        "student parameters + flat-bucket RCCL all-reduce (N > 1) + Adam(lr 6e-4)")
         out = {
-            "metric": METRIC,
+            "metric": METRIC_TRAIN if args.train else METRIC,
             "value": round(frames / el, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -223,8 +240,7 @@ def main():
             "dtype": "bf16" if args.precision == "mixed" else "fp32",
             "data": "synthetic (seeded 16 kHz enveloped-sinusoid clean + noise at 0-10 dB SNR; "
                     "recipe weights, SURVEY.md §8 d)",
-            "config": {"workload": "C2: DCCRN-CLSKD fwd+loss (teacher 3.67M + student 0.23M "
-                                   "params, ReviewKD enc+dec, 14 SPKD Grams, MRSTFT)",
+            "config": {"workload": workload,
                        "global_batch": world * B_PER_GPU, "per_gpu_batch": B_PER_GPU,
                        "clip_samples": L, "frames_per_clip": T, "parallelism": f"dp{world}",
                        "abf_reinit": args.abf_reinit, "loss": round(loss_v, 6),

@@ -241,3 +241,27 @@ def test_autograd_dropin_and_train_step():
     # the packed-weight caches see the update: the next forward uses the new weights
     l2 = kd.training_step((X, y), 0, return_parts=True)["loss"].item()
     assert l2 != loss.item()
+
+
+def test_clskd_backward_mixed_precision_close_to_fp32():
+    """precision='mixed' (teacher + ReviewKD activations in bf16, the bench default): the
+    student's gradients stay close to the all-fp32 step's (the ReviewKD backward reads bf16
+    saved activations; gradients themselves are fp32)."""
+    from clskd.data import synthetic_pairs
+    noisy, clean = synthetic_pairs(2, 8000, seed=23)
+    X, y = torch.from_numpy(noisy).to(DEV), torch.from_numpy(clean).to(DEV)
+    res = {}
+    for prec in ("fp32", "mixed"):
+        kd = _kd(prec)
+        grads = {n: torch.empty_like(p) for n, p in kd.student.named_parameters()}
+        pg = {p: grads[n] for n, p in kd.student.named_parameters()}
+        kd.backward_into(kd.forward_with_tape(X, y), pg)
+        res[prec] = grads
+    worst = []
+    for n in res["fp32"]:
+        if n.endswith("_conv.bias") and not n.startswith("decoder.5."):
+            continue  # analytically zero (conv bias before train-mode BN)
+        worst.append((_rel(_np(res["mixed"][n]), _np(res["fp32"][n])), n))
+    worst.sort(reverse=True)
+    print(worst[:5])
+    assert worst[0][0] < 5e-2, worst[:5]
