@@ -424,6 +424,17 @@ int clskd_spkd_grad_ranges(const float* const* s_slabs, const int32_t* s_nslab,
                            int32_t B, int32_t batchmean, float scale, float* coef, void* stream);
 int clskd_gram_bwd(const clskd_gram_bwd_job* jobs, int32_t njobs, int32_t B, void* stream);
 
+/* SPKD gradient fused into the train-mode BatchNorm backward of a Gram'd map whose BN apply was
+ * folded into the Gram (ReviewKD outputs, framework.py:183-186 + 150-172): for raw[b][p][c]
+ * (batch stride sB elements, P positions x C channels, storage dtype), z = round(raw*scale +
+ * shift), dz = M z (coef = M [B][B] of clskd_spkd_grad_ranges); writes d raw (storage
+ * draw_dtype) and dgamma / dbeta without materialising dz.  work: clskd_bn_bwd_workspace(nblk,
+ * C) doubles, nblk = clskd_bn_bwd_blocks(B*P, C). */
+int clskd_spkd_bn_bwd(const void* raw, int32_t dtype, int64_t sB, int64_t P, int32_t C, int32_t B,
+                      const float* scale, const float* shift, const float* coef, const float* mean,
+                      const float* var, float eps, const float* gamma, double* work, int32_t nblk,
+                      float* dgamma, float* dbeta, void* draw, int32_t draw_dtype, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

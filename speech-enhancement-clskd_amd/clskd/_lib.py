@@ -125,6 +125,8 @@ SIGNATURES = {
                                       C.POINTER(C.c_void_p), C.POINTER(C.c_int32), _i32, _i32,
                                       _i32, _f32, _p, _p]),
     "clskd_gram_bwd": (_i32, [_p, _i32, _i32, _p]),
+    "clskd_spkd_bn_bwd": (_i32, [_p, _i32, _i64, _i64, _i32, _i32, _p, _p, _p, _p, _p, _f32, _p, _p,
+                                 _i32, _p, _p, _p, _i32, _p]),
 }
 
 

@@ -147,12 +147,15 @@ def _dec_pack_fn(taps_kf):
     return fn
 
 
-def dccrn_backward(m, tape, enc, dec, dec_in, lstm_io, g, pg, acc_params=False):
+def dccrn_backward(m, tape, enc, dec, dec_in, lstm_io, g, pg, acc_params=False, join=None):
     """Reverse of DCCRN.run for a student `m` (fp32 activations).
     tape: the forward tape; enc/dec/dec_in/lstm_io: the forward's activations.
     g: upstream gradient buffers (fp32): g['wav'] [B][L] or None; g['enc'][i] like enc[i];
        g['dec'][k] (k < 5) like dec[k]; g['dec_in'] like dec_in.  Consumed (accumulated into).
-    pg: dict parameter -> fp32 gradient tensor (contiguous, same shape) receiving the gradients."""
+    pg: dict parameter -> fp32 gradient tensor (contiguous, same shape) receiving the gradients.
+    join(): called before the first accumulation into g['enc'] / g['dec'] / g['dec_in'] (after
+    the waveform tail and the last decoder layer's weight gradient), so a caller can produce
+    those buffers' first contributions on other streams meanwhile."""
     from .model import DCCRN
     B, T = tape["B"], tape["T"]
     dev = tape["spec"].device
@@ -189,6 +192,9 @@ def dccrn_backward(m, tape, enc, dec, dec_in, lstm_io, g, pg, acc_params=False):
         # gradient w.r.t. the raw (pre-BN) transposed-conv output
         if d == nl - 1:
             if dmask is None:
+                if join is not None:
+                    join()
+                    join = None
                 continue  # no waveform gradient: the last layer is dead for the loss
             draw = dmask
         else:
@@ -211,6 +217,9 @@ def dccrn_backward(m, tape, enc, dec, dec_in, lstm_io, g, pg, acc_params=False):
                            OutMap(2 * F * (T + 1) * Co, (T + 1) * Co, Co, of_mul=2, of_add=p), dw,
                            dbias, accumulate=False, accumulate_bias=p == 1)
         _dec_scatter(m, d, dwcat, Kps, dbias, pg, acc_params)
+        if join is not None:
+            join()
+            join = None
         # data gradients: one stride-2 gather over the raw-output gradient, per destination
         dseg = Seg(draw, 0, SegGeom(Co, 2 * F * (T + 1) * Co, (T + 1) * Co, Co, 2 * F, T + 1))
         taps_b = [(p - 2 * dF, kt) for p in (0, 1) for _, dF in DCCRN._DEC_TAPS[p] for kt in (0, 1)]
@@ -404,12 +413,17 @@ def _dec_scatter(m, d, dwcat, Kps, dbias, pg, acc):
 # ------------------------------------------------------------------------------------------
 # ReviewKD (framework.py:176-263), reverse — ABF weights are not trained (new modules per step)
 # ------------------------------------------------------------------------------------------
-def review_backward(review, tape, d_outs, d_feats, acc_feats):
-    """tape: ReviewKD.forward_bftc's per-level tapes (processing order); d_outs[j]: fp32 gradient
-    of level j's output (after its conv2 BatchNorm); d_feats[j]: student-feature gradient buffer
-    of level j, accumulated into when acc_feats[j]."""
+def review_backward(review, tape, coef_m, d_feats, acc_feats):
+    """tape: ReviewKD.forward_bftc's per-level tapes (processing order); coef_m[j]: the SPKD
+    gradient coefficients M = dG + dG^T [B][B] of level j's output Gram; d_feats[j]: student-
+    feature gradient buffer of level j, accumulated into when acc_feats[j].
+
+    The SPKD gradient dz = M z of each output is fused into its conv2 BatchNorm backward
+    (clskd_spkd_bn_bwd: dz never reaches HBM).  When the fusions ran in bf16 (precision='mixed')
+    the raw-output gradient is stored bf16 and the conv2 data gradient — the heaviest GEMM of
+    the backward — runs on the bf16 MFMA engine like its forward; fp32 otherwise."""
     n = len(tape)
-    d_res = None  # gradient w.r.t. level j's fused map, from level j+1's residual path
+    dyup_next = None  # level j+1's gradient w.r.t. its upsampled residual (= level j's fused map)
     for j in range(n - 1, -1, -1):
         tp = tape[j]
         abf = review.abfs[j]
@@ -418,17 +432,19 @@ def review_backward(review, tape, d_outs, d_feats, acc_feats):
         Bn, Fn, Tn, Cout = out_raw.shape
         mid = tp["x1"].shape[-1]
         bn2 = abf.conv2[1]
-        c2 = tp["coef2"]
-        d_oraw = _empty(out_raw.shape, dev)
-        ops.bn_bwd(out_raw, d_outs[j], c2[:Cout], c2[Cout:], tp["mv2"][0], tp["mv2"][1], bn2.eps,
-                   bn2.weight, None, d_oraw)
-        d_xf = d_res if d_res is not None else _empty((Bn, Fn, Tn, mid), dev)
+        lowp = out_raw.dtype == torch.bfloat16
+        d_oraw = torch.empty(out_raw.shape, device=dev, dtype=out_raw.dtype if lowp else f32)
+        ops.spkd_bn_bwd(out_raw, tp["coef2"], coef_m[j], tp["mv2"][0], tp["mv2"][1], bn2.eps,
+                        bn2.weight, d_oraw)
+        d_xf = _empty((Bn, Fn, Tn, mid), dev)
         w2 = abf.conv2[0].weight
-        w2t = _tw(("abf2_t", id(abf)), w2, lambda: ops.pack_weight(
-            w2.permute(1, 2, 3, 0).reshape(mid, 9, Cout).contiguous().float(), 9 * Cout))
+        w2t = _tw(("abf2_t", id(abf), lowp), w2, lambda: ops.pack_weight(
+            w2.permute(1, 2, 3, 0).reshape(mid, 9, Cout).contiguous().float(), 9 * Cout,
+            "bf16" if lowp else "fp32"))
         ops.conv([seg_bftc(d_oraw)], [(1 - kf, 1 - kt) for kf in range(3) for kt in range(3)], Bn, Fn,
-                 Tn, mid, w2t, None, d_xf, OutMap(Fn * Tn * mid, Tn * mid, mid),
-                 accumulate=d_res is not None)
+                 Tn, mid, w2t, None, d_xf, OutMap(Fn * Tn * mid, Tn * mid, mid))
+        if dyup_next is not None:  # residual path of level j+1 (nearest upsampling, folded back)
+            ops.nearest_down_sum(dyup_next, d_xf, accumulate=True)
         c1 = tp["coef1"]
         if abf.att_conv is not None:
             dxn = _empty(d_xf.shape, dev)
@@ -436,11 +452,10 @@ def review_backward(review, tape, d_outs, d_feats, acc_feats):
             aw = abf.att_conv[0].weight.reshape(2, -1).float().contiguous()
             ab = abf.att_conv[0].bias.float().contiguous()
             ops.abf_fuse_bwd(tp["x1"], tp["res"], aw, ab, c1, d_xf, dxn, dyup)
-            d_res = _empty(tp["res"].shape, dev)
-            ops.nearest_down_sum(dyup, d_res)
+            dyup_next = dyup
         else:
             dxn = d_xf
-            d_res = None
+            dyup_next = None
         bn1 = abf.conv1[1]
         d_x1 = _empty(tp["x1"].shape, dev)
         ops.bn_bwd(tp["x1"], dxn, c1[:mid], c1[mid:], tp["mv1"][0], tp["mv1"][1], bn1.eps,
@@ -507,27 +522,36 @@ def clskd_backward(res, student, review_encoder, review_decoder, pg, acc_params=
     g_enc, g_dec, g_t = res["gram_slabs"]
     s_refs = g_enc.refs + g_dec.refs
     M = ops.spkd_grad(s_refs, g_t.refs, B, True, upstream, device=dev)
-    s_enc, s_dec = res["s_enc_list"], res["s_dec_list"]
-    d_senc = [_empty(x.shape, dev) for x in s_enc]
-    d_sdec = [_empty(x.shape, dev) for x in s_dec]
-    items = []
-    for i, (x, dx) in enumerate(list(zip(s_enc, d_senc)) + list(zip(s_dec, d_sdec))):
-        _, Fn, Tn, Cn = x.shape
-        items.append((_gram_view_bftc(x), M[i], dx, Fn * Tn * Cn, Cn, 0, False))
+    n_enc = len(res["s_enc_list"])
     _, D4, T, C6 = dec_in.shape
     Ch = C6 // 2
-    for h in range(2):  # clstm real / imag taps = the two channel halves of dec_in
-        items.append((_gram_view_bftc(dec_in, h * Ch, Ch), M[12 + h], g["dec_in"], D4 * T * C6, C6,
-                      h * Ch, False))
-    ops.gram_bwd(items, B)
-    # ReviewKD: decoder levels in feature order; encoder levels process the reversed taps and
-    # insert results at the front (framework.py:245-261)
-    review_backward(review_decoder, tp["rd"], d_sdec, [g["dec_in"]] + g["dec"],
-                    [True] + [False] * 5)
+    # clstm real / imag taps = the two channel halves of dec_in (fp32, no BN): dz = M z directly
+    ops.gram_bwd([(_gram_view_bftc(dec_in, h * Ch, Ch), M[2 * n_enc + h], g["dec_in"], D4 * T * C6,
+                   C6, h * Ch, False) for h in range(2)], B)
+    # Three independent branches on three streams, joined before the student's first accumulation
+    # into the tap gradients: ReviewKD-decoder backward | ReviewKD-encoder backward (their
+    # SPKD gradients fused into the output BN backward) | the waveform tail on the calling
+    # stream (MRSTFT log-magnitude -> OLA -> iSTFT -> mask -> last decoder layer's wgrad).
+    # ReviewKD decoder levels follow the feature order; encoder levels process the reversed
+    # taps and insert results at the front (framework.py:245-261).
+    from .distill import _side_stream
+    main = torch.cuda.current_stream(dev)
+    s_dec, s_enc = _side_stream(dev, 0), _side_stream(dev, 1)
     n = len(enc)
-    review_backward(review_encoder, tp["re"], [d_senc[n - 1 - j] for j in range(n)],
-                    [g["enc"][n - 1 - j] for j in range(n)], [False] * n)
+    for st in (s_dec, s_enc):
+        st.wait_stream(main)
+    with torch.cuda.stream(s_dec):
+        review_backward(review_decoder, tp["rd"], [M[n_enc + j] for j in range(n_enc)],
+                        [g["dec_in"]] + g["dec"], [True] + [False] * 5)
+    with torch.cuda.stream(s_enc):
+        review_backward(review_encoder, tp["re"], [M[n - 1 - j] for j in range(n)],
+                        [g["enc"][n - 1 - j] for j in range(n)], [False] * n)
     # MRSTFT log-magnitude base loss (distill.py:100-101) -> d student waveform
     mrstft_backward(tp["ms"], g["wav"], upstream)
-    dccrn_backward(student, tp["s"], enc, dec, dec_in, sf["lstm_io"], g, pg, acc_params)
+
+    def join():
+        main.wait_stream(s_dec)
+        main.wait_stream(s_enc)
+
+    dccrn_backward(student, tp["s"], enc, dec, dec_in, sf["lstm_io"], g, pg, acc_params, join=join)
     return g

@@ -798,6 +798,25 @@ def gram_bwd(items, B):
     check(lib().clskd_gram_bwd(jobs, len(items), B, _stream()), "gram_bwd")
 
 
+def spkd_bn_bwd(raw, coef_bn, coef_m, mean, var, eps, gamma, draw, dgamma=None, dbeta=None):
+    """SPKD gradient (dz = M z, z = the deferred-BN Gram input) fused into the BN backward of a
+    BFTC map raw [B][F][T][C] (clskd_spkd_bn_bwd); writes draw (fp32 or bf16)."""
+    L = lib()
+    B = raw.shape[0]
+    Cn = raw.shape[-1]
+    P = raw.numel() // (B * Cn)
+    # a reduce thread covers one (position, 4 channels) over all B samples: size the grid by
+    # positions x channel quads, not by B*P rows
+    nblk = int(L.clskd_bn_bwd_blocks(P * Cn // 2, Cn))
+    work = torch.empty(int(L.clskd_bn_bwd_workspace(nblk, Cn)), dtype=torch.float64,
+                       device=raw.device)
+    sc = coef_bn.data_ptr()
+    check(L.clskd_spkd_bn_bwd(ptr(raw), _dt(raw), P * Cn, P, Cn, B, sc, sc + 4 * Cn, ptr(coef_m),
+                              ptr(mean), ptr(var), eps, ptr(gamma), ptr(work), nblk, ptr(dgamma),
+                              ptr(dbeta), ptr(draw), _dt(draw), _stream()), "spkd_bn_bwd")
+    return draw
+
+
 def index_gather(src, idx, sgn, out, accumulate=False):
     """out[i] (+)= sum_j sgn[i, j] * src.flat[idx[i, j]] (idx < 0 skipped)."""
     n, J = idx.shape

@@ -36,8 +36,8 @@ struct WgradArgs {
 template <bool VEC4>
 __global__ __launch_bounds__(256) void conv_wgrad_f32(const WgradArgs a) {
   const clskd_conv_desc& d = a.d;
-  __shared__ __attribute__((aligned(16))) float As[WG_RB][WG_TK + 4];
-  __shared__ __attribute__((aligned(16))) float Ds[WG_RB][WG_TN + 4];
+  __shared__ __attribute__((aligned(16))) float As[2][WG_RB][WG_TK + 4];
+  __shared__ __attribute__((aligned(16))) float Ds[2][WG_RB][WG_TN + 4];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -54,10 +54,21 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32(const WgradArgs a) {
   const int lr = tid >> 3;
   const int q0 = tid & 7;
   const int nsub = wave & 1, ksub = wave >> 1;
-  f32x16 acc = {};
-  float bacc = 0.f;  // dbias partial of column n0 + tid (tid < 64, k-tile 0 only)
+  // K-table entries of this thread's two 4-k quads are loop invariant
+  clskd_ktab_entry ke[2][4];
+  int ks_[2][4];
+#pragma unroll
+  for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = min(k0 + (q0 + 8 * qq) * 4 + j, d.K - 1);
+      ke[qq][j] = d.ktab[k];
+      ks_[qq][j] = d.kseg[k];
+      if (k0 + (q0 + 8 * qq) * 4 + j >= d.K) ke[qq][j].dF = -32768;
+    }
 
-  for (int64_t rs = r_begin; rs < r_end; rs += WG_RB) {
+  // one 32-row stage into registers: gathered A (2 x 4 k) and dY (2 x 4 n) of row rs + lr
+  auto load_stage = [&](int64_t rs, f32x4 (&av)[2], f32x4 (&dv)[2]) {
     const int64_t m = rs + lr;
     const bool valid = m < r_end;
     int64_t b = 0, fo = 0, to = 0;
@@ -67,41 +78,30 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32(const WgradArgs a) {
       fo = r / d.To;
       to = r - fo * d.To;
     }
-    // ---- gathered A: 16 consecutive k per thread as 2 x 4-k quads of the 64-k tile ----
 #pragma unroll
     for (int qq = 0; qq < 2; ++qq) {
-      const int kl = (q0 + 8 * qq) * 4;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (valid) {
         if constexpr (VEC4) {
-          const int k = k0 + kl;
-          if (k < d.K) {
-            const clskd_ktab_entry e = d.ktab[k];
-            const int s = d.kseg[k];
-            const clskd_seg& g = d.seg[s];
-            const int64_t fi = fo * d.stride_f + e.dF, ti = to * d.stride_t + e.dT;
-            if (fi >= 0 && fi < g.F && ti >= 0 && ti < g.T)
-              v = *reinterpret_cast<const f32x4*>(g.ptr + b * g.sB + fo * d.stride_f * g.sF +
-                                                  to * d.stride_t * g.sT + e.off);
-          }
+          const clskd_ktab_entry e = ke[qq][0];
+          const clskd_seg& g = d.seg[ks_[qq][0]];
+          const int64_t fi = fo * d.stride_f + e.dF, ti = to * d.stride_t + e.dT;
+          if (fi >= 0 && fi < g.F && ti >= 0 && ti < g.T)
+            v = *reinterpret_cast<const f32x4*>(g.ptr + b * g.sB + fo * d.stride_f * g.sF +
+                                                to * d.stride_t * g.sT + e.off);
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int k = k0 + kl + j;
-            if (k < d.K) {
-              const clskd_ktab_entry e = d.ktab[k];
-              const int s = d.kseg[k];
-              const clskd_seg& g = d.seg[s];
-              const int64_t fi = fo * d.stride_f + e.dF, ti = to * d.stride_t + e.dT;
-              if (fi >= 0 && fi < g.F && ti >= 0 && ti < g.T)
-                v[j] = g.ptr[b * g.sB + fo * d.stride_f * g.sF + to * d.stride_t * g.sT + e.off];
-            }
+            const clskd_ktab_entry e = ke[qq][j];
+            const clskd_seg& g = d.seg[ks_[qq][j]];
+            const int64_t fi = fo * d.stride_f + e.dF, ti = to * d.stride_t + e.dT;
+            if (fi >= 0 && fi < g.F && ti >= 0 && ti < g.T)
+              v[j] = g.ptr[b * g.sB + fo * d.stride_f * g.sF + to * d.stride_t * g.sT + e.off];
           }
         }
       }
-      *reinterpret_cast<f32x4*>(&As[lr][kl]) = v;
+      av[qq] = v;
     }
-    // ---- dY through the forward's output map ----
     const int64_t orow = b * d.oB + (fo * d.of_mul + d.of_add) * d.oF + to * d.oT;
 #pragma unroll
     for (int qq = 0; qq < 2; ++qq) {
@@ -118,22 +118,35 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32(const WgradArgs a) {
           }
         }
       }
-      *reinterpret_cast<f32x4*>(&Ds[lr][nl]) = v;
+      dv[qq] = v;
+    }
+  };
+
+  f32x16 acc = {};
+  float bacc = 0.f;  // dbias partial of column n0 + tid (tid < 64, k-tile 0 only)
+  f32x4 av[2], dv[2];
+  if (r_begin < r_end) load_stage(r_begin, av, dv);
+  int buf = 0;
+  for (int64_t rs = r_begin; rs < r_end; rs += WG_RB, buf ^= 1) {
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      *reinterpret_cast<f32x4*>(&As[buf][lr][(q0 + 8 * qq) * 4]) = av[qq];
+      *reinterpret_cast<f32x4*>(&Ds[buf][lr][(q0 + 8 * qq) * 4]) = dv[qq];
     }
     __syncthreads();
+    if (rs + WG_RB < r_end) load_stage(rs + WG_RB, av, dv);  // in flight under the MFMAs
     // ---- 16 MFMAs (2 rows each) per wave: C[n][k] += dY^T[n][r] A[r][k] ----
     const int cl = lane & 31, rh = lane >> 5;
 #pragma unroll
     for (int s = 0; s < WG_RB / 2; ++s) {
-      const float av = Ds[2 * s + rh][nsub * 32 + cl];
-      const float bv = As[2 * s + rh][ksub * 32 + cl];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+      const float x = Ds[buf][2 * s + rh][nsub * 32 + cl];
+      const float y = As[buf][2 * s + rh][ksub * 32 + cl];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x, y, acc, 0, 0, 0);
     }
     if (a.want_bias && blockIdx.z == 0 && tid < WG_TN) {
 #pragma unroll 8
-      for (int r = 0; r < WG_RB; ++r) bacc += Ds[r][tid];
+      for (int r = 0; r < WG_RB; ++r) bacc += Ds[buf][r][tid];
     }
-    __syncthreads();
   }
   // ---- partial tile out: work[split][n][k] ----
   const int Kp = d.K;
@@ -148,16 +161,20 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32(const WgradArgs a) {
     a.work[(int64_t)a.S * d.N * Kp + (int64_t)split * d.N + n0 + tid] = bacc;
 }
 
-// dw[i] (+)= sum_s work[s][i] in split order; i < total (N*Kp, then N bias entries)
+// dw[i] (+)= sum_s work[s][i]: 32 elements x 8 lanes per block; lane l sums splits l, l+8, ...
+// then a fixed xor tree over the 8 lanes (deterministic for a given S)
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ work, int S,
                                                           int64_t per, float* __restrict__ dw,
                                                           int accumulate) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < per;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int j = 0; j < S; ++j) s += work[(int64_t)j * per + i];
-    dw[i] = accumulate ? dw[i] + s : s;
-  }
+  const int l = threadIdx.x & 7;
+  const int64_t i = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+  float s = 0.f;
+  if (i < per)
+    for (int j = l; j < S; j += 8) s += work[(int64_t)j * per + i];
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 4, 64);
+  if (l == 0 && i < per) dw[i] = accumulate ? dw[i] + s : s;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -225,8 +242,8 @@ inline unsigned grid_for(int64_t n) { return (unsigned)std::min<int64_t>(cdiv(n,
 inline void wgrad_plan(const clskd_conv_desc& d, int& S, int64_t& rps) {
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
   const int64_t tiles = cdiv(d.N, WG_TN) * cdiv(d.K, WG_TK);
-  int64_t s = cdiv(2048, tiles);
-  s = std::max<int64_t>(1, std::min<int64_t>(s, cdiv(M, 256)));
+  int64_t s = cdiv(4096, tiles);
+  s = std::max<int64_t>(1, std::min<int64_t>({s, (int64_t)1024, cdiv(M, 256)}));
   rps = cdiv(cdiv(M, s), WG_RB) * WG_RB;
   S = (int)cdiv(M, rps);
 }
@@ -272,10 +289,10 @@ extern "C" int clskd_conv2d_wgrad(const clskd_conv_desc* dp, const float* dy, fl
     hipLaunchKernelGGL((conv_wgrad_f32<false>), grid, dim3(256), 0, st, a);
   CLSKD_LAUNCH_CHECK("conv2d_wgrad");
   const int64_t per = (int64_t)d.N * d.K;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(per)), dim3(256), 0, st, work, S, per, dw,
-                     accumulate & 1);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(per, 32)), dim3(256), 0, st, work, S,
+                     per, dw, accumulate & 1);
   if (dbias)
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(d.N)), dim3(256), 0, st,
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(d.N, 32)), dim3(256), 0, st,
                        work + (int64_t)S * per, S, (int64_t)d.N, dbias, (accumulate >> 1) & 1);
   CLSKD_LAUNCH_CHECK("conv2d_wgrad_reduce");
   return CLSKD_OK;

@@ -501,9 +501,7 @@ __global__ __launch_bounds__(256) void gram_bwd_kernel(const GramBwdJobsArg a, i
   for (int k = 1; k < a.n; ++k)
     if ((int)blockIdx.x >= a.blk0[k]) q = k;
   const clskd_gram_bwd_job& j = a.j[q];
-  __shared__ float Ms[BMAX * BMAX];
-  for (int i = threadIdx.x; i < B * B; i += 256) Ms[i] = j.coef[i];
-  __syncthreads();
+  const float* __restrict__ Ms = j.coef;  // uniform reads: scalar loads, no LDS staging
   const int CQ = j.Cs / 4;
   const int64_t nq = j.P * CQ;
   const int64_t qi = (int64_t)(blockIdx.x - a.blk0[q]) * 256 + threadIdx.x;

@@ -197,7 +197,8 @@ __global__ __launch_bounds__(NKS * H) void lstm_bwd_kernel(
   const int ks = tid % NKS;
   const int ws = blockIdx.y;
   const int seq = blockIdx.x;
-  __shared__ float das[2][G];
+  static_assert(NKS == 8 && GW % 4 == 0, "lstm_bwd: 8 k-slices of whole float4s");
+  __shared__ __attribute__((aligned(16))) float das[2][G];
   // column u of W_hh restricted to gate rows [ks*GW, (ks+1)*GW)
   float wc[GW];
 #pragma unroll
@@ -223,38 +224,65 @@ __global__ __launch_bounds__(NKS * H) void lstm_bwd_kernel(
       cp[(int64_t)t * H] = c;
     }
   }
+  // phase 1 wrote cbuf from lanes ks == 0 and phase 2 reads it from the same lanes: no barrier.
+  // Phase 2 keeps every global load off the serial chain: step t-1's operands (gate
+  // pre-activations, c_{t-1}, c_{t-2}, dh) are loaded right after step t's gate gradients, so
+  // they are in flight during the barrier and the W_hh^T reduction.
   float dc = 0.f, dhr = 0.f;
+  float q0 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f, cc = 0.f, cpv = 0.f, dhin = 0.f;
+  auto fetch = [&](int t) {
+    const float* q = pp + (int64_t)t * p_t;
+    q0 = q[0];
+    q1 = q[H];
+    q2 = q[2 * H];
+    q3 = q[3 * H];
+    cc = cp[(int64_t)t * H];
+    cpv = t > 0 ? cp[(int64_t)(t - 1) * H] : 0.f;
+    dhin = dp[(int64_t)t * d_t];
+  };
+  if (ks == 0) fetch(T - 1);
   for (int t = T - 1; t >= 0; --t) {
     const int buf = t & 1;
     if (ks == 0) {
-      float ig, fg, gg, og;
-      acts(t, ig, fg, gg, og);
-      const float ct = cp[(int64_t)t * H];
-      const float cprev = t > 0 ? cp[(int64_t)(t - 1) * H] : 0.f;
+      const float ig = sigm_fast(q0), fg = sigm_fast(q1);
+      const float gg = fmaf(2.f, sigm_fast(2.f * q2), -1.f), og = sigm_fast(q3);
+      const float ct = cc, cprev = cpv;
       const float tc = tanh_fast(ct);
-      const float dht = dp[(int64_t)t * d_t] + dhr;
+      const float dht = dhin + dhr;
       dc = fmaf(dht * og, 1.f - tc * tc, dc);
       const float a_i = dc * gg * ig * (1.f - ig);
       const float a_f = dc * cprev * fg * (1.f - fg);
       const float a_g = dc * ig * (1.f - gg * gg);
       const float a_o = dht * tc * og * (1.f - og);
       dc *= fg;
+      das[buf][u] = a_i;
+      das[buf][H + u] = a_f;
+      das[buf][2 * H + u] = a_g;
+      das[buf][3 * H + u] = a_o;
       float* o = gp + (int64_t)t * g_t;
       o[0] = a_i;
       o[H] = a_f;
       o[2 * H] = a_g;
       o[3 * H] = a_o;
-      das[buf][u] = a_i;
-      das[buf][H + u] = a_f;
-      das[buf][2 * H + u] = a_g;
-      das[buf][3 * H + u] = a_o;
+      if (t > 0) fetch(t - 1);
     }
-    __syncthreads();
-    float s = 0.f;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS-only barrier (loads stay in flight)
+    __builtin_amdgcn_s_barrier();
+    float s0 = 0.f, s1 = 0.f;
+    const f32x4* dv = reinterpret_cast<const f32x4*>(&das[buf][ks * GW]);
 #pragma unroll
-    for (int j = 0; j < GW; ++j) s = fmaf(wc[j], das[buf][ks * GW + j], s);
-#pragma unroll
-    for (int o = 1; o < NKS; o <<= 1) s += __shfl_xor(s, o, 64);
+    for (int j = 0; j < GW / 4; ++j) {  // ds_read_b128: 4 LDS reads per 16 gate rows
+      const f32x4 v = dv[j];
+      s0 = fmaf(wc[4 * j], v[0], s0);
+      s1 = fmaf(wc[4 * j + 1], v[1], s1);
+      s0 = fmaf(wc[4 * j + 2], v[2], s0);
+      s1 = fmaf(wc[4 * j + 3], v[3], s1);
+    }
+    float s = s0 + s1;
+    // NKS = 8 slices of a unit are 8 adjacent lanes: DPP xor1, xor2, half-row mirror
+    s += dpp<DPP_XOR1>(s);
+    s += dpp<DPP_XOR2>(s);
+    s += dpp<DPP_HALF_MIRROR>(s);
     dhr = s;
   }
 }

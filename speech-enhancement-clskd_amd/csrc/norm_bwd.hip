@@ -463,6 +463,147 @@ __global__ void complex_combine_bwd_kernel(const float* __restrict__ dre, const 
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// SPKD gradient fused into the BatchNorm backward of a ReviewKD output (framework.py:150-172 +
+// the ABF conv2 BatchNorm, framework.py:183-186).  The Gram read z_b = round(raw_b*scale + shift)
+// (the deferred BN); its gradient dz_b = sum_j M[b][j] z_j is never stored: the reduce pass
+// forms the BN statistics sums of dz from it and the apply pass recomputes it to write
+// d raw = k1*dz + k2*raw + k3.  One thread = (position, 4 channels) over all B samples.
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ f32x4 z_of(const T* p, const f32x4& sc, const f32x4& sh) {
+  f32x4 v = ld4<T>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float z = fmaf(v[i], sc[i], sh[i]);
+    v[i] = sizeof(T) == 2 ? (float)(__bf16)z : z;  // the Gram's rounding to the storage type
+  }
+  return v;
+}
+
+template <typename T, int BM>
+__global__ __launch_bounds__(256) void spkd_bn_bwd_reduce_kernel(
+    const T* __restrict__ raw, int64_t sB, int64_t P, int C, int B, int64_t ppb,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ Mc, const float* __restrict__ mean, const float* __restrict__ var,
+    float eps, double* __restrict__ partial) {
+  const int CG = C >> 2;
+  const int RP = 256 / CG;
+  const int tid = threadIdx.x;
+  const int cg = tid % CG;
+  const int rl = tid / CG;
+  // M [B][B] is read with uniform addresses: scalar loads into SGPRs feed the FMAs directly
+  f32x4 sc, sh, mu, rs;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = cg * 4 + j;
+    sc[j] = scale[c];
+    sh[j] = shift[c];
+    mu[j] = mean[c];
+    rs[j] = (float)(1.0 / sqrt((double)var[c] + (double)eps));
+  }
+  const int64_t p0 = (int64_t)blockIdx.x * ppb;
+  const int64_t p1 = min(P, p0 + ppb);
+  double sb[4] = {0, 0, 0, 0}, sg[4] = {0, 0, 0, 0};
+  if (rl < RP) {
+    for (int64_t p = p0 + rl; p < p1; p += RP) {
+      f32x4 z[BM];
+#pragma unroll
+      for (int b = 0; b < BM; ++b)
+        z[b] = b < B ? z_of<T>(raw + b * sB + p * C + cg * 4, sc, sh) : f32x4{0.f, 0.f, 0.f, 0.f};
+      float fb[4] = {0, 0, 0, 0}, fg[4] = {0, 0, 0, 0};
+      for (int b = 0; b < B; ++b) {
+        f32x4 dz = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < BM; ++k)
+          if (k < B) dz += Mc[b * B + k] * z[k];
+        const f32x4 x = ld4<T>(raw + b * sB + p * C + cg * 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          fb[j] += dz[j];
+          fg[j] = fmaf(dz[j], (x[j] - mu[j]) * rs[j], fg[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sb[j] += (double)fb[j];
+        sg[j] += (double)fg[j];
+      }
+    }
+  }
+  __shared__ double red[256][9];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    red[tid][j] = sb[j];
+    red[tid][4 + j] = sg[j];
+  }
+  __syncthreads();
+  if (tid < CG) {
+    double Bv[4] = {0, 0, 0, 0}, G[4] = {0, 0, 0, 0};
+    for (int l = 0; l < RP; ++l) {
+      const int t = l * CG + tid;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        Bv[j] += red[t][j];
+        G[j] += red[t][4 + j];
+      }
+    }
+    double* q = partial + ((int64_t)blockIdx.x * C + tid * 4) * 3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      q[3 * j] = Bv[j];
+      q[3 * j + 1] = G[j];
+      q[3 * j + 2] = 0.0;
+    }
+  }
+}
+
+template <typename T, typename OT, int BM>
+__global__ __launch_bounds__(256) void spkd_bn_bwd_apply_kernel(
+    const T* __restrict__ raw, int64_t sB, int64_t P, int C, int B,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ Mc, const float* __restrict__ k, OT* __restrict__ draw) {
+  const int CQ = C / 4;
+  const int64_t nq = P * CQ;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = q / CQ;
+    const int c0 = (int)(q - p * CQ) * 4;
+    f32x4 sc, sh, k1, k2, k3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sc[j] = scale[c0 + j];
+      sh[j] = shift[c0 + j];
+      k1[j] = k[c0 + j];
+      k2[j] = k[C + c0 + j];
+      k3[j] = k[2 * C + c0 + j];
+    }
+    f32x4 z[BM];
+#pragma unroll
+    for (int b = 0; b < BM; ++b)
+      z[b] = b < B ? z_of<T>(raw + b * sB + p * C + c0, sc, sh) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < B; ++b) {
+      f32x4 dz = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < BM; ++kk)
+        if (kk < B) dz += Mc[b * B + kk] * z[kk];
+      const f32x4 x = ld4<T>(raw + b * sB + p * C + c0);
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = fmaf(k1[j], dz[j], fmaf(k2[j], x[j], k3[j]));
+      OT* dst = draw + b * sB + p * C + c0;
+      if constexpr (sizeof(OT) == 2) {
+        bf16x4b ob;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ob[j] = (__bf16)o[j];
+        *reinterpret_cast<bf16x4b*>(dst) = ob;
+      } else {
+        *reinterpret_cast<f32x4*>(dst) = o;
+      }
+    }
+  }
+}
+
 inline unsigned grid_of(int64_t n, int64_t cap = 8192) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n, 256), cap));
 }
@@ -560,6 +701,51 @@ extern "C" int clskd_mask_e_bwd(const float* spec, int32_t ldspec, const float* 
   hipLaunchKernelGGL(mask_e_bwd_kernel, dim3(grid_of(total)), dim3(256), 0, as_stream(stream), spec,
                      ldspec, mask, Tm, B, T, dest, ldest, dmask);
   CLSKD_LAUNCH_CHECK("mask_e_bwd");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_spkd_bn_bwd(const void* raw, int32_t dtype, int64_t sB, int64_t P, int32_t C,
+                                 int32_t B, const float* scale, const float* shift, const float* coef,
+                                 const float* mean, const float* var, float eps, const float* gamma,
+                                 double* work, int32_t nblk, float* dgamma, float* dbeta,
+                                 void* draw, int32_t draw_dtype, void* stream) {
+  CLSKD_CHECK_ARG(raw && scale && shift && coef && mean && var && work && draw,
+                  "spkd_bn_bwd: null pointer");
+  CLSKD_CHECK_SHAPE(B >= 1 && B <= 32 && C >= 4 && C % 4 == 0 && C <= 1024 && P >= 1 && nblk >= 1,
+                    "spkd_bn_bwd: B=%d C=%d P=%lld nblk=%d", B, C, (long long)P, nblk);
+  CLSKD_CHECK_ARG((dtype == CLSKD_F32 || dtype == CLSKD_BF16) &&
+                      (draw_dtype == CLSKD_F32 || draw_dtype == CLSKD_BF16),
+                  "spkd_bn_bwd: dtype");
+  hipStream_t st = as_stream(stream);
+  double* partial = work;
+  float* k = reinterpret_cast<float*>(work + (int64_t)nblk * C * 3);
+  const int64_t ppb = cdiv(P, nblk);
+  const int64_t nq = P * (C / 4);
+  const unsigned ga = grid_of(nq, 16384);
+#define SBB_RED(T_, BM_)                                                                            \
+  hipLaunchKernelGGL((spkd_bn_bwd_reduce_kernel<T_, BM_>), dim3(nblk), dim3(256), 0, st,           \
+                     (const T_*)raw, sB, P, C, B, ppb, scale, shift, coef, mean, var, eps, partial)
+#define SBB_APP(T_, OT_, BM_)                                                                        \
+  hipLaunchKernelGGL((spkd_bn_bwd_apply_kernel<T_, OT_, BM_>), dim3(ga), dim3(256), 0, st,          \
+                     (const T_*)raw, sB, P, C, B, scale, shift, coef, k, (OT_*)draw)
+  const bool big = B > 16;
+  if (dtype == CLSKD_BF16) {
+    if (big) SBB_RED(__bf16, 32); else SBB_RED(__bf16, 16);
+  } else {
+    if (big) SBB_RED(float, 32); else SBB_RED(float, 16);
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, nblk,
+                     (int64_t)B * P, C, gamma, mean, var, eps, dgamma, dbeta, k, nullptr, 0);
+  if (dtype == CLSKD_BF16) {
+    if (draw_dtype == CLSKD_BF16) { if (big) SBB_APP(__bf16, __bf16, 32); else SBB_APP(__bf16, __bf16, 16); }
+    else { if (big) SBB_APP(__bf16, float, 32); else SBB_APP(__bf16, float, 16); }
+  } else {
+    if (draw_dtype == CLSKD_BF16) { if (big) SBB_APP(float, __bf16, 32); else SBB_APP(float, __bf16, 16); }
+    else { if (big) SBB_APP(float, float, 32); else SBB_APP(float, float, 16); }
+  }
+#undef SBB_RED
+#undef SBB_APP
+  CLSKD_LAUNCH_CHECK("spkd_bn_bwd");
   return CLSKD_OK;
 }
 
