@@ -52,3 +52,45 @@ def test_gloo_world2():
     np.testing.assert_allclose(g0a, np.full((3, 4), 1.5))
     np.testing.assert_allclose(g1b, np.arange(5) * 1.5)
     np.testing.assert_array_equal(g0b, g1b)
+
+
+def _train_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "speech-enhancement-clskd_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from clskd import dist as cdist
+    from clskd.train import FlatParams, allreduce_grads
+    cdist.init("gloo")
+    torch.manual_seed(0)  # identical initial parameters on every rank (as DDP broadcasts)
+    m = torch.nn.Sequential(torch.nn.Linear(5, 3), torch.nn.PReLU(), torch.nn.Linear(3, 2))
+    flat = FlatParams(m)
+    views_alias = all(p.data_ptr() >= flat.data.data_ptr() and
+                      p.data_ptr() < flat.data.data_ptr() + 4 * flat.numel for p in flat.params)
+    aligned = all((p.data_ptr() - flat.data.data_ptr()) % 256 == 0 for p in flat.params)
+    for i, p in enumerate(flat.params):  # rank-dependent local gradients
+        flat.gviews[p].fill_(float((rank + 1) * (i + 1)))
+    scale = allreduce_grads(flat)
+    q.put((rank, scale, views_alias, aligned,
+           [flat.gviews[p].reshape(-1)[0].item() for p in flat.params]))
+    torch.distributed.destroy_process_group()
+
+
+def test_gloo_world2_train_step_plumbing():
+    """C3 data parallelism: parameters re-homed into one flat buffer (256-B aligned views), the
+    student gradient summed across ranks by ONE all-reduce of the flat bucket; the returned
+    scale (1/world) turns the sum into the mean inside the Adam launch."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, scale, alias, aligned, g in res:
+        assert scale == 0.5 and alias and aligned
+        assert g == [3.0 * (i + 1) for i in range(len(g))]  # (1 + 2) * (i + 1) summed
