@@ -171,6 +171,13 @@ int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_seq, int64_t
                          const float* whh, int32_t nws, int32_t nseq, int32_t T, int32_t H,
                          float* out, int64_t o_ws, int64_t o_seq, int64_t o_t, void* stream);
 
+/* One recurrence step with carried state (streaming inference, config C5): per (ws, seq),
+ * gates = gx + W_hh h; c = f c + i g; h = o tanh(c) — h, c updated in place (strides s_ws,
+ * s_seq), h also written to out.  Same gate functions as clskd_lstm_recurrent. */
+int clskd_lstm_cell(const float* gx, int64_t gx_ws, int64_t gx_seq, const float* whh, int32_t nws,
+                    int32_t nseq, int32_t H, float* h, float* c, int64_t s_ws, int64_t s_seq,
+                    float* out, int64_t o_ws, int64_t o_seq, void* stream);
+
 /* real = a - b, imag = c + d  (tools_for_model.py:168-169); all [n] contiguous */
 int clskd_complex_combine(const float* rr, const float* ii, const float* ir, const float* ri,
                           float* real_out, float* imag_out, int64_t n, void* stream);

@@ -42,6 +42,25 @@ def _mark(label, stream):
 _PRIO = os.environ.get("CLSKD_STREAM_PRIO", "none")
 
 
+_SERIAL = False
+
+
+class serialized_streams:
+    """Context manager: every side stream of the step is the caller's stream (one serial
+    stream) — used by bench.py for its per-kernel census, so kernel durations are isolated ones
+    (as rocprofv3's kernel trace sees them) instead of times shared with concurrent streams."""
+
+    def __enter__(self):
+        global _SERIAL
+        self._prev, _SERIAL = _SERIAL, True
+        return self
+
+    def __exit__(self, *exc):
+        global _SERIAL
+        _SERIAL = self._prev
+        return False
+
+
 def _side_stream(dev, which=0):
     """Extra HIP streams per device.  which = 0, 1: the student chain and the ReviewKD-encoder /
     MRSTFT chain run beside the teacher, overlapping the latency-bound LSTM recurrences and small
@@ -49,6 +68,8 @@ def _side_stream(dev, which=0):
     three share the CUs).  CLSKD_STREAM_PRIO=teacher creates it at high priority; measured on
     MI355X that is 0.5-1 % slower than equal priorities (the default), since the side chains'
     small kernels then queue behind the teacher's large GEMMs."""
+    if _SERIAL:
+        return torch.cuda.current_stream(dev)
     key = (torch.device(dev).index, which)
     if key not in _SIDE:
         prio = -1 if (which == 2 and _PRIO == "teacher") else 0

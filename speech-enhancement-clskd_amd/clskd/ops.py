@@ -415,6 +415,12 @@ def lstm_recurrent(gx, gx_ws, gx_seq, gx_t, whh, nws, nseq, T, H, out, o_ws, o_s
     return out
 
 
+def lstm_cell(gx, gx_ws, gx_seq, whh, nws, nseq, H, h, c, s_ws, s_seq, out, o_ws, o_seq):
+    """One LSTM step with carried (h, c), updated in place (clskd_lstm_cell)."""
+    check(lib().clskd_lstm_cell(ptr(gx), gx_ws, gx_seq, ptr(whh), nws, nseq, H, ptr(h), ptr(c),
+                                s_ws, s_seq, ptr(out), o_ws, o_seq, _stream()), "lstm_cell")
+
+
 def complex_combine(rr, ii, ir, ri, ro, io):
     check(lib().clskd_complex_combine(ptr(rr), ptr(ii), ptr(ir), ptr(ri), ptr(ro), ptr(io),
                                       ro.numel(), _stream()), "complex_combine")

@@ -286,6 +286,45 @@ __global__ __launch_bounds__(NKS * H) void lstm_bwd_kernel(
     dhr = s;
   }
 }
+
+// ------------------------------------------------------------------------------------------
+// One recurrence step with carried state (streaming inference, config C5): for every (weight
+// set, sequence), gates = gx + W_hh h, c = f c + i g, h = o tanh(c), with h and c updated in
+// place (h read into LDS before any write).  Same activation functions as the offline
+// recurrence, so a stream of steps reproduces lstm_recurrent_kernel's sequence.
+// One workgroup per (ws, seq); thread g < 4H forms gate row g.
+// ------------------------------------------------------------------------------------------
+template <int H>
+__global__ __launch_bounds__(4 * H) void lstm_cell_kernel(const float* __restrict__ gx, int64_t gx_ws,
+                                                         int64_t gx_seq, const float* __restrict__ whh,
+                                                         float* __restrict__ h, float* __restrict__ c,
+                                                         int64_t s_ws, int64_t s_seq,
+                                                         float* __restrict__ out, int64_t o_ws,
+                                                         int64_t o_seq) {
+  constexpr int G = 4 * H;
+  const int g = threadIdx.x;
+  const int ws = blockIdx.y, seq = blockIdx.x;
+  __shared__ float hs[H];
+  __shared__ float act[G];
+  float* hp = h + ws * s_ws + seq * s_seq;
+  float* cp = c + ws * s_ws + seq * s_seq;
+  if (g < H) hs[g] = hp[g];
+  __syncthreads();
+  const float* w = whh + ((int64_t)ws * G + g) * H;
+  float a = gx[ws * gx_ws + seq * gx_seq + g];
+#pragma unroll 8
+  for (int j = 0; j < H; ++j) a = fmaf(w[j], hs[j], a);
+  const int gate = g / H;
+  act[g] = gate == 2 ? fmaf(2.f, sigm_fast(2.f * a), -1.f) : sigm_fast(a);
+  __syncthreads();
+  if (g < H) {
+    const float cn = act[H + g] * cp[g] + act[g] * act[2 * H + g];
+    const float hn = act[3 * H + g] * tanh_fast(cn);
+    cp[g] = cn;
+    hp[g] = hn;
+    out[ws * o_ws + seq * o_seq + g] = hn;
+  }
+}
 }  // namespace clskd
 
 using namespace clskd;
@@ -365,5 +404,26 @@ extern "C" int clskd_lstm_bwd(const float* pre, int64_t p_ws, int64_t p_seq, int
   }
 #undef LSTM_BWD
   CLSKD_LAUNCH_CHECK("lstm_bwd");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_lstm_cell(const float* gx, int64_t gx_ws, int64_t gx_seq, const float* whh,
+                               int32_t nws, int32_t nseq, int32_t H, float* h, float* c,
+                               int64_t s_ws, int64_t s_seq, float* out, int64_t o_ws, int64_t o_seq,
+                               void* stream) {
+  CLSKD_CHECK_ARG(gx && whh && h && c && out, "lstm_cell: null pointer");
+  CLSKD_CHECK_SHAPE(nws >= 1 && nseq >= 1, "lstm_cell: empty shape");
+  dim3 grid(nseq, nws);
+  hipStream_t st = as_stream(stream);
+  switch (H) {
+    case 16: hipLaunchKernelGGL(lstm_cell_kernel<16>, grid, dim3(64), 0, st, gx, gx_ws, gx_seq, whh, h, c, s_ws, s_seq, out, o_ws, o_seq); break;
+    case 32: hipLaunchKernelGGL(lstm_cell_kernel<32>, grid, dim3(128), 0, st, gx, gx_ws, gx_seq, whh, h, c, s_ws, s_seq, out, o_ws, o_seq); break;
+    case 64: hipLaunchKernelGGL(lstm_cell_kernel<64>, grid, dim3(256), 0, st, gx, gx_ws, gx_seq, whh, h, c, s_ws, s_seq, out, o_ws, o_seq); break;
+    case 128: hipLaunchKernelGGL(lstm_cell_kernel<128>, grid, dim3(512), 0, st, gx, gx_ws, gx_seq, whh, h, c, s_ws, s_seq, out, o_ws, o_seq); break;
+    default:
+      set_error("lstm_cell: hidden size %d not built (16, 32, 64, 128)", H);
+      return CLSKD_E_SHAPE;
+  }
+  CLSKD_LAUNCH_CHECK("lstm_cell");
   return CLSKD_OK;
 }

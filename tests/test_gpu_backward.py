@@ -265,3 +265,28 @@ def test_clskd_backward_mixed_precision_close_to_fp32():
     worst.sort(reverse=True)
     print(worst[:5])
     assert worst[0][0] < 5e-2, worst[:5]
+
+
+# ------------------------------------------------------------------------------------------
+# streaming inference (config C5)
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("graph", [False, True])
+def test_streaming_matches_offline_eval_forward(graph):
+    """Hop-by-hop enhancement (6.25 ms hops, 9-hop latency, decoder look-ahead drained at the
+    end) equals the offline eval-mode forward on the same clip (max |diff| <= 1e-5); the
+    hipGraph-replayed hop equals the eager hop."""
+    from clskd.data import synthetic_pairs
+    from clskd.model import DCCRN
+    from clskd.streaming import StreamingDCCRN
+    noisy, _ = synthetic_pairs(2, 16000, seed=31)
+    x = torch.from_numpy(noisy).to(DEV)
+    m = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.STUDENT), STUDENT_SEED).to(DEV)
+    m.train()
+    m(x)  # one train-mode pass: non-trivial running statistics for eval-mode BN
+    m.eval()
+    ref = m(x, is_feat=True)
+    out = StreamingDCCRN(m, 2, graph=graph).process(x)
+    torch.cuda.synchronize()
+    assert out.shape == ref.shape
+    err = (out - ref).abs().max().item()
+    assert err <= 1e-5, err
