@@ -132,7 +132,9 @@ def main():
             return kd.train_step((Xs[i % NBATCH], Ys[i % NBATCH]), flat, opt)
     elif (not args.graph):
         def step(i):
-            return kd.training_step((Xs[i % NBATCH], Ys[i % NBATCH]), i)
+            # fwd+loss only: no autograd tape (the C3 leg above records and consumes one)
+            with torch.no_grad():
+                return kd.training_step((Xs[i % NBATCH], Ys[i % NBATCH]), i)
     else:
         from clskd.graph import StepGraph
         graph = StepGraph(kd, Xs[0], Ys[0])
@@ -184,7 +186,8 @@ def main():
         # eager pass over the same K batches right after the timed replays (same kernels, shapes)
         ops.KernelTimer.start()
         for i in range(args.steps):
-            kd.training_step((Xs[i % NBATCH], Ys[i % NBATCH]), i)
+            with torch.no_grad():
+                kd.training_step((Xs[i % NBATCH], Ys[i % NBATCH]), i)
         ktimes = ops.KernelTimer.stop()
         timing = ("HIP events around every conv-engine launch of an eager pass over the K timed "
                   "batches (the timed region replays the captured hipGraph)")

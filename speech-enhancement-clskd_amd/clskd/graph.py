@@ -62,7 +62,7 @@ class StepGraph:
         saved = [b.clone() for b in _bn_buffers(self.kd)]
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(cur)
-        with torch.cuda.stream(s):
+        with torch.cuda.stream(s), torch.no_grad():
             for _ in range(self.warmup):
                 self.kd.training_step((self.X, self.y))
         cur.wait_stream(s)
