@@ -369,11 +369,28 @@ int clskd_bn_bwd(const void* x, const float* dy, int64_t rows, int32_t C, const 
  * output) and dyup = dL/d(upsampled residual) (fp32 [B][F][T][64]); operands as clskd_abf_fuse.
  * clskd_nearest_down_sum folds a gradient of a nearest upsampling (F.interpolate 'nearest',
  * framework.py:213-222) back onto the source grid: out[b][fr][tr][c] (+)= sum of g over the
- * destination pixels whose nearest source is (fr, tr). */
+ * destination pixels whose nearest source is (fr, tr).
+ * Fusions in clskd_abf_fuse_bwd: dnext (optional, fp32 [B][F2][T2][64]) = the NEXT ReviewKD
+ * level's dyup, folded onto this level's grid and added to dout on load (the residual path of
+ * framework.py:213-215 without a separate down-sum pass); bn_partial (optional, fp64
+ * [clskd_abf_fuse_bwd_blocks(B,F,T)][64][3]) receives the conv1-BatchNorm backward statistics of
+ * dx (mean1/var1: that BN's batch statistics) for clskd_bn_bwd_from_partials.  dyup may be NULL
+ * (the first level has no residual input). */
+int32_t clskd_abf_fuse_bwd_blocks(int32_t B, int32_t F, int32_t T);
 int clskd_abf_fuse_bwd(const void* x1, const void* res, int32_t B, int32_t F, int32_t T,
                        int32_t Fr, int32_t Tr, const float* w, const float* b,
                        const float* x_scale, const float* x_shift, const float* dout, float* dx,
-                       float* dyup, int32_t dtype, void* stream);
+                       float* dyup, const float* dnext, int32_t F2, int32_t T2,
+                       const float* mean1, const float* var1, float eps, double* bn_partial,
+                       int32_t dtype, void* stream);
+/* BatchNorm backward whose statistics partials [nblk][C][3] were produced by a fused producer
+ * (clskd_abf_fuse_bwd): finalize + apply of clskd_bn_bwd (no PReLU).  kbuf: 3*C floats. */
+int clskd_bn_bwd_from_partials(const void* x, const float* dy, int64_t rows, int32_t C,
+                               const float* scale, const float* shift, const float* mean,
+                               const float* var, float eps, const float* gamma,
+                               const double* partial, int32_t nblk, float* kbuf, float* dgamma,
+                               float* dbeta, float* dx, int32_t accumulate_dx, int32_t dtype,
+                               void* stream);
 int clskd_nearest_down_sum(const float* g, int32_t B, int32_t F, int32_t T, int32_t Fr,
                            int32_t Tr, int32_t C, float* out, int32_t accumulate, void* stream);
 
@@ -382,7 +399,8 @@ int clskd_nearest_down_sum(const float* g, int32_t B, int32_t F, int32_t T, int3
  * 95-107, DCCRN.py:237): dwav -> dframes [B][T][win] (pre-clamp samples recomputed from frames).
  * Framing pad backward (zero / reflect, as clskd_frame_pad): dxp [B][Lp] -> dx [B][L] (row ldx).
  * STFT log-magnitude L1 backward (framework.py:58-68): dX = d(scale * sum|log|Y| - log|X||)/dX
- * for raw spectra X, Y [rows][ld] (re at f, im at nbins+f).
+ * for raw spectra X, Y [rows][ld] (re at f, im at nbins+f), written with row pitch ldd (columns
+ * >= 2*nbins zero: a pitch padded to a multiple of 4 keeps the framing dgrad's gather vec4).
  * Complex-LSTM combine backward (tools_for_model.py:168-169): dh[2][2B][n] from dreal/dimag. */
 int clskd_mask_e_bwd(const float* spec, int32_t ldspec, const float* mask, int32_t Tm, int32_t B,
                      int32_t T, const float* dest, int32_t ldest, float* dmask, void* stream);
@@ -392,7 +410,7 @@ int clskd_ola_bwd(const float* frames, const float* window, const float* dwav, i
 int clskd_frame_pad_bwd(const float* dxp, int32_t B, int32_t L, int32_t pad, int32_t Lp,
                         int32_t mode, float* dx, int64_t ldx, int32_t accumulate, void* stream);
 int clskd_stft_mag_loss_bwd(const float* X, const float* Y, int64_t rows, int32_t ld,
-                            int32_t nbins, float scale, float* dX, void* stream);
+                            int32_t nbins, float scale, float* dX, int32_t ldd, void* stream);
 int clskd_complex_combine_bwd(const float* dreal, const float* dimag, int32_t B, int64_t n,
                               float* dh, void* stream);
 

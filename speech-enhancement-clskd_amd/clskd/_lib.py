@@ -113,13 +113,16 @@ SIGNATURES = {
     "clskd_bn_bwd_workspace": (_i64, [_i32, _i32]),
     "clskd_bn_bwd": (_i32, [_p, _p, _i64, _i32, _p, _p, _p, _p, _f32, _p, _p, _p, _i32, _p, _p,
                             _p, _p, _i32, _i32, _i32, _p]),
+    "clskd_abf_fuse_bwd_blocks": (_i32, [_i32, _i32, _i32]),
     "clskd_abf_fuse_bwd": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,
-                                  _p, _i32, _p]),
+                                  _p, _p, _i32, _i32, _p, _p, _f32, _p, _i32, _p]),
+    "clskd_bn_bwd_from_partials": (_i32, [_p, _p, _i64, _i32, _p, _p, _p, _p, _f32, _p, _p, _i32,
+                                          _p, _p, _p, _p, _i32, _i32, _p]),
     "clskd_nearest_down_sum": (_i32, [_p, _i32, _i32, _i32, _i32, _i32, _i32, _p, _i32, _p]),
     "clskd_mask_e_bwd": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _i32, _p, _p]),
     "clskd_ola_bwd": (_i32, [_p, _p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p]),
     "clskd_frame_pad_bwd": (_i32, [_p, _i32, _i32, _i32, _i32, _i32, _p, _i64, _i32, _p]),
-    "clskd_stft_mag_loss_bwd": (_i32, [_p, _p, _i64, _i32, _i32, _f32, _p, _p]),
+    "clskd_stft_mag_loss_bwd": (_i32, [_p, _p, _i64, _i32, _i32, _f32, _p, _i32, _p]),
     "clskd_complex_combine_bwd": (_i32, [_p, _p, _i32, _i64, _p, _p]),
     "clskd_lstm_bwd": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _i64, _i64, _p, _i32, _i32, _i32,
                               _i32, _p, _p, _i64, _i64, _i64, _p]),

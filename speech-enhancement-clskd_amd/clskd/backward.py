@@ -443,23 +443,28 @@ def review_backward(review, tape, coef_m, d_feats, acc_feats):
             "bf16" if lowp else "fp32"))
         ops.conv([seg_bftc(d_oraw)], [(1 - kf, 1 - kt) for kf in range(3) for kt in range(3)], Bn, Fn,
                  Tn, mid, w2t, None, d_xf, OutMap(Fn * Tn * mid, Tn * mid, mid))
-        if dyup_next is not None:  # residual path of level j+1 (nearest upsampling, folded back)
-            ops.nearest_down_sum(dyup_next, d_xf, accumulate=True)
         c1 = tp["coef1"]
+        bn1 = abf.conv1[1]
+        d_x1 = _empty(tp["x1"].shape, dev)
         if abf.att_conv is not None:
+            # one pass: residual path of level j+1 folded in on load, the attention-fusion
+            # backward, and the conv1-BN statistics partials (no down-sum / BN-reduce passes)
             dxn = _empty(d_xf.shape, dev)
             dyup = _empty(d_xf.shape, dev)
             aw = abf.att_conv[0].weight.reshape(2, -1).float().contiguous()
             ab = abf.att_conv[0].bias.float().contiguous()
-            ops.abf_fuse_bwd(tp["x1"], tp["res"], aw, ab, c1, d_xf, dxn, dyup)
+            part, nblk = ops.abf_fuse_bwd(tp["x1"], tp["res"], aw, ab, c1, d_xf, dxn, dyup,
+                                          dnext=dyup_next, mv1=tp["mv1"], eps=bn1.eps)
             dyup_next = dyup
+            ops.bn_bwd_from_partials(tp["x1"], dxn, c1[:mid], c1[mid:], tp["mv1"][0],
+                                     tp["mv1"][1], bn1.eps, bn1.weight, part, nblk, d_x1)
         else:
+            if dyup_next is not None:  # residual path of level j+1 (nearest upsampling)
+                ops.nearest_down_sum(dyup_next, d_xf, accumulate=True)
             dxn = d_xf
             dyup_next = None
-        bn1 = abf.conv1[1]
-        d_x1 = _empty(tp["x1"].shape, dev)
-        ops.bn_bwd(tp["x1"], dxn, c1[:mid], c1[mid:], tp["mv1"][0], tp["mv1"][1], bn1.eps,
-                   bn1.weight, None, d_x1)
+            ops.bn_bwd(tp["x1"], dxn, c1[:mid], c1[mid:], tp["mv1"][0], tp["mv1"][1], bn1.eps,
+                       bn1.weight, None, d_x1)
         w1 = abf.conv1[0].weight  # [mid, Cin, 1, 1]
         Cin = w1.shape[1]
         w1t = _tw(("abf1_t", id(abf)), w1, lambda: ops.pack_weight(
@@ -478,15 +483,22 @@ def mrstft_backward(tape, d_x, upstream=1.0):
         X, Y, plan = t["X"], t["Y"], t["plan"]
         B, Tm, W2 = X.shape
         nb = plan.fft // 2 + 1
-        dX = _empty(X.shape, X.device)
+        # the spectrum gradient gets a row pitch padded to a multiple of 4 (zero columns), so the
+        # framing data gradient below gathers it with 16-B loads (vec4 K table)
+        Wp = -(-W2 // 4) * 4
+        dX = _empty((B, Tm, Wp), X.device)
         ops.stft_mag_loss_bwd(X, Y, nb, upstream * t["factor_mag"] / t["count"], dX)
         Lr, L = t["Lr"], t["L"]
         dxr = _zeros((B, Lr), X.device)
         basis = plan.basis(X.device)  # [2nb][KT*hop]
         KT, hop = plan.KT, plan.hop
-        wt = _tw(("stft_t", id(plan)), basis, lambda: ops.pack_weight(
-            basis[:, :KT * hop].reshape(W2, KT, hop).permute(2, 1, 0).contiguous(), KT * W2))
-        ops.conv([Seg(dX, 0, SegGeom(W2, Tm * W2, 0, W2, 1, Tm))], [(0, -kt) for kt in range(KT)], B, 1,
+
+        def build():
+            w = basis[:, :KT * hop].reshape(W2, KT, hop)
+            w = torch.cat([w, w.new_zeros(Wp - W2, KT, hop)], 0)  # zero rows for the pad columns
+            return ops.pack_weight(w.permute(2, 1, 0).contiguous(), KT * Wp)
+        wt = _tw(("stft_t", id(plan)), basis, build)
+        ops.conv([Seg(dX, 0, SegGeom(Wp, Tm * Wp, 0, Wp, 1, Tm))], [(0, -kt) for kt in range(KT)], B, 1,
                  Tm + KT - 1, hop, wt, None, dxr, OutMap(Lr, 0, hop), out_offset=plan.off,
                  mfma_only=True)
         ops.frame_pad_bwd(dxr, L, plan.fft // 2, 1, d_x, accumulate=True)

@@ -77,6 +77,13 @@ def _side_stream(dev, which=0):
     return _SIDE[key]
 
 
+class _SlabRefs:
+    """Slab ranges of several GramSlabs launches (kept alive together) in pair order."""
+
+    def __init__(self, refs, owners):
+        self.refs, self.owners = refs, owners
+
+
 def _gram_bftc(t, c0=0, Cs=None):
     affine = None
     if isinstance(t, ops.DeferredBN):  # BatchNorm folded into the Gram's loads
@@ -284,15 +291,31 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     s_enc, g_enc = held["s_enc"], held["g_enc"]
     tstream = _side_stream(dev, 2)
     tstream.wait_stream(main)
+    # the teacher's encoder-tap Grams run on side2 (after its ReviewKD-encoder work) as soon as
+    # the teacher encoder is done, keeping them off the teacher chain — the step's critical path.
+    # (Four streams in all: GPU_MAX_HW_QUEUES is 4, a fifth would share a hardware queue.)
+    tgram = side2
+
+    def fork_teacher_grams(enc):
+        ev = torch.cuda.Event()
+        ev.record(tstream)
+        with torch.cuda.stream(tgram):
+            tgram.wait_event(ev)
+            held["g_te"] = ops.GramSlabs([_gram_bftc(a) for a in enc], B)
+            _mark("tgram: teacher enc grams done", tgram)
+
     with torch.cuda.stream(tstream):
-        tf = teacher.run(X, train=teacher.training, bn_updates=1, spec=spec, want_masks=False)
+        # the teacher's last decoder layer, mask and iSTFT are dead for the loss: stop at its taps
+        tf = teacher.run(X, train=teacher.training, bn_updates=1, spec=spec, want_masks=False,
+                         on_encoder=fork_teacher_grams, taps_only=True)
         _mark("teacher: done", tstream)
         t_dec = [tf["dec_in"]] + tf["dec"][:5]
         Cht = tf["dec_in"].shape[-1] // 2
-        g_t = ops.GramSlabs([_gram_bftc(a) for a in tf["enc"]] + [_gram_bftc(a) for a in t_dec] +
-                            [_gram_bftc(tf["dec_in"], 0, Cht), _gram_bftc(tf["dec_in"], Cht, Cht)],
-                            B)
+        g_td = ops.GramSlabs([_gram_bftc(a) for a in t_dec] +
+                             [_gram_bftc(tf["dec_in"], 0, Cht), _gram_bftc(tf["dec_in"], Cht, Cht)],
+                             B)
         _mark("teacher: grams done", tstream)
+    g_t = _SlabRefs(held["g_te"].refs + g_td.refs, (held["g_te"], g_td))
     main.wait_stream(tstream)
     main.wait_stream(side)
     main.wait_stream(side2)

@@ -351,13 +351,16 @@ class DCCRN(nn.Module):
         return spec
 
     def run(self, x, train=True, bn_updates=1, spec=None, want_masks=True, on_encoder=None,
-            tape=None):
+            tape=None, taps_only=False):
         """Full forward on the HIP device.  Returns a dict of BFTC buffers and NCHW views.
         on_encoder(enc): called (on the launching stream) right after the encoder, so a caller can
         fork work that only needs the encoder taps before the LSTM and decoder are enqueued.
         tape: a dict that receives what the backward pass (clskd.backward) needs — pre-BN conv
         outputs kept beside the activations, BN coefficients and batch statistics, the LSTM gate
-        inputs and hidden histories, the iSTFT frames."""
+        inputs and hidden histories, the iSTFT frames.
+        taps_only: stop after the taps a distillation step reads (encoder outputs, dec_in,
+        decoder outputs 0..nl-2): the last decoder layer, mask 'E' and ConviSTFT are dead for
+        the CLSKD loss (SURVEY.md §8 d) and are skipped — out_wav is None."""
         if not x.is_cuda:
             raise RuntimeError("clskd.DCCRN.forward needs inputs on the HIP device")
         x = x.float()
@@ -460,7 +463,7 @@ class DCCRN(nn.Module):
         dec = []
         out_t, out_t0, out_T = dec_in, 0, T
         F = D4
-        for d in range(nl):
+        for d in range(nl - 1 if taps_only else nl):
             skip = enc[-1 - d]
             Cof = out_t.shape[-1]
             Csk = skip.shape[-1]
@@ -504,6 +507,12 @@ class DCCRN(nn.Module):
             dec.append(raw)
             out_t, out_t0, out_T = raw, 1, T
             F = 2 * F
+        nchw = lambda t: t.permute(0, 3, 1, 2)
+        if taps_only:
+            return dict(out_wav=None, real=None, imag=None, mask_real=None, mask_imag=None,
+                        enc=enc, dec=dec, dec_in=dec_in, spec=spec, est=None, T=T,
+                        enc_nchw=[nchw(t) for t in enc], dec_nchw=[nchw(t) for t in dec],
+                        lstm_io=lstm_io)
         # ---------------- mask 'E' + ConviSTFT + clamp (DCCRN.py:207-237)
         mask = dec[-1]  # [B][256][T+1][2]
         est = torch.empty(B, T, 516, **f32)
@@ -522,7 +531,6 @@ class DCCRN(nn.Module):
         if tape is not None:
             tape.update(spec=spec, est=est, frames=frames, window=window, out_len=out_len, T=T,
                         B=B, train=train)
-        nchw = lambda t: t.permute(0, 3, 1, 2)
         return dict(
             out_wav=wav,
             real=est[:, :, :257].permute(0, 2, 1),

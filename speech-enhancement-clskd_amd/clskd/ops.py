@@ -721,15 +721,42 @@ def bn_bwd(x, dy, scale, shift, mean, var, eps, gamma, alpha, dx, dgamma=None, d
     return dx
 
 
-def abf_fuse_bwd(x1, res, w, b, x_coef, dout, dx, dyup):
+def abf_fuse_bwd(x1, res, w, b, x_coef, dout, dx, dyup, dnext=None, mv1=None, eps=1e-5):
+    """ABF fusion backward.  dnext: the next level's dyup, folded onto this grid and added to
+    dout on load.  mv1 = conv1 BN [mean; var]: also returns (partials, nblk) of that BN's
+    backward statistics for bn_bwd_from_partials."""
+    L = lib()
     B, F, T, Cm = x1.shape
     _, Fr, Tr, _ = res.shape
     sc = sh = None
     if x_coef is not None:
         sc = x_coef.data_ptr()
         sh = sc + 4 * Cm
-    check(lib().clskd_abf_fuse_bwd(ptr(x1), ptr(res), B, F, T, Fr, Tr, ptr(w), ptr(b), sc, sh,
-                                   ptr(dout), ptr(dx), ptr(dyup), _dt(x1), _stream()), "abf_fuse_bwd")
+    F2 = T2 = 0
+    if dnext is not None:
+        _, F2, T2, _ = dnext.shape
+    part, nblk = None, 0
+    if mv1 is not None:
+        nblk = int(L.clskd_abf_fuse_bwd_blocks(B, F, T))
+        part = torch.empty(nblk * Cm * 3, dtype=torch.float64, device=x1.device)
+    check(L.clskd_abf_fuse_bwd(ptr(x1), ptr(res), B, F, T, Fr, Tr, ptr(w), ptr(b), sc, sh,
+                               ptr(dout), ptr(dx), ptr(dyup), ptr(dnext), F2, T2,
+                               ptr(mv1[0]) if mv1 is not None else None,
+                               ptr(mv1[1]) if mv1 is not None else None, eps, ptr(part),
+                               _dt(x1), _stream()), "abf_fuse_bwd")
+    return part, nblk
+
+
+def bn_bwd_from_partials(x, dy, scale, shift, mean, var, eps, gamma, partial, nblk, dx,
+                         accumulate_dx=False):
+    Cn = x.shape[-1]
+    kbuf = torch.empty(3 * Cn, dtype=torch.float32, device=x.device)
+    check(lib().clskd_bn_bwd_from_partials(ptr(x), ptr(dy), x.numel() // Cn, Cn, ptr(scale),
+                                           ptr(shift), ptr(mean), ptr(var), eps, ptr(gamma),
+                                           ptr(partial), nblk, ptr(kbuf), None, None, ptr(dx),
+                                           int(accumulate_dx), _dt(x), _stream()),
+          "bn_bwd_from_partials")
+    return dx
 
 
 def nearest_down_sum(g, out, accumulate=False):
@@ -760,7 +787,7 @@ def frame_pad_bwd(dxp, L, pad, mode, dx, accumulate=False):
 def stft_mag_loss_bwd(X, Y, nbins, scale, dX):
     rows = X.numel() // X.shape[-1]
     check(lib().clskd_stft_mag_loss_bwd(ptr(X), ptr(Y), rows, X.shape[-1], nbins, scale, ptr(dX),
-                                        _stream()), "stft_mag_loss_bwd")
+                                        dX.shape[-1], _stream()), "stft_mag_loss_bwd")
 
 
 def complex_combine_bwd(dre, dim, dh):

@@ -199,15 +199,39 @@ __device__ __forceinline__ int nearest_src_b(int dst, int in_size, int out_size)
   return s < in_size - 1 ? s : in_size - 1;
 }
 
+// smallest dst with nearest_src(dst) >= s (nearest_src is non-decreasing in dst)
+__device__ __forceinline__ int first_dst_b(int s, int in_size, int out_size) {
+  int d0 = (int)((double)s * out_size / in_size) - 2;
+  if (d0 < 0) d0 = 0;
+  while (d0 < out_size && nearest_src_b(d0, in_size, out_size) < s) ++d0;
+  return d0;
+}
+
+// Fused ReviewKD mid-channel backward: dout = d(conv2 input) of this level plus, when dnext is
+// given, the NEXT level's gradient w.r.t. its upsampled residual folded back onto this grid
+// (nearest upsampling (F, T) -> (F2, T2), framework.py:213-215) — so no separate down-sum pass;
+// when bnpart is given, per-block fp64 partials {sum dx, sum dx*xhat1, 0} of the conv1 BatchNorm
+// backward (xhat1 = (x1 - mean1) * rstd1) are emitted — so no separate BN reduce pass.
 template <typename DT>
 __global__ __launch_bounds__(256) void abf_fuse_bwd_kernel(
     const DT* __restrict__ x1, const DT* __restrict__ res, int B, int F, int T, int Fr, int Tr,
     const float* __restrict__ w, const float* __restrict__ bias, const float* __restrict__ xs,
     const float* __restrict__ xh, const float* __restrict__ dout, float* __restrict__ dx,
-    float* __restrict__ dyup) {
+    float* __restrict__ dyup, const float* __restrict__ dnext, int F2, int T2,
+    const float* __restrict__ mean1, const float* __restrict__ var1, float eps,
+    double* __restrict__ bnpart) {
   const int lane = threadIdx.x & 63;
   const int sub = lane & 15;
   const int c = sub * 4;
+  f32x4 mu = {0.f, 0.f, 0.f, 0.f}, rs = {0.f, 0.f, 0.f, 0.f};
+  if (bnpart) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mu[j] = mean1[c + j];
+      rs[j] = (float)(1.0 / sqrt((double)var1[c + j] + (double)eps));
+    }
+  }
+  double sb[4] = {0, 0, 0, 0}, sg[4] = {0, 0, 0, 0};
   f32x4 sx = {1.f, 1.f, 1.f, 1.f}, hx = {0.f, 0.f, 0.f, 0.f};
   if (xs) {
 #pragma unroll
@@ -235,11 +259,18 @@ __global__ __launch_bounds__(256) void abf_fuse_bwd_kernel(
     const int b = (int)(bf / F);
     const int fr = nearest_src_b(f, Fr, F);
     const int tr = nearest_src_b(t, Tr, T);
-    f32x4 xv = ld4<DT>(x1 + p * 64 + c);
+    const f32x4 xraw = ld4<DT>(x1 + p * 64 + c);
+    f32x4 xv;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) xv[j] = fmaf(xv[j], sx[j], hx[j]);
+    for (int j = 0; j < 4; ++j) xv[j] = fmaf(xraw[j], sx[j], hx[j]);
     const f32x4 yv = ld4<DT>(res + (((int64_t)b * Fr + fr) * Tr + tr) * 64 + c);
-    const f32x4 g = *reinterpret_cast<const f32x4*>(dout + p * 64 + c);
+    f32x4 g = *reinterpret_cast<const f32x4*>(dout + p * 64 + c);
+    if (dnext) {  // children of (f, t) on the next level's grid
+      const int fa = first_dst_b(f, F, F2), ta = first_dst_b(t, T, T2);
+      for (int f2 = fa; f2 < F2 && nearest_src_b(f2, F, F2) == f; ++f2)
+        for (int t2 = ta; t2 < T2 && nearest_src_b(t2, T, T2) == t; ++t2)
+          g += *reinterpret_cast<const f32x4*>(dnext + ((((int64_t)b * F2 + f2) * T2 + t2) * 64) + c);
+    }
     float d0 = 0.f, d1 = 0.f, e0 = 0.f, e1 = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -266,7 +297,35 @@ __global__ __launch_bounds__(256) void abf_fuse_bwd_kernel(
       oy[j] = g[j] * z1 + a0 * w0y[j] + a1 * w1y[j];
     }
     *reinterpret_cast<f32x4*>(dx + p * 64 + c) = ox;
-    *reinterpret_cast<f32x4*>(dyup + p * 64 + c) = oy;
+    if (dyup) *reinterpret_cast<f32x4*>(dyup + p * 64 + c) = oy;
+    if (bnpart) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sb[j] += (double)ox[j];
+        sg[j] += (double)ox[j] * (double)((xraw[j] - mu[j]) * rs[j]);
+      }
+    }
+  }
+  if (bnpart) {  // the block's 16 pixel slots share the channel mapping: fixed-order slot sum
+    __shared__ double red[16][64][2];
+    const int slot = threadIdx.x >> 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[slot][c + j][0] = sb[j];
+      red[slot][c + j][1] = sg[j];
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      double S = 0.0, G = 0.0;
+      for (int s2 = 0; s2 < 16; ++s2) {
+        S += red[s2][threadIdx.x][0];
+        G += red[s2][threadIdx.x][1];
+      }
+      double* q = bnpart + ((int64_t)blockIdx.x * 64 + threadIdx.x) * 3;
+      q[0] = S;
+      q[1] = G;
+      q[2] = 0.0;
+    }
   }
 }
 
@@ -419,12 +478,12 @@ __global__ void frame_pad_bwd_kernel(const float* __restrict__ dxp, int B, int L
 // ------------------------------------------------------------------------------------------
 __global__ void stft_mag_loss_bwd_kernel(const float* __restrict__ X, const float* __restrict__ Y,
                                          int64_t rows, int ld, int nbins, float scale,
-                                         float* __restrict__ dX) {
-  const int64_t total = rows * ld;
+                                         float* __restrict__ dX, int ldd) {
+  const int64_t total = rows * ldd;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int col = (int)(i % ld);
-    const int64_t r = i / ld;
+    const int col = (int)(i % ldd);
+    const int64_t r = i / ldd;
     float g = 0.f;
     if (col < 2 * nbins) {
       const int f = col < nbins ? col : col - nbins;
@@ -660,23 +719,54 @@ extern "C" int64_t clskd_bn_bwd_workspace(int32_t nblk, int32_t C) {
   return (int64_t)nblk * C * 3 + cdiv(3 * C, 2) + C;  // doubles
 }
 
+extern "C" int32_t clskd_abf_fuse_bwd_blocks(int32_t B, int32_t F, int32_t T) {
+  const int64_t npix = (int64_t)B * F * T;
+  return (int32_t)std::min<int64_t>(cdiv(npix * 16, 256), 16384);
+}
+
 extern "C" int clskd_abf_fuse_bwd(const void* x1, const void* res, int32_t B, int32_t F, int32_t T,
                                   int32_t Fr, int32_t Tr, const float* w, const float* b,
                                   const float* x_scale, const float* x_shift, const float* dout,
-                                  float* dx, float* dyup, int32_t dtype, void* stream) {
-  CLSKD_CHECK_ARG(x1 && res && w && b && dout && dx && dyup, "abf_fuse_bwd: null pointer");
+                                  float* dx, float* dyup, const float* dnext, int32_t F2,
+                                  int32_t T2, const float* mean1, const float* var1, float eps,
+                                  double* bn_partial, int32_t dtype, void* stream) {
+  CLSKD_CHECK_ARG(x1 && res && w && b && dout && dx, "abf_fuse_bwd: null pointer");
   CLSKD_CHECK_ARG((x_scale == nullptr) == (x_shift == nullptr), "abf_fuse_bwd: scale/shift pair");
-  const int64_t npix = (int64_t)B * F * T;
-  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(npix * 16, 256), 16384);
+  CLSKD_CHECK_ARG(!bn_partial || (mean1 && var1), "abf_fuse_bwd: BN partials need mean1/var1");
+  CLSKD_CHECK_SHAPE(!dnext || (F2 >= F && T2 >= T), "abf_fuse_bwd: next grid smaller than this one");
+  const unsigned grid = (unsigned)clskd_abf_fuse_bwd_blocks(B, F, T);
   if (dtype == CLSKD_BF16)
     hipLaunchKernelGGL(abf_fuse_bwd_kernel<__bf16>, dim3(grid), dim3(256), 0, as_stream(stream),
                        (const __bf16*)x1, (const __bf16*)res, B, F, T, Fr, Tr, w, b, x_scale,
-                       x_shift, dout, dx, dyup);
+                       x_shift, dout, dx, dyup, dnext, F2, T2, mean1, var1, eps, bn_partial);
   else
     hipLaunchKernelGGL(abf_fuse_bwd_kernel<float>, dim3(grid), dim3(256), 0, as_stream(stream),
                        (const float*)x1, (const float*)res, B, F, T, Fr, Tr, w, b, x_scale,
-                       x_shift, dout, dx, dyup);
+                       x_shift, dout, dx, dyup, dnext, F2, T2, mean1, var1, eps, bn_partial);
   CLSKD_LAUNCH_CHECK("abf_fuse_bwd");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_bn_bwd_from_partials(const void* x, const float* dy, int64_t rows, int32_t C,
+                                          const float* scale, const float* shift,
+                                          const float* mean, const float* var, float eps,
+                                          const float* gamma, const double* partial, int32_t nblk,
+                                          float* kbuf, float* dgamma, float* dbeta, float* dx,
+                                          int32_t accumulate_dx, int32_t dtype, void* stream) {
+  CLSKD_CHECK_ARG(x && dy && scale && shift && mean && var && partial && kbuf && dx,
+                  "bn_bwd_from_partials: null pointer");
+  CLSKD_CHECK_SHAPE(rows > 0 && C >= 4 && C % 4 == 0 && nblk >= 1, "bn_bwd_from_partials: shape");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, nblk, rows, C,
+                     gamma, mean, var, eps, dgamma, dbeta, kbuf, nullptr, 0);
+  const int64_t nq = rows * C / 4;
+  if (dtype == CLSKD_BF16)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<__bf16>, dim3(grid_of(nq)), dim3(256), 0, st,
+                       (const __bf16*)x, dy, rows, C, scale, shift, nullptr, kbuf, dx, accumulate_dx);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(grid_of(nq)), dim3(256), 0, st,
+                       (const float*)x, dy, rows, C, scale, shift, nullptr, kbuf, dx, accumulate_dx);
+  CLSKD_LAUNCH_CHECK("bn_bwd_from_partials");
   return CLSKD_OK;
 }
 
@@ -773,11 +863,12 @@ extern "C" int clskd_frame_pad_bwd(const float* dxp, int32_t B, int32_t L, int32
 }
 
 extern "C" int clskd_stft_mag_loss_bwd(const float* X, const float* Y, int64_t rows, int32_t ld,
-                                       int32_t nbins, float scale, float* dX, void* stream) {
+                                       int32_t nbins, float scale, float* dX, int32_t ldd,
+                                       void* stream) {
   CLSKD_CHECK_ARG(X && Y && dX, "stft_mag_loss_bwd: null pointer");
-  CLSKD_CHECK_SHAPE(ld >= 2 * nbins, "stft_mag_loss_bwd: ld");
-  hipLaunchKernelGGL(stft_mag_loss_bwd_kernel, dim3(grid_of(rows * ld)), dim3(256), 0,
-                     as_stream(stream), X, Y, rows, ld, nbins, scale, dX);
+  CLSKD_CHECK_SHAPE(ld >= 2 * nbins && ldd >= 2 * nbins, "stft_mag_loss_bwd: ld");
+  hipLaunchKernelGGL(stft_mag_loss_bwd_kernel, dim3(grid_of(rows * ldd)), dim3(256), 0,
+                     as_stream(stream), X, Y, rows, ld, nbins, scale, dX, ldd);
   CLSKD_LAUNCH_CHECK("stft_mag_loss_bwd");
   return CLSKD_OK;
 }
