@@ -40,6 +40,12 @@ def _mark(label, stream):
 
 
 _PRIO = os.environ.get("CLSKD_STREAM_PRIO", "none")
+# ReviewKD-decoder placement (A/B knob): "pipelined" runs it level by level on the caller's
+# stream behind the student decoder; "after" runs it on the student stream after the student
+_RKD_DEC = os.environ.get("CLSKD_RKD_DEC", "after")
+# host enqueue order of the step's two chains (A/B knob): "1" enqueues the teacher chain — the
+# critical path — before the student-side chains
+_TEACHER_FIRST = os.environ.get("CLSKD_TEACHER_FIRST", "1") == "1"
 
 
 _SERIAL = False
@@ -268,53 +274,105 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
             held["g_enc"] = ops.GramSlabs([_gram_bftc(a) for a in s_enc], B)
             _mark("side2: enc grams done", side2)
 
-    with torch.cuda.stream(side):
-        sf = student.run(X, train=student.training, bn_updates=2 if student.training else 0,
-                         spec=s_spec, want_masks=False, on_encoder=fork_review_encoder,
-                         tape=tapes["s"] if tapes else None)
-        student_done = torch.cuda.Event()
-        student_done.record(side)
-        _mark("side: student done", side)
-        if reinit is not None:
-            reinit("decoder")
-        s_dec = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5], defer_bn=True,
-                                            tape=tapes["rd"] if tapes else None)
-        Chs = sf["dec_in"].shape[-1] // 2
-        g_dec = ops.GramSlabs([_gram_bftc(a) for a in s_dec] +
-                              [_gram_bftc(sf["dec_in"], 0, Chs), _gram_bftc(sf["dec_in"], Chs, Chs)],
-                              B)
-        _mark("side: review decoder + grams done", side)
-    with torch.cuda.stream(side2):
-        side2.wait_event(student_done)
-        stft_loss(sf["out_wav"], y, out2=buf[0:2], tape=tapes["ms"] if tapes else None)
-        _mark("side2: mrstft done", side2)
+    # ReviewKD-decoder pipelined behind the student decoder on the caller's stream: level j
+    # (framework.py:254-261, forward order) starts as soon as its student tap exists
+    rd = dict(res=None, outs=[], taps=[])
+
+    def review_decoder_level(tap):
+        ev = torch.cuda.Event()
+        ev.record(side)
+        with torch.cuda.stream(main):
+            main.wait_event(ev)
+            j = len(rd["outs"])
+            if j == 0 and reinit is not None:
+                reinit("decoder")
+            abf = review_decoder.abfs[j]
+            tp = {} if tapes else None
+            if j == 0:
+                out, res = abf.forward_bftc(tap, out_shape=review_decoder.out_shapes[0],
+                                            defer_bn=True, tape=tp)
+            else:
+                out, res = abf.forward_bftc(tap, rd["res"], review_decoder.shapes[j],
+                                            review_decoder.out_shapes[j], defer_bn=True, tape=tp)
+            if tapes:
+                tapes["rd"].append(tp)
+            rd["res"] = res
+            rd["outs"].append(out)
+            rd["taps"].append(tap)
+
+    def run_student():
+        with torch.cuda.stream(side):
+            pipelined = _RKD_DEC == "pipelined"
+            sf = student.run(X, train=student.training, bn_updates=2 if student.training else 0,
+                             spec=s_spec, want_masks=False, on_encoder=fork_review_encoder,
+                             tape=tapes["s"] if tapes else None,
+                             on_decoder_tap=review_decoder_level if pipelined else None)
+            student_done = torch.cuda.Event()
+            student_done.record(side)
+            _mark("side: student done", side)
+            if not pipelined:
+                if reinit is not None:
+                    reinit("decoder")
+                rd["outs"] = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5],
+                                                         defer_bn=True,
+                                                         tape=tapes["rd"] if tapes else None)
+        rstream = main if pipelined else side
+        with torch.cuda.stream(rstream):
+            s_dec = rd["outs"]
+            assert len(s_dec) == len(review_decoder.abfs)
+            Chs = sf["dec_in"].shape[-1] // 2
+            g_dec = ops.GramSlabs([_gram_bftc(a) for a in s_dec] +
+                                  [_gram_bftc(sf["dec_in"], 0, Chs), _gram_bftc(sf["dec_in"], Chs, Chs)],
+                                  B)
+            _mark("review decoder + grams done", rstream)
+        with torch.cuda.stream(side2):
+            side2.wait_event(student_done)
+            stft_loss(sf["out_wav"], y, out2=buf[0:2], tape=tapes["ms"] if tapes else None)
+            _mark("side2: mrstft done", side2)
+        out_s.update(sf=sf, s_dec=s_dec, g_dec=g_dec)
+
+    def run_teacher():
+        tstream = _side_stream(dev, 2)
+        tstream.wait_stream(main)
+        # the teacher's encoder-tap Grams run on the caller's stream (idle until the join) as soon
+        # as the teacher encoder is done, keeping them off the teacher chain — the step's critical
+        # path.  (Four streams in all: GPU_MAX_HW_QUEUES is 4; a fifth would share a hardware queue.)
+        tgram = main
+
+        def fork_teacher_grams(enc):
+            ev = torch.cuda.Event()
+            ev.record(tstream)
+            with torch.cuda.stream(tgram):
+                tgram.wait_event(ev)
+                held["g_te"] = ops.GramSlabs([_gram_bftc(a) for a in enc], B)
+                _mark("tgram: teacher enc grams done", tgram)
+
+        with torch.cuda.stream(tstream):
+            # the teacher's last decoder layer, mask and iSTFT are dead for the loss: stop at its taps
+            tf = teacher.run(X, train=teacher.training, bn_updates=1, spec=spec, want_masks=False,
+                             on_encoder=fork_teacher_grams, taps_only=True,
+                             mark=(lambda lab: _mark("teacher: " + lab, tstream))
+                             if _MARKS is not None else None)
+            _mark("teacher: done", tstream)
+            t_dec = [tf["dec_in"]] + tf["dec"][:5]
+            Cht = tf["dec_in"].shape[-1] // 2
+            g_td = ops.GramSlabs([_gram_bftc(a) for a in t_dec] +
+                                 [_gram_bftc(tf["dec_in"], 0, Cht), _gram_bftc(tf["dec_in"], Cht, Cht)],
+                                 B)
+            _mark("teacher: grams done", tstream)
+        out_t.update(tf=tf, g_td=g_td)
+
+    out_s, out_t = {}, {}
+    if _TEACHER_FIRST:
+        run_teacher()
+        run_student()
+    else:
+        run_student()
+        run_teacher()
+    sf, s_dec, g_dec = out_s["sf"], out_s["s_dec"], out_s["g_dec"]
+    tf, g_td = out_t["tf"], out_t["g_td"]
     s_enc, g_enc = held["s_enc"], held["g_enc"]
     tstream = _side_stream(dev, 2)
-    tstream.wait_stream(main)
-    # the teacher's encoder-tap Grams run on side2 (after its ReviewKD-encoder work) as soon as
-    # the teacher encoder is done, keeping them off the teacher chain — the step's critical path.
-    # (Four streams in all: GPU_MAX_HW_QUEUES is 4, a fifth would share a hardware queue.)
-    tgram = side2
-
-    def fork_teacher_grams(enc):
-        ev = torch.cuda.Event()
-        ev.record(tstream)
-        with torch.cuda.stream(tgram):
-            tgram.wait_event(ev)
-            held["g_te"] = ops.GramSlabs([_gram_bftc(a) for a in enc], B)
-            _mark("tgram: teacher enc grams done", tgram)
-
-    with torch.cuda.stream(tstream):
-        # the teacher's last decoder layer, mask and iSTFT are dead for the loss: stop at its taps
-        tf = teacher.run(X, train=teacher.training, bn_updates=1, spec=spec, want_masks=False,
-                         on_encoder=fork_teacher_grams, taps_only=True)
-        _mark("teacher: done", tstream)
-        t_dec = [tf["dec_in"]] + tf["dec"][:5]
-        Cht = tf["dec_in"].shape[-1] // 2
-        g_td = ops.GramSlabs([_gram_bftc(a) for a in t_dec] +
-                             [_gram_bftc(tf["dec_in"], 0, Cht), _gram_bftc(tf["dec_in"], Cht, Cht)],
-                             B)
-        _mark("teacher: grams done", tstream)
     g_t = _SlabRefs(held["g_te"].refs + g_td.refs, (held["g_te"], g_td))
     main.wait_stream(tstream)
     main.wait_stream(side)

@@ -351,13 +351,16 @@ class DCCRN(nn.Module):
         return spec
 
     def run(self, x, train=True, bn_updates=1, spec=None, want_masks=True, on_encoder=None,
-            tape=None, taps_only=False):
+            tape=None, taps_only=False, mark=None, on_decoder_tap=None):
         """Full forward on the HIP device.  Returns a dict of BFTC buffers and NCHW views.
         on_encoder(enc): called (on the launching stream) right after the encoder, so a caller can
         fork work that only needs the encoder taps before the LSTM and decoder are enqueued.
         tape: a dict that receives what the backward pass (clskd.backward) needs — pre-BN conv
         outputs kept beside the activations, BN coefficients and batch statistics, the LSTM gate
         inputs and hidden histories, the iSTFT frames.
+        on_decoder_tap(t): called (on the launching stream) as each decoder-side tap exists —
+        dec_in, then decoder outputs 0..nl-2 — so a consumer (ReviewKD-decoder) can pipeline
+        behind the decoder on another stream.
         taps_only: stop after the taps a distillation step reads (encoder outputs, dec_in,
         decoder outputs 0..nl-2): the last decoder layer, mask 'E' and ConviSTFT are dead for
         the CLSKD loss (SURVEY.md §8 d) and are skipped — out_wav is None."""
@@ -415,6 +418,8 @@ class DCCRN(nn.Module):
                                     alpha=pr.weight, partial=(part, nmb) if train else None)
                 enc.append(raw)
             F = Fo
+        if mark is not None:
+            mark("encoder done")
         if on_encoder is not None:
             on_encoder(enc)
         # ---------------- complex LSTM (DCCRN.py:178-199, tools_for_model.py:159-174)
@@ -459,6 +464,10 @@ class DCCRN(nn.Module):
             wpp, bp = packs[3 + 2 * half], packs[4 + 2 * half]
             ops.conv(segs, [(0, 0)], B, 1, T, P, wpp, bp,
                      dec_in, OutMap(D4 * T * C6, 0, C6, 1, T * C6, D4), out_offset=half * Ch)
+        if mark is not None:
+            mark("lstm + projection done")
+        if on_decoder_tap is not None:
+            on_decoder_tap(dec_in)
         # ---------------- decoder (DCCRN.py:201-206, tools_for_model.py:303-330), polyphase
         dec = []
         out_t, out_t0, out_T = dec_in, 0, T
@@ -505,6 +514,8 @@ class DCCRN(nn.Module):
             elif tape is not None:
                 tape.setdefault("dec_bn", []).append(None)
             dec.append(raw)
+            if on_decoder_tap is not None and d < nl - 1:
+                on_decoder_tap(raw)
             out_t, out_t0, out_T = raw, 1, T
             F = 2 * F
         nchw = lambda t: t.permute(0, 3, 1, 2)
