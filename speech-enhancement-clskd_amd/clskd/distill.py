@@ -46,6 +46,9 @@ _RKD_DEC = os.environ.get("CLSKD_RKD_DEC", "after")
 # host enqueue order of the step's two chains (A/B knob): "1" enqueues the teacher chain — the
 # critical path — before the student-side chains
 _TEACHER_FIRST = os.environ.get("CLSKD_TEACHER_FIRST", "1") == "1"
+# A/B knob: CLSKD_RKD_FORK=1 forks every ReviewKD conv2 (+ BN, Grams) onto the caller's stream
+# (measured: 6.18 vs 6.08 ms per C2 step, the step is throughput- not chain-bound — off)
+_RKD_FORK = os.environ.get("CLSKD_RKD_FORK", "0") == "1"
 
 
 _SERIAL = False
@@ -254,13 +257,18 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     # ReviewKD: distill.py:92-96, tap contract SURVEY.md §8 a11.
     held = {}
     tapes = dict(s={}, re=[], rd=[], ms=[]) if tape else None
+    # the ReviewKD conv2s (+ BN, SPKD Grams) run on the caller's stream, which is otherwise idle
+    # between the teacher's encoder Grams and the join: they are off the level-to-level residual
+    # chain of the fusions (framework.py:254-261), which stays on side / side2
+    c2 = main if _RKD_FORK else None
     if reinit is not None:  # fresh ABF modules (distill.py:92-96): only ReviewKD reads them
         with torch.cuda.stream(side2):
             reinit("encoder")
 
     # SPKD Gram partials run on the stream that produced their features, as soon as those
-    # exist (side2: ReviewKD-encoder maps, side: ReviewKD-decoder maps + student dec_in halves,
-    # main: teacher taps); one finalize on main after the join (framework.py:150-172).
+    # exist (main: ReviewKD maps (conv2 fork) + student dec_in halves and the teacher's encoder
+    # taps; tstream: teacher decoder taps); one finalize on main after the join
+    # (framework.py:150-172).
     def fork_review_encoder(enc):
         ev = torch.cuda.Event()
         ev.record(side)
@@ -268,11 +276,13 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
             side2.wait_event(ev)
             _mark("side2: student encoder ready", side2)
             s_enc = review_encoder.forward_bftc(enc, defer_bn=True,
-                                                tape=tapes["re"] if tapes else None)
+                                                tape=tapes["re"] if tapes else None,
+                                                conv2_stream=c2)
             _mark("side2: review encoder done", side2)
             held["s_enc"] = s_enc
+        with torch.cuda.stream(c2 or side2):
             held["g_enc"] = ops.GramSlabs([_gram_bftc(a) for a in s_enc], B)
-            _mark("side2: enc grams done", side2)
+            _mark("enc grams done", c2 or side2)
 
     # ReviewKD-decoder pipelined behind the student decoder on the caller's stream: level j
     # (framework.py:254-261, forward order) starts as soon as its student tap exists
@@ -314,9 +324,10 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
                 if reinit is not None:
                     reinit("decoder")
                 rd["outs"] = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5],
+                                                         conv2_stream=c2,
                                                          defer_bn=True,
                                                          tape=tapes["rd"] if tapes else None)
-        rstream = main if pipelined else side
+        rstream = main if pipelined else (c2 or side)
         with torch.cuda.stream(rstream):
             s_dec = rd["outs"]
             assert len(s_dec) == len(review_decoder.abfs)

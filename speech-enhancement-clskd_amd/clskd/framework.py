@@ -247,12 +247,15 @@ class ABF(nn.Module):
         return ent[1]
 
     def forward_bftc(self, x, y=None, shape=None, out_shape=None, train=None, defer_bn=False,
-                     tape=None):
+                     tape=None, conv2_stream=None):
         """x: BFTC [B][F][T][Cin]; y: BFTC residual [B][Fr][Tr][mid].  Returns (out, x_fused) BFTC.
         defer_bn: conv2's BatchNorm is left unapplied — out is an ops.DeferredBN (raw output +
         coefficients) for a consumer that folds the affine into its loads (the SPKD Gram).
         tape: a dict receiving what ABF.backward_bftc needs (raw conv outputs, BN coefficients and
-        batch statistics, the fused map and the residual)."""
+        batch statistics, the fused map and the residual).
+        conv2_stream: run the 3x3 conv2 and its BatchNorm on this stream (after the fused map
+        exists) — it is off the level-to-level residual chain, which then continues on the
+        current stream; `out` belongs to conv2_stream."""
         train = self.training if train is None else train
         if tape is not None and not train:
             raise ValueError("ABF tape (backward) needs train-mode BatchNorm")
@@ -302,6 +305,20 @@ class ABF(nn.Module):
         if Tn != out_shape and Fn != out_shape:
             raise NotImplementedError(
                 f"ABF output interpolation to ({out_shape}, {Tn}) from F={Fn} is not on the CLSKD path")
+        if conv2_stream is not None:
+            ev = torch.cuda.Event()
+            ev.record()
+            x1.record_stream(conv2_stream)
+            conv2_stream.wait_event(ev)
+            with torch.cuda.stream(conv2_stream):
+                return self._conv2_bftc(x1, w2p, train, defer_bn, tape, nmb)
+        return self._conv2_bftc(x1, w2p, train, defer_bn, tape, nmb)
+
+    def _conv2_bftc(self, x1, w2p, train, defer_bn, tape, nmb):
+        B, Fn, Tn, _ = x1.shape
+        dev = x1.device
+        act = dict(device=dev, dtype=self.act_dtype)
+        f64 = dict(device=dev, dtype=torch.float64)
         Cout = w2p.shape[0]
         out = torch.empty(B, Fn, Tn, Cout, **act)
         part2 = torch.empty(nmb * Cout * 2, **f64) if train else None
@@ -351,22 +368,25 @@ class ReviewKD(nn.Module):
             abf.compute = compute
         return self
 
-    def forward_bftc(self, feats, defer_bn=False, tape=None):
+    def forward_bftc(self, feats, defer_bn=False, tape=None, conv2_stream=None):
         """feats: BFTC student features in the reference's list order.  Returns BFTC outputs
         (ops.DeferredBN entries when defer_bn: the ABF output BatchNorms left for the consumer).
-        tape: a list receiving one ABF tape dict per level, in processing order."""
+        tape: a list receiving one ABF tape dict per level, in processing order.
+        conv2_stream: every level's conv2 + BatchNorm runs there (ABF.forward_bftc); the outputs
+        belong to that stream."""
         xs = feats[::-1] if self.ft_type == "encoder" else list(feats)
         results = []
         tp = {} if tape is not None else None
         out, res = self.abfs[0].forward_bftc(xs[0], out_shape=self.out_shapes[0],
-                                             defer_bn=defer_bn, tape=tp)
+                                             defer_bn=defer_bn, tape=tp, conv2_stream=conv2_stream)
         if tape is not None:
             tape.append(tp)
         results.append(out)
         for feature, abf, shape, out_shape in zip(xs[1:], self.abfs[1:], self.shapes[1:],
                                                   self.out_shapes[1:]):
             tp = {} if tape is not None else None
-            out, res = abf.forward_bftc(feature, res, shape, out_shape, defer_bn=defer_bn, tape=tp)
+            out, res = abf.forward_bftc(feature, res, shape, out_shape, defer_bn=defer_bn, tape=tp,
+                                        conv2_stream=conv2_stream)
             if tape is not None:
                 tape.append(tp)
             if self.ft_type == "encoder":

@@ -78,6 +78,8 @@ struct HaloArgs {
   int32_t nblk128;                 // statistics slots (ceil(M/128))
   int32_t tap_pix[16];             // halo pixel offset of tap t for output (0, 0)
   int32_t tap_k[16];               // k offset of tap t (t * ctot)
+  int32_t stats_ld;                // channels per statistics slot row (N, or the full N of a
+                                   // column-split launch whose stats pointer is pre-offset)
 };
 
 // Kernel arguments are re-read by the compiler under SGPR pressure (s_load inside the loop),
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const HaloArgs a) {
   if (tid < 16) ttab[tid] = a.tap_pix[tid] | (a.tap_k[tid] << 16);
   if (d.stats) {
     for (int64_t s = (int64_t)blockIdx.x + gridDim.x; s < a.nblk128; s += gridDim.x)
-      for (int i = tid; i < d.N * 2; i += 512) d.stats[s * d.N * 2 + i] = 0.0;
+      for (int i = tid; i < d.N * 2; i += 512) d.stats[s * a.stats_ld * 2 + i] = 0.0;
   }
   float bcol[NB];
   int64_t coff[NB];
@@ -363,8 +365,8 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const HaloArgs a) {
           S += red[(w * BN + n) * 2];
           Q += red[(w * BN + n) * 2 + 1];
         }
-        d.stats[((int64_t)blockIdx.x * d.N + n) * 2] = S;
-        d.stats[((int64_t)blockIdx.x * d.N + n) * 2 + 1] = Q;
+        d.stats[((int64_t)blockIdx.x * a.stats_ld + n) * 2] = S;
+        d.stats[((int64_t)blockIdx.x * a.stats_ld + n) * 2 + 1] = Q;
       }
     }
   }
@@ -426,14 +428,50 @@ static bool halo_plan(const clskd_conv_desc& d, HaloArgs& a, size_t& lds) {
   if (nt < 32 || nt > (1 << 30)) return false;
   a.ntiles = (int)nt;
   a.nblk128 = (int)cdiv((int64_t)d.B * d.Fo * d.To, 128);
+  a.stats_ld = d.N;
   return true;
 }
 
+static int launch_halo_planned(const HaloArgs& a, size_t lds, hipStream_t st, bool* launched);
+
+// Layers with 32 < N <= 64 whose [64][K] weight block does not fit LDS beside the halo buffers
+// (the teacher's 64-channel decoder layer: K = 6 x 256) run as two 32-column launches; each
+// re-reads the input halo (~N/K of the staged-bytes saving is kept) but stays on the halo path
+// instead of the im2col engine.  Output columns, bias and the statistics slots of the second
+// launch are offset by 32 (statistics rows keep the full N as leading dimension).
 int launch_conv_halo(const clskd_conv_desc& d, hipStream_t st, bool* launched) {
   HaloArgs a;
   size_t lds = 0;
   *launched = false;
-  if (!halo_plan(d, a, lds)) return CLSKD_OK;
+  if (halo_plan(d, a, lds)) return launch_halo_planned(a, lds, st, launched);
+  if (d.N <= 32 || d.N > 64 || d.nlo < d.N || d.in_dtype != CLSKD_BF16) return CLSKD_OK;
+  HaloArgs a2;
+  size_t lds2 = 0;
+  clskd_conv_desc d1 = d, d2 = d;
+  d1.N = 32;
+  d2.N = d.N - 32;
+  d2.weight = reinterpret_cast<const __bf16*>(d.weight) + (int64_t)32 * d.K;
+  if (d.bias) d2.bias = d.bias + 32;
+  const size_t osz = d.out_dtype == CLSKD_F32 ? 4 : 2;
+  d2.out = reinterpret_cast<char*>(d.out) + (int64_t)32 * d.oNlo * (int64_t)osz;
+  if (d.stats) d2.stats = d.stats + 64;
+  if (!halo_plan(d1, a, lds) || !halo_plan(d2, a2, lds2)) return CLSKD_OK;
+  a.stats_ld = a2.stats_ld = d.N;
+  bool l1 = false, l2 = false;
+  int rc = launch_halo_planned(a, lds, st, &l1);
+  if (rc != CLSKD_OK || !l1) return rc;
+  rc = launch_halo_planned(a2, lds2, st, &l2);
+  if (rc == CLSKD_OK && !l2) {
+    set_error("conv halo: second column half not launchable");
+    return CLSKD_E_ARG;
+  }
+  *launched = true;
+  return rc;
+}
+
+static int launch_halo_planned(const HaloArgs& a, size_t lds, hipStream_t st, bool* launched) {
+  const clskd_conv_desc& d = a.d;
+  *launched = false;
   static int ncu = [] {
     int v = 256;
     (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, 0);

@@ -172,6 +172,9 @@ HALO_CASES = {
     "abf3x3_n64": ((64,), 64, [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], 1, 24, 24, 1, 0, True),
     "enc5x2_s2": ((32,), 64, [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)], 2, 48, 24, 1, 0, True),
     "dec_parity1": ((32, 32), 32, [(dF, -kt) for dF in (1, 0) for kt in (0, 1)], 1, 24, 24, 2, 1, False),
+    # [64][1536] weights exceed LDS beside the halo buffers: two 32-column launches
+    "dec_parity0_n64_split": ((128, 128), 64, [(dF, -kt) for dF in (1, 0, -1) for kt in (0, 1)], 1,
+                              24, 24, 2, 0, True),
 }
 
 
@@ -210,6 +213,7 @@ def test_conv_halo_kernel_against_torch(case):
     st = torch.full((nblk * N * 2,), float("nan"), device=DEV, dtype=torch.float64)
     ops.conv([ops.seg_bftc(s.to(DEV)) for s in segs_h], taps, B, Fo, T, N, wp, bias.to(DEV), out,
              ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add), stride_f=sf, stats=st)
+    assert ops.conv_kernel_of_last_launch().startswith("conv_halo_kernel"), ops.conv_kernel_of_last_launch()
     o = out.double().cpu()[:, of_add::of_mul]
     tol = 8e-3 if out_bf16 else 1e-4
     np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=tol, atol=tol)
