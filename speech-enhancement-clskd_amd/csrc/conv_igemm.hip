@@ -315,6 +315,8 @@ int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st);
 
 int launch_conv_direct(const clskd_conv_desc& d, hipStream_t st);
 
+int launch_conv_pointwise(const clskd_conv_desc& d, hipStream_t st, bool* launched);
+
 }  // namespace clskd
 
 using namespace clskd;
@@ -370,6 +372,15 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
     if (rc != CLSKD_OK) return rc;
     CLSKD_LAUNCH_CHECK("conv2d_bf16");
     return CLSKD_OK;
+  }
+  {  // 1x1 channel lifts with short K: the streaming pointwise kernel (conv_pointwise.hip)
+    bool launched = false;
+    const int rc = launch_conv_pointwise(d, st, &launched);
+    if (rc != CLSKD_OK) return rc;
+    if (launched) {
+      CLSKD_LAUNCH_CHECK("conv2d_pointwise");
+      return CLSKD_OK;
+    }
   }
   ConvArgs a{d};
   const size_t ctab_bytes = (size_t)(d.K / 4) * 8;  // VEC4 K-chunk table (dynamic LDS)
