@@ -7,7 +7,7 @@ A step = one KnowledgeDistillation.training_step (distill.py:72-148) over B=16 s
 4 s noisy/clean pairs per GPU: teacher + student DCCRN forwards (train-mode BN), ReviewKD
 fusions, 14 SPKD Gram losses and the MRSTFT base loss; frames = B * T with T = L/100 + 3 = 643.
 Each rank processes its own batch shard (weak scaling; forward+loss has no exchange step).
-The step runs on three HIP streams (teacher | student -> ReviewKD-decoder | ReviewKD-encoder ->
+The step runs on four HIP streams (caller | teacher | student -> ReviewKD-decoder | ReviewKD-encoder ->
 MRSTFT), launched eagerly (the host enqueues ahead of the device); --graph replays a captured
 hipGraph of the same step instead (clskd.graph.StepGraph: every replay recomputes the step from
 the batch copied into its static inputs).
@@ -54,8 +54,8 @@ def build_kd(dev, abf_reinit, precision="fp32"):
 
 def cpu_baseline(seconds):
     """The CPU oracle (fp32 PyTorch-CPU restatement of the reference, oracle/ref_cpu.py) timed on
-    this host on a bounded sample of the same workload: B=2 x 4 s clips per step, repeated until
-    `seconds` of CPU work."""
+    this host on a bounded sample of the same workload: the same B=16 x 4 s step as the GPU leg
+    (one warm-up step at B=2), repeated until `seconds` of CPU work (at least one step)."""
     from oracle import ref_cpu as R
     from clskd.data import synthetic_pairs
     from clskd.weights import ABF_SEED, STUDENT_SEED, TEACHER_SEED, recipe_state_dict
@@ -65,11 +65,11 @@ def cpu_baseline(seconds):
     ps = R.to_torch_params(recipe_state_dict(cfg.dccrn_param_shapes(**cfg.STUDENT), STUDENT_SEED))
     pa = R.to_torch_params(recipe_state_dict(
         {**cfg.review_param_shapes("encoder"), **cfg.review_param_shapes("decoder")}, ABF_SEED))
-    Bc = 2
+    Bc = B_PER_GPU
     noisy, clean = synthetic_pairs(Bc, L, seed=99)
     X, Y = torch.from_numpy(noisy), torch.from_numpy(clean)
     with torch.no_grad():
-        R.clskd_step(pt, ps, pa, X, Y)  # warm-up
+        R.clskd_step(pt, ps, pa, X[:2], Y[:2])  # warm-up
         n, t0 = 0, time.perf_counter()
         while True:
             R.clskd_step(pt, ps, pa, X, Y)
@@ -79,8 +79,10 @@ def cpu_baseline(seconds):
                 break
     frames = n * Bc * cfg.n_frames(L)
     return dict(value=round(frames / el, 2), unit="frames/s", cores=threads, kind="port",
-                sample=f"oracle/ref_cpu.clskd_step, B={Bc} x 4 s @16 kHz, {n} step(s) in {el:.1f} s, "
-                       f"fp32, torch CPU {threads} threads")
+                batch=Bc,
+                sample=f"oracle/ref_cpu.clskd_step on the bench workload (B={Bc} x 4 s @16 kHz, "
+                       f"same step as the GPU leg), {n} step(s) in {el:.1f} s, fp32, torch CPU "
+                       f"{threads} threads")
 
 
 def main():
@@ -174,7 +176,7 @@ def main():
     if (not args.graph):
         ktimes = ops.KernelTimer.stop()
         timing = ("HIP events around every launch of the dominant conv kernel inside the timed "
-                  "region (3 concurrent streams: a launch's event span includes time it shares the "
+                  "region (4 concurrent streams: a launch's event span includes time it shares the "
                   "CUs); dominant = largest total isolated time in the census step (the last "
                   "warm-up step run on one stream, every conv launch timed: conv_all_kernels)")
         if census is None:
@@ -235,6 +237,9 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not args.train:
             cpu = cpu_baseline(args.cpu_seconds)
+            # GPU / CPU-oracle ratio on the same workload.  `vs_baseline` stays null: it is
+            # reserved for a published number for this metric, and BASELINE.md has none
+            cpu["gpu_over_cpu"] = round(frames / el / cpu["value"], 1)
         workload = ("C2: DCCRN-CLSKD fwd+loss (teacher 3.67M + student 0.23M params, ReviewKD "
                     "enc+dec, 14 SPKD Grams, MRSTFT)")
         if args.train:
@@ -258,7 +263,8 @@ def main():
                        "global_batch": world * B_PER_GPU, "per_gpu_batch": B_PER_GPU,
                        "clip_samples": L, "frames_per_clip": T, "parallelism": f"dp{world}",
                        "abf_reinit": args.abf_reinit, "loss": round(loss_v, 6),
-                       "launch": ("eager, 3 HIP streams" if (not args.graph)
+                       "launch": ("eager, 4 HIP streams (caller, teacher, student, ReviewKD-"
+                                  "encoder/MRSTFT)" if (not args.graph)
                                   else "hipGraph replay (clskd.graph.StepGraph)"),
                        "precision": ("teacher+ReviewKD GEMMs bf16 MFMA operands / fp32 accumulate; "
                                      "student, STFT/iSTFT, LSTM recurrence, BN, losses fp32")

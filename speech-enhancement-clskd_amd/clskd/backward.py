@@ -427,6 +427,12 @@ def review_backward(review, tape, coef_m, d_feats, acc_feats):
     for j in range(n - 1, -1, -1):
         tp = tape[j]
         abf = review.abfs[j]
+        if "wver" in tp and tp["wver"] != abf.param_versions():
+            # same contract as autograd's saved-tensor version check: the ABF weights this
+            # tape's forward used were rewritten (a later step's re-draw) before its backward
+            raise RuntimeError(
+                "ReviewKD ABF weights were modified in place (abf_reinit='step' re-draw) after the "
+                "forward that recorded this tape; run its backward before the next step's forward")
         dev = tp["x1"].device
         out_raw = tp["out_raw"]
         Bn, Fn, Tn, Cout = out_raw.shape

@@ -194,6 +194,9 @@ class ABF(nn.Module):
             ps += [self.att_conv[0].weight, self.att_conv[0].bias]
         return ps
 
+    def param_versions(self):
+        return tuple(p._version for p in self._params())
+
     def redraw_jobs(self):
         """Draw jobs (clskd_uniform_redraw) re-initialising this ABF like framework.py:179-195:
         conv1/conv2 kaiming_uniform(a=1) -> U(+-sqrt(3/fan_in)); att_conv default Conv2d init ->
@@ -274,7 +277,9 @@ class ABF(nn.Module):
         mv1 = torch.empty(2, mid, device=dev, dtype=torch.float32) if tape is not None else None
         so1 = (mv1[0], mv1[1]) if tape is not None else None
         if tape is not None:
-            tape.update(x_in=x, x1=x1, mv1=mv1, res=y)
+            # versions of the weights this forward used: a re-draw (abf_reinit='step') before the
+            # backward rewrites them in place, which backward.review_backward refuses
+            tape.update(x_in=x, x1=x1, mv1=mv1, res=y, wver=self.param_versions())
         if self.att_conv is not None:
             if shape != Fn:  # the reference's torch.cat would fail as well (framework.py:213-216)
                 raise ValueError(f"ABF fuse: residual upsampled to F={shape} but x has F={Fn}")

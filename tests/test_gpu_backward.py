@@ -130,7 +130,8 @@ def _kd(precision="fp32"):
     from clskd.model import DCCRN
     t = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.TEACHER), TEACHER_SEED)
     s = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.STUDENT), STUDENT_SEED)
-    kd = KnowledgeDistillation(t.train(), s.train(), precision=precision).to(DEV)
+    kd = KnowledgeDistillation(t.train(), s.train(), abf_reinit="once",
+                               precision=precision).to(DEV)
     apply_recipe(kd.review_encoder, ABF_SEED, "encoder.")
     apply_recipe(kd.review_decoder, ABF_SEED, "decoder.")
     return kd
@@ -241,6 +242,28 @@ def test_autograd_dropin_and_train_step():
     # the packed-weight caches see the update: the next forward uses the new weights
     l2 = kd.training_step((X, y), 0, return_parts=True)["loss"].item()
     assert l2 != loss.item()
+
+
+def test_backward_refuses_redrawn_abf_weights():
+    """abf_reinit='step' re-draws the ABF weights in place at every forward: the backward of an
+    older tape must refuse (autograd's saved-tensor version check), the newest tape still runs."""
+    from clskd.data import synthetic_pairs
+    from clskd.distill import KnowledgeDistillation
+    from clskd.model import DCCRN
+    noisy, clean = synthetic_pairs(2, 8000, seed=24)
+    X, y = torch.from_numpy(noisy).to(DEV), torch.from_numpy(clean).to(DEV)
+    t = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.TEACHER), TEACHER_SEED)
+    s = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.STUDENT), STUDENT_SEED)
+    kd = KnowledgeDistillation(t.train(), s.train()).to(DEV)
+    assert kd.abf_reinit == "step"  # the reference's semantics are the default
+    old = kd.forward_with_tape(X, y)
+    new = kd.forward_with_tape(X, y)
+    grads = {p: torch.empty_like(p) for p in kd.student.parameters()}
+    with pytest.raises(RuntimeError, match="modified in place"):
+        kd.backward_into(old, grads)
+    kd.backward_into(new, grads)
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(g).all() for g in grads.values())
 
 
 def test_clskd_backward_mixed_precision_close_to_fp32():

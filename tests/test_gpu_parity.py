@@ -347,7 +347,8 @@ def test_feature_extraction_api():
 # ------------------------------------------------------------------------------------------
 def _kd(abf_seed=ABF_SEED):
     from clskd.distill import KnowledgeDistillation
-    kd = KnowledgeDistillation(_models("teacher").train(), _models("student").train()).to(DEV)
+    kd = KnowledgeDistillation(_models("teacher").train(), _models("student").train(),
+                               abf_reinit="once").to(DEV)
     apply_recipe(kd.review_encoder, abf_seed, "encoder.")
     apply_recipe(kd.review_decoder, abf_seed, "decoder.")
     return kd
