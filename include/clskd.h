@@ -221,6 +221,29 @@ int clskd_abf_fuse(const void* x, const void* res, int32_t B, int32_t F, int32_t
                    void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * ABF level with conv1 folded (framework.py:179-222, replaces ABF.conv1's nn.Conv2d(1x1) +
+ * nn.BatchNorm2d and the fuse above): conv1's 64-channel output never reaches HBM.
+ *   s:  student tap, fp32 BFTC rows [B][F][T][cin] at element strides (sB, sF, sT), channels
+ *       contiguous, 16-B aligned rows; cin in {8, 16, 32, 64}; w1: conv1 weight [64][cin] fp32.
+ * clskd_abf_bn1_partials: partial[nblk][64][2] (fp64) = {sum, sumsq} of x1 = W1 s over block
+ *   `blk`'s rows, from that block's moments S1 = sum s, S2 = sum s s^T (sum_n = w_n.S1,
+ *   sumsq_n = w_n^T S2 w_n): the fused-statistics contract of the conv engines, finalised by
+ *   clskd_bn_compact / clskd_bn_finalize.  nblk = clskd_abf_moment_blocks(B*F*T, cin).
+ * clskd_abf_conv1_fuse: out[r] = x(r) := (W1 s[r])*scale + shift, or with a residual
+ *   res [B][Fr][Tr][64] the attention fusion of clskd_abf_fuse applied to x(r); x1_raw
+ *   (optional) receives W1 s[r] (the training tape).  out / x1_raw / res storage: `dtype`.
+ * -------------------------------------------------------------------------------------- */
+int32_t clskd_abf_moment_blocks(int64_t rows, int32_t cin);
+int clskd_abf_bn1_partials(const float* s, int32_t B, int32_t F, int32_t T, int64_t sB,
+                           int64_t sF, int64_t sT, int32_t cin, const float* w1, double* partial,
+                           int32_t nblk, void* stream);
+int clskd_abf_conv1_fuse(const float* s, int32_t B, int32_t F, int32_t T, int64_t sB, int64_t sF,
+                         int64_t sT, int32_t cin, const float* w1, const float* scale,
+                         const float* shift, const void* res, int32_t Fr, int32_t Tr,
+                         const float* w, const float* b, void* out, void* x1_raw, int32_t dtype,
+                         void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Uniform weight re-draw (replaces the per-step ABF rebuild of framework.py:194-195 —
  * nn.init.kaiming_uniform_(w, a=1) on conv1/conv2 and Conv2d.reset_parameters on att_conv —
  * and the repacking of the drawn weights).  Job k draws numel values U(-bound, bound) into

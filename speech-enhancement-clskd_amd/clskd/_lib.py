@@ -91,6 +91,11 @@ SIGNATURES = {
     "clskd_ola": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p]),
     "clskd_abf_fuse": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _i32,
                               _p]),
+    "clskd_abf_moment_blocks": (_i32, [_i64, _i32]),
+    "clskd_abf_bn1_partials": (_i32, [_p, _i32, _i32, _i32, _i64, _i64, _i64, _i32, _p, _p, _i32,
+                                      _p]),
+    "clskd_abf_conv1_fuse": (_i32, [_p, _i32, _i32, _i32, _i64, _i64, _i64, _i32, _p, _p, _p, _p,
+                                    _i32, _i32, _p, _p, _p, _p, _i32, _p]),
     "clskd_gram_partial": (_i32, [_p, _i32, _i32, _p, _p]),
     "clskd_spkd_finalize": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
     "clskd_uniform_redraw": (_i32, [_p, _i32, C.c_uint64, _p, _p]),

@@ -6,6 +6,7 @@ tensors; BFTC buffers produced by ``clskd.DCCRN`` (exposed as permuted NCHW view
 without copies.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -13,6 +14,9 @@ import torch.nn as nn
 
 from . import ops
 from .ops import OutMap, Seg, SegGeom, seg_bftc
+
+# ABF conv1 folded into its consumers (clskd_abf_*; CLSKD_ABF_FOLD=0: the materialising path)
+_ABF_FOLD = os.environ.get("CLSKD_ABF_FOLD", "1") != "0"
 
 # --------------------------------------------------------------------------------------------
 # helpers
@@ -265,10 +269,59 @@ class ABF(nn.Module):
         B, Fn, Tn, Cin = x.shape
         w1p, w2p, att = self._weights(x.dtype)
         mid = w1p.shape[0]
+        nmb = ops.conv_mblocks(B, Fn, Tn)
+        if _ABF_FOLD and mid == 64 and ops.abf_tap_ok(x):
+            x1 = self._level_folded(x, y, shape, att, train, tape)
+        else:
+            x1 = self._level_conv1(x, y, shape, w1p, att, train, tape, nmb)
+        if Tn != out_shape and Fn != out_shape:
+            raise NotImplementedError(
+                f"ABF output interpolation to ({out_shape}, {Tn}) from F={Fn} is not on the CLSKD path")
+        if conv2_stream is not None:
+            ev = torch.cuda.Event()
+            ev.record()
+            x1.record_stream(conv2_stream)
+            conv2_stream.wait_event(ev)
+            with torch.cuda.stream(conv2_stream):
+                return self._conv2_bftc(x1, w2p, train, defer_bn, tape, nmb)
+        return self._conv2_bftc(x1, w2p, train, defer_bn, tape, nmb)
+
+    def _level_folded(self, x, y, shape, att, train, tape):
+        """conv1 + BN1 [+ attention fusion] with conv1 folded (clskd_abf_*): the BatchNorm
+        statistics of W1 x come from x's moments and the fused kernel recomputes W1 x per row,
+        so conv1's 64-channel output never reaches HBM (only the raw copy the tape keeps)."""
+        B, Fn, Tn, Cin = x.shape
+        dev = x.device
+        act = dict(device=dev, dtype=self.act_dtype)
+        w1 = self.conv1[0].weight
+        bn = self.conv1[1]
+        mv1 = torch.empty(2, 64, device=dev, dtype=torch.float32) if tape is not None else None
+        coef = ops.abf_bn1_coef(x, w1, bn, train,
+                                stats_out=(mv1[0], mv1[1]) if tape is not None else None)
+        res = None
+        if self.att_conv is not None:
+            if shape != Fn:  # the reference's torch.cat would fail as well (framework.py:213-216)
+                raise ValueError(f"ABF fuse: residual upsampled to F={shape} but x has F={Fn}")
+            res = y if y.dtype == act["dtype"] else y.to(act["dtype"])
+            res = res.contiguous()
+        xf = torch.empty(B, Fn, Tn, 64, **act)
+        x1_raw = torch.empty(B, Fn, Tn, 64, **act) if tape is not None else None
+        ops.abf_conv1_fuse(x, w1, coef, res, att, xf, x1_raw)
+        if tape is not None:
+            # versions of the weights this forward used: a re-draw (abf_reinit='step') before the
+            # backward rewrites them in place, which backward.review_backward refuses
+            tape.update(x_in=x, x1=x1_raw, mv1=mv1, res=res, coef1=coef,
+                        wver=self.param_versions())
+        return xf
+
+    def _level_conv1(self, x, y, shape, w1p, att, train, tape, nmb):
+        """conv1 as a pointwise conv with its 64-channel output materialised (fallback for taps
+        the folded kernels cannot read in place; CLSKD_ABF_FOLD=0 selects it everywhere)."""
+        B, Fn, Tn, Cin = x.shape
+        mid = w1p.shape[0]
         dev = x.device
         act = dict(device=dev, dtype=self.act_dtype)
         x1 = torch.empty(B, Fn, Tn, mid, **act)
-        nmb = ops.conv_mblocks(B, Fn, Tn)
         f64 = dict(device=dev, dtype=torch.float64)
         part = torch.empty(nmb * mid * 2, **f64) if train else None
         ops.conv([seg_bftc(x)], [(0, 0)], B, Fn, Tn, mid, w1p, None, x1,
@@ -307,17 +360,7 @@ class ABF(nn.Module):
             ops.batch_norm_bftc(x1, x1, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                 train, bn.momentum, bn.eps, 1,
                                 partial=(part, nmb) if train else None)
-        if Tn != out_shape and Fn != out_shape:
-            raise NotImplementedError(
-                f"ABF output interpolation to ({out_shape}, {Tn}) from F={Fn} is not on the CLSKD path")
-        if conv2_stream is not None:
-            ev = torch.cuda.Event()
-            ev.record()
-            x1.record_stream(conv2_stream)
-            conv2_stream.wait_event(ev)
-            with torch.cuda.stream(conv2_stream):
-                return self._conv2_bftc(x1, w2p, train, defer_bn, tape, nmb)
-        return self._conv2_bftc(x1, w2p, train, defer_bn, tape, nmb)
+        return x1
 
     def _conv2_bftc(self, x1, w2p, train, defer_bn, tape, nmb):
         B, Fn, Tn, _ = x1.shape

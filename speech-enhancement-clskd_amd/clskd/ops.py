@@ -470,6 +470,90 @@ def abf_fuse(x, res, w, b, out, x_coef=None):
     return out
 
 
+ABF_CIN = (8, 16, 32, 64)
+
+
+def abf_tap_ok(x):
+    """Can the folded-conv1 ABF kernels read this student tap in place?  (fp32 BFTC rows,
+    channels contiguous, 16-B aligned rows, cin in ABF_CIN, 32-bit element offsets)."""
+    if x.dtype != torch.float32 or x.dim() != 4 or x.shape[-1] not in ABF_CIN or x.stride(3) != 1:
+        return False
+    B, F, T, C = x.shape
+    sB, sF, sT, _ = x.stride()
+    if x.data_ptr() % 16 or sB % 4 or sF % 4 or sT % 4:
+        return False
+    return B * F * T < 2 ** 31 and (B - 1) * sB + (F - 1) * sF + (T - 1) * sT + C < 2 ** 31
+
+
+def abf_bn1_coef(x, w1, bn, train, stats_out=None):
+    """conv1 BatchNorm of an ABF level from the tap's moments (clskd_abf_bn1_partials, then the
+    common finalize; eval: running statistics).  Returns [scale | shift] (64 + 64 fp32) and
+    updates the running statistics like every other train-mode BatchNorm."""
+    L = lib()
+    B, F, T, C = x.shape
+    rows = B * F * T
+    dev = x.device
+    mid = w1.shape[0]
+    coef = torch.empty(2 * mid, device=dev, dtype=torch.float32)
+    scale = coef.data_ptr()
+    shift = scale + 4 * mid
+    st = _stream()
+    if not train:
+        check(L.clskd_bn_eval_coeffs(ptr(bn.running_mean), ptr(bn.running_var), ptr(bn.weight),
+                                     ptr(bn.bias), bn.eps, mid, scale, shift, st), "bn_eval")
+        return coef
+    nblk = int(L.clskd_abf_moment_blocks(rows, C))
+    part = torch.empty(nblk * mid * 2, device=dev, dtype=torch.float64)
+    sB, sF, sT, _ = x.stride()
+    check(L.clskd_abf_bn1_partials(ptr(x), B, F, T, sB, sF, sT, C, ptr(w1.reshape(mid, C)),
+                                   ptr(part), nblk, st), "abf_bn1_partials")
+    return bn_coef_from_partials(part, nblk, rows, mid, bn, coef, stats_out)
+
+
+def bn_coef_from_partials(part, nblk, rows, C, bn, coef, stats_out=None):
+    """Train-mode BatchNorm coefficients [scale | shift] into `coef` from fused {sum, sumsq}
+    partials [nblk][C][2] (clskd_bn_compact when nblk > 256, clskd_bn_finalize); updates bn's
+    running statistics once."""
+    L = lib()
+    st = _stream()
+    if nblk > 256:
+        grp = 64
+        ng = -(-nblk // grp)
+        part2 = torch.empty(ng * C * 2, device=part.device, dtype=torch.float64)
+        check(L.clskd_bn_compact(ptr(part), nblk, C, grp, ptr(part2), st), "bn_compact")
+        part, nblk = part2, ng
+    mean_o = var_o = None
+    if stats_out is not None:
+        mean_o, var_o = stats_out
+    scale = coef.data_ptr()
+    check(L.clskd_bn_finalize(ptr(part), nblk, rows, C, ptr(bn.weight), ptr(bn.bias), bn.eps,
+                              ptr(bn.running_mean), ptr(bn.running_var), bn.momentum, 1, scale,
+                              scale + 4 * C, ptr(mean_o), ptr(var_o), st), "bn_finalize")
+    return coef
+
+
+def abf_conv1_fuse(x, w1, coef, res, att, out, x1_raw=None):
+    """out = ABF level map: BN1(W1 x) [attention-fused with the nearest-upsampled residual res]
+    (clskd_abf_conv1_fuse); x1_raw (optional) receives W1 x."""
+    B, F, T, C = x.shape
+    mid = w1.shape[0]
+    assert mid == 64 and out.shape == (B, F, T, 64) and out.is_contiguous()
+    sB, sF, sT, _ = x.stride()
+    Fr = Tr = 1
+    aw = ab = None
+    if res is not None:
+        assert res.dtype == out.dtype and res.is_contiguous() and res.shape[-1] == 64
+        _, Fr, Tr, _ = res.shape
+        aw, ab = att
+    if x1_raw is not None:
+        assert x1_raw.dtype == out.dtype and x1_raw.shape == out.shape and x1_raw.is_contiguous()
+    sc = coef.data_ptr()
+    check(lib().clskd_abf_conv1_fuse(ptr(x), B, F, T, sB, sF, sT, C, ptr(w1.reshape(mid, C)), sc,
+                                     sc + 4 * mid, ptr(res), Fr, Tr, ptr(aw), ptr(ab), ptr(out),
+                                     ptr(x1_raw), _dt(out), _stream()), "abf_conv1_fuse")
+    return out
+
+
 # ------------------------------------------------------------------------------------------
 # Gram / SPKD
 # ------------------------------------------------------------------------------------------

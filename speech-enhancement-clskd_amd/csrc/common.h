@@ -51,6 +51,36 @@ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// 4 channels of fp32 / bf16 storage <-> f32x4 (8- or 16-B accesses)
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ f32x4 load4(const T* p);
+template <>
+__device__ __forceinline__ f32x4 load4<float>(const float* p) {
+  return *reinterpret_cast<const f32x4*>(p);
+}
+template <>
+__device__ __forceinline__ f32x4 load4<__bf16>(const __bf16* p) {
+  const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+template <typename T>
+__device__ __forceinline__ void store4(T* p, f32x4 v);
+template <>
+__device__ __forceinline__ void store4<float>(float* p, f32x4 v) {
+  *reinterpret_cast<f32x4*>(p) = v;
+}
+template <>
+__device__ __forceinline__ void store4<__bf16>(__bf16* p, f32x4 v) {
+  bf16x4 o;
+  o[0] = (__bf16)v[0];
+  o[1] = (__bf16)v[1];
+  o[2] = (__bf16)v[2];
+  o[3] = (__bf16)v[3];
+  *reinterpret_cast<bf16x4*>(p) = o;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -73,5 +103,46 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// scale/shift (and batch mean/var, running stats) of one channel from its totals.
+__device__ __forceinline__ void bn_channel_coeffs(int c, double S, double Q, int64_t rows,
+                                                  const float* gamma, const float* beta, float eps,
+                                                  float* running_mean, float* running_var,
+                                                  float momentum, int n_updates, float* scale,
+                                                  float* shift, float* mean_out, float* var_out) {
+  const double n = (double)rows;
+  const double mean = S / n;
+  double var = Q / n - mean * mean;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f;
+  const float bb = beta ? beta[c] : 0.f;
+  const float sc = invstd * g;
+  scale[c] = sc;
+  shift[c] = bb - (float)mean * sc;
+  if (mean_out) mean_out[c] = (float)mean;
+  if (var_out) var_out[c] = (float)var;
+  if (running_mean && running_var) {
+    const float unb = (float)(rows > 1 ? var * n / (n - 1.0) : var);
+    float rm = running_mean[c], rv = running_var[c];
+    for (int u = 0; u < n_updates; ++u) {
+      rm = (1.f - momentum) * rm + momentum * (float)mean;
+      rv = (1.f - momentum) * rv + momentum * unb;
+    }
+    running_mean[c] = rm;
+    running_var[c] = rv;
+  }
+}
+
+
+// ATen nearest_idx (UpSample.h) for F.interpolate(mode="nearest"): source index of dst.
+__device__ __forceinline__ int nearest_src(int dst, int in_size, int out_size) {
+  // ATen nearest_idx (UpSample.h): identity / >>1 fast paths, else floorf(dst*scale), scale in f32
+  if (out_size == in_size) return dst;
+  if (out_size == 2 * in_size) return dst >> 1;
+  const float scale = (float)in_size / (float)out_size;
+  const int s = (int)floorf((float)dst * scale);
+  return s < in_size - 1 ? s : in_size - 1;
+}
 
 }  // namespace clskd

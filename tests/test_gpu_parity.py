@@ -224,6 +224,78 @@ def test_conv_halo_kernel_against_torch(case):
     np.testing.assert_allclose(stc[:, :, 0].sum(0).numpy(), ref.sum((0, 1, 2)).numpy(), rtol=1e-5, atol=1e-3)
     np.testing.assert_allclose(stc[:, :, 1].sum(0).numpy(), (ref ** 2).sum((0, 1, 2)).numpy(), rtol=1e-5)
 
+
+def _abf_torch(x, y, shape, abf):
+    """framework.py:204-222 in torch fp64 (train-mode BatchNorm): returns (out, x_fused, mean1,
+    var1) from NCHW inputs."""
+    import torch.nn.functional as Fn
+    d = lambda t: t.detach().double().cpu()  # noqa: E731
+    x1 = Fn.conv2d(x, d(abf.conv1[0].weight))
+    m1, v1 = x1.mean((0, 2, 3)), x1.var((0, 2, 3), unbiased=False)
+    xb = Fn.batch_norm(x1, None, None, d(abf.conv1[1].weight), d(abf.conv1[1].bias), True, 0.1, 1e-5)
+    if abf.att_conv is not None:
+        yu = Fn.interpolate(y, (shape, x.shape[-1]), mode="nearest")
+        z = torch.sigmoid(Fn.conv2d(torch.cat([xb, yu], 1), d(abf.att_conv[0].weight),
+                                    d(abf.att_conv[0].bias)))
+        xb = xb * z[:, 0:1] + yu * z[:, 1:2]
+    o = Fn.conv2d(xb, d(abf.conv2[0].weight), padding=1)
+    o = Fn.batch_norm(o, None, None, d(abf.conv2[1].weight), d(abf.conv2[1].bias), True, 0.1, 1e-5)
+    return o, xb, m1, v1
+
+
+@pytest.mark.parametrize("cin", [8, 16, 32, 64])
+@pytest.mark.parametrize("fuse", [False, True])
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+def test_abf_folded_level_against_torch(cin, fuse, compute):
+    """ABF level with conv1 folded (clskd_abf_moments / _bn1_finalize / _conv1_fuse): conv1's
+    BatchNorm statistics from the tap's moments, conv1 recomputed in the fused kernel.  Against
+    torch fp64 (framework.py:204-222) on a strided tap (a channel sub-range view), plus the BN1
+    running statistics and the tape's raw conv1 output / batch mean-var.  Tolerances: fp32
+    storage 2e-5 (fused map) / 1e-4 (output); bf16 storage 2e-2 / 5e-2 (relative to max)."""
+    from clskd.framework import ABF
+    g = torch.Generator().manual_seed(cin * 10 + fuse)
+    B, F, T = 3, 16, 37
+    base = torch.randn(B, F, T, cin + 4, generator=g).abs()  # PReLU-like, non-zero mean
+    x = base.to(DEV)[..., 4:]                                  # strided view: channels 4..cin+3
+    abf = ABF(cin, 64, 32, fuse).to(DEV).train()
+    abf.compute = compute
+    with torch.no_grad():
+        for bn in (abf.conv1[1], abf.conv2[1]):
+            bn.weight.uniform_(0.5, 1.5, generator=None)
+            bn.bias.uniform_(-0.2, 0.2)
+    y = torch.randn(B, F // 2, T, 64, generator=g).to(DEV).to(abf.act_dtype) if fuse else None
+    rm0, rv0 = abf.conv1[1].running_mean.clone(), abf.conv1[1].running_var.clone()
+    tape = {}
+    out, xf = abf.forward_bftc(x, y, F if fuse else None, F, tape=tape)
+    torch.cuda.synchronize()
+    xn = x.permute(0, 3, 1, 2).double().cpu()
+    yn = y.permute(0, 3, 1, 2).double().cpu() if fuse else None
+    o_ref, xf_ref, m1, v1 = _abf_torch(xn, yn, F, abf)
+    tol_f, tol_o = (2e-5, 1e-4) if compute == "fp32" else (2e-2, 5e-2)
+    got_xf = xf.permute(0, 3, 1, 2).double().cpu()
+    got_o = out.permute(0, 3, 1, 2).double().cpu()
+    assert float((got_xf - xf_ref).abs().max()) <= tol_f * float(xf_ref.abs().max())
+    assert float((got_o - o_ref).abs().max()) <= tol_o * float(o_ref.abs().max())
+    np.testing.assert_allclose(_np(tape["mv1"][0]), m1.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(_np(tape["mv1"][1]), v1.numpy(), rtol=1e-4, atol=1e-6)
+    n = B * F * T
+    np.testing.assert_allclose(_np(abf.conv1[1].running_mean), 0.9 * _np(rm0) + 0.1 * m1.numpy(),
+                               rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(_np(abf.conv1[1].running_var),
+                               0.9 * _np(rv0) + 0.1 * v1.numpy() * n / (n - 1), rtol=1e-4)
+    x1_ref = torch.einsum("bcft,nc->bnft", xn, abf.conv1[0].weight.detach().double().cpu().reshape(64, cin))
+    got_x1 = tape["x1"].permute(0, 3, 1, 2).double().cpu()
+    tol_x1 = 1e-5 if compute == "fp32" else 1e-2
+    assert float((got_x1 - x1_ref).abs().max()) <= tol_x1 * float(x1_ref.abs().max())
+    # the materialising path (pointwise conv + BN + fuse) agrees with the folded one
+    w1p, _, att = abf._weights(x.dtype)
+    x1_old = abf._level_conv1(x.contiguous(), y, F if fuse else None, w1p, att, True, None,
+                              __import__("clskd.ops", fromlist=["ops"]).conv_mblocks(B, F, T))
+    torch.cuda.synchronize()
+    diff = float((x1_old.double() - xf.double()).abs().max())
+    assert diff <= (1e-5 if compute == "fp32" else 3e-2) * float(xf.double().abs().max()), diff
+
+
 def test_stft_istft_golden():
     st = golden("stft.npz")
     m = _models("student")
