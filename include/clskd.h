@@ -244,6 +244,26 @@ int clskd_abf_conv1_fuse(const float* s, int32_t B, int32_t F, int32_t T, int64_
                          void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Validation metrics of KnowledgeDistillation.validation_step (distill.py:149-199,
+ * COMPUTE_METRICS = ["si_sdr", "stoi"], distill.py:35), per utterance, float64 results.
+ * clskd_sisdr_f64: asteroid get_metrics' si_sdr = pb_bss_eval.evaluation.si_sdr(ref, est)
+ *   (the formula of tools_for_loss.py:50-92 without eps; no mean removal):
+ *   out[r] = 10 log10(|a ref|^2 / |est - a ref|^2), a = <ref, est> / <ref, ref>.
+ * clskd_stoi: pystoi.stoi(clean, est, fs, extended=False) (tools_for_model.py:595-600):
+ *   resampling to 10 kHz (Octave resample filter, scipy resample_poly alignment), silent-frame
+ *   removal (40 dB below the loudest clean frame), 512-point STFT of 256-sample Hanning frames,
+ *   15 one-third-octave bands, 30-frame segments with -15 dB clipping, mean correlation.
+ *   Rows of `clean` / `est` at strides ld_clean / ld_est (fp32); workspace: device memory of
+ *   clskd_stoi_workspace(B, L, fs) bytes; at most 6144 energy frames (78 s) per utterance.
+ * -------------------------------------------------------------------------------------- */
+int clskd_sisdr_f64(const float* ref, const float* est, int32_t rows, int32_t L, int64_t ld_ref,
+                    int64_t ld_est, double* out, void* stream);
+int64_t clskd_stoi_workspace(int32_t B, int32_t L, int32_t fs);
+int clskd_stoi(const float* clean, const float* est, int32_t B, int32_t L, int64_t ld_clean,
+               int64_t ld_est, int32_t fs, void* workspace, int64_t ws_bytes, double* out,
+               void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Uniform weight re-draw (replaces the per-step ABF rebuild of framework.py:194-195 —
  * nn.init.kaiming_uniform_(w, a=1) on conv1/conv2 and Conv2d.reset_parameters on att_conv —
  * and the repacking of the drawn weights).  Job k draws numel values U(-bound, bound) into

@@ -96,6 +96,9 @@ SIGNATURES = {
                                       _p]),
     "clskd_abf_conv1_fuse": (_i32, [_p, _i32, _i32, _i32, _i64, _i64, _i64, _i32, _p, _p, _p, _p,
                                     _i32, _i32, _p, _p, _p, _p, _i32, _p]),
+    "clskd_sisdr_f64": (_i32, [_p, _p, _i32, _i32, _i64, _i64, _p, _p]),
+    "clskd_stoi_workspace": (_i64, [_i32, _i32, _i32]),
+    "clskd_stoi": (_i32, [_p, _p, _i32, _i32, _i64, _i64, _i32, _p, _i64, _p, _p]),
     "clskd_gram_partial": (_i32, [_p, _i32, _i32, _p, _p]),
     "clskd_spkd_finalize": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p]),
     "clskd_uniform_redraw": (_i32, [_p, _i32, C.c_uint64, _p, _p]),

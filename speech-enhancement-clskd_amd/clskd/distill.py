@@ -103,6 +103,31 @@ def _gram_bftc(t, c0=0, Cs=None):
     return ops.GramView(t, 0, Fn * Tn * Ct, Fn * Tn, Ct, c0, Cs, affine)
 
 
+def _validation_step(module, batch):
+    """distill.py:149-199 (and distill_SPKD.py's copy): for every utterance of the batch the
+    student's estimate (eval-mode forward, as Lightning's validation loop runs it, no grad; the
+    one-source PIT of the reference is the identity), asteroid get_metrics' si_sdr and stoi of
+    the estimate and of the unprocessed mixture against the clean source, then the batch means
+    of si_sdr, stoi and their improvements — the dict the reference passes to self.log_dict.
+    All metrics run on the device (clskd.metrics); returned as Python floats."""
+    from . import metrics
+    x, y = batch
+    x = x.float().reshape(x.shape[0], -1).contiguous()
+    y = y.float().reshape(x.shape[0], -1).contiguous()
+    student = module.student
+    was = student.training
+    student.eval()
+    try:
+        with torch.no_grad():
+            est = student(x, is_feat=True)
+            utt = metrics.get_metrics(x, y, est, sample_rate=module.cfg.fs)
+            res = metrics.summarize(utt)
+    finally:
+        student.train(was)
+    module.last_val = {k: float(v) for k, v in res.items()}
+    return module.last_val
+
+
 class KnowledgeDistillation(nn.Module):
     """distill.py:38-229 without Lightning: same constructor and step signature."""
 
@@ -200,6 +225,10 @@ class KnowledgeDistillation(nn.Module):
         if return_parts:
             return out
         return out["loss"]
+
+    def validation_step(self, batch, batch_idx=0):
+        """distill.py:149-199: {si_sdr, si_sdr_imp, stoi, stoi_imp} over the batch."""
+        return _validation_step(self, batch)
 
     def forward_with_tape(self, X, y):
         out = clskd_step(self.teacher, self.student, self.review_encoder, self.review_decoder,
@@ -439,6 +468,10 @@ class SPKDDistillation(nn.Module):
 
     def forward(self, x):
         return self.student(x)
+
+    def validation_step(self, batch, batch_idx=0):
+        """distill_SPKD.py's validation step (the same as distill.py:149-199)."""
+        return _validation_step(self, batch)
 
     @torch.no_grad()
     def training_step(self, batch, batch_idx=0, return_parts=False):
