@@ -159,6 +159,11 @@ int clskd_bn_eval_coeffs(const float* running_mean, const float* running_var,
                          float* scale, float* shift, void* stream);
 int clskd_bn_apply(const void* x, void* y, int64_t rows, int32_t C, const float* scale,
                    const float* shift, const float* alpha, int32_t dtype, void* stream);
+/* clskd_bn_apply_reim: as clskd_bn_apply with asteroid's OnReIm(PReLU) (one slope per part):
+ * alpha_re_im[0] for channels [0, C/2) (real), alpha_re_im[1] for [C/2, C) (imaginary). */
+int clskd_bn_apply_reim(const void* x, void* y, int64_t rows, int32_t C, const float* scale,
+                        const float* shift, const float* alpha_re_im, int32_t dtype,
+                        void* stream);
 int32_t clskd_bn_partial_blocks(int64_t rows, int32_t C);
 
 /* ------------------------------------------------------------------------------------------
@@ -195,7 +200,12 @@ int clskd_complex_combine(const float* rr, const float* ii, const float* ir, con
  *                  imag at 257.., zero tail) and optionally mask_r/mask_i [B][T][257].
  * clskd_ola:       ConviSTFT overlap-add (tools_for_model.py:95-107): frames [B][T][400] ->
  *                  wav[b][n] = (sum frames) / (sum window^2 + 1e-8), trimmed, clamp(-1,1)
- *                  (DCCRN.py:235-237) when clamp != 0.
+ *                  (DCCRN.py:235-237) when clamp != 0.  window == NULL: the plain sum
+ *                  (asteroid's STFT Decoder, conv_transpose1d with the synthesis filters).
+ * clskd_mask_bdt:  asteroid DCCRNet mask (complex_nn.BoundComplexMask('tanh') then
+ *                  DCCRNet.apply_masks): est = tanh(|M|) e^{i angle M} * X on bins 0..255 of
+ *                  spec rows [B][T][ldspec] (re 0.., im 257..), bin 256 = 0; mask BFTC
+ *                  [B][256][Tm][2]; est rows [B][T][ldest] (zero tail columns 514..).
  * -------------------------------------------------------------------------------------- */
 int clskd_frame_pad(const float* x, int64_t ldx, int32_t B, int32_t L, int32_t pad, int32_t Lp,
                     int32_t mode, float* xp, void* stream);
@@ -204,6 +214,8 @@ int clskd_spec_bftc(const float* spec, int32_t B, int32_t T, int32_t ld, int32_t
 int clskd_mask_e(const float* spec, int32_t ldspec, const float* mask, int32_t Tm, int32_t B,
                  int32_t T, float* est, int32_t ldest, float* mask_r, float* mask_i,
                  void* stream);
+int clskd_mask_bdt(const float* spec, int32_t ldspec, const float* mask, int32_t Tm, int32_t B,
+                   int32_t T, float* est, int32_t ldest, void* stream);
 int clskd_ola(const float* frames, const float* window, int32_t B, int32_t T, int32_t win,
               int32_t hop, int32_t out_len, int32_t trim, int32_t clamp, float* wav,
               void* stream);

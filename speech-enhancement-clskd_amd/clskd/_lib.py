@@ -80,6 +80,8 @@ SIGNATURES = {
                                  _p, _p, _p]),
     "clskd_bn_eval_coeffs": (_i32, [_p, _p, _p, _p, _f32, _i32, _p, _p, _p]),
     "clskd_bn_apply": (_i32, [_p, _p, _i64, _i32, _p, _p, _p, _i32, _p]),
+    "clskd_bn_apply_reim": (_i32, [_p, _p, _i64, _i32, _p, _p, _p, _i32, _p]),
+    "clskd_mask_bdt": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _i32, _p]),
     "clskd_lstm_recurrent": (_i32, [_p, _i64, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _i64,
                                     _i64, _i64, _p]),
     "clskd_complex_combine": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p]),

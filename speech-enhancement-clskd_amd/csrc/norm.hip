@@ -137,8 +137,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
                                                        T* __restrict__ y, int64_t items, int CG,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
-                                                       const float* __restrict__ alpha) {
+                                                       const float* __restrict__ alpha,
+                                                       int split) {
+  // PReLU slope: alpha[0], or alpha[0] below channel `split` and alpha[1] from it (split > 0:
+  // asteroid's OnReIm(PReLU), one slope for the real and one for the imaginary channels)
   const float a = alpha ? alpha[0] : 0.f;
+  const float a1 = (alpha && split > 0) ? alpha[1] : a;
   const bool act = alpha != nullptr;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -167,7 +171,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x,
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float t = fmaf(v[j], sc[j], sh[j]);
-      if (act) t = t >= 0.f ? t : a * t;
+      if (act) t = t >= 0.f ? t : (split > 0 && cg * 8 + j >= split ? a1 : a) * t;
       v[j] = t;
     }
     Vec8<T>::store(y + i * 8, v);
@@ -239,6 +243,36 @@ __global__ void mask_e_kernel(const float* __restrict__ spec, int ldspec,
   }
 }
 
+// asteroid DCCRNet: mask = tanh(|M|) e^{i angle(M)} (complex_nn.BoundComplexMask('tanh')), est =
+// mask * X on bins 0..255 (the Nyquist bin was dropped before the masker and is padded back as
+// zero); mask BFTC [B][256][Tm][2] read at t, spectrum / est rows [B][T][ld] (re 0.., im 257..)
+__global__ void mask_bdt_kernel(const float* __restrict__ spec, int ldspec,
+                                const float* __restrict__ mask, int Tm, int B, int T,
+                                float* __restrict__ est, int ldest) {
+  const int64_t total = (int64_t)B * T * 257;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int f = (int)(i % 257);
+    const int64_t bt = i / 257;
+    const int t = (int)(bt % T);
+    const int b = (int)(bt / T);
+    float er = 0.f, ei = 0.f;
+    if (f < 256) {
+      const float* mp = mask + (((int64_t)b * 256 + f) * Tm + t) * 2;
+      const float mr = mp[0], mi = mp[1];
+      const float mag = tanhf(hypotf(mr, mi));
+      const float ph = atan2f(mi, mr);
+      const float br = mag * cosf(ph), bi = mag * sinf(ph);
+      const float xr = spec[bt * ldspec + f], xi = spec[bt * ldspec + 257 + f];
+      er = br * xr - bi * xi;
+      ei = br * xi + bi * xr;
+    }
+    est[bt * ldest + f] = er;
+    est[bt * ldest + 257 + f] = ei;
+    if (f < ldest - 514) est[bt * ldest + 514 + f] = 0.f;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // ConviSTFT overlap-add + window-energy normalisation + trim (+ clamp)
 // ------------------------------------------------------------------------------------------
@@ -258,10 +292,12 @@ __global__ void ola_kernel(const float* __restrict__ frames, const float* __rest
     for (int t = t_lo; t <= t_hi; ++t) {
       const int o = p - t * hop;
       acc += frames[((int64_t)b * T + t) * win + o];
-      const float w = window[o];
-      coff += w * w;
+      if (window) {
+        const float w = window[o];
+        coff += w * w;
+      }
     }
-    float v = acc / (coff + 1e-8f);
+    float v = window ? acc / (coff + 1e-8f) : acc;
     if (clamp) v = fminf(fmaxf(v, -1.f), 1.f);
     wav[i] = v;
   }
@@ -478,9 +514,9 @@ extern "C" int clskd_bn_eval_coeffs(const float* running_mean, const float* runn
   return CLSKD_OK;
 }
 
-extern "C" int clskd_bn_apply(const void* x, void* y, int64_t rows, int32_t C,
-                              const float* scale, const float* shift, const float* alpha,
-                              int32_t dtype, void* stream) {
+static int bn_apply_impl(const void* x, void* y, int64_t rows, int32_t C, const float* scale,
+                         const float* shift, const float* alpha, int split, int32_t dtype,
+                         void* stream) {
   CLSKD_CHECK_ARG(x && y && scale && shift, "bn_apply: null pointer");
   CLSKD_CHECK_SHAPE(C % 8 == 0 && rows > 0, "bn_apply: C=%d must be a multiple of 8", C);
   CLSKD_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0, "bn_apply: alignment");
@@ -492,12 +528,26 @@ extern "C" int clskd_bn_apply(const void* x, void* y, int64_t rows, int32_t C,
   if (g > 4096) g = 4096;
   if (dtype == CLSKD_BF16)
     hipLaunchKernelGGL(bn_apply_kernel<__bf16>, dim3((unsigned)g), dim3(256), 0, as_stream(stream),
-                       (const __bf16*)x, (__bf16*)y, items, CG, scale, shift, alpha);
+                       (const __bf16*)x, (__bf16*)y, items, CG, scale, shift, alpha, split);
   else
     hipLaunchKernelGGL(bn_apply_kernel<float>, dim3((unsigned)g), dim3(256), 0, as_stream(stream),
-                       (const float*)x, (float*)y, items, CG, scale, shift, alpha);
+                       (const float*)x, (float*)y, items, CG, scale, shift, alpha, split);
   CLSKD_LAUNCH_CHECK("bn_apply");
   return CLSKD_OK;
+}
+
+extern "C" int clskd_bn_apply(const void* x, void* y, int64_t rows, int32_t C,
+                              const float* scale, const float* shift, const float* alpha,
+                              int32_t dtype, void* stream) {
+  return bn_apply_impl(x, y, rows, C, scale, shift, alpha, 0, dtype, stream);
+}
+
+extern "C" int clskd_bn_apply_reim(const void* x, void* y, int64_t rows, int32_t C,
+                                   const float* scale, const float* shift,
+                                   const float* alpha_re_im, int32_t dtype, void* stream) {
+  CLSKD_CHECK_ARG(alpha_re_im, "bn_apply_reim: null alpha");
+  CLSKD_CHECK_SHAPE(C % 2 == 0, "bn_apply_reim: C=%d must be even", C);
+  return bn_apply_impl(x, y, rows, C, scale, shift, alpha_re_im, C / 2, dtype, stream);
 }
 
 extern "C" int clskd_frame_pad(const float* x, int64_t ldx, int32_t B, int32_t L, int32_t pad,
@@ -535,10 +585,21 @@ extern "C" int clskd_mask_e(const float* spec, int32_t ldspec, const float* mask
   return CLSKD_OK;
 }
 
+extern "C" int clskd_mask_bdt(const float* spec, int32_t ldspec, const float* mask, int32_t Tm,
+                              int32_t B, int32_t T, float* est, int32_t ldest, void* stream) {
+  CLSKD_CHECK_ARG(spec && mask && est, "mask_bdt: null pointer");
+  CLSKD_CHECK_SHAPE(ldspec >= 514 && ldest >= 514 && ldest - 514 <= 257 && Tm >= T,
+                    "mask_bdt: bad strides");
+  hipLaunchKernelGGL(mask_bdt_kernel, dim3(grid_for((int64_t)B * T * 257)), dim3(256), 0,
+                     as_stream(stream), spec, ldspec, mask, Tm, B, T, est, ldest);
+  CLSKD_LAUNCH_CHECK("mask_bdt");
+  return CLSKD_OK;
+}
+
 extern "C" int clskd_ola(const float* frames, const float* window, int32_t B, int32_t T,
                          int32_t win, int32_t hop, int32_t out_len, int32_t trim, int32_t clamp,
                          float* wav, void* stream) {
-  CLSKD_CHECK_ARG(frames && window && wav, "ola: null pointer");
+  CLSKD_CHECK_ARG(frames && wav, "ola: null pointer");
   CLSKD_CHECK_SHAPE(out_len > 0 && T > 0 && hop > 0 && win >= hop, "ola: shape");
   hipLaunchKernelGGL(ola_kernel, dim3(grid_for((int64_t)B * out_len)), dim3(256), 0,
                      as_stream(stream), frames, window, B, T, win, hop, out_len, trim, clamp, wav);
