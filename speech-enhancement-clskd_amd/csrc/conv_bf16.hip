@@ -219,11 +219,15 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
     if constexpr (DBG == 1) return;  // timing experiment: no operand traffic
     // the DMAs, back to back
     const unsigned sl = stage_lds0 + stage * SB;
+    if constexpr (DBG != 5 && DBG != 8) {  // DBG 5/8: timing experiments, A operand not staged
 #pragma unroll
-    for (int i = 0; i < NGA; ++i) glds16((const void*)srcA[i], sl + (wave * NGA + i) * 1024);
+      for (int i = 0; i < NGA; ++i) glds16((const void*)srcA[i], sl + (wave * NGA + i) * 1024);
+    }
+    if constexpr (DBG != 4 && DBG != 7) {  // DBG 4/7: timing experiments, B operand not staged
 #pragma unroll
-    for (int i = 0; i < NGB; ++i) {
-      if (i < NGB - 1 || fullB) glds16((const void*)srcB[i], sl + BM * ROWB + (wave + NW * i) * 1024);
+      for (int i = 0; i < NGB; ++i) {
+        if (i < NGB - 1 || fullB) glds16((const void*)srcB[i], sl + BM * ROWB + (wave + NW * i) * 1024);
+      }
     }
   };
 
@@ -272,7 +276,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
         const int row = wn * (BN / WN) + j * 32 + l32;
         bfr[j] = *reinterpret_cast<const bf16x8*>(sb + row * ROWB + ((c ^ swz<BK>(row)) << 4));
       }
-      if constexpr (DBG != 2) {  // DBG 2: timing experiment without the MFMAs
+      if constexpr (DBG != 2 && DBG != 7 && DBG != 8) {  // DBG 2/7/8: timing experiments without the MFMAs
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -465,6 +469,16 @@ int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
   if (dbg == 1 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 3, __bf16, 1>(d, st);
   if (dbg == 2 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 3, __bf16, 2>(d, st);
   if (dbg == 3 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 3, __bf16, 3>(d, st);
+  if (dbg == 4 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 32, 256, 16, 4, __bf16, 4>(d, st);
+  if (dbg == 5 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 32, 256, 16, 4, __bf16, 5>(d, st);
+  if (dbg == 4 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 4, __bf16, 4>(d, st);
+  if (dbg == 5 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 4, __bf16, 5>(d, st);
+  if (dbg == 7 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 32, 256, 16, 4, __bf16, 7>(d, st);
+  if (dbg == 8 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 32, 256, 16, 4, __bf16, 8>(d, st);
+  if (dbg == 7 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 4, __bf16, 7>(d, st);
+  if (dbg == 8 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 4, __bf16, 8>(d, st);
+  if (dbg == 6 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 32, 256, 16, 4, __bf16, 0>(d, st);
+  if (dbg == 6 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 4, __bf16, 0>(d, st);
   if (d.N > 32 && d.K % 32 == 0 && tilecfg != 128) {
     // 256-row tiles stage a third fewer bytes per FLOP (measured 1.1-1.25x faster per tile
     // worth of work) but halve the workgroup count: pick them unless the tail rounds eat the
