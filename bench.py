@@ -35,7 +35,7 @@ PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (f32-in MF
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
 B_PER_GPU = 16
 NBATCH = 4
-TRAFFIC_FILE = "r1_pmc_traffic.json"  # written by tools/pmc_traffic.py
+TRAFFIC_FILE = "r2_pmc_traffic.json"  # written by tools/pmc_traffic.py
 L = 64000
 
 
