@@ -10,7 +10,7 @@ OUT = os.path.join(HERE, "libclskd_hip.so")
 OBJDIR = os.path.join(os.path.dirname(HERE), "build", "obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-SOURCES = ["capi.cpp", "conv_igemm.hip", "conv_bf16.hip", "conv_halo.hip", "conv_direct.hip", "conv_pointwise.hip", "norm.hip", "lstm.hip", "loss.hip", "redraw.hip", "grad.hip", "norm_bwd.hip", "abf.hip", "metrics.hip"]
+SOURCES = ["capi.cpp", "conv_igemm.hip", "conv_bf16.hip", "conv_halo.hip", "conv_gemm8.hip", "conv_direct.hip", "conv_pointwise.hip", "norm.hip", "lstm.hip", "loss.hip", "redraw.hip", "grad.hip", "norm_bwd.hip", "abf.hip", "metrics.hip"]
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
 
 

@@ -437,6 +437,7 @@ static int launch_big(const clskd_conv_desc& d, hipStream_t st) { return launch_
 // BN >= 64).  BN = 32 keeps 4 waves (four 32x32 MFMA tiles).  CLSKD_BF16_WAVES=4 selects the
 // 4-wave tiles everywhere (A/B measurements).
 int launch_conv_halo(const clskd_conv_desc& d, hipStream_t st, bool* launched);
+int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched);
 
 int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
   static const bool no_halo = [] {  // A/B switch: CLSKD_NO_HALO=1 keeps narrow layers on the engine
@@ -446,6 +447,15 @@ int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
   if (!no_halo) {
     bool launched = false;
     const int rc = launch_conv_halo(d, st, &launched);
+    if (rc != CLSKD_OK || launched) return rc;
+  }
+  static const int dbg0 = [] {
+    const char* e = getenv("CLSKD_BF16_DEBUG_MODE");
+    return e ? atoi(e) : 0;
+  }();
+  if (dbg0 == 0) {
+    bool launched = false;
+    const int rc = launch_conv_gemm8(d, st, &launched);
     if (rc != CLSKD_OK || launched) return rc;
   }
   static const int nw = [] {

@@ -1,0 +1,549 @@
+// Persistent, software-pipelined bf16 implicit-GEMM convolution for the wide teacher / ReviewKD
+// layers (N > 64; gfx950).
+//
+// Same descriptor contract as the LDS-DMA engine in conv_bf16.hip (K-table gather of bf16 BFTC
+// segments, packed [N][K] bf16 weights with K % 64 == 0, bias-initialised fp32 accumulators,
+// fused per-128-row BatchNorm partials, out_row map).  What it changes, measured on the
+// teacher shapes (tools/conv_micro.py; tools/g8_sweep.sh ablations):
+//
+//  * The one-tile-per-workgroup engines pay a fixed cost per tile — row tables with int64
+//    divisions, the K-table and bias loads, the first K-tile's full memory round trip, the
+//    BatchNorm-statistics and store epilogue — with nothing else on the CU to hide it (one
+//    workgroup per CU): 12-20 us per tile round against 1.1-1.7 us per K-tile of MFMA work.
+//    Here a grid of at most one workgroup per CU walks a list of tiles; the LDS-DMA pipeline
+//    runs straight across tile boundaries (the next tile's first K-tile is in flight while the
+//    current tile's last one computes and its epilogue runs), and the row tables of tile j+1
+//    are built (double-buffered in LDS) while tile j runs.
+//  * 8 waves (512 threads), BK = 64, tile BM x BN with each wave owning a 128x64 (256x256) or
+//    64x64 (256x128) block of v_mfma_f32_32x32x16_bf16 accumulators; the K-tile is walked in
+//    four 16-deep substeps with the NEXT substep's fragments read while the current one's MFMAs
+//    run (two fragment register sets), one raw s_barrier per K-tile (DMA visibility + stage
+//    reuse; no __syncthreads in the pipeline: its vmcnt(0) would drain the in-flight DMAs), the
+//    K-tile's LDS-DMA pieces interleaved between the substeps.
+//  * Two LDS stages; 128-B rows with the 16-B chunk XOR-swizzled by (row >> 1) & 7 on the DMA
+//    source address and on the fragment read (conflict-free for the 32x32x16 operand reads).
+//    One glds piece = 8 rows x 128 B; a lane's chunk position is the same in every piece it
+//    issues, so the K-table entry of a K-tile is ONE LDS read per lane.
+//  * Tiles are dealt to workgroups XCD-aware: each XCD's workgroups take one contiguous run of
+//    M-tiles, so the rows concurrently gathered on an XCD (overlapping through the taps) share
+//    its L2.
+#include <stdlib.h>
+
+#include "common.h"
+
+namespace clskd {
+
+typedef short bf16x8s __attribute__((ext_vector_type(8)));
+
+namespace g8 {
+
+__device__ __attribute__((aligned(64))) unsigned char zero_page[64];
+
+// One 1-KiB LDS-DMA wave instruction: lane l copies 16 B from gsrc to lds_base + 16*l.  Inline
+// asm (cdna_hip_programming.md §5.7): hipcc neither tracks nor waits for it, so the counted
+// vmcnt waits below are the only synchronisation.
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+template <typename T>
+__device__ __forceinline__ T sel4(int s, T a0, T a1, T a2, T a3) {
+  return s == 0 ? a0 : (s == 1 ? a1 : (s == 2 ? a2 : a3));
+}
+
+// raw workgroup barrier that leaves LDS-DMA in flight: this wave's LDS reads/writes retired
+// first (lgkmcnt), then s_barrier; the compiler may not move memory operations across it
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Row table of one tile (double-buffered in LDS).
+template <int BM>
+struct RowTable {
+  int4 info[BM];     // fi0, ti0, valid, -
+  int base[4][BM];   // per-segment element offset of the row
+  int64_t orow[BM];  // output element offset (-1: past M)
+};
+
+}  // namespace g8
+
+struct ConvArgsG8 {
+  clskd_conv_desc d;
+  int n_mt, ntiles;  // M-tiles per N-block, tiles in the list
+};
+
+// DBG (timing experiments only, wrong results): 1 = no LDS-DMA, 2 = no MFMA, 3 = neither.
+template <int BM, int BN, int WM, int PHI, typename OutT, int DBG = 0, int STAG = 0, int NL = 8>
+__global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) {
+  using namespace g8;
+  const clskd_conv_desc& d = args.d;
+  constexpr int NW = 8, NT = 512, BK = 64, ROWB = 128, NS = 2;
+  constexpr int WN = NW / WM;
+  constexpr int WR = BM / WM, WC = BN / WN;  // wave block
+  constexpr int FM = WR / 32, FN = WC / 32;  // 32x32 tiles per wave
+  // NL loader waves (0 .. NL-1) issue the DMA pieces: NGA + NGB per loader wave per K-tile
+  constexpr int NGA = BM / 8 / NL, NGB = BN / 8 / NL;
+  constexpr int G = NGA + NGB;
+  constexpr int GP = (G + PHI - 1) / PHI;
+  constexpr int SB = (BM + BN) * ROWB;  // stage bytes
+  static_assert(WM * WN == NW && FM >= 1 && FN >= 1, "tile split");
+  static_assert((BM / 8) % NL == 0 && (BN / 8) % NL == 0 && NL <= NW && NL % 2 == 0, "DMA piece split");
+  static_assert(PHI >= 1 && PHI + STAG <= 4, "issue substeps");
+  static_assert(WM * BN * 16 <= SB, "statistics scratch fits one stage");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* stages = smem;
+  RowTable<BM>* tabs = reinterpret_cast<RowTable<BM>*>(smem + NS * SB);  // [2]
+  float* bias_l = reinterpret_cast<float*>(tabs + 2);                    // [N]
+  int2* ctab = reinterpret_cast<int2*>(bias_l + ((d.N + 3) & ~3));       // [K/8]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int64_t M = (int64_t)d.B * d.Fo * d.To;
+  const int nk = d.K / BK;
+  const int64_t FoTo = (int64_t)d.Fo * d.To;
+
+  // ---- this workgroup's tile list (XCD-aware contiguous runs) ------------------------------
+  const int grid = gridDim.x, b = blockIdx.x;
+  int t_first, t_step, ntl;
+  if ((grid & 7) == 0 && args.ntiles >= grid) {
+    const int c = b & 7, s = b >> 3, cpx = grid >> 3;
+    const int q = args.ntiles >> 3, r = args.ntiles & 7;
+    const int len = q + (c < r ? 1 : 0), start = c * q + (c < r ? c : r);
+    t_first = start + s;
+    t_step = cpx;
+    ntl = s < len ? (len - s + cpx - 1) / cpx : 0;
+  } else {
+    t_first = b;
+    t_step = grid;
+    ntl = b < args.ntiles ? (args.ntiles - b + grid - 1) / grid : 0;
+  }
+  if (ntl == 0) return;  // whole workgroup: no barrier is left waiting
+  auto tile_mt = [&](int j) { return (t_first + j * t_step) % args.n_mt; };
+  auto tile_nt = [&](int j) { return (t_first + j * t_step) / args.n_mt; };
+
+  auto build_table = [&](int j, int buf) {
+    RowTable<BM>& tb = tabs[buf];
+    if (tid < BM) {
+      const int64_t m = (int64_t)tile_mt(j) * BM + tid;
+      const bool valid = m < M;
+      const int64_t mm = valid ? m : 0;
+      const int64_t bb = mm / FoTo;
+      const int64_t r = mm - bb * FoTo;
+      const int fo = (int)(r / d.To);
+      const int to = (int)(r - (int64_t)fo * d.To);
+      const int fi0 = fo * d.stride_f, ti0 = to * d.stride_t;
+      tb.info[tid] = make_int4(fi0, ti0, valid ? 1 : 0, 0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        tb.base[s][tid] = (int)(bb * d.seg[s].sB + (int64_t)fi0 * d.seg[s].sF + (int64_t)ti0 * d.seg[s].sT);
+      tb.orow[tid] = valid ? bb * d.oB + (int64_t)(fo * d.of_mul + d.of_add) * d.oF + (int64_t)to * d.oT : -1;
+    }
+  };
+
+  // ---- layer tables: K-chunk entries, bias; row tables of the first two tiles ---------------
+  for (int q = tid; q < d.K / 8; q += NT) {
+    const clskd_ktab_entry e = d.ktab[q * 8];
+    const int s = d.kseg[q * 8];
+    ctab[q] = make_int2(e.off, (int)(((unsigned)e.dF & 0xFFFFu) | (((unsigned)e.dT & 0xFFu) << 16) |
+                                     ((unsigned)s << 24)));
+  }
+  for (int n = tid; n < d.N; n += NT) bias_l[n] = d.bias ? d.bias[n] : 0.f;
+  build_table(0, 0);
+  if (ntl > 1) build_table(1, 1);
+  __syncthreads();
+
+  // ---- per-lane DMA geometry (reloaded when the DMA stream moves on to the next tile) --------
+  // piece rows (i*NL + wave)*8 + lane/8: (row >> 1) & 7 = (wave & 1) * 4 + lane / 16 (NL even).
+  // Per A piece: (fi0, ti0) packed in one register (an invalid row carries fi0 = -32768, out of
+  // every bound) and the row's element offset in segments 0 and 1 (the kernel takes <= 2).
+  const int csrc = (lane & 7) ^ (((wave & 1) << 2) + (lane >> 4));
+  const int prow = lane >> 3;
+  int a_ft[NGA], a_rb0[NGA], a_rb1[NGA];
+  int b_n0 = 0;  // weight row of this lane's first B piece
+  const unsigned short* wgt = reinterpret_cast<const unsigned short*>(d.weight);
+  auto load_geometry = [&](int j, int buf) {
+    const RowTable<BM>& tb = tabs[buf];
+#pragma unroll
+    for (int i = 0; i < NGA; ++i) {
+      const int r = (i * NL + (wave % NL)) * 8 + prow;
+      const int4 ri = tb.info[r];
+      a_ft[i] = (int)(((unsigned)(ri.z ? ri.x : -32768) << 16) | ((unsigned)ri.y & 0xFFFFu));
+      a_rb0[i] = tb.base[0][r];
+      a_rb1[i] = tb.base[1][r];
+    }
+    b_n0 = tile_nt(j) * BN + (wave % NL) * 8 + prow;
+  };
+  load_geometry(0, 0);
+
+  const uint64_t zero_addr = (uint64_t)(uintptr_t)g8::zero_page;
+  const unsigned stage_lds0 = __builtin_amdgcn_readfirstlane(lds_addr(stages));
+  const uint64_t sp0 = (uint64_t)(uintptr_t)d.seg[0].ptr, sp1 = (uint64_t)(uintptr_t)d.seg[1].ptr;
+  // K-chunk entry of K-tile kt for this lane, decoded
+  struct KEnt {
+    int off, dF, dT, Fb, Tb, s1;
+  };
+  auto kdecode = [&](int2 ce) -> KEnt {
+    KEnt e;
+    e.s1 = (int)((unsigned)ce.y >> 24);
+    e.off = ce.x;
+    e.dF = (int)(short)(ce.y & 0xFFFF);
+    e.dT = (int)(signed char)((ce.y >> 16) & 0xFF);
+    e.Fb = e.s1 ? d.seg[1].F : d.seg[0].F;
+    e.Tb = e.s1 ? d.seg[1].T : d.seg[0].T;
+    return e;
+  };
+  auto kentry = [&](int kt) -> KEnt { return kdecode(ctab[kt * 8 + csrc]); };
+  // source address of piece g (A pieces first, then B) of K-tile kt
+  auto piece_src = [&](int g, int kt, const KEnt& e) -> uint64_t {
+    if (g < NGA) {
+      const int fi = (a_ft[g] >> 16) + e.dF;
+      const int ti = (int)(short)(a_ft[g] & 0xFFFF) + e.dT;
+      const bool ok = (unsigned)fi < (unsigned)e.Fb && (unsigned)ti < (unsigned)e.Tb;
+      const int rb = e.s1 ? a_rb1[g] : a_rb0[g];
+      const uint64_t base = e.s1 ? sp1 : sp0;
+      const uint64_t a = base + (uint64_t)(int64_t)(rb + e.off) * 2u;
+      const uint64_t msk = 0ull - (uint64_t)ok;  // branch-free select of the zero page
+      return (a & msk) | (zero_addr & ~msk);
+    }
+    const int n = b_n0 + (g - NGA) * NL * 8;
+    const uint64_t a = (uint64_t)(uintptr_t)wgt + ((uint64_t)(uint32_t)n * (uint32_t)d.K + (uint32_t)(kt * BK + csrc * 8)) * 2u;
+    const uint64_t msk = 0ull - (uint64_t)(n < d.N);
+    return (a & msk) | (zero_addr & ~msk);
+  };
+  auto dst = [&](int g, int s) -> unsigned {
+    const unsigned sl = stage_lds0 + s * SB;
+    return g < NGA ? sl + (g * NL + wave) * 1024 : sl + BM * ROWB + ((g - NGA) * NL + wave) * 1024;
+  };
+
+  const int h = lane >> 5, l32 = lane & 31;
+  f32x16 acc[FM][FN];
+  auto init_acc = [&](int j) {
+    const int nb = tile_nt(j) * BN;
+#pragma unroll
+    for (int jj = 0; jj < FN; ++jj) {
+      const int n = nb + wn * WC + jj * 32 + l32;
+      const float bv = n < d.N ? bias_l[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][jj][r] = bv;
+    }
+  };
+  init_acc(0);
+
+  // fragment reads of substep s (k = 16s .. 16s+15) of the stage at `sa`
+  auto read_frags = [&](const unsigned char* sa, int s, bf16x8s (&af)[FM], bf16x8s (&bfr)[FN]) {
+    const unsigned char* sb = sa + BM * ROWB;
+    const int c = 2 * s + h;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = wm * WR + i * 32 + l32;
+      af[i] = *reinterpret_cast<const bf16x8s*>(sa + row * ROWB + ((c ^ ((row >> 1) & 7)) << 4));
+    }
+#pragma unroll
+    for (int jj = 0; jj < FN; ++jj) {
+      const int row = wn * WC + jj * 32 + l32;
+      bfr[jj] = *reinterpret_cast<const bf16x8s*>(sb + row * ROWB + ((c ^ ((row >> 1) & 7)) << 4));
+    }
+  };
+  auto mfmas = [&](const bf16x8s (&af)[FM], const bf16x8s (&bfr)[FN]) {
+    if constexpr ((DBG & 2) == 0) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < FN; ++jj)
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[jj], acc[i][jj], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) asm volatile("" ::"v"(bfr[jj]));
+    }
+  };
+
+  // ---- prologue: K-tile 0 of tile 0 ----------------------------------------------------------
+  if (!(DBG & 1) && wave < NL) {
+    const KEnt e = kentry(0);
+#pragma unroll
+    for (int g = 0; g < G; ++g) glds16((const void*)piece_src(g, 0, e), dst(g, 0));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  raw_barrier();
+
+  bf16x8s fa0[FM], fb0[FN], fa1[FM], fb1[FN];
+  read_frags(stages, 0, fa0, fb0);
+  // K-chunk entry of the K-tile issued next (read one K-tile ahead: no LDS round trip in front
+  // of the DMA issue)
+  int2 ce_next = ctab[(nk > 1 ? 1 : 0) * 8 + csrc];
+  const int total = ntl * nk;  // K-tiles this workgroup computes, over all its tiles
+  int gk = 0;                  // running index of the K-tile being computed
+  for (int j = 0; j < ntl; ++j) {
+    for (int kt = 0; kt < nk; ++kt, ++gk) {
+      const unsigned char* sa = stages + (gk & 1) * SB;
+      // the K-tile issued during this one is gk + 1: the next K-tile of this tile, or K-tile 0
+      // of the next tile (the per-lane geometry moves on to that tile first)
+      const bool last_kt = kt == nk - 1;
+      if (last_kt && j + 1 < ntl) load_geometry(j + 1, (j + 1) & 1);
+      const bool do_issue = gk + 1 < total && !(DBG & 1) && wave < NL;
+      const int kin = last_kt ? 0 : kt + 1;  // K-tile (of its tile) being issued
+      const KEnt e = kdecode(ce_next);
+      {  // the entry for the K-tile after it
+        const int kin2 = kin + 1 < nk ? kin + 1 : 0;
+        ce_next = ctab[kin2 * 8 + csrc];
+      }
+      const int sn = (gk + 1) & 1;
+      // the two waves of a SIMD (w, w + 4) issue their pieces in different substeps, so one's
+      // DMA issue runs beside the other's MFMAs (STAG: waves 4-7 start STAG substeps later)
+      auto issue = [&](int sub) {
+        const int part = sub - (wave >= 4 ? STAG : 0);
+        if (part >= 0 && part < PHI && do_issue) {
+#pragma unroll
+          for (int g = part * GP; g < (part + 1) * GP && g < G; ++g)
+            glds16((const void*)piece_src(g, kin, e), dst(g, sn));
+        }
+      };
+      // sched_barriers pin the two-set fragment pipeline (the scheduler would otherwise hoist
+      // every substep's reads to the top and spill)
+      read_frags(sa, 1, fa1, fb1);
+      issue(0);
+      mfmas(fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      read_frags(sa, 2, fa0, fb0);
+      issue(1);
+      mfmas(fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      read_frags(sa, 3, fa1, fb1);
+      issue(2);
+      mfmas(fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      issue(3);
+      mfmas(fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      // the next K-tile's pieces (this wave's) landed; then every wave's are visible and every
+      // wave is done reading this K-tile's stage
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      raw_barrier();
+      if (!last_kt) read_frags(stages + sn * SB, 0, fa0, fb0);
+    }
+
+    // ---- tile epilogue (the next tile's K-tile 0 is resident in the other stage) -------------
+    unsigned char* scratch = stages + ((gk - 1) & 1) * SB;  // the stage just computed from
+    const RowTable<BM>& tb = tabs[j & 1];
+    const int64_t m0 = (int64_t)tile_mt(j) * BM;
+    const int n0 = tile_nt(j) * BN;
+    if (d.stats) {  // fused BatchNorm statistics: one fp64 partial per 128 output rows
+      constexpr int HALVES = BM / 128;
+      constexpr int WPH = WM / HALVES;  // waves along M per 128-row half
+      double* red = reinterpret_cast<double*>(scratch);  // [WM][BN][2]
+      // rows of this lane's accumulators: wm*WR + 4h + (a compile-time offset); the ones at or
+      // past `lim` lie beyond M (only in the last M-tile: a uniform branch skips the checks)
+      const int64_t left = M - m0 - wm * WR - 4 * h;
+      const int lim = left < BM ? (int)left : BM;
+      const bool full = __builtin_amdgcn_readfirstlane(M - m0 >= BM ? 1 : 0) != 0;
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) {
+        const int col = wn * WC + jj * 32 + l32;
+        float sm = 0.f, sq = 0.f;
+        if (full) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float v = acc[i][jj][r];
+              sm += v;
+              sq = fmaf(v, v, sq);
+            }
+        } else {
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float v = (i * 32 + (r & 3) + 8 * (r >> 2)) < lim ? acc[i][jj][r] : 0.f;
+              sm += v;
+              sq = fmaf(v, v, sq);
+            }
+        }
+        const double ds = (double)sm + (double)__shfl_xor(sm, 32, 64);
+        const double dq = (double)sq + (double)__shfl_xor(sq, 32, 64);
+        if (h == 0) {
+          red[(wm * BN + col) * 2] = ds;
+          red[(wm * BN + col) * 2 + 1] = dq;
+        }
+      }
+      raw_barrier();
+      const int64_t nblk128 = (M + 127) / 128;
+      for (int idx = tid; idx < HALVES * BN; idx += NT) {
+        const int hv = idx / BN, c = idx % BN;
+        const int n = n0 + c;
+        const int64_t blk = m0 / 128 + hv;
+        if (n >= d.N || blk >= nblk128) continue;
+        double S = 0.0, Q = 0.0;
+#pragma unroll
+        for (int w = 0; w < WPH; ++w) {
+          S += red[((hv * WPH + w) * BN + c) * 2];
+          Q += red[((hv * WPH + w) * BN + c) * 2 + 1];
+        }
+        d.stats[(blk * d.N + n) * 2] = S;
+        d.stats[(blk * d.N + n) * 2 + 1] = Q;
+      }
+      raw_barrier();  // the statistics scratch is read before the output strips reuse it
+    }
+
+    // output: each wave stages a column strip of its block in the scratch stage, 16-B row chunks
+    OutT* out = reinterpret_cast<OutT*>(d.out);
+    constexpr int CH = 16 / (int)sizeof(OutT);
+    // strips of 32-column multiples that fit the scratch stage (else the direct stores: a wave
+    // instruction then still writes 32 consecutive channels of two rows)
+    constexpr int STRIPS = WR * WC * (int)sizeof(OutT) * NW <= SB ? 1 : 2;
+    constexpr int SC = WC / STRIPS;
+    constexpr int SBYTES = WR * SC * (int)sizeof(OutT);
+    constexpr bool VEC_FITS = NW * SBYTES <= SB && SC % 32 == 0 && WC % STRIPS == 0;
+    const bool vec = VEC_FITS && d.oNlo == 1 && d.nlo >= d.N && d.N % CH == 0 && (((uintptr_t)d.out) & 15) == 0 &&
+                     d.oB % CH == 0 && d.oF % CH == 0 && d.oT % CH == 0;
+    if (VEC_FITS && vec) {
+      OutT* wt = reinterpret_cast<OutT*>(scratch + wave * SBYTES);  // [WR][SC], this wave's
+#pragma unroll
+      for (int st = 0; st < STRIPS; ++st) {
+#pragma unroll
+        for (int jj = 0; jj < SC / 32; ++jj)
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              wt[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * SC + jj * 32 + l32] =
+                  (OutT)acc[i][st * (SC / 32) + jj][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: strip written
+        constexpr int CPRW = SC / CH;
+#pragma unroll
+        for (int q0 = 0; q0 < WR * CPRW; q0 += 64) {
+          const int q = q0 + lane;
+          const int rr = q / CPRW, cc = q % CPRW;
+          const int64_t ro = tb.orow[wm * WR + rr];
+          const int n = n0 + wn * WC + st * SC + cc * CH;
+          if (q < WR * CPRW && ro >= 0 && n < d.N)
+            *reinterpret_cast<uint4*>(out + ro + n) = *reinterpret_cast<const uint4*>(wt + rr * SC + cc * CH);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: strip read back
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) {
+        const int n = n0 + wn * WC + jj * 32 + l32;
+        if (n >= d.N) continue;
+        const int64_t coff = (int64_t)(n / d.nlo) * d.oNhi + (int64_t)(n % d.nlo) * d.oNlo;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = wm * WR + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int64_t ro = tb.orow[row];
+            if (ro >= 0) out[ro + coff] = (OutT)acc[i][jj][r];
+          }
+      }
+    }
+    if (j + 1 < ntl) {
+      // every wave is done with tile j's row table and the scratch stage: build tile j+2's table
+      // into the freed buffer (first read at tile j+1's last K-tile, after >= 1 more barrier)
+      raw_barrier();
+      if (j + 2 < ntl) build_table(j + 2, j & 1);
+      raw_barrier();
+      init_acc(j + 1);
+      read_frags(stages + (gk & 1) * SB, 0, fa0, fb0);
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int PHI, typename OutT, int DBG = 0, int STAG = 0, int NL = 8>
+static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
+  using namespace g8;
+  constexpr int SB = (BM + BN) * 128;
+  const size_t lds = 2 * (size_t)SB + 2 * sizeof(RowTable<BM>) + (size_t)((d.N + 3) & ~3) * 4 +
+                     (size_t)(d.K / 8) * 8;
+  if (lds > 160 * 1024) {
+    set_error("conv2d(bf16 g8): K=%d N=%d needs %zu B of LDS", d.K, d.N, lds);
+    return CLSKD_E_SHAPE;
+  }
+  auto kern = conv_gemm8_kernel<BM, BN, WM, PHI, OutT, DBG, STAG, NL>;
+  static bool attr_set = false;  // per instantiation
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  static const int ncu = [] {
+    int v = 256;
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, 0);
+    return v > 0 ? v : 256;
+  }();
+  const int64_t M = (int64_t)d.B * d.Fo * d.To;
+  const int64_t n_mt = cdiv(M, BM), n_nt = cdiv(d.N, BN);
+  const int64_t ntiles = n_mt * n_nt;
+  // one tile per workgroup when they all fit; otherwise whole XCD groups of workgroups for the
+  // contiguous-run tile deal
+  const int grid = ntiles <= ncu ? (int)ntiles : (ncu & ~7);
+  ConvArgsG8 a{d, (int)n_mt, (int)ntiles};
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), lds, st, a);
+  note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%s,%d,%d,%d>", BM, BN, WM, PHI, type_name<OutT>(), DBG, STAG, NL);
+  return CLSKD_OK;
+}
+
+// Entry from launch_conv_bf16 for N > 64 bf16 layers.  *launched = false leaves the layer to the
+// older engine (CLSKD_G8=0 selects that everywhere; an A/B switch).  CLSKD_G8 = 10*cfg + dbg
+// selects timing-experiment variants (bf16 outputs only).
+int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) {
+  *launched = false;
+  static const int mode = [] {
+    const char* e = getenv("CLSKD_G8");
+    return e ? atoi(e) : 1;
+  }();
+  if (mode == 0 || d.N <= 64 || d.K % 64 != 0 || d.nseg > 2 || (int64_t)d.B * d.Fo * d.To >= ((int64_t)1 << 31))
+    return CLSKD_OK;
+  const bool f32 = d.out_dtype == CLSKD_F32;
+  *launched = true;
+  if (mode >= 10 && !f32) {
+    const int cfg = mode / 10, dbg = mode % 10;
+#define G8X(BM_, BN_, WM_, PHI_, T_, D_, S_, NL_)                             \
+  switch (dbg) {                                                              \
+    case 2: return launch_g8<BM_, BN_, WM_, PHI_, T_, 2, S_, NL_>(d, st);     \
+    case 3: return launch_g8<BM_, BN_, WM_, PHI_, T_, 3, S_, NL_>(d, st);     \
+    default: return launch_g8<BM_, BN_, WM_, PHI_, T_, 0, S_, NL_>(d, st);    \
+  }
+    if (cfg == 5) {  // waves 0-3 issue every piece (4 per substep), waves 4-7 only compute
+      if (d.N <= 128) { G8X(256, 128, 4, 4, __bf16, 0, 0, 4) }
+      G8X(256, 256, 2, 4, __bf16, 0, 0, 4)
+    }
+    if (cfg == 6) {  // as 5, pieces in the first two substeps
+      if (d.N <= 128) { G8X(256, 128, 4, 2, __bf16, 0, 0, 4) }
+      G8X(256, 256, 2, 2, __bf16, 0, 0, 4)
+    }
+    if (d.N <= 128 || cfg == 2) { G8X(256, 128, 4, 2, __bf16, 0, 0, 8) }
+    if (cfg == 3) { G8X(256, 256, 2, 1, __bf16, 0, 0, 8) }
+    if (cfg == 4) { G8X(256, 256, 2, 4, __bf16, 0, 0, 8) }
+    G8X(256, 256, 2, 2, __bf16, 0, 0, 8)
+#undef G8X
+  }
+  if (d.N <= 128) {
+    return f32 ? launch_g8<256, 128, 4, 2, float>(d, st) : launch_g8<256, 128, 4, 2, __bf16>(d, st);
+  }
+  return f32 ? launch_g8<256, 256, 2, 2, float>(d, st) : launch_g8<256, 256, 2, 2, __bf16>(d, st);
+}
+
+}  // namespace clskd

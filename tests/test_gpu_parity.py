@@ -632,3 +632,62 @@ def test_abf_redraw_kernel():
             for j, (w, *_r) in enumerate(abf.redraw_jobs()):
                 assert not torch.equal(snap[(name, i, j)], w.detach().float().reshape(-1))
     assert math.isfinite(float(kd.last["loss"]))
+
+
+G8_CASES = {
+    # name: (segment channels, N, taps, stride_f, Fi, Fo, of_mul, of_add, out_bf16)
+    "enc5x2_n256": ((128,), 256, [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)], 2, 40, 20, 1, 0, True),
+    "dec_parity0_n256": ((256, 256), 256, [(dF, -kt) for dF in (1, 0, -1) for kt in (0, 1)], 1, 10, 10, 2, 0, True),
+    "dec_parity1_n128": ((128, 128), 128, [(dF, -kt) for dF in (1, 0) for kt in (0, 1)], 1, 12, 12, 2, 1, False),
+    "abf3x3_n128": ((64,), 128, [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], 1, 16, 16, 1, 0, True),
+    "pw_k64_nk1_n256": ((64,), 200, [(0, 0)], 1, 9, 9, 1, 0, False),
+    "pw_k128_nk2_n128": ((128,), 128, [(0, 0)], 1, 9, 9, 1, 0, True),
+    "pw_k192_nk3_n256": ((192,), 256, [(0, 0)], 1, 9, 9, 1, 0, True),
+}
+
+
+@pytest.mark.parametrize("case", sorted(G8_CASES))
+def test_conv_gemm8_against_torch(case):
+    """Phase-interleaved 8-wave bf16 GEMM engine (conv_gemm8.hip; N > 64): im2col 5x2 stride-2,
+    two-segment polyphase decoder layers with an interleaved output map, ABF 3x3, and pointwise
+    layers with 1-3 K-tiles (pipeline prologue/drain edge cases), fused BN statistics, M not a
+    tile multiple; vs torch fp64 on the same bf16 operands.  Tolerance 1e-4 relative (fp32 out)
+    / 8e-3 (bf16 out); statistics 1e-5."""
+    from clskd import ops
+    segc, N, taps, sf, Fi, Fo, of_mul, of_add, out_bf16 = G8_CASES[case]
+    g = torch.Generator().manual_seed(len(case) * 13 + N)
+    B, T = 3, 97
+    segs_h = [torch.randn(B, Fi, T, c, generator=g).to(torch.bfloat16) for c in segc]
+    Cin = sum(segc)
+    K = len(taps) * Cin
+    w = torch.randn(N, len(taps), Cin, generator=g) * (0.5 / K ** 0.5)
+    bias = torch.randn(N, generator=g)
+    wp = ops.pack_weight(w.to(DEV), K, "bf16")
+    wq = wp[:, :K].float().cpu().double().view(N, len(taps), Cin)
+    x = torch.cat([s.double() for s in segs_h], 3)
+    ref = bias.double().view(1, 1, 1, N).expand(B, Fo, T, N).clone()
+    for ti, (dF, dT) in enumerate(taps):
+        fi = torch.arange(Fo) * sf + dF
+        tt = torch.arange(T) + dT
+        vf = (fi >= 0) & (fi < Fi)
+        vt = (tt >= 0) & (tt < T)
+        sub = torch.zeros(B, Fo, T, Cin, dtype=torch.float64)
+        sub[:, vf.nonzero()[:, 0][:, None], vt.nonzero()[:, 0][None, :]] = \
+            x[:, fi[vf][:, None], tt[vt][None, :]]
+        ref += torch.einsum("bftc,nc->bftn", sub, wq[:, ti])
+    Fout = Fo * of_mul
+    out = torch.zeros(B, Fout, T, N, device=DEV, dtype=torch.bfloat16 if out_bf16 else torch.float32)
+    nblk = ops.conv_mblocks(B, Fo, T)
+    st = torch.full((nblk * N * 2,), float("nan"), device=DEV, dtype=torch.float64)
+    ops.conv([ops.seg_bftc(s.to(DEV)) for s in segs_h], taps, B, Fo, T, N, wp, bias.to(DEV), out,
+             ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add), stride_f=sf, stats=st)
+    assert ops.conv_kernel_of_last_launch().startswith("conv_gemm8_kernel"), ops.conv_kernel_of_last_launch()
+    o = out.double().cpu()[:, of_add::of_mul]
+    tol = 8e-3 if out_bf16 else 1e-4
+    np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=tol, atol=tol)
+    if of_mul > 1:
+        assert torch.all(out.double().cpu()[:, (of_add + 1) % of_mul::of_mul] == 0)
+    stc = st.view(nblk, N, 2).cpu()
+    assert torch.isfinite(stc).all(), "every statistics slot must be written"
+    np.testing.assert_allclose(stc[:, :, 0].sum(0).numpy(), ref.sum((0, 1, 2)).numpy(), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(stc[:, :, 1].sum(0).numpy(), (ref ** 2).sum((0, 1, 2)).numpy(), rtol=1e-5)
