@@ -205,7 +205,7 @@ def main():
         conv_total_fl = sum(v[2] for v in census.values())
         avg_ms = ms / n_l
         achieved = flops / n_l / (avg_ms * 1e-3) / 1e12
-        bf16_ops = name.startswith("conv_igemm_bf16") or name.startswith("conv_halo_kernel")
+        bf16_ops = name.startswith(("conv_igemm_bf16", "conv_halo_kernel", "conv_gemm8"))
         peak = PEAK_BF16_MFMA_TFLOPS if bf16_ops else PEAK_F32_MFMA_TFLOPS
         traffic, traffic_src = None, None
         tpath = os.path.join(REPO, "profiles", TRAFFIC_FILE)

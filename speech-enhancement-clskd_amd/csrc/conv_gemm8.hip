@@ -73,6 +73,17 @@ __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// vmcnt takes immediates only: wait until at most n of this wave's VMEM ops are outstanding
+template <int MAXN>
+__device__ __forceinline__ void wait_vm(int n) {
+  if constexpr (MAXN <= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (n >= MAXN) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MAXN) : "memory");
+    else wait_vm<MAXN - 1>(n);
+  }
+}
+
 // Row table of one tile (double-buffered in LDS).
 template <int BM>
 struct RowTable {
@@ -88,24 +99,31 @@ struct ConvArgsG8 {
   int n_mt, ntiles;  // M-tiles per N-block, tiles in the list
 };
 
-// DBG (timing experiments only, wrong results): 1 = no LDS-DMA, 2 = no MFMA, 3 = neither.
-template <int BM, int BN, int WM, int PHI, typename OutT, int DBG = 0, int STAG = 0, int NL = 8>
+// BM x BN tile, 8 waves as WM x WN, BK-deep K-tiles (64: 128-B LDS rows; 32: 64-B rows) in NS
+// LDS stages (NS - 1 K-tiles in flight), the DMA pieces of a K-tile issued over the first PHI
+// 16-deep substeps.  DBG (timing experiments only, wrong results): 1 = no LDS-DMA, 2 = no MFMA,
+// 3 = neither.
+template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0>
 __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) {
   using namespace g8;
   const clskd_conv_desc& d = args.d;
-  constexpr int NW = 8, NT = 512, BK = 64, ROWB = 128, NS = 2;
+  constexpr int NW = 8, NT = 512;
+  constexpr int ROWB = 2 * BK;               // LDS row bytes
+  constexpr int CPR = ROWB / 16;             // 16-B chunks per row
+  constexpr int RPP = 64 / CPR;              // rows per 1-KiB DMA piece
+  constexpr int NSUB = BK / 16;              // 16-deep MFMA substeps per K-tile
   constexpr int WN = NW / WM;
   constexpr int WR = BM / WM, WC = BN / WN;  // wave block
   constexpr int FM = WR / 32, FN = WC / 32;  // 32x32 tiles per wave
-  // NL loader waves (0 .. NL-1) issue the DMA pieces: NGA + NGB per loader wave per K-tile
-  constexpr int NGA = BM / 8 / NL, NGB = BN / 8 / NL;
-  constexpr int G = NGA + NGB;
+  constexpr int NGA = BM / RPP / NW, NGB = BN / RPP / NW;
+  constexpr int G = NGA + NGB;               // DMA pieces per wave per K-tile
   constexpr int GP = (G + PHI - 1) / PHI;
-  constexpr int SB = (BM + BN) * ROWB;  // stage bytes
+  constexpr int SB = (BM + BN) * ROWB;       // stage bytes
+  static_assert(BK == 32 || BK == 64, "K-tile depth");
   static_assert(WM * WN == NW && FM >= 1 && FN >= 1, "tile split");
-  static_assert((BM / 8) % NL == 0 && (BN / 8) % NL == 0 && NL <= NW && NL % 2 == 0, "DMA piece split");
-  static_assert(PHI >= 1 && PHI + STAG <= 4, "issue substeps");
-  static_assert(WM * BN * 16 <= SB, "statistics scratch fits one stage");
+  static_assert((BM / RPP) % NW == 0 && (BN / RPP) % NW == 0 && NGA >= 1, "DMA piece split");
+  static_assert(PHI >= 1 && PHI <= NSUB && NSUB % 2 == 0, "issue substeps");
+  static_assert(NS >= 2 && WM * BN * 16 <= SB, "statistics scratch fits one stage");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* stages = smem;
@@ -171,33 +189,35 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
   if (ntl > 1) build_table(1, 1);
   __syncthreads();
 
-  // ---- per-lane DMA geometry (reloaded when the DMA stream moves on to the next tile) --------
-  // piece rows (i*NL + wave)*8 + lane/8: (row >> 1) & 7 = (wave & 1) * 4 + lane / 16 (NL even).
+  // ---- per-lane DMA geometry (reloaded when the DMA stream moves on to another tile) ---------
+  // Piece i of this wave covers tile rows (i*NW + wave)*RPP .. +RPP; lane -> row lane/CPR, LDS
+  // chunk position lane%CPR, source chunk position ^ swizzle(row):
+  //   BK 64: swizzle (row >> 1) & 7 = (wave & 1) * 4 + lane / 16
+  //   BK 32: swizzle (row >> 2) & 3 = (lane / 16) & 3
   // Per A piece: (fi0, ti0) packed in one register (an invalid row carries fi0 = -32768, out of
   // every bound) and the row's element offset in segments 0 and 1 (the kernel takes <= 2).
-  const int csrc = (lane & 7) ^ (((wave & 1) << 2) + (lane >> 4));
-  const int prow = lane >> 3;
+  const int csrc = BK == 64 ? ((lane & 7) ^ (((wave & 1) << 2) + (lane >> 4))) : ((lane & 3) ^ ((lane >> 4) & 3));
+  const int prow = lane / CPR;
   int a_ft[NGA], a_rb0[NGA], a_rb1[NGA];
-  int b_n0 = 0;  // weight row of this lane's first B piece
+  int b_n0 = 0, geo_tile = -1;
   const unsigned short* wgt = reinterpret_cast<const unsigned short*>(d.weight);
-  auto load_geometry = [&](int j, int buf) {
-    const RowTable<BM>& tb = tabs[buf];
+  auto load_geometry = [&](int j) {
+    const RowTable<BM>& tb = tabs[j & 1];
 #pragma unroll
     for (int i = 0; i < NGA; ++i) {
-      const int r = (i * NL + (wave % NL)) * 8 + prow;
+      const int r = (i * NW + wave) * RPP + prow;
       const int4 ri = tb.info[r];
       a_ft[i] = (int)(((unsigned)(ri.z ? ri.x : -32768) << 16) | ((unsigned)ri.y & 0xFFFFu));
       a_rb0[i] = tb.base[0][r];
       a_rb1[i] = tb.base[1][r];
     }
-    b_n0 = tile_nt(j) * BN + (wave % NL) * 8 + prow;
+    b_n0 = tile_nt(j) * BN + wave * RPP + prow;
+    geo_tile = j;
   };
-  load_geometry(0, 0);
 
   const uint64_t zero_addr = (uint64_t)(uintptr_t)g8::zero_page;
   const unsigned stage_lds0 = __builtin_amdgcn_readfirstlane(lds_addr(stages));
   const uint64_t sp0 = (uint64_t)(uintptr_t)d.seg[0].ptr, sp1 = (uint64_t)(uintptr_t)d.seg[1].ptr;
-  // K-chunk entry of K-tile kt for this lane, decoded
   struct KEnt {
     int off, dF, dT, Fb, Tb, s1;
   };
@@ -211,8 +231,7 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
     e.Tb = e.s1 ? d.seg[1].T : d.seg[0].T;
     return e;
   };
-  auto kentry = [&](int kt) -> KEnt { return kdecode(ctab[kt * 8 + csrc]); };
-  // source address of piece g (A pieces first, then B) of K-tile kt
+  // source address of piece g (A pieces first, then B) of K-tile kt (of the geometry's tile)
   auto piece_src = [&](int g, int kt, const KEnt& e) -> uint64_t {
     if (g < NGA) {
       const int fi = (a_ft[g] >> 16) + e.dF;
@@ -224,14 +243,15 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
       const uint64_t msk = 0ull - (uint64_t)ok;  // branch-free select of the zero page
       return (a & msk) | (zero_addr & ~msk);
     }
-    const int n = b_n0 + (g - NGA) * NL * 8;
-    const uint64_t a = (uint64_t)(uintptr_t)wgt + ((uint64_t)(uint32_t)n * (uint32_t)d.K + (uint32_t)(kt * BK + csrc * 8)) * 2u;
+    const int n = b_n0 + (g - NGA) * NW * RPP;
+    const uint64_t a = (uint64_t)(uintptr_t)wgt +
+                       ((uint64_t)(uint32_t)n * (uint32_t)d.K + (uint32_t)(kt * BK + csrc * 8)) * 2u;
     const uint64_t msk = 0ull - (uint64_t)(n < d.N);
     return (a & msk) | (zero_addr & ~msk);
   };
   auto dst = [&](int g, int s) -> unsigned {
     const unsigned sl = stage_lds0 + s * SB;
-    return g < NGA ? sl + (g * NL + wave) * 1024 : sl + BM * ROWB + ((g - NGA) * NL + wave) * 1024;
+    return g < NGA ? sl + (g * NW + wave) * 1024 : sl + BM * ROWB + ((g - NGA) * NW + wave) * 1024;
   };
 
   const int h = lane >> 5, l32 = lane & 31;
@@ -251,18 +271,19 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
   init_acc(0);
 
   // fragment reads of substep s (k = 16s .. 16s+15) of the stage at `sa`
+  auto swz = [](int row) { return BK == 64 ? ((row >> 1) & 7) : ((row >> 2) & 3); };
   auto read_frags = [&](const unsigned char* sa, int s, bf16x8s (&af)[FM], bf16x8s (&bfr)[FN]) {
     const unsigned char* sb = sa + BM * ROWB;
     const int c = 2 * s + h;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int row = wm * WR + i * 32 + l32;
-      af[i] = *reinterpret_cast<const bf16x8s*>(sa + row * ROWB + ((c ^ ((row >> 1) & 7)) << 4));
+      af[i] = *reinterpret_cast<const bf16x8s*>(sa + row * ROWB + ((c ^ swz(row)) << 4));
     }
 #pragma unroll
     for (int jj = 0; jj < FN; ++jj) {
       const int row = wn * WC + jj * 32 + l32;
-      bfr[jj] = *reinterpret_cast<const bf16x8s*>(sb + row * ROWB + ((c ^ ((row >> 1) & 7)) << 4));
+      bfr[jj] = *reinterpret_cast<const bf16x8s*>(sb + row * ROWB + ((c ^ swz(row)) << 4));
     }
   };
   auto mfmas = [&](const bf16x8s (&af)[FM], const bf16x8s (&bfr)[FN]) {
@@ -280,73 +301,72 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
     }
   };
 
-  // ---- prologue: K-tile 0 of tile 0 ----------------------------------------------------------
-  if (!(DBG & 1) && wave < NL) {
-    const KEnt e = kentry(0);
+  // ---- stream of K-tiles over the tile list: K-tile w belongs to tile w / nk ---------------------
+  const int total = ntl * nk;
+  // issue every piece of stream K-tile w into its stage (geometry moved to its tile first)
+  auto issue_all = [&](int w) {
+    const int jt = w / nk, kt = w - jt * nk;
+    if (jt != geo_tile) load_geometry(jt);
+    const KEnt e = kdecode(ctab[kt * CPR + csrc]);
 #pragma unroll
-    for (int g = 0; g < G; ++g) glds16((const void*)piece_src(g, 0, e), dst(g, 0));
+    for (int g = 0; g < G; ++g) glds16((const void*)piece_src(g, kt, e), dst(g, w % NS));
+  };
+  if (!(DBG & 1)) {
+#pragma unroll
+    for (int w = 0; w < NS - 1; ++w)
+      if (w < total) issue_all(w);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  g8::wait_vm<(NS - 2) * G>(min(NS - 2, total - 1) * G);
   raw_barrier();
 
   bf16x8s fa0[FM], fb0[FN], fa1[FM], fb1[FN];
   read_frags(stages, 0, fa0, fb0);
-  // K-chunk entry of the K-tile issued next (read one K-tile ahead: no LDS round trip in front
-  // of the DMA issue)
-  int2 ce_next = ctab[(nk > 1 ? 1 : 0) * 8 + csrc];
-  const int total = ntl * nk;  // K-tiles this workgroup computes, over all its tiles
-  int gk = 0;                  // running index of the K-tile being computed
+  int gk = 0;  // stream index of the K-tile being computed
   for (int j = 0; j < ntl; ++j) {
     for (int kt = 0; kt < nk; ++kt, ++gk) {
-      const unsigned char* sa = stages + (gk & 1) * SB;
-      // the K-tile issued during this one is gk + 1: the next K-tile of this tile, or K-tile 0
-      // of the next tile (the per-lane geometry moves on to that tile first)
-      const bool last_kt = kt == nk - 1;
-      if (last_kt && j + 1 < ntl) load_geometry(j + 1, (j + 1) & 1);
-      const bool do_issue = gk + 1 < total && !(DBG & 1) && wave < NL;
-      const int kin = last_kt ? 0 : kt + 1;  // K-tile (of its tile) being issued
-      const KEnt e = kdecode(ce_next);
-      {  // the entry for the K-tile after it
-        const int kin2 = kin + 1 < nk ? kin + 1 : 0;
-        ce_next = ctab[kin2 * 8 + csrc];
+      const unsigned char* sa = stages + (gk % NS) * SB;
+      // the K-tile issued during this one: stream gk + NS - 1
+      const int wi = gk + NS - 1;
+      const bool do_issue = wi < total && !(DBG & 1);
+      int kti = 0;
+      KEnt e{};
+      if (do_issue) {
+        const int jt = wi / nk;
+        kti = wi - jt * nk;
+        if (jt != geo_tile) load_geometry(jt);
+        e = kdecode(ctab[kti * CPR + csrc]);
       }
-      const int sn = (gk + 1) & 1;
-      // the two waves of a SIMD (w, w + 4) issue their pieces in different substeps, so one's
-      // DMA issue runs beside the other's MFMAs (STAG: waves 4-7 start STAG substeps later)
-      auto issue = [&](int sub) {
-        const int part = sub - (wave >= 4 ? STAG : 0);
-        if (part >= 0 && part < PHI && do_issue) {
+      const int sn = wi % NS;
+      auto issue = [&](int part) {
+        if (part < PHI && do_issue) {
 #pragma unroll
           for (int g = part * GP; g < (part + 1) * GP && g < G; ++g)
-            glds16((const void*)piece_src(g, kin, e), dst(g, sn));
+            glds16((const void*)piece_src(g, kti, e), dst(g, sn));
         }
       };
-      // sched_barriers pin the two-set fragment pipeline (the scheduler would otherwise hoist
-      // every substep's reads to the top and spill)
-      read_frags(sa, 1, fa1, fb1);
-      issue(0);
-      mfmas(fa0, fb0);
-      __builtin_amdgcn_sched_barrier(0);
-      read_frags(sa, 2, fa0, fb0);
-      issue(1);
-      mfmas(fa1, fb1);
-      __builtin_amdgcn_sched_barrier(0);
-      read_frags(sa, 3, fa1, fb1);
-      issue(2);
-      mfmas(fa0, fb0);
-      __builtin_amdgcn_sched_barrier(0);
-      issue(3);
-      mfmas(fa1, fb1);
-      __builtin_amdgcn_sched_barrier(0);
-      // the next K-tile's pieces (this wave's) landed; then every wave's are visible and every
-      // wave is done reading this K-tile's stage
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // two fragment register sets: substep s + 1 is read while substep s computes; the
+      // sched_barriers pin that (the scheduler would otherwise hoist every read and spill)
+#pragma unroll
+      for (int s = 0; s < NSUB; ++s) {
+        if (s + 1 < NSUB) {
+          if (s & 1) read_frags(sa, s + 1, fa0, fb0);
+          else read_frags(sa, s + 1, fa1, fb1);
+        }
+        if (s & 1) mfmas(fa1, fb1);
+        else mfmas(fa0, fb0);
+        issue(s);  // behind the MFMAs: the K-entry read / address ALU overlap them
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // the next K-tile's pieces (this wave's) landed — younger K-tiles stay in flight; then
+      // every wave's are visible and every wave is done reading this K-tile's stage
+      if (gk + 1 < total) g8::wait_vm<(NS - 2) * G>(min(NS - 2, total - 2 - gk) * G);
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       raw_barrier();
-      if (!last_kt) read_frags(stages + sn * SB, 0, fa0, fb0);
+      if (kt + 1 < nk) read_frags(stages + ((gk + 1) % NS) * SB, 0, fa0, fb0);
     }
 
-    // ---- tile epilogue (the next tile's K-tile 0 is resident in the other stage) -------------
-    unsigned char* scratch = stages + ((gk - 1) & 1) * SB;  // the stage just computed from
+    // ---- tile epilogue: the stage of the K-tile just computed is free ------------------------
+    unsigned char* scratch = stages + ((gk - 1) % NS) * SB;
     const RowTable<BM>& tb = tabs[j & 1];
     const int64_t m0 = (int64_t)tile_mt(j) * BM;
     const int n0 = tile_nt(j) * BN;
@@ -405,45 +425,39 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
         d.stats[(blk * d.N + n) * 2] = S;
         d.stats[(blk * d.N + n) * 2 + 1] = Q;
       }
-      raw_barrier();  // the statistics scratch is read before the output strips reuse it
+      raw_barrier();  // the statistics scratch is read before the output staging reuses it
     }
 
-    // output: each wave stages a column strip of its block in the scratch stage, 16-B row chunks
+    // output: each wave stages one 32x32 accumulator tile at a time in its slice of the scratch
+    // stage and writes it back as 16-B row chunks (else direct stores: a wave instruction then
+    // still writes 32 consecutive channels of two rows)
     OutT* out = reinterpret_cast<OutT*>(d.out);
     constexpr int CH = 16 / (int)sizeof(OutT);
-    // strips of 32-column multiples that fit the scratch stage (else the direct stores: a wave
-    // instruction then still writes 32 consecutive channels of two rows)
-    constexpr int STRIPS = WR * WC * (int)sizeof(OutT) * NW <= SB ? 1 : 2;
-    constexpr int SC = WC / STRIPS;
-    constexpr int SBYTES = WR * SC * (int)sizeof(OutT);
-    constexpr bool VEC_FITS = NW * SBYTES <= SB && SC % 32 == 0 && WC % STRIPS == 0;
-    const bool vec = VEC_FITS && d.oNlo == 1 && d.nlo >= d.N && d.N % CH == 0 && (((uintptr_t)d.out) & 15) == 0 &&
+    constexpr int UB = 32 * 32 * (int)sizeof(OutT);  // bytes per staged tile
+    static_assert(NW * UB <= SB, "epilogue staging");
+    const bool vec = d.oNlo == 1 && d.nlo >= d.N && d.N % CH == 0 && (((uintptr_t)d.out) & 15) == 0 &&
                      d.oB % CH == 0 && d.oF % CH == 0 && d.oT % CH == 0;
-    if (VEC_FITS && vec) {
-      OutT* wt = reinterpret_cast<OutT*>(scratch + wave * SBYTES);  // [WR][SC], this wave's
+    if (vec) {
+      OutT* wt = reinterpret_cast<OutT*>(scratch + wave * UB);  // [32][32], this wave's
+      constexpr int CPRW = 32 / CH;
 #pragma unroll
-      for (int st = 0; st < STRIPS; ++st) {
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int jj = 0; jj < SC / 32; ++jj)
+        for (int jj = 0; jj < FN; ++jj) {
 #pragma unroll
-          for (int i = 0; i < FM; ++i)
+          for (int r = 0; r < 16; ++r) wt[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + l32] = (OutT)acc[i][jj][r];
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: tile written
 #pragma unroll
-            for (int r = 0; r < 16; ++r)
-              wt[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * SC + jj * 32 + l32] =
-                  (OutT)acc[i][st * (SC / 32) + jj][r];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: strip written
-        constexpr int CPRW = SC / CH;
-#pragma unroll
-        for (int q0 = 0; q0 < WR * CPRW; q0 += 64) {
-          const int q = q0 + lane;
-          const int rr = q / CPRW, cc = q % CPRW;
-          const int64_t ro = tb.orow[wm * WR + rr];
-          const int n = n0 + wn * WC + st * SC + cc * CH;
-          if (q < WR * CPRW && ro >= 0 && n < d.N)
-            *reinterpret_cast<uint4*>(out + ro + n) = *reinterpret_cast<const uint4*>(wt + rr * SC + cc * CH);
+          for (int q0 = 0; q0 < 32 * CPRW; q0 += 64) {
+            const int q = q0 + lane;
+            const int rr = q / CPRW, cc = q % CPRW;
+            const int64_t ro = tb.orow[wm * WR + i * 32 + rr];
+            const int n = n0 + wn * WC + jj * 32 + cc * CH;
+            if (ro >= 0 && n < d.N)
+              *reinterpret_cast<uint4*>(out + ro + n) = *reinterpret_cast<const uint4*>(wt + rr * 32 + cc * CH);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: tile read back
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: strip read back
-      }
     } else {
 #pragma unroll
       for (int jj = 0; jj < FN; ++jj) {
@@ -462,27 +476,27 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
     }
     if (j + 1 < ntl) {
       // every wave is done with tile j's row table and the scratch stage: build tile j+2's table
-      // into the freed buffer (first read at tile j+1's last K-tile, after >= 1 more barrier)
+      // into the freed buffer (the DMA stream reaches tile j+2 only after >= 1 more barrier)
       raw_barrier();
       if (j + 2 < ntl) build_table(j + 2, j & 1);
       raw_barrier();
       init_acc(j + 1);
-      read_frags(stages + (gk & 1) * SB, 0, fa0, fb0);
+      read_frags(stages + (gk % NS) * SB, 0, fa0, fb0);
     }
   }
 }
 
-template <int BM, int BN, int WM, int PHI, typename OutT, int DBG = 0, int STAG = 0, int NL = 8>
+template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0>
 static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   using namespace g8;
-  constexpr int SB = (BM + BN) * 128;
-  const size_t lds = 2 * (size_t)SB + 2 * sizeof(RowTable<BM>) + (size_t)((d.N + 3) & ~3) * 4 +
+  constexpr int SB = (BM + BN) * 2 * BK;
+  const size_t lds = NS * (size_t)SB + 2 * sizeof(RowTable<BM>) + (size_t)((d.N + 3) & ~3) * 4 +
                      (size_t)(d.K / 8) * 8;
   if (lds > 160 * 1024) {
     set_error("conv2d(bf16 g8): K=%d N=%d needs %zu B of LDS", d.K, d.N, lds);
     return CLSKD_E_SHAPE;
   }
-  auto kern = conv_gemm8_kernel<BM, BN, WM, PHI, OutT, DBG, STAG, NL>;
+  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG>;
   static bool attr_set = false;  // per instantiation
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -501,49 +515,54 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   const int grid = ntiles <= ncu ? (int)ntiles : (ncu & ~7);
   ConvArgsG8 a{d, (int)n_mt, (int)ntiles};
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), lds, st, a);
-  note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%s,%d,%d,%d>", BM, BN, WM, PHI, type_name<OutT>(), DBG, STAG, NL);
+  note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d>", BM, BN, WM, BK, NS, PHI, type_name<OutT>(), DBG);
   return CLSKD_OK;
 }
 
 // Entry from launch_conv_bf16 for N > 64 bf16 layers.  *launched = false leaves the layer to the
 // older engine (CLSKD_G8=0 selects that everywhere; an A/B switch).  CLSKD_G8 = 10*cfg + dbg
-// selects timing-experiment variants (bf16 outputs only).
+// selects timing-experiment variants (bf16 outputs only); read per launch (tests switch it).
 int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) {
   *launched = false;
-  static const int mode = [] {
-    const char* e = getenv("CLSKD_G8");
-    return e ? atoi(e) : 1;
-  }();
+  const char* env = getenv("CLSKD_G8");
+  const int mode = env ? atoi(env) : 1;
   if (mode == 0 || d.N <= 64 || d.K % 64 != 0 || d.nseg > 2 || (int64_t)d.B * d.Fo * d.To >= ((int64_t)1 << 31))
     return CLSKD_OK;
   const bool f32 = d.out_dtype == CLSKD_F32;
   *launched = true;
   if (mode >= 10 && !f32) {
     const int cfg = mode / 10, dbg = mode % 10;
-#define G8X(BM_, BN_, WM_, PHI_, T_, D_, S_, NL_)                             \
+#define G8X(BM_, BN_, WM_, BK_, NS_, PHI_)                                    \
   switch (dbg) {                                                              \
-    case 2: return launch_g8<BM_, BN_, WM_, PHI_, T_, 2, S_, NL_>(d, st);     \
-    case 3: return launch_g8<BM_, BN_, WM_, PHI_, T_, 3, S_, NL_>(d, st);     \
-    default: return launch_g8<BM_, BN_, WM_, PHI_, T_, 0, S_, NL_>(d, st);    \
+    case 1: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 1>(d, st);  \
+    case 2: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 2>(d, st);  \
+    case 3: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 3>(d, st);  \
+    default: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 0>(d, st); \
   }
-    if (cfg == 5) {  // waves 0-3 issue every piece (4 per substep), waves 4-7 only compute
-      if (d.N <= 128) { G8X(256, 128, 4, 4, __bf16, 0, 0, 4) }
-      G8X(256, 256, 2, 4, __bf16, 0, 0, 4)
+    const int nk64 = d.K / 64;
+    switch (cfg) {
+      case 2:  // BK 32, four stages (three K-tiles in flight)
+        if (d.N <= 128) { G8X(256, 128, 4, 32, 5, 1) }
+        G8X(256, 256, 2, 32, 4, 1)
+      case 3:  // BK 32, three stages
+        if (d.N <= 128) { G8X(256, 128, 4, 32, 4, 1) }
+        G8X(256, 256, 2, 32, 3, 1)
+      case 4:  // BK 32, pieces over both substeps
+        if (d.N <= 128) { G8X(256, 128, 4, 32, 5, 2) }
+        G8X(256, 256, 2, 32, 4, 2)
+      case 5:  // 256 x 128 tiles everywhere, BK 32 four stages
+        G8X(256, 128, 4, 32, 5, 1)
+      default:  // BK 64, two stages
+        (void)nk64;
+        if (d.N <= 128) { G8X(256, 128, 4, 64, 2, 2) }
+        G8X(256, 256, 2, 64, 2, 2)
     }
-    if (cfg == 6) {  // as 5, pieces in the first two substeps
-      if (d.N <= 128) { G8X(256, 128, 4, 2, __bf16, 0, 0, 4) }
-      G8X(256, 256, 2, 2, __bf16, 0, 0, 4)
-    }
-    if (d.N <= 128 || cfg == 2) { G8X(256, 128, 4, 2, __bf16, 0, 0, 8) }
-    if (cfg == 3) { G8X(256, 256, 2, 1, __bf16, 0, 0, 8) }
-    if (cfg == 4) { G8X(256, 256, 2, 4, __bf16, 0, 0, 8) }
-    G8X(256, 256, 2, 2, __bf16, 0, 0, 8)
 #undef G8X
   }
   if (d.N <= 128) {
-    return f32 ? launch_g8<256, 128, 4, 2, float>(d, st) : launch_g8<256, 128, 4, 2, __bf16>(d, st);
+    return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float>(d, st) : launch_g8<256, 128, 4, 64, 2, 2, __bf16>(d, st);
   }
-  return f32 ? launch_g8<256, 256, 2, 2, float>(d, st) : launch_g8<256, 256, 2, 2, __bf16>(d, st);
+  return f32 ? launch_g8<256, 256, 2, 64, 2, 2, float>(d, st) : launch_g8<256, 256, 2, 64, 2, 2, __bf16>(d, st);
 }
 
 }  // namespace clskd

@@ -681,7 +681,7 @@ def test_conv_gemm8_against_torch(case):
     st = torch.full((nblk * N * 2,), float("nan"), device=DEV, dtype=torch.float64)
     ops.conv([ops.seg_bftc(s.to(DEV)) for s in segs_h], taps, B, Fo, T, N, wp, bias.to(DEV), out,
              ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add), stride_f=sf, stats=st)
-    assert ops.conv_kernel_of_last_launch().startswith("conv_gemm8_kernel"), ops.conv_kernel_of_last_launch()
+    assert ops.conv_kernel_of_last_launch().startswith("conv_gemm8"), ops.conv_kernel_of_last_launch()
     o = out.double().cpu()[:, of_add::of_mul]
     tol = 8e-3 if out_bf16 else 1e-4
     np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=tol, atol=tol)
