@@ -82,7 +82,7 @@ def _side_stream(dev, which=0):
         return torch.cuda.current_stream(dev)
     key = (torch.device(dev).index, which)
     if key not in _SIDE:
-        prio = -1 if (which == 2 and _PRIO == "teacher") else 0
+        prio = -1 if ((which == 2 and _PRIO == "teacher") or (which == 0 and _PRIO == "student")) else 0
         _SIDE[key] = torch.cuda.Stream(device=dev, priority=prio)
     return _SIDE[key]
 

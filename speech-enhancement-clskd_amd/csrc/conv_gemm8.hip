@@ -103,7 +103,7 @@ struct ConvArgsG8 {
 // LDS stages (NS - 1 K-tiles in flight), the DMA pieces of a K-tile issued over the first PHI
 // 16-deep substeps.  DBG (timing experiments only, wrong results): 1 = no LDS-DMA, 2 = no MFMA,
 // 3 = neither.
-template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0>
+template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1>
 __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) {
   using namespace g8;
   const clskd_conv_desc& d = args.d;
@@ -319,8 +319,14 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
   g8::wait_vm<(NS - 2) * G>(min(NS - 2, total - 1) * G);
   raw_barrier();
 
-  bf16x8s fa0[FM], fb0[FN], fa1[FM], fb1[FN];
-  read_frags(stages, 0, fa0, fb0);
+  constexpr int NSET = PF + 1;
+  static_assert(PF >= 1 && PF < NSUB, "fragment prefetch distance");
+  bf16x8s fa[NSET][FM], fb[NSET][FN];
+  auto read_head = [&](const unsigned char* sa) {  // the first PF substeps of a K-tile
+#pragma unroll
+    for (int s = 0; s < PF; ++s) read_frags(sa, s, fa[s], fb[s]);
+  };
+  read_head(stages);
   int gk = 0;  // stream index of the K-tile being computed
   for (int j = 0; j < ntl; ++j) {
     for (int kt = 0; kt < nk; ++kt, ++gk) {
@@ -344,16 +350,12 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
             glds16((const void*)piece_src(g, kti, e), dst(g, sn));
         }
       };
-      // two fragment register sets: substep s + 1 is read while substep s computes; the
+      // PF + 1 fragment register sets: substep s + PF is read while substep s computes; the
       // sched_barriers pin that (the scheduler would otherwise hoist every read and spill)
 #pragma unroll
       for (int s = 0; s < NSUB; ++s) {
-        if (s + 1 < NSUB) {
-          if (s & 1) read_frags(sa, s + 1, fa0, fb0);
-          else read_frags(sa, s + 1, fa1, fb1);
-        }
-        if (s & 1) mfmas(fa1, fb1);
-        else mfmas(fa0, fb0);
+        if (s + PF < NSUB) read_frags(sa, s + PF, fa[(s + PF) % NSET], fb[(s + PF) % NSET]);
+        mfmas(fa[s % NSET], fb[s % NSET]);
         issue(s);  // behind the MFMAs: the K-entry read / address ALU overlap them
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -362,7 +364,7 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
       if (gk + 1 < total) g8::wait_vm<(NS - 2) * G>(min(NS - 2, total - 2 - gk) * G);
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       raw_barrier();
-      if (kt + 1 < nk) read_frags(stages + ((gk + 1) % NS) * SB, 0, fa0, fb0);
+      if (kt + 1 < nk) read_head(stages + ((gk + 1) % NS) * SB);
     }
 
     // ---- tile epilogue: the stage of the K-tile just computed is free ------------------------
@@ -481,12 +483,12 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
       if (j + 2 < ntl) build_table(j + 2, j & 1);
       raw_barrier();
       init_acc(j + 1);
-      read_frags(stages + (gk % NS) * SB, 0, fa0, fb0);
+      read_head(stages + (gk % NS) * SB);
     }
   }
 }
 
-template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0>
+template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1>
 static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   using namespace g8;
   constexpr int SB = (BM + BN) * 2 * BK;
@@ -496,7 +498,7 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
     set_error("conv2d(bf16 g8): K=%d N=%d needs %zu B of LDS", d.K, d.N, lds);
     return CLSKD_E_SHAPE;
   }
-  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG>;
+  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG, PF>;
   static bool attr_set = false;  // per instantiation
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -512,10 +514,14 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   const int64_t ntiles = n_mt * n_nt;
   // one tile per workgroup when they all fit; otherwise whole XCD groups of workgroups for the
   // contiguous-run tile deal
-  const int grid = ntiles <= ncu ? (int)ntiles : (ncu & ~7);
+  // CLSKD_G8_GRID caps the workgroup count (leaves CUs to concurrent streams; A/B knob)
+  const char* ge = getenv("CLSKD_G8_GRID");
+  const int cap = ge ? atoi(ge) : ncu;
+  const int ncap = cap > 0 && cap < ncu ? cap : ncu;
+  const int grid = ntiles <= ncap ? (int)ntiles : (ncap >= 8 ? (ncap & ~7) : ncap);
   ConvArgsG8 a{d, (int)n_mt, (int)ntiles};
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), lds, st, a);
-  note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d>", BM, BN, WM, BK, NS, PHI, type_name<OutT>(), DBG);
+  note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d>", BM, BN, WM, BK, NS, PHI, type_name<OutT>(), DBG, PF);
   return CLSKD_OK;
 }
 
@@ -526,7 +532,8 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
   *launched = false;
   const char* env = getenv("CLSKD_G8");
   const int mode = env ? atoi(env) : 1;
-  if (mode == 0 || d.N <= 64 || d.K % 64 != 0 || d.nseg > 2 || (int64_t)d.B * d.Fo * d.To >= ((int64_t)1 << 31))
+  if (mode == 0 || d.N <= 64 || d.K % 64 != 0 || d.nseg > 2 || (int64_t)d.B * d.Fo * d.To >= ((int64_t)1 << 31) ||
+      (int64_t)d.Fo * d.stride_f >= 32768 || (int64_t)d.To * d.stride_t >= 32768)  // 16-bit row origins
     return CLSKD_OK;
   const bool f32 = d.out_dtype == CLSKD_F32;
   *launched = true;
@@ -552,6 +559,13 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
         G8X(256, 256, 2, 32, 4, 2)
       case 5:  // 256 x 128 tiles everywhere, BK 32 four stages
         G8X(256, 128, 4, 32, 5, 1)
+      case 6:  // fragment prefetch two substeps ahead (three register sets)
+        if (d.N <= 128) return launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 2>(d, st);
+        return launch_g8<256, 256, 2, 64, 2, 2, __bf16, 0, 2>(d, st);
+      case 7:  // prefetch two ahead, 256 x 128 tiles everywhere
+        return launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 2>(d, st);
+      case 8:  // prefetch three ahead, 256 x 128 tiles everywhere
+        return launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 3>(d, st);
       default:  // BK 64, two stages
         (void)nk64;
         if (d.N <= 128) { G8X(256, 128, 4, 64, 2, 2) }

@@ -477,7 +477,11 @@ static int launch_halo_planned(const HaloArgs& a, size_t lds, hipStream_t st, bo
     (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, 0);
     return v > 0 ? v : 256;
   }();
-  const int grid = a.ntiles < ncu ? a.ntiles : ncu;
+  // CLSKD_HALO_GRID caps the workgroup count (leaves CUs to concurrent streams; A/B knob)
+  const char* ge = getenv("CLSKD_HALO_GRID");
+  const int cap = ge ? atoi(ge) : ncu;
+  const int ncap = cap > 0 && cap < ncu ? cap : ncu;
+  const int grid = a.ntiles < ncap ? a.ntiles : ncap;
   if (d.stats && grid > a.nblk128) return CLSKD_OK;  // (never for eligible shapes)
   const bool f32out = d.out_dtype == CLSKD_F32;
 #define HALO_LAUNCH(BN_, O_, NT_)                                                              \

@@ -691,3 +691,4 @@ def test_conv_gemm8_against_torch(case):
     assert torch.isfinite(stc).all(), "every statistics slot must be written"
     np.testing.assert_allclose(stc[:, :, 0].sum(0).numpy(), ref.sum((0, 1, 2)).numpy(), rtol=1e-5, atol=1e-3)
     np.testing.assert_allclose(stc[:, :, 1].sum(0).numpy(), (ref ** 2).sum((0, 1, 2)).numpy(), rtol=1e-5)
+
