@@ -41,9 +41,11 @@ def _mark(label, stream):
 
 
 _PRIO = os.environ.get("CLSKD_STREAM_PRIO", "none")
-# ReviewKD-decoder placement (A/B knob): "pipelined" runs it level by level on the caller's
-# stream behind the student decoder; "after" runs it on the student stream after the student
-_RKD_DEC = os.environ.get("CLSKD_RKD_DEC", "after")
+# ReviewKD-decoder placement (A/B knob): "pipelined" (default) runs it level by level on the
+# caller's stream behind the student decoder; "after" runs it on the student stream after the
+# student.  Measured on MI355X with the persistent conv engines (round 2, four passes each,
+# one box): 5.71-5.81 vs 5.89-5.95 ms per C2 step (round 1's engines: "after" was faster).
+_RKD_DEC = os.environ.get("CLSKD_RKD_DEC", "pipelined")
 # host enqueue order of the step's two chains (A/B knob): "1" enqueues the teacher chain — the
 # critical path — before the student-side chains
 _TEACHER_FIRST = os.environ.get("CLSKD_TEACHER_FIRST", "1") == "1"

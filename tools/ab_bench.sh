@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/ab
 mkdir -p $O
 i=0
-for pass in 1 2; do
+for pass in ${PASSES:-1 2}; do
   i=0
   IFS=';' read -ra CS <<< "$CASES"
   for c in "${CS[@]}"; do
