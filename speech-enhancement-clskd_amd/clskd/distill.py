@@ -49,9 +49,10 @@ _RKD_DEC = os.environ.get("CLSKD_RKD_DEC", "pipelined")
 # host enqueue order of the step's two chains (A/B knob): "1" enqueues the teacher chain — the
 # critical path — before the student-side chains
 _TEACHER_FIRST = os.environ.get("CLSKD_TEACHER_FIRST", "1") == "1"
-# A/B knob: CLSKD_RKD_FORK=1 forks every ReviewKD conv2 (+ BN, Grams) onto the caller's stream
-# (measured: 6.18 vs 6.08 ms per C2 step, the step is throughput- not chain-bound — off)
-_RKD_FORK = os.environ.get("CLSKD_RKD_FORK", "0") == "1"
+# A/B knob: CLSKD_RKD_FORK=1 (default) forks every ReviewKD-encoder conv2 (+ BN, Grams) onto the
+# caller's stream, off the level-to-level residual chain (round 1's engines: 6.18 vs 6.08 ms,
+# off; round 2, persistent conv engines + pipelined ReviewKD decoder: 5.52 vs 5.64 ms, on)
+_RKD_FORK = os.environ.get("CLSKD_RKD_FORK", "1") == "1"
 
 
 _SERIAL = False
