@@ -14,6 +14,8 @@
 // the gathered A per step in LDS and issuing v_mfma_f32_32x32x2_f32 with the ROW axis as the
 // MFMA reduction axis (A operand = dY^T, B operand = A).  Range partials go to a workspace
 // [S][N][Kp] and a second kernel sums them in a fixed order: deterministic, no float atomics.
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "common.h"
@@ -238,11 +240,18 @@ __global__ void axpy_f32_kernel(const float* __restrict__ x, float* __restrict__
 
 inline unsigned grid_for(int64_t n) { return (unsigned)std::min<int64_t>(cdiv(n, 256), 8192); }
 
-// splits of the row axis: ~2048 workgroups in flight, at least 256 rows per split
+// splits of the row axis: about CLSKD_WGRAD_WG workgroups (default 4096), at least 256 rows
+// per split.  The [S][N][K] partials are written once and re-read by wgrad_reduce_kernel, so
+// S trades occupancy against partial traffic.
+inline int wgrad_target() {
+  const char* e = getenv("CLSKD_WGRAD_WG");
+  const int v = e ? atoi(e) : 4096;
+  return v >= 64 ? v : 4096;
+}
 inline void wgrad_plan(const clskd_conv_desc& d, int& S, int64_t& rps) {
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
   const int64_t tiles = cdiv(d.N, WG_TN) * cdiv(d.K, WG_TK);
-  int64_t s = cdiv(4096, tiles);
+  int64_t s = cdiv(wgrad_target(), tiles);
   s = std::max<int64_t>(1, std::min<int64_t>({s, (int64_t)1024, cdiv(M, 256)}));
   rps = cdiv(cdiv(M, s), WG_RB) * WG_RB;
   S = (int)cdiv(M, rps);

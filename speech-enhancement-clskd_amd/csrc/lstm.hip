@@ -172,6 +172,116 @@ __global__ __launch_bounds__(NKS * H) void lstm_recurrent_kernel(
 }
 
 
+// Single-wave recurrence for small H (H * S = 64 lanes: S = 64 / H k-slices per unit; H = 32:
+// S = 2, H = 16: S = 4).  The student's H = 32 layers sit on the step's critical chain, where
+// the 8-wave layout above pays an s_barrier and a cross-wave LDS round trip every step: here
+// one wave holds the whole recurrence, h is exchanged through a double-buffered LDS row that
+// the same wave writes and then reads (LDS operations of one wave complete in order: no
+// barrier), the S slices of a unit reduce with log2(S) DPP adds, lane s < 4 of a unit applies
+// gate(s) as in the k-sliced kernel, lane 0 keeps the cell, and h_t goes straight to `out`
+// (one 4*H-byte store per step).  Inputs prefetched two steps ahead.
+template <int H>
+__global__ __launch_bounds__(64) void lstm_wave_kernel(
+    const float* __restrict__ gx, int64_t gx_ws, int64_t gx_seq, int64_t gx_t,
+    const float* __restrict__ whh, int T, float* __restrict__ out, int64_t o_ws, int64_t o_seq,
+    int64_t o_t) {
+  constexpr int S = 64 / H;   // k-slices per unit
+  constexpr int KW = H / S;   // k-slice width
+  constexpr int G = 4 * H;
+  static_assert((S == 2 || S == 4) && KW % 4 == 0, "single-wave layout");
+  const int lane = threadIdx.x;
+  const int u = lane / S, ks = lane % S;
+  const int ws = blockIdx.y, seq = blockIdx.x;
+  __shared__ __attribute__((aligned(16))) float hb[2][H];
+  f32x2l w[4][KW / 2];
+#pragma unroll
+  for (int gt = 0; gt < 4; ++gt) {
+    const float* wrow = whh + ((int64_t)ws * G + gt * H + u) * H + ks * KW;
+#pragma unroll
+    for (int j = 0; j < KW; j += 2) w[gt][j / 2] = *reinterpret_cast<const f32x2l*>(wrow + j);
+  }
+  if (lane < H) hb[1][lane] = 0.f;  // h(-1) = 0
+  float cstate = 0.f;
+  // this lane's gates: S = 4 -> gate ks; S = 2 -> gates ks, ks + 2
+  const float* gp = gx + ws * gx_ws + seq * gx_seq + u;
+  float* op = out + ws * o_ws + seq * o_seq + u;
+  auto load_g = [&](int t, float& g0, float& g1) {
+    const float* q = gp + (int64_t)min(t, T - 1) * gx_t;
+    g0 = q[ks * H];
+    if constexpr (S == 2) g1 = q[(ks + 2) * H];
+  };
+  float ga0 = 0.f, ga1 = 0.f, gb0 = 0.f, gb1 = 0.f;
+  load_g(0, ga0, ga1);
+  load_g(1, gb0, gb1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  auto step = [&](int t, float g0, float g1) {
+    const float* hp = hb[(t + 1) & 1] + ks * KW;  // h(t-1)
+    f32x4 hv[KW / 4];
+#pragma unroll
+    for (int j = 0; j < KW / 4; ++j) hv[j] = reinterpret_cast<const f32x4*>(hp)[j];
+    f32x2l acc[4][2] = {};
+#pragma unroll
+    for (int j = 0; j < KW / 4; ++j) {
+      const f32x2l h01 = {hv[j][0], hv[j][1]}, h23 = {hv[j][2], hv[j][3]};
+#pragma unroll
+      for (int gt = 0; gt < 4; ++gt) {
+        acc[gt][j & 1] = __builtin_elementwise_fma(w[gt][2 * j], h01, acc[gt][j & 1]);
+        acc[gt][j & 1] = __builtin_elementwise_fma(w[gt][2 * j + 1], h23, acc[gt][j & 1]);
+      }
+    }
+    float pre[4];
+#pragma unroll
+    for (int gt = 0; gt < 4; ++gt) {
+      const f32x2l a2 = acc[gt][0] + acc[gt][1];
+      float v = a2[0] + a2[1];
+      v += dpp<DPP_XOR1>(v);
+      if constexpr (S == 4) v += dpp<DPP_XOR2>(v);
+      pre[gt] = v;
+    }
+    float ig, fg, gg, og;
+    if constexpr (S == 4) {
+      const float p01 = (ks & 1) ? pre[1] : pre[0];
+      const float p23 = (ks & 1) ? pre[3] : pre[2];
+      const float pg = ((ks & 2) ? p23 : p01) + g0;
+      const float k = ks == 2 ? 2.f : 1.f;
+      const float act = fmaf(k, sigm_fast(k * pg), ks == 2 ? -1.f : 0.f);
+      ig = act;
+      fg = dpp<DPP_BCAST1>(act);
+      gg = dpp<DPP_BCAST2>(act);
+      og = dpp<DPP_BCAST3>(act);
+    } else {
+      // lane 0: i (sig) and g (tanh); lane 1: f (sig) and o (sig)
+      const float pa = (ks ? pre[1] : pre[0]) + g0;
+      const float pb = (ks ? pre[3] : pre[2]) + g1;
+      const float a0 = sigm_fast(pa);
+      const float kb = ks ? 1.f : 2.f;
+      const float a1 = fmaf(kb, sigm_fast(kb * pb), ks ? 0.f : -1.f);
+      ig = a0;
+      gg = a1;
+      // lane 0 of each pair reads lane 1: quad_perm [1,1,3,3]
+      fg = dpp<0xF5>(a0);
+      og = dpp<0xF5>(a1);
+    }
+    if (ks == 0) {
+      cstate = fg * cstate + ig * gg;
+      const float hn = og * tanh_fast(cstate);
+      hb[t & 1][u] = hn;
+      op[(int64_t)t * o_t] = hn;
+    }
+    // one wave: its LDS write completes before its next read is served (in-order LDS queue);
+    // the wait + clobber keep the compiler from moving the next step's reads above the write
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+
+  for (int t = 0; t < T; t += 2) {
+    step(t, ga0, ga1);
+    load_g(t + 2, ga0, ga1);
+    if (t + 1 < T) step(t + 1, gb0, gb1);
+    load_g(t + 3, gb0, gb1);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Backward of the recurrence (BPTT) for one (weight set, sequence) per workgroup.
 // Inputs: pre[ws][seq][t][4H] = the gate PRE-activations of the forward (x W_ih^T + b + h_{t-1}
@@ -347,11 +457,10 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
     const int v = e ? atoi(e) : 4;
     return (v == 2 || v == 8) ? v : 4;
   }();
-  static const int nks32 = [] {
-    const char* e = getenv("CLSKD_LSTM_NKS32");
-    const int v = e ? atoi(e) : 8;
-    return (v == 2 || v == 4) ? v : 8;
-  }();
+  // H = 32: CLSKD_LSTM_NKS32 = 2 | 4 | 8 selects the k-sliced multi-wave kernel, 1 (default)
+  // the single-wave kernel (lstm_wave_kernel)
+  const char* e32 = getenv("CLSKD_LSTM_NKS32");
+  const int nks32 = e32 ? atoi(e32) : 1;
 #define LSTM_LAUNCH(H_, NKS_) \
   hipLaunchKernelGGL((lstm_recurrent_kernel<H_, NKS_>), grid, dim3(NKS_ * H_), 0, st, gx, gx_ws, \
                      gx_seq, gx_t, whh, T, out, o_ws, o_seq, o_t)
@@ -362,7 +471,9 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
     case 32:
       if (nks32 == 4) LSTM_LAUNCH(32, 4);
       else if (nks32 == 2) LSTM_LAUNCH(32, 2);
-      else LSTM_LAUNCH(32, 8);
+      else if (nks32 == 8) LSTM_LAUNCH(32, 8);
+      else hipLaunchKernelGGL(lstm_wave_kernel<32>, grid, dim3(64), 0, st, gx, gx_ws, gx_seq, gx_t,
+                              whh, T, out, o_ws, o_seq, o_t);
       break;
     case 64:
       LSTM_LAUNCH(64, 4);

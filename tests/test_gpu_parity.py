@@ -692,3 +692,32 @@ def test_conv_gemm8_against_torch(case):
     np.testing.assert_allclose(stc[:, :, 0].sum(0).numpy(), ref.sum((0, 1, 2)).numpy(), rtol=1e-5, atol=1e-3)
     np.testing.assert_allclose(stc[:, :, 1].sum(0).numpy(), (ref ** 2).sum((0, 1, 2)).numpy(), rtol=1e-5)
 
+
+
+@pytest.mark.parametrize("variant", ["1", "8"])
+def test_lstm_recurrence_against_torch(variant, monkeypatch):
+    """Complex-LSTM recurrence (tools_for_model.py:159-174, nn.LSTM gates i, f, g, o, zero
+    state) at the student's H = 32: the single-wave kernel (CLSKD_LSTM_NKS32=1, default) and the
+    8-slice multi-wave kernel, vs a torch fp64 recurrence on the same gate inputs.  Tolerance
+    2e-5 (v_exp / v_rcp gate activations, fp32 state)."""
+    from clskd import ops
+    monkeypatch.setenv("CLSKD_LSTM_NKS32", variant)
+    g = torch.Generator().manual_seed(3)
+    nws, nseq, T, H = 2, 5, 37, 32
+    gx = torch.randn(nseq, T, nws * 4 * H, generator=g)
+    whh = torch.randn(nws, 4 * H, H, generator=g) * 0.2
+    out = torch.empty(nws, nseq, T, H, device=DEV)
+    ops.lstm_recurrent(gx.to(DEV), 4 * H, T * nws * 4 * H, nws * 4 * H, whh.to(DEV), nws, nseq, T, H,
+                       out, nseq * T * H, T * H, H)
+    ref = torch.empty(nws, nseq, T, H, dtype=torch.float64)
+    for ws in range(nws):
+        W = whh[ws].double()
+        h = torch.zeros(nseq, H, dtype=torch.float64)
+        c = torch.zeros(nseq, H, dtype=torch.float64)
+        for t in range(T):
+            z = gx[:, t, ws * 4 * H:(ws + 1) * 4 * H].double() + h @ W.t()
+            i, f, gg, o = z.split(H, 1)
+            c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+            h = torch.sigmoid(o) * torch.tanh(c)
+            ref[ws, :, t] = h
+    np.testing.assert_allclose(out.double().cpu().numpy(), ref.numpy(), rtol=2e-5, atol=2e-5)
