@@ -102,7 +102,8 @@ struct ConvArgsG8 {
 // BM x BN tile, 8 waves as WM x WN, BK-deep K-tiles (64: 128-B LDS rows; 32: 64-B rows) in NS
 // LDS stages (NS - 1 K-tiles in flight), the DMA pieces of a K-tile issued over the first PHI
 // 16-deep substeps.  DBG (timing experiments only, wrong results): 1 = no LDS-DMA, 2 = no MFMA,
-// 3 = neither.
+// 3 = neither, 4 = B operand only (no A gather), 5 = A operand only.  Correct-result variants:
+// 6 = s_setprio 1 around each substep's MFMA cluster, 7 = static priority 1 for waves 4-7, 8 = both.
 template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1>
 __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) {
   using namespace g8;
@@ -287,12 +288,14 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
     }
   };
   auto mfmas = [&](const bf16x8s (&af)[FM], const bf16x8s (&bfr)[FN]) {
-    if constexpr ((DBG & 2) == 0) {
+    if constexpr (DBG != 2 && DBG != 3) {
+      if constexpr (DBG == 6 || DBG == 8) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int jj = 0; jj < FN; ++jj)
           acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[jj], acc[i][jj], 0, 0, 0);
+      if constexpr (DBG == 6 || DBG == 8) __builtin_amdgcn_s_setprio(0);
     } else {
 #pragma unroll
       for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(af[i]));
@@ -311,7 +314,7 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
 #pragma unroll
     for (int g = 0; g < G; ++g) glds16((const void*)piece_src(g, kt, e), dst(g, w % NS));
   };
-  if (!(DBG & 1)) {
+  if (DBG != 1 && DBG != 3) {
 #pragma unroll
     for (int w = 0; w < NS - 1; ++w)
       if (w < total) issue_all(w);
@@ -327,13 +330,15 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
     for (int s = 0; s < PF; ++s) read_frags(sa, s, fa[s], fb[s]);
   };
   read_head(stages);
+  if constexpr (DBG == 7 || DBG == 8)
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   int gk = 0;  // stream index of the K-tile being computed
   for (int j = 0; j < ntl; ++j) {
     for (int kt = 0; kt < nk; ++kt, ++gk) {
       const unsigned char* sa = stages + (gk % NS) * SB;
       // the K-tile issued during this one: stream gk + NS - 1
       const int wi = gk + NS - 1;
-      const bool do_issue = wi < total && !(DBG & 1);
+      const bool do_issue = wi < total && DBG != 1 && DBG != 3;
       int kti = 0;
       KEnt e{};
       if (do_issue) {
@@ -346,8 +351,10 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
       auto issue = [&](int part) {
         if (part < PHI && do_issue) {
 #pragma unroll
-          for (int g = part * GP; g < (part + 1) * GP && g < G; ++g)
+          for (int g = part * GP; g < (part + 1) * GP && g < G; ++g) {
+            if ((DBG == 4 && g < NGA) || (DBG == 5 && g >= NGA)) continue;  // A- / B-only timing
             glds16((const void*)piece_src(g, kti, e), dst(g, sn));
+          }
         }
       };
       // PF + 1 fragment register sets: substep s + PF is read while substep s computes; the
@@ -361,8 +368,8 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
       }
       // the next K-tile's pieces (this wave's) landed — younger K-tiles stay in flight; then
       // every wave's are visible and every wave is done reading this K-tile's stage
-      if (gk + 1 < total) g8::wait_vm<(NS - 2) * G>(min(NS - 2, total - 2 - gk) * G);
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (DBG >= 4 || gk + 1 >= total) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else g8::wait_vm<(NS - 2) * G>(min(NS - 2, total - 2 - gk) * G);
       raw_barrier();
       if (kt + 1 < nk) read_head(stages + ((gk + 1) % NS) * SB);
     }
@@ -544,6 +551,11 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
     case 1: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 1>(d, st);  \
     case 2: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 2>(d, st);  \
     case 3: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 3>(d, st);  \
+    case 4: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 4>(d, st);  \
+    case 5: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 5>(d, st);  \
+    case 6: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 6>(d, st);  \
+    case 7: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 7>(d, st);  \
+    case 8: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 8>(d, st);  \
     default: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 0>(d, st); \
   }
     const int nk64 = d.K / 64;
