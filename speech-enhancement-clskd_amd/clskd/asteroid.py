@@ -193,9 +193,7 @@ class DCCRNet_mini(nn.Module):
             w = torch.cat([top, bot], 0)    # rows [prev_re, skip_re, prev_im, skip_im]
             ci = wr.shape[0]
             ns = ci - nprev
-            perm = torch.cat([torch.arange(0, nprev), torch.arange(ci, ci + nprev),
-                              torch.arange(nprev, ci), torch.arange(ci + nprev, ci + nprev + ns)])
-            w = w[perm.to(w.device)]
+            w = torch.cat([w[0:nprev], w[ci:ci + nprev], w[nprev:ci], w[ci + nprev:ci + nprev + ns]], 0)
             taps = [(kf, kt) for kf, _ in self._DEC_TAPS[parity] for kt in (0, 1)]
             w = torch.stack([w[:, :, kf, kt] for kf, kt in taps], 0).permute(2, 0, 1)
             Co = w.shape[0]

@@ -358,8 +358,10 @@ def dccrn_backward(m, tape, enc, dec, dec_in, lstm_io, g, pg, acc_params=False, 
         for p in (0, 1):
             kfs = [kf for kf in range(5) if kf % 2 == p]
             taps_b = [((p - kf + 2) // 2, 1 - kt) for kf in kfs for kt in range(2)]
+            # kfs = p, p+2, ...: a strided slice — a Python-list index would build an index
+            # tensor and copy it host-to-device synchronously every step (host stalls on the GPU)
             wt = _tw(("enc_t", id(m), i, p), wp, lambda: ops.pack_weight(
-                wp[:, :10 * Ci].reshape(Co, 5, 2, Ci)[:, kfs].permute(3, 1, 2, 0)
+                wp[:, :10 * Ci].reshape(Co, 5, 2, Ci)[:, p::2].permute(3, 1, 2, 0)
                 .reshape(Ci, len(kfs) * 2, Co).contiguous(), len(kfs) * 2 * Co))
             ops.conv([dseg], taps_b, B, Fo, T, Ci, wt, None, g["enc"][i - 1],
                      OutMap(2 * Fo * T * Ci, T * Ci, Ci, of_mul=2, of_add=p), accumulate=True)

@@ -272,10 +272,10 @@ class DCCRN(nn.Module):
             # K order per tap: [out_t (re, im), skip (re, im)] — two contiguous segments (the
             # decoder input and the skip tensor, each whole): fewer, wider gather runs, and
             # 32-channel segments make narrow layers eligible for the halo kernel
+            # (row blocks by slicing: an index tensor built on the host would be copied to the
+            # device synchronously on every re-pack, i.e. every training step)
             h = Ci // 4
-            perm = torch.cat([torch.arange(0, h), torch.arange(2 * h, 3 * h),
-                              torch.arange(h, 2 * h), torch.arange(3 * h, 4 * h)]).to(w.device)
-            w = w[perm]
+            w = torch.cat([w[0:h], w[2 * h:3 * h], w[h:2 * h], w[3 * h:4 * h]], 0)
             taps = [(kf, kt) for kf, _ in self._DEC_TAPS[parity] for kt in (0, 1)]
             w = torch.stack([w[:, :, kf, kt] for kf, kt in taps], 0)  # [ntap, Ci, Co]
             w = w.permute(2, 0, 1)  # [Co, ntap, Ci]

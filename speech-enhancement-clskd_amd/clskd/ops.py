@@ -633,20 +633,29 @@ def gram_view(t):
     return GramView(tc, 0, n, n // g, g, 0, g)
 
 
+# Elements per row per slab (one workgroup each).  Smaller slabs mean more workgroups in flight
+# and more partials for the finalize; tools/gram_micro.py on MI355X (one view, isolated):
+# bf16 8192 -> 5.4-5.9 TB/s (16384: 3.5-5.9), fp32 2048 -> 4.0-4.9 TB/s (16384: 1.0-1.9, about
+# 100 workgroups).  A/B knobs CLSKD_GRAM_CHUNK_BF16 / CLSKD_GRAM_CHUNK_F32.
+_GRAM_CHUNK_BF16 = int(os.environ.get("CLSKD_GRAM_CHUNK_BF16", "16384"))
+_GRAM_CHUNK_F32 = int(os.environ.get("CLSKD_GRAM_CHUNK_F32", "16384"))
+
+
 class GramSlabs:
     """Gram partials of some views, launched on the current stream into a slab buffer of their
     own (clskd_gram_partial).  `refs[i]` = (device address of view i's first slab, slab count)
     for clskd_spkd_finalize_ranges; the object owns the buffer (keep it until the finalize ran)."""
 
-    def __init__(self, views, B, chunk_elems=16384):
+    def __init__(self, views, B, chunk_elems=None):
         dev = views[0].tensor.device
         jobs = (_lib.GramJob * len(views))()
         first = 0
         spans = []
         for j, v in enumerate(views):
-            chunk = max(1, chunk_elems // v.Cs)
-            ns = -(-v.P // chunk)
             dt = _dt(v.tensor)
+            ce = chunk_elems or (_GRAM_CHUNK_BF16 if dt == _lib.BF16 else _GRAM_CHUNK_F32)
+            chunk = max(1, ce // v.Cs)
+            ns = -(-v.P // chunk)
             assert v.Cs % (8 if dt == _lib.BF16 else 4) == 0
             sc = sh = None
             if v.affine is not None:
@@ -686,7 +695,7 @@ def spkd_finalize(s_refs, t_refs, B, batchmean=True, out=None, return_grams=Fals
     return losses
 
 
-def spkd_losses(pairs_views, B, batchmean=True, return_grams=False, chunk_elems=16384, out=None):
+def spkd_losses(pairs_views, B, batchmean=True, return_grams=False, chunk_elems=None, out=None):
     """pairs_views: list of (student GramView, teacher GramView).  One gram launch for every
     view, one finalize launch for every pair.  Returns losses [npairs] (and grams)."""
     views = [v for pr in pairs_views for v in pr]

@@ -103,12 +103,13 @@ struct ConvArgsG8 {
 // LDS stages (NS - 1 K-tiles in flight), the DMA pieces of a K-tile issued over the first PHI
 // 16-deep substeps.  DBG (timing experiments only, wrong results): 1 = no LDS-DMA, 2 = no MFMA,
 // 3 = neither, 4 = B operand only (no A gather), 5 = A operand only.  Correct-result variants:
-// 6 = s_setprio 1 around each substep's MFMA cluster, 7 = static priority 1 for waves 4-7, 8 = both.
-template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1>
-__global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) {
+// 6 = s_setprio 1 around each substep's MFMA cluster, 7 = static priority 1 for waves 4-7, 8 = both;
+// 9 = no DMA wait inside the stream (timing only: DMA latency vs issue cost).
+template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8>
+__global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 args) {
   using namespace g8;
   const clskd_conv_desc& d = args.d;
-  constexpr int NW = 8, NT = 512;
+  constexpr int NW = NWV, NT = NWV * 64;
   constexpr int ROWB = 2 * BK;               // LDS row bytes
   constexpr int CPR = ROWB / 16;             // 16-B chunks per row
   constexpr int RPP = 64 / CPR;              // rows per 1-KiB DMA piece
@@ -368,8 +369,12 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
       }
       // the next K-tile's pieces (this wave's) landed — younger K-tiles stay in flight; then
       // every wave's are visible and every wave is done reading this K-tile's stage
-      if (DBG >= 4 || gk + 1 >= total) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else g8::wait_vm<(NS - 2) * G>(min(NS - 2, total - 2 - gk) * G);
+      if (DBG == 9 && gk + 1 < total) {  // timing only: never wait for the DMA inside the stream
+      } else if ((DBG >= 4 && DBG <= 5) || gk + 1 >= total) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        g8::wait_vm<(NS - 2) * G>(min(NS - 2, total - 2 - gk) * G);
+      }
       raw_barrier();
       if (kt + 1 < nk) read_head(stages + ((gk + 1) % NS) * SB);
     }
@@ -495,7 +500,7 @@ __global__ __launch_bounds__(512) void conv_gemm8_kernel(const ConvArgsG8 args) 
   }
 }
 
-template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1>
+template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8>
 static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   using namespace g8;
   constexpr int SB = (BM + BN) * 2 * BK;
@@ -505,7 +510,7 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
     set_error("conv2d(bf16 g8): K=%d N=%d needs %zu B of LDS", d.K, d.N, lds);
     return CLSKD_E_SHAPE;
   }
-  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG, PF>;
+  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG, PF, NWV>;
   static bool attr_set = false;  // per instantiation
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -527,8 +532,8 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   const int ncap = cap > 0 && cap < ncu ? cap : ncu;
   const int grid = ntiles <= ncap ? (int)ntiles : (ncap >= 8 ? (ncap & ~7) : ncap);
   ConvArgsG8 a{d, (int)n_mt, (int)ntiles};
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), lds, st, a);
-  note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d>", BM, BN, WM, BK, NS, PHI, type_name<OutT>(), DBG, PF);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NWV * 64), lds, st, a);
+  note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d>", BM, BN, WM, BK, NS, PHI, type_name<OutT>(), DBG, PF, NWV);
   return CLSKD_OK;
 }
 
@@ -556,6 +561,7 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
     case 6: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 6>(d, st);  \
     case 7: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 7>(d, st);  \
     case 8: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 8>(d, st);  \
+    case 9: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 9>(d, st);  \
     default: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 0>(d, st); \
   }
     const int nk64 = d.K / 64;
@@ -578,6 +584,9 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
         return launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 2>(d, st);
       case 8:  // prefetch three ahead, 256 x 128 tiles everywhere
         return launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 3>(d, st);
+      case 9:  // four waves (one per SIMD), each a 128 x 128 (N > 128) or 128 x 64 block
+        if (dbg == 1 || d.N <= 128) return launch_g8<256, 128, 2, 64, 2, 2, __bf16, 0, 1, 4>(d, st);
+        return launch_g8<256, 256, 2, 64, 2, 2, __bf16, 0, 1, 4>(d, st);
       default:  // BK 64, two stages
         (void)nk64;
         if (d.N <= 128) { G8X(256, 128, 4, 64, 2, 2) }

@@ -36,52 +36,69 @@ struct SpkdPairsArg {
 // the workgroup (aff[0][ch] = scale, aff[1][ch] = shift, ch in [0, Ctot)).
 constexpr int GRAM_AFF_MAX = 1024;
 
+// Slab-relative element e -> row-relative offset (p - p0) * Ctot + c0 + c with p - p0 = e / Cs
+// and c = e % Cs by a 32-bit multiply-high (exact for e * Cs < 2^32: the kernel only asks for
+// e < nel = (p1 - p0) * Cs <= max(16384, Cs) elements per row per slab, and a slab of one
+// position needs no split at all); no 64-bit division per load.
+struct ESplit {
+  uint32_t cs, magic, ctot, c0;
+  bool one;  // the slab holds one position: e < Cs
+};
+__device__ __forceinline__ ESplit make_split(const clskd_gram_job& j, int64_t p0, int64_t p1) {
+  ESplit s;
+  s.cs = (uint32_t)j.Cs;
+  s.magic = 0xFFFFFFFFu / s.cs + 1u;
+  s.ctot = (uint32_t)j.Ctot;
+  s.c0 = (uint32_t)j.c0;
+  s.one = p1 - p0 <= 1;
+  return s;
+}
+__device__ __forceinline__ void split_e(uint32_t e, const ESplit& s, uint32_t& pr, uint32_t& c) {
+  if (s.one) {
+    pr = 0;
+    c = e;
+  } else {
+    pr = __umulhi(e, s.magic);
+    c = e - pr * s.cs;
+  }
+}
+
 template <bool AFF>
-__device__ __forceinline__ f32x4 load_row4_f32(const clskd_gram_job& j, int b, int B, int64_t e,
-                                               int64_t p0, int64_t p1,
+__device__ __forceinline__ f32x4 load_row4_f32(const clskd_gram_job& j, const ESplit& sp,
+                                               int64_t rowbase, uint32_t e,
                                                const float (*aff)[GRAM_AFF_MAX]) {
-  // 4 fp32 elements at slab-relative element e (Cs % 4 == 0, e % 4 == 0)
-  f32x4 v = {0.f, 0.f, 0.f, 0.f};
-  if (b < B) {
-    const int64_t p = p0 + e / j.Cs;
-    const int c = (int)(e % j.Cs);
-    if (p < p1) {
-      v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(j.ptr) +
-                                          (int64_t)b * j.sB + p * j.Ctot + j.c0 + c);
-      if constexpr (AFF) {
-        const f32x4 sc = *reinterpret_cast<const f32x4*>(&aff[0][j.c0 + c]);
-        const f32x4 sh = *reinterpret_cast<const f32x4*>(&aff[1][j.c0 + c]);
+  // 4 fp32 elements at slab-relative element e (Cs % 4 == 0, e % 4 == 0; e < nel)
+  uint32_t pr, c;
+  split_e(e, sp, pr, c);
+  f32x4 v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(j.ptr) + rowbase +
+                                            (int64_t)((uint64_t)pr * sp.ctot + c));
+  if constexpr (AFF) {
+    const f32x4 sc = *reinterpret_cast<const f32x4*>(&aff[0][sp.c0 + c]);
+    const f32x4 sh = *reinterpret_cast<const f32x4*>(&aff[1][sp.c0 + c]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = fmaf(v[i], sc[i], sh[i]);
-      }
-    }
+    for (int i = 0; i < 4; ++i) v[i] = fmaf(v[i], sc[i], sh[i]);
   }
   return v;
 }
 
 template <bool AFF>
-__device__ __forceinline__ bf16x8g load_row8_bf16(const clskd_gram_job& j, int b, int B, int64_t e,
-                                                  int64_t p0, int64_t p1,
+__device__ __forceinline__ bf16x8g load_row8_bf16(const clskd_gram_job& j, const ESplit& sp,
+                                                  int64_t rowbase, uint32_t e,
                                                   const float (*aff)[GRAM_AFF_MAX]) {
   // 8 bf16 elements (one 16-B load) at slab-relative element e (Cs % 8 == 0, e % 8 == 0)
-  bf16x8g v = {};
-  if (b < B) {
-    const int64_t p = p0 + e / j.Cs;
-    const int c = (int)(e % j.Cs);
-    if (p < p1) {
-      v = *reinterpret_cast<const bf16x8g*>(reinterpret_cast<const __bf16*>(j.ptr) +
-                                            (int64_t)b * j.sB + p * j.Ctot + j.c0 + c);
-      if constexpr (AFF) {  // the same fmaf + RNE rounding as clskd_bn_apply
-        const f32x4 s0 = *reinterpret_cast<const f32x4*>(&aff[0][j.c0 + c]);
-        const f32x4 s1 = *reinterpret_cast<const f32x4*>(&aff[0][j.c0 + c + 4]);
-        const f32x4 h0 = *reinterpret_cast<const f32x4*>(&aff[1][j.c0 + c]);
-        const f32x4 h1 = *reinterpret_cast<const f32x4*>(&aff[1][j.c0 + c + 4]);
+  uint32_t pr, c;
+  split_e(e, sp, pr, c);
+  bf16x8g v = *reinterpret_cast<const bf16x8g*>(reinterpret_cast<const __bf16*>(j.ptr) + rowbase +
+                                                (int64_t)((uint64_t)pr * sp.ctot + c));
+  if constexpr (AFF) {  // the same fmaf + RNE rounding as clskd_bn_apply
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(&aff[0][sp.c0 + c]);
+    const f32x4 s1 = *reinterpret_cast<const f32x4*>(&aff[0][sp.c0 + c + 4]);
+    const f32x4 h0 = *reinterpret_cast<const f32x4*>(&aff[1][sp.c0 + c]);
+    const f32x4 h1 = *reinterpret_cast<const f32x4*>(&aff[1][sp.c0 + c + 4]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          v[i] = (__bf16)fmaf((float)v[i], s0[i], h0[i]);
-          v[i + 4] = (__bf16)fmaf((float)v[i + 4], s1[i], h1[i]);
-        }
-      }
+    for (int i = 0; i < 4; ++i) {
+      v[i] = (__bf16)fmaf((float)v[i], s0[i], h0[i]);
+      v[i + 4] = (__bf16)fmaf((float)v[i + 4], s1[i], h1[i]);
     }
   }
   return v;
@@ -122,18 +139,24 @@ __device__ __forceinline__ void gram_accumulate(const clskd_gram_job& j, int B, 
   const int wave = threadIdx.x >> 6;
   const int r = lane & 15;
   const int g = lane >> 4;
+  const ESplit sp = make_split(j, p0, p1);
+  // rows past B read row 0 (valid memory) and are zeroed: the MFMA sees zeros for them
+  const bool in0 = r < B, in1 = r + 16 < B;
+  const int64_t rb0 = (int64_t)(in0 ? r : 0) * j.sB + p0 * j.Ctot + j.c0;
+  const int64_t rb1 = (int64_t)(in1 ? r + 16 : 0) * j.sB + p0 * j.Ctot + j.c0;
+  const uint32_t n32 = (uint32_t)nel;
   if (j.dtype == CLSKD_BF16) {
     // 16x16x32 bf16 MFMA: lane (r, g) holds row r, 8 consecutive k; A and B are the same
     // register (G = Z Z^T), so one 16-B load feeds both operands.  64 B per row per load.
     constexpr int U = 8;
-    for (int64_t base = (int64_t)wave * 32; base < nel; base += 128 * U) {
+    for (uint32_t base = (uint32_t)wave * 32; base < n32; base += 128 * U) {
       bf16x8g v0[U], v1[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t e = base + (int64_t)u * 128 + 8 * g;
-        const bool ok = e < nel;
-        v0[u] = ok ? load_row8_bf16<AFF>(j, r, B, e, p0, p1, aff) : bf16x8g{};
-        if constexpr (NB == 2) v1[u] = ok ? load_row8_bf16<AFF>(j, r + 16, B, e, p0, p1, aff) : bf16x8g{};
+        const uint32_t e = base + (uint32_t)u * 128 + 8 * g;
+        const bool ok = e < n32;
+        v0[u] = ok && in0 ? load_row8_bf16<AFF>(j, sp, rb0, e, aff) : bf16x8g{};
+        if constexpr (NB == 2) v1[u] = ok && in1 ? load_row8_bf16<AFF>(j, sp, rb1, e, aff) : bf16x8g{};
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -147,14 +170,14 @@ __device__ __forceinline__ void gram_accumulate(const clskd_gram_job& j, int B, 
   } else {
     // fp32: 16x16x4 f32 MFMA, lane (r, g) holds row r, 4 consecutive elements per load
     constexpr int U = 4;
-    for (int64_t base = (int64_t)wave * 16; base < nel; base += 64 * U) {
+    for (uint32_t base = (uint32_t)wave * 16; base < n32; base += 64 * U) {
       f32x4 v0[U], v1[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t e = base + (int64_t)u * 64 + 4 * g;
-        const bool ok = e < nel;
-        v0[u] = ok ? load_row4_f32<AFF>(j, r, B, e, p0, p1, aff) : f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (NB == 2) v1[u] = ok ? load_row4_f32<AFF>(j, r + 16, B, e, p0, p1, aff) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const uint32_t e = base + (uint32_t)u * 64 + 4 * g;
+        const bool ok = e < n32;
+        v0[u] = ok && in0 ? load_row4_f32<AFF>(j, sp, rb0, e, aff) : f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (NB == 2) v1[u] = ok && in1 ? load_row4_f32<AFF>(j, sp, rb1, e, aff) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -574,6 +597,8 @@ static int validate_gram_jobs(const clskd_gram_job* jobs, int32_t njobs, int32_t
                           j.sB % g == 0 && j.P > 0 && j.chunk > 0,
                       "gram: job %d geometry (Cs %d, c0 %d, Ctot %d) needs multiples of %d", k,
                       j.Cs, j.c0, j.Ctot, g);
+    CLSKD_CHECK_SHAPE(j.chunk == 1 || (uint64_t)j.chunk * (uint64_t)j.Cs * (uint64_t)j.Cs < (1ull << 32),
+                      "gram: job %d chunk %lld x Cs %d^2 must stay below 2^32", k, (long long)j.chunk, j.Cs);
     CLSKD_CHECK_ARG((j.scale == nullptr) == (j.shift == nullptr),
                     "gram: job %d scale and shift go together", k);
     CLSKD_CHECK_SHAPE(!j.scale || j.Ctot <= GRAM_AFF_MAX, "gram: job %d folded affine needs Ctot <= %d",

@@ -469,6 +469,7 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
       LSTM_LAUNCH(16, 4);
       break;
     case 32:
+      if (const char* td = getenv("CLSKD_LSTM32_TDIV")) T = max(1, T / max(1, atoi(td)));  // timing only
       if (nks32 == 4) LSTM_LAUNCH(32, 4);
       else if (nks32 == 2) LSTM_LAUNCH(32, 2);
       else if (nks32 == 8) LSTM_LAUNCH(32, 8);
@@ -479,6 +480,8 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
       LSTM_LAUNCH(64, 4);
       break;
     case 128:
+      // timing experiment only (wrong results): CLSKD_LSTM128_TDIV = d runs T / d steps
+      if (const char* td = getenv("CLSKD_LSTM128_TDIV")) T = max(1, T / max(1, atoi(td)));
       if (nks128 == 8) LSTM_LAUNCH(128, 8);
       else if (nks128 == 4) LSTM_LAUNCH(128, 4);
       else LSTM_LAUNCH(128, 2);
