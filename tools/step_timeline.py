@@ -31,38 +31,27 @@ def main():
         for k, (busy, cnt, a, b) in sorted(per.items(), key=lambda kv: kv[1][2]):
             print(f"  queue {k:>4}: {cnt:4d} kernels, busy {busy / 1e3:7.1f} us, "
                   f"first start +{(a - t0) / 1e3:7.1f}, last end +{(b - t0) / 1e3:7.1f}")
-        # concurrency histogram
-        ev = []
-        for r in sel:
-            ev.append((int(r["Start_Timestamp"]), 1, r))
-            ev.append((int(r["End_Timestamp"]), -1, r))
-        ev.sort(key=lambda e: (e[0], e[1]))
+        # concurrency histogram: sweep start/end events, attributing single-kernel spans
+        ev = sorted([(int(r["Start_Timestamp"]), 1, i) for i, r in enumerate(sel)] +
+                    [(int(r["End_Timestamp"]), -1, i) for i, r in enumerate(sel)],
+                    key=lambda e: (e[0], e[1]))
         hist = collections.Counter()
         solo = collections.Counter()
-        cur, last = 0, t0
-        running = set()
-        for t, d, r in ev:
+        running, last = set(), t0
+        for t, d, i in ev:
             if t > last:
-                hist[cur] += t - last
-                if cur == 1:
-                    solo[canonical(next(iter(running))["Kernel_Name"])] += t - last
+                hist[len(running)] += t - last
+                if len(running) == 1:
+                    solo[canonical(sel[next(iter(running))]["Kernel_Name"])] += t - last
                 last = t
-            cur += d
             if d > 0:
-                running.add(id(r)) if False else None
-            # track running rows
-            if d > 0:
-                running_rows[id(r)] = r
+                running.add(i)
             else:
-                running_rows.pop(id(r), None)
-            running = set() if not running_rows else {0}
-            running = [running_rows[k] for k in running_rows]
+                running.discard(i)
         print("  time by concurrent kernels: " +
               ", ".join(f"{c}: {v / 1e3:.0f} us" for c, v in sorted(hist.items())))
         print("  running alone (top): " + ", ".join(f"{k[:40]} {v / 1e3:.0f}" for k, v in solo.most_common(8)))
 
-
-running_rows = {}
 
 if __name__ == "__main__":
     main()
