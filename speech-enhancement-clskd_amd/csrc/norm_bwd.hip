@@ -111,13 +111,29 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
     double* alpha_part, int accumulate) {
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
-  double SB = 0, SG = 0, SA = 0;
-  for (int b = tid; b < nblk; b += 256) {
-    const double* p = partial + ((int64_t)b * C + c) * 3;
-    SB += p[0];
-    SG += p[1];
-    SA += p[2];
+  // eight independent accumulators: eight strided partial rows in flight per thread (the loop
+  // was one L2 round trip per 256 rows — latency-bound at nblk ~ 16k); fixed combine order
+  double sb[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sg[8] = {0, 0, 0, 0, 0, 0, 0, 0},
+         sa[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int b = tid;
+  for (; b + 7 * 256 < nblk; b += 8 * 256) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double* p = partial + ((int64_t)(b + u * 256) * C + c) * 3;
+      sb[u] += p[0];
+      sg[u] += p[1];
+      sa[u] += p[2];
+    }
   }
+  for (; b < nblk; b += 256) {
+    const double* p = partial + ((int64_t)b * C + c) * 3;
+    sb[0] += p[0];
+    sg[0] += p[1];
+    sa[0] += p[2];
+  }
+  double SB = ((sb[0] + sb[1]) + (sb[2] + sb[3])) + ((sb[4] + sb[5]) + (sb[6] + sb[7]));
+  double SG = ((sg[0] + sg[1]) + (sg[2] + sg[3])) + ((sg[4] + sg[5]) + (sg[6] + sg[7]));
+  const double SA = ((sa[0] + sa[1]) + (sa[2] + sa[3])) + ((sa[4] + sa[5]) + (sa[6] + sa[7]));
   __shared__ double r0[256], r1[256], r2[256];
   r0[tid] = SB;
   r1[tid] = SG;
@@ -163,22 +179,31 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     int accumulate) {
   const int64_t nq = rows * C / 4;
   const float al = alpha ? alpha[0] : 1.f;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
-       q += (int64_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)((q * 4) % C);
+  // channel of the thread's first quad, then advanced by the grid stride (mod C): no 64-bit
+  // modulo per quad; the per-channel vectors are 16-B loads (C % 4 == 0, 16-B aligned: host)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cstep = (int)((stride * 4) % C);
+  int c0 = (int)((q0 * 4) % C);
+  for (int64_t q = q0; q < nq; q += stride) {
     const f32x4 xv = ld4<T>(x + q * 4);
     const f32x4 gv = *reinterpret_cast<const f32x4*>(dy + q * 4);
+    const f32x4 k0 = *reinterpret_cast<const f32x4*>(k + c0);
+    const f32x4 k1 = *reinterpret_cast<const f32x4*>(k + C + c0);
+    const f32x4 k2 = *reinterpret_cast<const f32x4*>(k + 2 * C + c0);
+    f32x4 dz = gv;
+    if (alpha) {
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + c0);
+      const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + c0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (!(fmaf(xv[j], sc[j], sh[j]) > 0.f)) dz[j] = al * gv[j];
+    }
     f32x4 o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = c0 + j;
-      float dz = gv[j];
-      if (alpha) {
-        const float yb = fmaf(xv[j], scale[c], shift[c]);
-        if (!(yb > 0.f)) dz = al * gv[j];
-      }
-      o[j] = fmaf(k[c], dz, fmaf(k[C + c], xv[j], k[2 * C + c]));
-    }
+    for (int j = 0; j < 4; ++j) o[j] = fmaf(k0[j], dz[j], fmaf(k1[j], xv[j], k2[j]));
+    c0 += cstep;
+    if (c0 >= C) c0 -= C;
     if (accumulate) o += *reinterpret_cast<const f32x4*>(dx + q * 4);
     *reinterpret_cast<f32x4*>(dx + q * 4) = o;
   }
@@ -201,6 +226,8 @@ __device__ __forceinline__ int nearest_src_b(int dst, int in_size, int out_size)
 
 // smallest dst with nearest_src(dst) >= s (nearest_src is non-decreasing in dst)
 __device__ __forceinline__ int first_dst_b(int s, int in_size, int out_size) {
+  if (out_size == in_size) return s;           // the nearest_src_b fast paths, inverted
+  if (out_size == 2 * in_size) return 2 * s;
   int d0 = (int)((double)s * out_size / in_size) - 2;
   if (d0 < 0) d0 = 0;
   while (d0 < out_size && nearest_src_b(d0, in_size, out_size) < s) ++d0;
@@ -253,10 +280,11 @@ __global__ __launch_bounds__(256) void abf_fuse_bwd_kernel(
   const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
   const int64_t nslots = ((int64_t)gridDim.x * blockDim.x) >> 4;
   for (int64_t p = gw; p < npix; p += nslots) {
-    const int t = (int)(p % T);
-    const int64_t bf = p / T;
-    const int f = (int)(bf % F);
-    const int b = (int)(bf / F);
+    // 32-bit index split (npix < 2^31, checked by the host): no 64-bit division per pixel
+    const uint32_t p32 = (uint32_t)p, bf = p32 / (uint32_t)T;
+    const int t = (int)(p32 - bf * (uint32_t)T);
+    const int b = (int)(bf / (uint32_t)F);
+    const int f = (int)(bf - (uint32_t)b * (uint32_t)F);
     const int fr = nearest_src_b(f, Fr, F);
     const int tr = nearest_src_b(t, Tr, T);
     const f32x4 xraw = ld4<DT>(x1 + p * 64 + c);
@@ -686,6 +714,9 @@ extern "C" int clskd_bn_bwd(const void* x, const float* dy, int64_t rows, int32_
   CLSKD_CHECK_SHAPE(rows > 0 && C >= 4 && C % 4 == 0 && C <= 1024 && nblk >= 1,
                     "bn_bwd: rows=%lld C=%d nblk=%d", (long long)rows, C, nblk);
   CLSKD_CHECK_ARG(dtype == CLSKD_F32 || dtype == CLSKD_BF16, "bn_bwd: dtype");
+  CLSKD_CHECK_ARG(((uintptr_t)work & 15) == 0 &&
+                      (!alpha || (((uintptr_t)scale & 15) == 0 && ((uintptr_t)shift & 15) == 0)),
+                  "bn_bwd: work (and scale/shift with PReLU) must be 16-byte aligned");
   hipStream_t st = as_stream(stream);
   // work layout: partial[nblk][C][3] | k[3C] (as floats) | alpha_part[C]
   double* partial = work;
@@ -734,6 +765,8 @@ extern "C" int clskd_abf_fuse_bwd(const void* x1, const void* res, int32_t B, in
   CLSKD_CHECK_ARG((x_scale == nullptr) == (x_shift == nullptr), "abf_fuse_bwd: scale/shift pair");
   CLSKD_CHECK_ARG(!bn_partial || (mean1 && var1), "abf_fuse_bwd: BN partials need mean1/var1");
   CLSKD_CHECK_SHAPE(!dnext || (F2 >= F && T2 >= T), "abf_fuse_bwd: next grid smaller than this one");
+  CLSKD_CHECK_SHAPE(B > 0 && F > 0 && T > 0 && (int64_t)B * F * T < ((int64_t)1 << 31),
+                    "abf_fuse_bwd: B*F*T must be positive and below 2^31");
   const unsigned grid = (unsigned)clskd_abf_fuse_bwd_blocks(B, F, T);
   if (dtype == CLSKD_BF16)
     hipLaunchKernelGGL(abf_fuse_bwd_kernel<__bf16>, dim3(grid), dim3(256), 0, as_stream(stream),
@@ -756,6 +789,7 @@ extern "C" int clskd_bn_bwd_from_partials(const void* x, const float* dy, int64_
   CLSKD_CHECK_ARG(x && dy && scale && shift && mean && var && partial && kbuf && dx,
                   "bn_bwd_from_partials: null pointer");
   CLSKD_CHECK_SHAPE(rows > 0 && C >= 4 && C % 4 == 0 && nblk >= 1, "bn_bwd_from_partials: shape");
+  CLSKD_CHECK_ARG(((uintptr_t)kbuf & 15) == 0, "bn_bwd_from_partials: kbuf must be 16-byte aligned");
   hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, nblk, rows, C,
                      gamma, mean, var, eps, dgamma, dbeta, kbuf, nullptr, 0);
