@@ -127,3 +127,22 @@ def test_gram_job_validation_without_gpu():
     assert lib.clskd_spkd_finalize((J * 1)(good), 1, pairs, 1, 4, 1, fake, None, None, fake,
                                    None) == -1
     assert b"outside" in lib.clskd_last_error()
+
+
+def test_gram_chunk_and_bn_bwd_alignment_validation_without_gpu():
+    """Validation added with the division-free Gram loads and the vectorised backward BN apply:
+    a slab whose chunk * Cs^2 reaches 2^32 (the 32-bit multiply-high split would be inexact) and
+    a misaligned bn_bwd workspace are reported before any launch."""
+    lib = _lib.load(require_gpu=False)
+    J = _lib.GramJob
+    fake = 1 << 20
+    big = (J * 1)(J(fake, 1024 * 100, 100, 1024, 0, 1024, 8192, 0, 1, _lib.F32, 0))
+    assert lib.clskd_gram_partial(big, 1, 4, fake, None) == -1
+    assert b"2^32" in lib.clskd_last_error()
+    ok = (J * 1)(J(fake, 1024 * 100, 100, 1024, 0, 1024, 16, 0, 7, _lib.F32, 0))
+    assert lib.clskd_gram_partial(ok, 1, 4, 0, None) < 0  # passes the chunk check, then null slabs
+    assert b"null slab" in lib.clskd_last_error()
+    f = fake
+    rc = lib.clskd_bn_bwd(f, f, 1024, 64, f, f, f, f, 1e-5, None, None, f + 8, 16, None, None,
+                          None, f, 0, 0, _lib.F32, None)
+    assert rc < 0 and b"16-byte aligned" in lib.clskd_last_error()
