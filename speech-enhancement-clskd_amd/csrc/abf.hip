@@ -17,6 +17,10 @@
 //    as conv_pointwise_kernel did), applies the BN affine, the attention fusion and writes only
 //    the fused 64-channel map (and, for the training tape, optionally the raw x1).
 // Deterministic: fixed reduction orders, no atomics.
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "common.h"
 
 namespace clskd {
@@ -457,7 +461,14 @@ using namespace clskd;
 
 extern "C" int32_t clskd_abf_moment_blocks(int64_t rows, int32_t cin) {
   // rows per block: the S2 MFMA work grows with cin^2 (10 tile MFMAs per 4 rows at cin = 64)
-  const int64_t per = cin >= 64 ? 768 : cin >= 32 ? 1024 : 2048;
+  int64_t per = cin >= 64 ? 768 : cin >= 32 ? 1024 : 2048;
+  // A/B knob: CLSKD_ABF_MOMENT_DIV = d divides the rows per block (more blocks in flight)
+  static const int div = [] {
+    const char* e = getenv("CLSKD_ABF_MOMENT_DIV");
+    const int v = e ? atoi(e) : 1;
+    return v >= 1 && v <= 16 ? v : 1;
+  }();
+  per = std::max<int64_t>(64, per / div);
   int64_t n = cdiv(rows, per);
   if (n < 1) n = 1;
   if (n > 1024) n = 1024;

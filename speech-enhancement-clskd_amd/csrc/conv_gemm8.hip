@@ -105,7 +105,8 @@ struct ConvArgsG8 {
 // 3 = neither, 4 = B operand only (no A gather), 5 = A operand only.  Correct-result variants:
 // 6 = s_setprio 1 around each substep's MFMA cluster, 7 = static priority 1 for waves 4-7, 8 = both;
 // 9 = no DMA wait inside the stream (timing only: DMA latency vs issue cost).
-template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8>
+template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8,
+          int EB = 0>
 __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 args) {
   using namespace g8;
   const clskd_conv_desc& d = args.d;
@@ -360,23 +361,31 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
       };
       // PF + 1 fragment register sets: substep s + PF is read while substep s computes; the
       // sched_barriers pin that (the scheduler would otherwise hoist every read and spill)
+      // the next K-tile's pieces (this wave's) landed — younger K-tiles stay in flight; then
+      // every wave's are visible and every wave is done reading this K-tile's stage
+      auto k_boundary = [&]() {
+        if (DBG == 9 && gk + 1 < total) {  // timing only: never wait for the DMA inside the stream
+        } else if ((DBG >= 4 && DBG <= 5) || gk + 1 >= total) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+          g8::wait_vm<(NS - 2) * G>(min(NS - 2, total - 2 - gk) * G);
+        }
+        raw_barrier();
+        if (kt + 1 < nk) read_head(stages + ((gk + 1) % NS) * SB);
+      };
+      // EB: the boundary sits before the last substep's MFMAs (its fragments are already in
+      // registers), so the next K-tile's head reads return under those MFMAs instead of after
+      // the barrier with the MFMA pipe idle
+      static_assert(!EB || (NSUB - 1) % NSET >= PF, "EB: the last substep's set must not be a head set");
 #pragma unroll
       for (int s = 0; s < NSUB; ++s) {
+        if (EB && s == NSUB - 1) k_boundary();
         if (s + PF < NSUB) read_frags(sa, s + PF, fa[(s + PF) % NSET], fb[(s + PF) % NSET]);
         mfmas(fa[s % NSET], fb[s % NSET]);
         issue(s);  // behind the MFMAs: the K-entry read / address ALU overlap them
         __builtin_amdgcn_sched_barrier(0);
       }
-      // the next K-tile's pieces (this wave's) landed — younger K-tiles stay in flight; then
-      // every wave's are visible and every wave is done reading this K-tile's stage
-      if (DBG == 9 && gk + 1 < total) {  // timing only: never wait for the DMA inside the stream
-      } else if ((DBG >= 4 && DBG <= 5) || gk + 1 >= total) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else {
-        g8::wait_vm<(NS - 2) * G>(min(NS - 2, total - 2 - gk) * G);
-      }
-      raw_barrier();
-      if (kt + 1 < nk) read_head(stages + ((gk + 1) % NS) * SB);
+      if (!EB) k_boundary();
     }
 
     // ---- tile epilogue: the stage of the K-tile just computed is free ------------------------
@@ -500,7 +509,8 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
   }
 }
 
-template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8>
+template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8,
+          int EB = 0>
 static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   using namespace g8;
   constexpr int SB = (BM + BN) * 2 * BK;
@@ -510,7 +520,7 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
     set_error("conv2d(bf16 g8): K=%d N=%d needs %zu B of LDS", d.K, d.N, lds);
     return CLSKD_E_SHAPE;
   }
-  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG, PF, NWV>;
+  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG, PF, NWV, EB>;
   static bool attr_set = false;  // per instantiation
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -533,7 +543,8 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   const int grid = ntiles <= ncap ? (int)ntiles : (ncap >= 8 ? (ncap & ~7) : ncap);
   ConvArgsG8 a{d, (int)n_mt, (int)ntiles};
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NWV * 64), lds, st, a);
-  note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d>", BM, BN, WM, BK, NS, PHI, type_name<OutT>(), DBG, PF, NWV);
+  note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d>", BM, BN, WM, BK, NS, PHI, type_name<OutT>(), DBG, PF,
+              NWV, EB);
   return CLSKD_OK;
 }
 
@@ -584,9 +595,11 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
         return launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 2>(d, st);
       case 8:  // prefetch three ahead, 256 x 128 tiles everywhere
         return launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 3>(d, st);
-      case 9:  // four waves (one per SIMD), each a 128 x 128 (N > 128) or 128 x 64 block
-        if (dbg == 1 || d.N <= 128) return launch_g8<256, 128, 2, 64, 2, 2, __bf16, 0, 1, 4>(d, st);
-        return launch_g8<256, 256, 2, 64, 2, 2, __bf16, 0, 1, 4>(d, st);
+      case 9:  // dbg 0: K-tile boundary before the last substep (EB); 1: four waves (one per
+               // SIMD), each a 128 x 64 block (measured 1.4-1.9x slower)
+        if (dbg == 1) return launch_g8<256, 128, 2, 64, 2, 2, __bf16, 0, 1, 4>(d, st);
+        if (d.N <= 128) return launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 1, 8, 1>(d, st);
+        return launch_g8<256, 256, 2, 64, 2, 2, __bf16, 0, 1, 8, 1>(d, st);
       default:  // BK 64, two stages
         (void)nk64;
         if (d.N <= 128) { G8X(256, 128, 4, 64, 2, 2) }
@@ -594,10 +607,14 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
     }
 #undef G8X
   }
+  // default: BK 64, two stages, the K-tile boundary before the last substep (EB; 3-5 % on the
+  // N = 256 layers against the boundary after it, CLSKD_G8=10)
   if (d.N <= 128) {
-    return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float>(d, st) : launch_g8<256, 128, 4, 64, 2, 2, __bf16>(d, st);
+    return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float, 0, 1, 8, 1>(d, st)
+               : launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 1, 8, 1>(d, st);
   }
-  return f32 ? launch_g8<256, 256, 2, 64, 2, 2, float>(d, st) : launch_g8<256, 256, 2, 64, 2, 2, __bf16>(d, st);
+  return f32 ? launch_g8<256, 256, 2, 64, 2, 2, float, 0, 1, 8, 1>(d, st)
+             : launch_g8<256, 256, 2, 64, 2, 2, __bf16, 0, 1, 8, 1>(d, st);
 }
 
 }  // namespace clskd
