@@ -31,6 +31,8 @@ from clskd import config as cfg  # noqa: E402
 
 METRIC = "frames/sec/GPU DCCRN-CLSKD fwd+loss @16k 4s; SI-SNR parity ±0.01 dB"
 METRIC_TRAIN = "frames/sec/GPU DCCRN-CLSKD training step (fwd+loss+bwd+Adam) @16k 4s"
+METRIC_SPKD = "frames/sec/GPU DCCRN SPKD-output fwd+loss (distill_SPKD.py) @16k 4s"
+B_SPKD = 32  # config C4: batch 32 x 4 s
 PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (f32-in MFMA), dense
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
 B_PER_GPU = 16
@@ -39,12 +41,14 @@ TRAFFIC_FILE = "r2_pmc_traffic.json"  # written by tools/pmc_traffic.py
 L = 64000
 
 
-def build_kd(dev, abf_reinit, precision="fp32"):
-    from clskd.distill import KnowledgeDistillation
+def build_kd(dev, abf_reinit, precision="fp32", spkd=False):
+    from clskd.distill import KnowledgeDistillation, SPKDDistillation
     from clskd.model import DCCRN
     from clskd.weights import ABF_SEED, STUDENT_SEED, TEACHER_SEED, apply_recipe
     teacher = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.TEACHER), TEACHER_SEED)
     student = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.STUDENT), STUDENT_SEED)
+    if spkd:
+        return SPKDDistillation(teacher, student, precision=precision).to(dev).train()
     kd = KnowledgeDistillation(teacher, student, abf_reinit=abf_reinit,
                                precision=precision).to(dev).train()
     apply_recipe(kd.review_encoder, ABF_SEED, "encoder.")
@@ -101,6 +105,10 @@ def main():
                     help="config C3: the full training step — fwd+loss, HIP backward into the flat "
                          "student gradient, one RCCL all-reduce (N > 1), one Adam launch "
                          "(KnowledgeDistillation.train_step); reported under its own metric")
+    ap.add_argument("--spkd", action="store_true",
+                    help="config C4: distill_SPKD.py's step (student + teacher full forwards, MRSTFT "
+                         "base, one SPKD Gram over the output waveforms) at B=32 x 4 s per GPU; "
+                         "reported under its own metric")
     ap.add_argument("--precision", default="mixed", choices=["mixed", "fp32"],
                     help="mixed: teacher + ReviewKD GEMMs on bf16 MFMA operands (fp32 accumulate), "
                          "student fp32; fp32: every GEMM on exact-f32 MFMA")
@@ -116,11 +124,14 @@ def main():
 
     from clskd import ops
     from clskd.data import synthetic_pairs
-    kd = build_kd(dev, args.abf_reinit, args.precision)
+    if args.train and args.spkd:
+        raise SystemExit("--train and --spkd are separate legs")
+    bsz = B_SPKD if args.spkd else B_PER_GPU
+    kd = build_kd(dev, args.abf_reinit, args.precision, spkd=args.spkd)
     # NBATCH distinct batches resident in HBM; step i consumes batch i % NBATCH
     Xs, Ys = [], []
     for k in range(NBATCH):
-        noisy, clean = synthetic_pairs(B_PER_GPU, L, seed=cdist.shard_seed(1000 + k, rank))
+        noisy, clean = synthetic_pairs(bsz, L, seed=cdist.shard_seed(1000 + k, rank))
         Xs.append(torch.from_numpy(noisy).to(dev))
         Ys.append(torch.from_numpy(clean).to(dev))
     T = cfg.n_frames(L)
@@ -199,7 +210,7 @@ def main():
     loss_v = float(loss.item())
 
     if rank == 0:
-        frames = world * B_PER_GPU * T * args.steps
+        frames = world * bsz * T * args.steps
         # dominant kernel = conv kernel instance with the largest total time
         name, (n_l, ms, flops) = max(ktimes.items(), key=lambda kv: kv[1][1])
         conv_total_ms = sum(v[1] for v in census.values())
@@ -236,7 +247,7 @@ def main():
                                             tflops=round(v[2] / (v[1] * 1e-3) / 1e12, 1))
                                     for k, v in sorted(census.items(), key=lambda kv: -kv[1][1])}))
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and not args.train:
+        if world == 1 and not args.no_cpu_baseline and not args.train and not args.spkd:
             cpu = cpu_baseline(args.cpu_seconds)
             # GPU / CPU-oracle ratio on the same workload.  `vs_baseline` stays null: it is
             # reserved for a published number for this metric, and BASELINE.md has none
@@ -246,8 +257,11 @@ def main():
         if args.train:
             workload = ("C3: DCCRN-CLSKD training step = C2 fwd+loss + HIP backward to the 231,565 "
                         "student parameters + flat-bucket RCCL all-reduce (N > 1) + Adam(lr 6e-4)")
+        if args.spkd:
+            workload = ("C4: distill_SPKD.py fwd+loss (student + full teacher forward incl. mask "
+                        "and iSTFT, MRSTFT base, SPKD Gram over the 32 output waveforms)")
         out = {
-            "metric": METRIC_TRAIN if args.train else METRIC,
+            "metric": METRIC_TRAIN if args.train else (METRIC_SPKD if args.spkd else METRIC),
             "value": round(frames / el, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -262,7 +276,7 @@ def main():
             "data": "synthetic (seeded 16 kHz enveloped-sinusoid clean + noise at 0-10 dB SNR; "
                     "recipe weights, SURVEY.md §8 d)",
             "config": {"workload": workload,
-                       "global_batch": world * B_PER_GPU, "per_gpu_batch": B_PER_GPU,
+                       "global_batch": world * bsz, "per_gpu_batch": bsz,
                        "clip_samples": L, "frames_per_clip": T, "parallelism": f"dp{world}",
                        "abf_reinit": args.abf_reinit, "loss": round(loss_v, 6),
                        "launch": ("eager, 4 HIP streams (caller, teacher, student, ReviewKD-"

@@ -459,7 +459,7 @@ class SPKDDistillation(nn.Module):
     """distill_SPKD.py:37-87: MRSTFT base + SPKD on the output waveforms (config C4)."""
 
     def __init__(self, teacher, student, sftf_loss=MultiResolutionSTFTLoss, spkd_loss=SPKDLoss,
-                 cfg=cfg):
+                 cfg=cfg, precision="fp32"):
         super().__init__()
         self.teacher = teacher
         for p in self.teacher.parameters():
@@ -468,6 +468,18 @@ class SPKDDistillation(nn.Module):
         self.spkd_loss = spkd_loss
         self.stft_loss = sftf_loss(fft_sizes=[512], win_lengths=[400], hop_sizes=[100])
         self.cfg = cfg
+        self.set_precision(precision)
+
+    def set_precision(self, precision):
+        """As KnowledgeDistillation.set_precision: "mixed" runs the frozen teacher (no_grad in
+        distill_SPKD.py:75-76; its waveform only feeds the SPKD Gram) on bf16 MFMA operands with
+        fp32 accumulation; the student stays fp32."""
+        if precision not in ("fp32", "mixed"):
+            raise ValueError(precision)
+        self.precision = precision
+        self.teacher.compute = "bf16" if precision == "mixed" else "fp32"
+        self.student.compute = "fp32"
+        return self
 
     def forward(self, x):
         return self.student(x)

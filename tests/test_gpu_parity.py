@@ -456,6 +456,22 @@ def test_spkd_output_step_golden():
     assert abs(out["loss"].item() - float(fx["loss/total"])) < 5e-5
 
 
+def test_spkd_output_step_mixed_precision():
+    """C4 as bench.py --spkd runs it: the teacher on bf16 MFMA operands (fp32 accumulate), the
+    student fp32.  The base loss depends on the student only, so it stays at the fp32 golden;
+    the SPKD term (teacher waveform Gram) within 2 % of the golden (bf16 operand rounding)."""
+    from clskd.distill import SPKDDistillation
+    fx = golden("spkd_output_step.npz")
+    kd = SPKDDistillation(_models("teacher").train(), _models("student").train(),
+                          precision="mixed").to(DEV)
+    assert kd.teacher.compute == "bf16" and kd.student.compute == "fp32"
+    out = kd.training_step((torch.from_numpy(fx["x"]).to(DEV), torch.from_numpy(fx["y"]).to(DEV)),
+                           0, return_parts=True)
+    assert abs(out["base"].item() - float(fx["loss/base"])) < 2e-5
+    assert abs(out["spkd"].item() - float(fx["loss/spkd"])) <= 2e-2 * float(fx["loss/spkd"]) + 1e-6
+    assert torch.isfinite(out["teacher_wav"]).all()
+
+
 def test_clskd_step_4s_against_oracle():
     """Configuration-C2 clip length (4 s @ 16 kHz, T=643) at B=4: every loss term and the
     student waveform against the CPU oracle; SI-SNR of the enhanced waveform within 0.01 dB.
