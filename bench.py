@@ -124,8 +124,8 @@ def main():
 
     from clskd import ops
     from clskd.data import synthetic_pairs
-    if args.train and args.spkd:
-        raise SystemExit("--train and --spkd are separate legs")
+    if args.spkd and (args.train or args.graph):
+        raise SystemExit("--spkd is its own eager leg (no --train / --graph)")
     bsz = B_SPKD if args.spkd else B_PER_GPU
     kd = build_kd(dev, args.abf_reinit, args.precision, spkd=args.spkd)
     # NBATCH distinct batches resident in HBM; step i consumes batch i % NBATCH
@@ -221,7 +221,7 @@ def main():
         peak = PEAK_BF16_MFMA_TFLOPS if bf16_ops else PEAK_F32_MFMA_TFLOPS
         traffic, traffic_src = None, None
         tpath = os.path.join(REPO, "profiles", TRAFFIC_FILE)
-        if os.path.exists(tpath):
+        if os.path.exists(tpath) and not args.spkd:  # the PMC passes profile the C2 leg
             tk = json.load(open(tpath))["kernels"].get(name)
             if tk is not None:
                 traffic = round(tk["hbm_bytes_per_launch"])
@@ -279,10 +279,15 @@ def main():
                        "global_batch": world * bsz, "per_gpu_batch": bsz,
                        "clip_samples": L, "frames_per_clip": T, "parallelism": f"dp{world}",
                        "abf_reinit": args.abf_reinit, "loss": round(loss_v, 6),
-                       "launch": ("eager, 4 HIP streams (caller, teacher, student, ReviewKD-"
+                       "launch": ("eager, 2 HIP streams (caller: teacher; side: student + "
+                                  "MRSTFT)" if args.spkd else
+                                  "eager, 4 HIP streams (caller, teacher, student, ReviewKD-"
                                   "encoder/MRSTFT)" if (not args.graph)
                                   else "hipGraph replay (clskd.graph.StepGraph)"),
-                       "precision": ("teacher+ReviewKD GEMMs bf16 MFMA operands / fp32 accumulate; "
+                       "precision": ("teacher GEMMs bf16 MFMA operands / fp32 accumulate; "
+                                     "student, STFT/iSTFT, LSTM recurrence, BN, losses fp32")
+                       if (args.spkd and args.precision == "mixed") else
+                                    ("teacher+ReviewKD GEMMs bf16 MFMA operands / fp32 accumulate; "
                                      "student, STFT/iSTFT, LSTM recurrence, BN, losses fp32")
                        if args.precision == "mixed" else "fp32 MFMA everywhere"},
             "roofline": roof,

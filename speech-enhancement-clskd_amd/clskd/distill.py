@@ -494,12 +494,20 @@ class SPKDDistillation(nn.Module):
         X = X.float().reshape(X.shape[0], -1).contiguous()
         y = y.float().reshape(X.shape[0], -1).contiguous()
         spec = self.teacher.spectrum(X)
-        s = self.student.run(X, train=self.student.training, bn_updates=1, spec=spec,
-                             want_masks=False)["out_wav"]
+        buf = torch.empty(3, dtype=torch.float32, device=X.device)
+        # two chains joined before the SPKD Gram: the teacher forward (the critical path) on the
+        # caller's stream, the student forward + MRSTFT base loss (distill_SPKD.py:73-79) beside
+        # it on a side stream; the side stream first waits for spec and the previous step
+        main = torch.cuda.current_stream(X.device)
+        side = _side_stream(X.device, 0)
+        side.wait_stream(main)
         t = self.teacher.run(X, train=self.teacher.training, bn_updates=1, spec=spec,
                              want_masks=False)["out_wav"]
-        buf = torch.empty(3, dtype=torch.float32, device=X.device)
-        self.stft_loss(s, y, out2=buf[0:2])
+        with torch.cuda.stream(side):
+            s = self.student.run(X, train=self.student.training, bn_updates=1, spec=spec,
+                                 want_masks=False)["out_wav"]
+            self.stft_loss(s, y, out2=buf[0:2])
+        main.wait_stream(side)
         ops.spkd_losses([(ops.gram_view(s), ops.gram_view(t))], X.shape[0], out=buf[2:3])
         total = torch.empty((), dtype=torch.float32, device=X.device)
         ops.sum_f32(buf[1:], total)
