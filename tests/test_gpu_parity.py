@@ -79,6 +79,54 @@ def test_conv_engine_against_torch():
 
 
 
+@pytest.mark.parametrize("dt,C1,C2,N,ntap_f,lpr",
+                         [("f32", 8, 8, 2, 3, 4), ("f32", 8, 8, 2, 2, 4), ("f32", 4, 4, 2, 3, 2),
+                          ("f32", 16, 16, 2, 3, 8), ("f32", 2, 2, 2, 3, 2), ("f32", 8, 8, 1, 3, 4),
+                          ("bf16", 32, 32, 2, 3, 8), ("bf16", 32, 32, 2, 2, 8),
+                          ("bf16", 64, 64, 2, 3, 16), ("bf16", 8, 8, 1, 3, 2)])
+def test_conv_direct_coop_last_layer(dt, C1, C2, N, ntap_f, lpr):
+    """Row-cooperative direct kernel (N <= 2, no fused statistics — the decoders' last layer as
+    run per polyphase parity: 3 or 2 freq taps x 2 time taps over [out_t, skip]): against torch
+    fp64 on the same (bf16-rounded) operands, and the dispatched instance is the cooperative one
+    with LPR = channel runs per tap.  Tolerance 1e-5 relative (fp32 accumulation order)."""
+    import re
+    from clskd import _lib, ops
+    g = torch.Generator().manual_seed(C1 * 7 + ntap_f * 3 + N)
+    B, F, T = 3, 37, 45
+    tdt = torch.bfloat16 if dt == "bf16" else torch.float32
+    segs_h = [torch.randn(B, F, T, C1, generator=g).to(tdt),
+              torch.randn(B, F, T, C2, generator=g).to(tdt)]
+    Cin = C1 + C2
+    w = torch.randn(N, Cin, ntap_f, 2, generator=g) * 0.2
+    bias = torch.randn(N, generator=g)
+    taps = [(kf - 1, kt - 1) for kf in range(ntap_f) for kt in range(2)]
+    wk = w.permute(0, 2, 3, 1).reshape(N, 2 * ntap_f, Cin)
+    wp = ops.pack_weight(wk.to(DEV), 2 * ntap_f * Cin, "bf16" if dt == "bf16" else "fp32")
+    wq = wp[:, :2 * ntap_f * Cin].float().cpu().reshape(N, ntap_f, 2, Cin).permute(0, 3, 1, 2).double()
+    xin = torch.cat([x.double() for x in segs_h], 3).permute(0, 3, 1, 2)
+    # out[fo, to] = sum x[fo + kf - 1, to + kt - 1] w[kf, kt]
+    ref = torch.nn.functional.conv2d(torch.nn.functional.pad(xin, (1, 1, 1, 2)), wq,
+                                     bias.double())[..., :F, :T]
+    assert ops.direct_ok(N, wp.shape[1])
+    out = torch.empty(B, F, T, N, device=DEV, dtype=torch.float32)
+    segs = [ops.seg_bftc(x.to(DEV)) for x in segs_h]
+    prev = os.environ.get("CLSKD_DIRECT_COOP")
+    os.environ["CLSKD_DIRECT_COOP"] = "1"  # opt-in dispatch, read per launch
+    try:
+        ops.conv(segs, taps, B, F, T, N, wp, bias.to(DEV), out, ops.OutMap(F * T * N, T * N, N))
+    finally:
+        if prev is None:
+            del os.environ["CLSKD_DIRECT_COOP"]
+        else:
+            os.environ["CLSKD_DIRECT_COOP"] = prev
+    torch.cuda.synchronize()
+    name = _lib.load().clskd_conv_last_kernel().decode()
+    assert re.fullmatch(rf"conv_direct_coop_kernel<{N if N > 1 else 2},\d,\w+,float,{lpr},\d>",
+                        name.replace("__bf16", "bf16")), name
+    np.testing.assert_allclose(out.permute(0, 3, 1, 2).double().cpu().numpy(), ref.numpy(),
+                               rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("C1,C2,N", [(2, 0, 8), (2, 0, 16), (8, 8, 2), (16, 16, 2), (6, 0, 4),
                                      (6, 2, 3), (3, 0, 1), (1, 0, 16), (2, 0, 32), (3, 0, 32)])
