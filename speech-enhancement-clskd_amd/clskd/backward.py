@@ -21,6 +21,8 @@ Gradients are fp32; every reduction has a fixed order, so a step's gradients are
 repeatable.  Parity: ``tests/test_gpu_parity.py::test_clskd_backward_*`` against the CPU oracle's
 autograd (``oracle/ref_cpu.py``).
 """
+import weakref
+
 import numpy as np
 import torch
 
@@ -105,13 +107,18 @@ _TW = {}
 
 
 def _tw(key, src, build):
-    k = (key, src.data_ptr(), src._version)
+    """Transposed/packed weight cache.  An entry is valid only for the very tensor object it was
+    built from (weak reference) at the same in-place version: keys carry id()s of modules, and a
+    module or tensor freed by an earlier step can hand its id and storage address to a new one
+    (seen as a flaky mixed-precision gradient test: a new model's ABF backward ran with the
+    previous model's re-drawn ABF weights)."""
+    k = (src.data_ptr(), src._version)
     ent = _TW.get(key)
-    if ent is not None and ent[0] == k:
+    if ent is not None and ent[0] == k and ent[2]() is src:
         return ent[1]
     with torch.no_grad():
         w = build()
-    _TW[key] = (k, w)
+    _TW[key] = (k, w, weakref.ref(src))
     return w
 
 
