@@ -56,14 +56,42 @@ def build_kd(dev, abf_reinit, precision="fp32", spkd=False):
     return kd
 
 
-def cpu_baseline(seconds):
+def host_cpu_info():
+    """Host CPU model, the machine's logical CPU count, and the CPUs this process may use
+    (affinity mask, capped by the cgroup CPU quota: on the GPU box nproc shows the whole
+    machine while the job's share is smaller)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    total = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else total
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            usable = max(1, min(usable, int(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    return model, total, usable
+
+
+def cpu_baseline(n_timed=3, n_warm=3):
     """The CPU oracle (fp32 PyTorch-CPU restatement of the reference, oracle/ref_cpu.py) timed on
-    this host on a bounded sample of the same workload: the same B=16 x 4 s step as the GPU leg
-    (one warm-up step at B=2), repeated until `seconds` of CPU work (at least one step)."""
+    this host following BASELINE.md §2: every usable host core, the same seeded B=16 x 4 s
+    workload as the GPU leg, warm-up iterations, then the median of `n_timed` full B=16 steps.
+    The warm-ups run at B=4 (thread pools and allocator warmed on the same code path at a
+    quarter of the cost) so the default bench stays within a few minutes."""
     from oracle import ref_cpu as R
     from clskd.data import synthetic_pairs
     from clskd.weights import ABF_SEED, STUDENT_SEED, TEACHER_SEED, recipe_state_dict
-    threads = min(16, os.cpu_count() or 1)
+    model, total, usable = host_cpu_info()
+    threads = usable
     torch.set_num_threads(threads)
     pt = R.to_torch_params(recipe_state_dict(cfg.dccrn_param_shapes(**cfg.TEACHER), TEACHER_SEED))
     ps = R.to_torch_params(recipe_state_dict(cfg.dccrn_param_shapes(**cfg.STUDENT), STUDENT_SEED))
@@ -72,21 +100,120 @@ def cpu_baseline(seconds):
     Bc = B_PER_GPU
     noisy, clean = synthetic_pairs(Bc, L, seed=99)
     X, Y = torch.from_numpy(noisy), torch.from_numpy(clean)
+    times = []
     with torch.no_grad():
-        R.clskd_step(pt, ps, pa, X[:2], Y[:2])  # warm-up
-        n, t0 = 0, time.perf_counter()
-        while True:
+        for _ in range(n_warm):
+            R.clskd_step(pt, ps, pa, X[:4], Y[:4])
+        for _ in range(n_timed):
+            t0 = time.perf_counter()
             R.clskd_step(pt, ps, pa, X, Y)
-            n += 1
-            el = time.perf_counter() - t0
-            if el >= seconds:
-                break
-    frames = n * Bc * cfg.n_frames(L)
-    return dict(value=round(frames / el, 2), unit="frames/s", cores=threads, kind="port",
-                batch=Bc,
+            times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    frames = Bc * cfg.n_frames(L)
+    return dict(value=round(frames / med, 2), unit="frames/s", cores=threads, kind="port",
+                batch=Bc, host_cpus=total, cpu_model=model,
+                step_s=[round(t, 3) for t in times],
                 sample=f"oracle/ref_cpu.clskd_step on the bench workload (B={Bc} x 4 s @16 kHz, "
-                       f"same step as the GPU leg), {n} step(s) in {el:.1f} s, fp32, torch CPU "
-                       f"{threads} threads")
+                       f"same step as the GPU leg): {n_warm} warm-up steps (B=4), median of "
+                       f"{n_timed} timed B={Bc} steps, fp32, torch CPU {threads} threads = every "
+                       f"CPU this job may use ({total} logical CPUs on the host), {model}")
+
+
+METRIC_C1 = "frames/sec DCCRN student eval forward, batch 1 (framework.py eval path, no KD)"
+
+
+def run_c1(args, dev):
+    """Configuration C1 (BASELINE.json configs[0]): the student's eval-mode forward (BatchNorm
+    running statistics, DCCRN.py:149-240) on one clip, 16000 samples (1 s @16 kHz) and 8000
+    samples ("8 kHz 1 s" restated as 8000 samples), as a latency: each
+    forward is synchronised.  GPU legs: the Python eager launch path and the same forward
+    captured once and replayed by the C++ step executor (clskd.graph.CapturedCall).  CPU leg:
+    the oracle's eval forward (oracle/ref_cpu.dccrn_forward(train=False)) on every usable host
+    core and on one thread, 3 warm-ups + median of 10."""
+    from oracle import ref_cpu as R
+    from clskd.data import synthetic_pairs
+    from clskd.graph import CapturedCall
+    from clskd.model import DCCRN
+    from clskd.weights import STUDENT_SEED, apply_recipe, recipe_state_dict
+    student = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.STUDENT),
+                           STUDENT_SEED).to(dev).eval()
+    ps = R.to_torch_params(recipe_state_dict(cfg.dccrn_param_shapes(**cfg.STUDENT), STUDENT_SEED))
+    model, total, usable = host_cpu_info()
+    legs = {}
+    K = max(args.steps, 10)
+    for n in (16000, 8000):
+        noisy, _ = synthetic_pairs(1, n, seed=5)
+        x = torch.from_numpy(noisy).to(dev)
+        frames = cfg.n_frames(n)
+        fwd = (lambda t: student(t, is_feat=True))
+        with torch.no_grad():
+            for _ in range(args.warmup):
+                fwd(x)
+            torch.cuda.synchronize()
+            eager = []
+            for _ in range(K):
+                t0 = time.perf_counter()
+                fwd(x)
+                torch.cuda.synchronize()
+                eager.append(time.perf_counter() - t0)
+            ref_out = fwd(x).clone()
+        cc = CapturedCall(fwd, x)
+        for _ in range(args.warmup):
+            cc(x)
+        torch.cuda.synchronize()
+        ex = []
+        for _ in range(K):
+            t0 = time.perf_counter()
+            cc(x)
+            torch.cuda.synchronize()
+            ex.append(time.perf_counter() - t0)
+        assert torch.equal(cc.out, ref_out), "executor replay differs from the eager forward"
+        xc = torch.from_numpy(noisy)
+        cpu = {}
+        for threads in (usable, 1):
+            torch.set_num_threads(threads)
+            with torch.no_grad():
+                for _ in range(3):
+                    R.dccrn_forward(ps, xc, train=False)
+                ts = []
+                for _ in range(10):
+                    t0 = time.perf_counter()
+                    o = R.dccrn_forward(ps, xc, train=False)
+                    ts.append(time.perf_counter() - t0)
+            cpu[threads] = float(np.median(ts))
+        rms = float((o["out_wav"].reshape(-1) - ref_out.cpu().reshape(-1)).pow(2).mean().sqrt())
+        lat = float(np.median(ex))
+        legs[n] = dict(frames=frames, gpu_exec_ms=round(lat * 1e3, 4),
+                       gpu_eager_ms=round(float(np.median(eager)) * 1e3, 4),
+                       gpu_frames_per_s=round(frames / lat, 1),
+                       cpu_ms=round(cpu[usable] * 1e3, 3), cpu_1thread_ms=round(cpu[1] * 1e3, 3),
+                       cpu_frames_per_s=round(frames / cpu[usable], 1),
+                       gpu_over_cpu=round(cpu[usable] / lat, 1),
+                       kernels=cc.info["kernels"], wav_rms_vs_oracle=rms)
+    main_leg = legs[16000]
+    mflop = 7.6e6 * main_leg["frames"]  # SURVEY.md §8 d: 3.79 MMAC/frame
+    out = {
+        "metric": METRIC_C1, "value": main_leg["gpu_frames_per_s"], "unit": "frames/s",
+        "n_gpus": 1, "steps": K, "warmup": args.warmup,
+        "ms_per_step": main_leg["gpu_exec_ms"], "higher_is_better": True, "scaling": "none",
+        "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (seeded 16 kHz enveloped-sinusoid clean + noise); recipe weights",
+        "config": {"workload": "C1: student DCCRN eval forward (running-stat BN), batch 1, "
+                               "16000 samples (value) and 8000 samples; latency per forward",
+                   "legs": {str(k): v for k, v in legs.items()}},
+        "roofline": {"bound": "latency", "achieved": round(mflop / (main_leg["gpu_exec_ms"] * 1e-3) / 1e12, 4),
+                     "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(mflop / (main_leg["gpu_exec_ms"] * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 6),
+                     "traffic": None,
+                     "note": "one 1 s clip is ~70 dependent small launches: the forward is bound by "
+                             "launch latency and the 163-step LSTM recurrence, not by MFMA or HBM"},
+        "cpu_baseline": {"value": main_leg["cpu_frames_per_s"], "unit": "frames/s", "cores": usable,
+                         "kind": "port", "cpu_model": model, "host_cpus": total,
+                         "sample": "oracle/ref_cpu.dccrn_forward(train=False), B=1 x 16000 samples, "
+                                   f"3 warm-ups + median of 10, fp32, {usable} threads "
+                                   f"(1 thread: {main_leg['cpu_1thread_ms']} ms)"},
+    }
+    print(json.dumps(out))
 
 
 def main():
@@ -94,13 +221,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU-oracle B=16 steps (median)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--abf-reinit", default="step", choices=["step", "once"])
-    ap.add_argument("--graph", action="store_true",
-                    help="replay the captured hipGraph of the step (clskd.graph.StepGraph) instead "
-                         "of launching the three-stream schedule eagerly; ROCm's graph executor "
-                         "does not keep the three streams concurrent, so eager is faster here")
+    ap.add_argument("--launch", default="exec", choices=["exec", "eager", "graph"],
+                    help="exec (default, C2): capture the step once and replay it with the "
+                         "library's C++ multi-stream executor (clskd.graph.StepExecutor: no Python "
+                         "per launch, branches concurrent); eager: launch the four-stream schedule "
+                         "from Python every step; graph: hipGraphLaunch of the capture (ROCm's "
+                         "graph executor runs the branches one after another)")
+    ap.add_argument("--graph", action="store_true", help="same as --launch graph")
     ap.add_argument("--train", action="store_true",
                     help="config C3: the full training step — fwd+loss, HIP backward into the flat "
                          "student gradient, one RCCL all-reduce (N > 1), one Adam launch "
@@ -109,6 +239,9 @@ def main():
                     help="config C4: distill_SPKD.py's step (student + teacher full forwards, MRSTFT "
                          "base, one SPKD Gram over the output waveforms) at B=32 x 4 s per GPU; "
                          "reported under its own metric")
+    ap.add_argument("--c1", action="store_true",
+                    help="config C1: the student's eval forward at batch 1 (16000 and 8000 "
+                         "samples) as a latency, GPU (eager and executor) beside the CPU oracle")
     ap.add_argument("--precision", default="mixed", choices=["mixed", "fp32"],
                     help="mixed: teacher + ReviewKD GEMMs on bf16 MFMA operands (fp32 accumulate), "
                          "student fp32; fp32: every GEMM on exact-f32 MFMA")
@@ -124,8 +257,15 @@ def main():
 
     from clskd import ops
     from clskd.data import synthetic_pairs
-    if args.spkd and (args.train or args.graph):
-        raise SystemExit("--spkd is its own eager leg (no --train / --graph)")
+    if args.c1:
+        return run_c1(args, dev)
+    if args.graph:
+        args.launch = "graph"
+    if args.spkd and args.train:
+        raise SystemExit("--spkd is its own leg (no --train)")
+    if args.train or args.spkd:
+        args.launch = "eager"  # the C3 / C4 legs launch eagerly (their capture is not wired yet)
+    args.graph = args.launch == "graph"
     bsz = B_SPKD if args.spkd else B_PER_GPU
     kd = build_kd(dev, args.abf_reinit, args.precision, spkd=args.spkd)
     # NBATCH distinct batches resident in HBM; step i consumes batch i % NBATCH
@@ -143,9 +283,19 @@ def main():
 
         def step(i):
             return kd.train_step((Xs[i % NBATCH], Ys[i % NBATCH]), flat, opt)
-    elif (not args.graph):
+    elif args.launch == "eager":
         def step(i):
             # fwd+loss only: no autograd tape (the C3 leg above records and consumes one)
+            with torch.no_grad():
+                return kd.training_step((Xs[i % NBATCH], Ys[i % NBATCH]), i)
+    elif args.launch == "exec":
+        from clskd.graph import StepExecutor
+        executor = StepExecutor(kd, Xs[0], Ys[0])
+
+        def step(i):
+            return executor(Xs[i % NBATCH], Ys[i % NBATCH])
+
+        def eager_step(i):
             with torch.no_grad():
                 return kd.training_step((Xs[i % NBATCH], Ys[i % NBATCH]), i)
     else:
@@ -168,16 +318,21 @@ def main():
         if last:
             ops.KernelTimer.start()
             with serialized_streams():
-                step(i)
+                (eager_step if args.launch == "exec" else step)(i)
             census = ops.KernelTimer.stop()
         else:
             step(i)
     torch.cuda.synchronize()
     dominant = max(census.items(), key=lambda kv: kv[1][1])[0] if census else None
+    if args.launch == "exec":
+        # live HIP-event timing of the dominant instance inside the executor's launches
+        n_dom = census[dominant][0]
+        ops.check(ops.lib().clskd_exec_profile(executor._ex, ops.KernelTimer.fns[dominant],
+                                               n_dom * args.steps), "exec_profile")
 
     # ---- timed region: exactly K steps, barrier + sync on both sides --------------------
     cdist.barrier(dev)
-    if (not args.graph):
+    if args.launch == "eager":
         ops.KernelTimer.start(only=dominant)
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -185,7 +340,20 @@ def main():
     host_el = time.perf_counter() - t0  # host enqueue of K steps (no sync inside the loop)
     cdist.barrier(dev)
     el = time.perf_counter() - t0
-    if (not args.graph):
+    if args.launch == "exec":
+        import ctypes
+        tot, cnt = ctypes.c_double(0), ctypes.c_int32(0)
+        ops.check(ops.lib().clskd_exec_profile_read(executor._ex, ctypes.byref(tot),
+                                                    ctypes.byref(cnt)), "exec_profile_read")
+        fl = census[dominant][2] / census[dominant][0]
+        ktimes = {dominant: [cnt.value, tot.value, fl * cnt.value]}
+        timing = ("HIP events around every launch of the dominant conv kernel inside the timed "
+                  "region, recorded by the step executor on the kernel's own stream (4 concurrent "
+                  "streams: a launch's event span includes time it shares the CUs); dominant = "
+                  "largest total isolated time in the census step (the last warm-up step run "
+                  "eagerly on one stream, every conv launch timed: conv_all_kernels)")
+        census_steps = 1
+    elif (not args.graph):
         ktimes = ops.KernelTimer.stop()
         timing = ("HIP events around every launch of the dominant conv kernel inside the timed "
                   "region (4 concurrent streams: a launch's event span includes time it shares the "
@@ -248,7 +416,7 @@ def main():
                                     for k, v in sorted(census.items(), key=lambda kv: -kv[1][1])}))
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not args.train and not args.spkd:
-            cpu = cpu_baseline(args.cpu_seconds)
+            cpu = cpu_baseline(args.cpu_steps)
             # GPU / CPU-oracle ratio on the same workload.  `vs_baseline` stays null: it is
             # reserved for a published number for this metric, and BASELINE.md has none
             cpu["gpu_over_cpu"] = round(frames / el / cpu["value"], 1)
@@ -282,7 +450,12 @@ def main():
                        "launch": ("eager, 2 HIP streams (caller: teacher; side: student + "
                                   "MRSTFT)" if args.spkd else
                                   "eager, 4 HIP streams (caller, teacher, student, ReviewKD-"
-                                  "encoder/MRSTFT)" if (not args.graph)
+                                  "encoder/MRSTFT)" if args.launch == "eager" else
+                                  "C++ step executor (clskd_exec_launch): the captured step "
+                                  "replayed on 4 HIP streams along its dependency edges "
+                                  f"({executor.info['kernels']} kernels, "
+                                  f"{executor.info['waits']} cross-stream waits per step)"
+                                  if args.launch == "exec"
                                   else "hipGraph replay (clskd.graph.StepGraph)"),
                        "precision": ("teacher GEMMs bf16 MFMA operands / fp32 accumulate; "
                                      "student, STFT/iSTFT, LSTM recurrence, BN, losses fp32")

@@ -38,6 +38,19 @@ typedef enum { CLSKD_F32 = 0, CLSKD_BF16 = 1 } clskd_compute;
 const char* clskd_last_error(void);
 int clskd_version(void);
 
+/* Dispatch knobs (engine A/B switches, grid caps, LSTM k-slicing): each is read from the
+ * environment variable of the same name once, at the library's first launch, and can be changed
+ * afterwards only through clskd_set_knob (tests, tools) — never per launch from the environment.
+ * Every knob selects between kernels that compute the same result.  The timing-only experiment
+ * modes that do not (CLSKD_G8 >= 10, CLSKD_LSTM128_TDIV, CLSKD_LSTM32_TDIV,
+ * CLSKD_BF16_DEBUG_MODE) exist only in a -DCLSKD_EXPERIMENTS build; in the product build a
+ * non-zero value makes the affected launch return CLSKD_E_ARG instead of a wrong result.
+ * clskd_set_knob / clskd_get_knob return CLSKD_E_ARG for an unknown name. */
+int clskd_set_knob(const char* name, int32_t value);
+int clskd_get_knob(const char* name, int32_t* value);
+/* 1 when the library was built with -DCLSKD_EXPERIMENTS (timing-only modes present), else 0. */
+int clskd_experiments_build(void);
+
 /* ------------------------------------------------------------------------------------------
  * Implicit-GEMM convolution over BFTC activations.
  * Replaces: ComplexConv2d.forward (tools_for_model.py:236-262, packed [[Wr,-Wi],[Wi,Wr]]),
@@ -126,6 +139,8 @@ int clskd_conv2d_fwd(const clskd_conv_desc* d, void* stream);
  * thread's last successful clskd_conv2d_fwd launched — the dispatch policy (direct / halo /
  * 128- or 256-row bf16 engine / fp32 engine) is the library's, so hosts label timings with it. */
 const char* clskd_conv_last_kernel(void);
+/* Host function (kernel stub address) of that kernel: the key clskd_exec_profile times by. */
+const void* clskd_conv_last_kernel_fn(void);
 /* Direct-path helpers: padded output width NP of the direct layout, and whether an (N, K)
  * GEMM is served by the direct kernel (returns 1) — hosts pack CLSKD_WLAYOUT_DIRECT weights
  * exactly when this is 1. */
@@ -514,6 +529,32 @@ int clskd_spkd_bn_bwd(const void* raw, int32_t dtype, int64_t sB, int64_t P, int
                       const float* scale, const float* shift, const float* coef, const float* mean,
                       const float* var, float eps, const float* gamma, double* work, int32_t nblk,
                       float* dgamma, float* dbeta, void* draw, int32_t draw_dtype, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Step executor.
+ * Replaces: the host side of KnowledgeDistillation.training_step (distill.py:72-148) — the
+ * ~400 per-step launches a Python host issues one by one.  Takes a hipGraph captured from one
+ * step (stream capture of the library's own calls, e.g. torch.cuda.CUDAGraph(keep_graph=True)
+ * + raw_cuda_graph()) and replays its kernel / memset / memcpy nodes with their captured
+ * arguments on `nstreams` HIP streams along the graph's dependency edges (one event record /
+ * wait per cross-stream edge not already implied; resolved once here).  Unlike hipGraphLaunch
+ * the independent branches run concurrently.  Stream 0 is the launch stream: the others fork
+ * from it and join back into it, so a launch is stream-ordered like any other call.  The graph is
+ * BORROWED: the caller keeps it (its nodes hold the kernels' arguments) and the memory its
+ * nodes address alive while the executor exists.
+ * info[0..7] = nodes, kernel nodes, memset nodes, memcpy nodes, empty nodes, cross-stream
+ * waits, event records, program length; info[8..8+nstreams) = nodes per stream (n >= 8). */
+typedef struct clskd_exec clskd_exec;
+int clskd_exec_create(void* hip_graph, int32_t nstreams, clskd_exec** out);
+int clskd_exec_launch(clskd_exec* ex, void* stream);
+int clskd_exec_info(const clskd_exec* ex, int32_t* info, int32_t n);
+void clskd_exec_destroy(clskd_exec* ex);
+/* Live timing of one kernel under the executor: every launch of host function `fn` (e.g.
+ * clskd_conv_last_kernel_fn() after a conv call) gets a HIP event pair around it on its stream,
+ * for up to max_launches launches (fn NULL disables).  clskd_exec_profile_read (after a
+ * synchronize) returns the summed event spans and the number of timed launches. */
+int clskd_exec_profile(clskd_exec* ex, const void* fn, int32_t max_launches);
+int clskd_exec_profile_read(clskd_exec* ex, double* total_ms, int32_t* count);
 
 #ifdef __cplusplus
 }

@@ -9,7 +9,9 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libclskd_hip.so")
+# CLSKD_LIB=exp selects the timing-experiments build (clskd.build: never the product library)
+LIB_PATH = os.path.join(_HERE, "libclskd_hip_exp.so" if os.environ.get("CLSKD_LIB") == "exp"
+                        else "libclskd_hip.so")
 
 MAX_SEGS = 4
 F32, BF16 = 0, 1
@@ -69,7 +71,11 @@ _p, _i32, _i64, _f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float
 SIGNATURES = {
     "clskd_last_error": (C.c_char_p, []),
     "clskd_conv_last_kernel": (C.c_char_p, []),
+    "clskd_conv_last_kernel_fn": (_p, []),
     "clskd_version": (_i32, []),
+    "clskd_set_knob": (_i32, [C.c_char_p, _i32]),
+    "clskd_get_knob": (_i32, [C.c_char_p, C.POINTER(C.c_int32)]),
+    "clskd_experiments_build": (_i32, []),
     "clskd_conv2d_fwd": (_i32, [C.POINTER(ConvDesc), _p]),
     "clskd_conv_direct_np": (_i32, [_i32]),
     "clskd_conv_direct_ok": (_i32, [_i32, _i32]),
@@ -140,6 +146,12 @@ SIGNATURES = {
                                       C.POINTER(C.c_void_p), C.POINTER(C.c_int32), _i32, _i32,
                                       _i32, _f32, _p, _p]),
     "clskd_gram_bwd": (_i32, [_p, _i32, _i32, _p]),
+    "clskd_exec_create": (_i32, [_p, _i32, C.POINTER(C.c_void_p)]),
+    "clskd_exec_launch": (_i32, [_p, _p]),
+    "clskd_exec_info": (_i32, [_p, C.POINTER(C.c_int32), _i32]),
+    "clskd_exec_destroy": (None, [_p]),
+    "clskd_exec_profile": (_i32, [_p, _p, _i32]),
+    "clskd_exec_profile_read": (_i32, [_p, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
     "clskd_spkd_bn_bwd": (_i32, [_p, _i32, _i64, _i64, _i32, _i32, _p, _p, _p, _p, _p, _f32, _p, _p,
                                  _i32, _p, _p, _p, _i32, _p]),
 }
@@ -177,6 +189,16 @@ def load(require_gpu=True):
             raise RuntimeError("clskd: no HIP device visible; the MI355X path has no CPU fallback")
         _GPU_OK = True
     return _LIB
+
+
+def set_knob(name, value):
+    """Switch a dispatch knob of the loaded library (include/clskd.h: read from the environment
+    once, then only through this call).  Returns the previous value."""
+    lib = load(require_gpu=False)
+    prev = C.c_int32(0)
+    check(lib.clskd_get_knob(name.encode(), C.byref(prev)), f"get_knob {name}")
+    check(lib.clskd_set_knob(name.encode(), int(value)), f"set_knob {name}")
+    return prev.value
 
 
 def check(rc, what=""):

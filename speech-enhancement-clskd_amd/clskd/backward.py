@@ -104,6 +104,7 @@ def _scatter(src, maps, grads, acc):
 # transposed (data-gradient) weights, cached per packed forward weight
 # ------------------------------------------------------------------------------------------
 _TW = {}
+_TW_MAX = 512  # entries; a C3 step of one model uses ~60
 
 
 def _tw(key, src, build):
@@ -111,13 +112,21 @@ def _tw(key, src, build):
     built from (weak reference) at the same in-place version: keys carry id()s of modules, and a
     module or tensor freed by an earlier step can hand its id and storage address to a new one
     (seen as a flaky mixed-precision gradient test: a new model's ABF backward ran with the
-    previous model's re-drawn ABF weights)."""
+    previous model's re-drawn ABF weights; regression test
+    tests/test_host_cpu.py::test_tw_cache_rebuilds_for_a_new_source_identity).  Entries whose
+    source died are dropped on every insert, and the cache is bounded (oldest first), so freed
+    models do not keep device copies of their weights alive."""
     k = (src.data_ptr(), src._version)
     ent = _TW.get(key)
     if ent is not None and ent[0] == k and ent[2]() is src:
         return ent[1]
     with torch.no_grad():
         w = build()
+    _TW.pop(key, None)
+    for dead in [kk for kk, e in _TW.items() if e[2]() is None]:
+        del _TW[dead]
+    while len(_TW) >= _TW_MAX:
+        del _TW[next(iter(_TW))]
     _TW[key] = (k, w, weakref.ref(src))
     return w
 

@@ -1,5 +1,10 @@
 """In-tree build of libclskd_hip.so for gfx950 (hipcc, no JIT cache): the built .so lives next to
-this file so it travels with the repo snapshot to the GPU box."""
+this file so it travels with the repo snapshot to the GPU box.
+
+``build(experiments=True)`` (or ``CLSKD_EXPERIMENTS=1 python -m clskd.build``) builds a separate
+libclskd_hip_exp.so with -DCLSKD_EXPERIMENTS: the timing-only kernel modes that produce wrong
+results (engine operand-isolation variants, truncated LSTM recurrences).  Tools load it with
+CLSKD_LIB=exp; the product library never contains them."""
 import concurrent.futures as cf
 import os
 import subprocess
@@ -7,10 +12,12 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 OUT = os.path.join(HERE, "libclskd_hip.so")
+OUT_EXP = os.path.join(HERE, "libclskd_hip_exp.so")
 OBJDIR = os.path.join(os.path.dirname(HERE), "build", "obj")
+OBJDIR_EXP = os.path.join(os.path.dirname(HERE), "build", "obj_exp")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-SOURCES = ["capi.cpp", "conv_igemm.hip", "conv_bf16.hip", "conv_halo.hip", "conv_gemm8.hip", "conv_direct.hip", "conv_pointwise.hip", "norm.hip", "lstm.hip", "loss.hip", "redraw.hip", "grad.hip", "norm_bwd.hip", "abf.hip", "metrics.hip"]
+SOURCES = ["capi.cpp", "conv_igemm.hip", "conv_bf16.hip", "conv_halo.hip", "conv_gemm8.hip", "conv_direct.hip", "conv_pointwise.hip", "norm.hip", "lstm.hip", "loss.hip", "redraw.hip", "grad.hip", "norm_bwd.hip", "abf.hip", "metrics.hip", "exec.cpp"]
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
 
 
@@ -21,31 +28,35 @@ def _newer(src_files, target):
     return any(os.path.getmtime(s) > t for s in src_files)
 
 
-def build(verbose=False, force=False):
-    os.makedirs(OBJDIR, exist_ok=True)
+def build(verbose=False, force=False, experiments=None):
+    if experiments is None:
+        experiments = os.environ.get("CLSKD_EXPERIMENTS") == "1"
+    objdir, out = (OBJDIR_EXP, OUT_EXP) if experiments else (OBJDIR, OUT)
+    flags = FLAGS + (["-DCLSKD_EXPERIMENTS"] if experiments else [])
+    os.makedirs(objdir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "clskd.h"))
     objs = []
     jobs = []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
-        obj = os.path.join(OBJDIR, s + ".o")
+        obj = os.path.join(objdir, s + ".o")
         objs.append(obj)
         if force or _newer([src] + headers, obj):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
-            jobs.append([HIPCC] + FLAGS + lang + ["-c", src, "-o", obj])
+            jobs.append([HIPCC] + flags + lang + ["-c", src, "-o", obj])
     with cf.ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         for cmd, res in zip(jobs, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs)):
             if res.returncode != 0:
                 raise RuntimeError(f"hipcc failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
             if verbose and res.stderr.strip():
                 print(res.stderr)
-    if force or jobs or _newer(objs, OUT):
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", OUT] + objs
+    if force or jobs or _newer(objs, out):
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out] + objs
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
-    return OUT
+    return out
 
 
 if __name__ == "__main__":

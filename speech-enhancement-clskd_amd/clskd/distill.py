@@ -132,7 +132,15 @@ def _validation_step(module, batch):
 
 
 class KnowledgeDistillation(nn.Module):
-    """distill.py:38-229 without Lightning: same constructor and step signature."""
+    """distill.py:38-229 without Lightning: same constructor and step signature.
+
+    Limitation of abf_reinit='step' (the default): the ABF re-draw rewrites the ReviewKD weights
+    in place at the start of every training_step, and the autograd tape of a step checks their
+    version, so two forwards before one backward (e.g. loss1 + loss2 summed for manual gradient
+    accumulation) raise a RuntimeError in the first step's backward instead of using the
+    overwritten weights.  The reference builds fresh ABF modules per step (distill.py:92-96) and
+    allows that pattern; here, call backward after each training_step (Lightning's automatic
+    optimisation does), or use abf_reinit='once'."""
 
     def __init__(self, teacher, student, sftf_loss=MultiResolutionSTFTLoss, spkd_loss=SPKDLoss,
                  cfg=cfg, abf_reinit="step", precision="fp32"):
@@ -421,6 +429,9 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     main.wait_stream(tstream)
     main.wait_stream(side)
     main.wait_stream(side2)
+    # returned side-stream tensors: their blocks must not be recycled by a later side-stream
+    # allocation before the caller's reads on `main` are done
+    sf["out_wav"].record_stream(main)
     _mark("main: joined", main)
     s_refs = g_enc.refs + g_dec.refs
     assert len(s_refs) == 14 and len(g_t.refs) == 14
@@ -508,6 +519,7 @@ class SPKDDistillation(nn.Module):
                                  want_masks=False)["out_wav"]
             self.stft_loss(s, y, out2=buf[0:2])
         main.wait_stream(side)
+        s.record_stream(main)  # side-stream allocation read (and returned) on the caller's stream
         ops.spkd_losses([(ops.gram_view(s), ops.gram_view(t))], X.shape[0], out=buf[2:3])
         total = torch.empty((), dtype=torch.float32, device=X.device)
         ops.sum_f32(buf[1:], total)

@@ -30,6 +30,7 @@ class KernelTimer:
     active = False
     records = []
     only = None  # optional kernel-instance name: time just that kernel's launches
+    fns = {}  # kernel-instance name -> host function (clskd_exec_profile key)
 
     @classmethod
     def start(cls, only=None):
@@ -222,7 +223,7 @@ def conv_mblocks(B, Fo, To):
 
 class _ConvPlan:
     """Launch descriptor of one conv signature, built once; per call only the pointers change."""
-    __slots__ = ("desc", "segs", "nseg", "direct", "name", "flops", "shape", "nstats", "osize")
+    __slots__ = ("desc", "segs", "nseg", "direct", "name", "fn", "flops", "shape", "nstats", "osize")
 
 
 _CONV_PLANS = {}
@@ -283,6 +284,7 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
     pl.desc, pl.nseg, pl.direct = d, len(segs), direct
     pl.segs = [d.seg[i] for i in range(_lib.MAX_SEGS)]  # views into d (patched per call)
     pl.name = None  # kernel instance the library dispatches to (read after the first launch)
+    pl.fn = None  # its host function (the executor times launches by it)
     pl.flops = 2.0 * B * Fo * To * N * K
     pl.shape = (B * Fo * To, N, K, "bf16" if bf16 else "f32")
     pl.nstats = conv_mblocks(B, Fo, To) * N * 2
@@ -338,11 +340,14 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
         e1.record()
         if pl.name is None:
             pl.name = L.clskd_conv_last_kernel().decode()
+            pl.fn = L.clskd_conv_last_kernel_fn()
         KernelTimer.records.append((pl.name, pl.flops, e0, e1, pl.shape))
+        KernelTimer.fns[pl.name] = pl.fn
     else:
         check(L.clskd_conv2d_fwd(d, _stream()), "conv2d")
         if pl.name is None:
             pl.name = L.clskd_conv_last_kernel().decode()
+            pl.fn = L.clskd_conv_last_kernel_fn()
     return out
 
 

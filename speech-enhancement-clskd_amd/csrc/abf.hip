@@ -463,9 +463,8 @@ extern "C" int32_t clskd_abf_moment_blocks(int64_t rows, int32_t cin) {
   // rows per block: the S2 MFMA work grows with cin^2 (10 tile MFMAs per 4 rows at cin = 64)
   int64_t per = cin >= 64 ? 768 : cin >= 32 ? 1024 : 2048;
   // A/B knob: CLSKD_ABF_MOMENT_DIV = d divides the rows per block (more blocks in flight)
-  static const int div = [] {
-    const char* e = getenv("CLSKD_ABF_MOMENT_DIV");
-    const int v = e ? atoi(e) : 1;
+  const int div = [] {
+    const int v = knob(KNOB_ABF_MOMENT_DIV);
     return v >= 1 && v <= 16 ? v : 1;
   }();
   per = std::max<int64_t>(64, per / div);

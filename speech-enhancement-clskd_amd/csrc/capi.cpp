@@ -1,6 +1,11 @@
-// C-ABI plumbing: thread-local error message and version.  (Kernels live in *.hip.)
+// C-ABI plumbing: thread-local error message, version and the dispatch-knob registry.
+// (Kernels live in *.hip.)
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
+
+#include <atomic>
+#include <mutex>
 
 #include "common.h"
 
@@ -19,8 +24,85 @@ void note_kernel(const char* fmt, ...) {
   vsnprintf(g_kernel, sizeof(g_kernel), fmt, ap);
   va_end(ap);
 }
+
+static thread_local const void* g_kernel_fn = nullptr;
+void note_kernel_fn(const void* fn) { g_kernel_fn = fn; }
+
+// ---- dispatch knobs: env read once, then only clskd_set_knob changes them ---------------------
+struct KnobDef {
+  const char* name;
+  int dflt;
+};
+// order = KnobId
+static const KnobDef kKnobs[KNOB_COUNT] = {
+    {"CLSKD_G8", 1},          {"CLSKD_G8_GRID", 0},      {"CLSKD_HALO_GRID", 0},
+    {"CLSKD_DIRECT_COOP", 0}, {"CLSKD_LSTM_NKS", 4},     {"CLSKD_LSTM_NKS32", 1},
+    {"CLSKD_WGRAD_WG", 4096}, {"CLSKD_NO_HALO", 0},      {"CLSKD_BF16_WAVES", 8},
+    {"CLSKD_BF16_STAGES", 3}, {"CLSKD_BF16_TILE", 0},    {"CLSKD_NO_POINTWISE", 0},
+    {"CLSKD_ABF_MOMENT_DIV", 1}, {"CLSKD_F32_WAVES", 4}, {"CLSKD_LSTM128_TDIV", 0},
+    {"CLSKD_LSTM32_TDIV", 0}, {"CLSKD_BF16_DEBUG_MODE", 0},
+};
+static std::atomic<int> g_knob[KNOB_COUNT];
+static std::once_flag g_knob_once;
+
+static void init_knobs() {
+  for (int i = 0; i < KNOB_COUNT; ++i) {
+    const char* e = getenv(kKnobs[i].name);
+    g_knob[i].store(e && *e ? atoi(e) : kKnobs[i].dflt, std::memory_order_relaxed);
+  }
+}
+
+int knob(KnobId k) {
+  std::call_once(g_knob_once, init_knobs);
+  return g_knob[k].load(std::memory_order_relaxed);
+}
+
+static int knob_index(const char* name) {
+  if (!name) return -1;
+  for (int i = 0; i < KNOB_COUNT; ++i)
+    if (strcmp(name, kKnobs[i].name) == 0) return i;
+  return -1;
+}
+
+int experiment_guard(const char* what, int value) {
+#ifdef CLSKD_EXPERIMENTS
+  (void)what;
+  (void)value;
+  return CLSKD_OK;
+#else
+  if (value == 0) return CLSKD_OK;
+  set_error("%s = %d selects a timing-only experiment mode (wrong results); it exists only in a "
+            "-DCLSKD_EXPERIMENTS build of libclskd_hip.so",
+            what, value);
+  return CLSKD_E_ARG;
+#endif
+}
 }  // namespace clskd
 
 extern "C" const char* clskd_last_error(void) { return clskd::g_err; }
 extern "C" const char* clskd_conv_last_kernel(void) { return clskd::g_kernel; }
+extern "C" const void* clskd_conv_last_kernel_fn(void) { return clskd::g_kernel_fn; }
 extern "C" int clskd_version(void) { return 1; }
+
+extern "C" int clskd_set_knob(const char* name, int32_t value) {
+  const int i = clskd::knob_index(name);
+  CLSKD_CHECK_ARG(i >= 0, "set_knob: unknown knob '%s'", name ? name : "(null)");
+  std::call_once(clskd::g_knob_once, clskd::init_knobs);
+  clskd::g_knob[i].store(value, std::memory_order_relaxed);
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_get_knob(const char* name, int32_t* value) {
+  const int i = clskd::knob_index(name);
+  CLSKD_CHECK_ARG(i >= 0 && value, "get_knob: unknown knob '%s' or null output", name ? name : "(null)");
+  *value = clskd::knob((clskd::KnobId)i);
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_experiments_build(void) {
+#ifdef CLSKD_EXPERIMENTS
+  return 1;
+#else
+  return 0;
+#endif
+}

@@ -14,6 +14,21 @@ void set_error(const char* fmt, ...);
 // Instance name of the kernel the calling thread's last conv launch ran ("base<arg,...>", the
 // template arguments rocprof shows); read back through clskd_conv_last_kernel().
 void note_kernel(const char* fmt, ...);
+// Host function of that kernel (clskd_conv_last_kernel_fn: the executor's per-kernel timing key).
+void note_kernel_fn(const void* fn);
+// Dispatch knobs (capi.cpp): env read once at first use, changed only by clskd_set_knob.
+enum KnobId {
+  KNOB_G8, KNOB_G8_GRID, KNOB_HALO_GRID, KNOB_DIRECT_COOP, KNOB_LSTM_NKS, KNOB_LSTM_NKS32,
+  KNOB_WGRAD_WG, KNOB_NO_HALO, KNOB_BF16_WAVES, KNOB_BF16_STAGES, KNOB_BF16_TILE,
+  KNOB_NO_POINTWISE, KNOB_ABF_MOMENT_DIV, KNOB_F32_WAVES,
+  // timing-only experiment modes (wrong results): -DCLSKD_EXPERIMENTS builds only
+  KNOB_LSTM128_TDIV, KNOB_LSTM32_TDIV, KNOB_BF16_DEBUG_MODE,
+  KNOB_COUNT
+};
+int knob(KnobId k);
+// CLSKD_OK, or CLSKD_E_ARG (with the error message set) when `value` selects a timing-only mode
+// in a product build.
+int experiment_guard(const char* what, int value);
 template <typename T> inline const char* type_name();
 template <> inline const char* type_name<float>() { return "float"; }
 template <> inline const char* type_name<__bf16>() { return "bf16"; }

@@ -405,6 +405,7 @@ static int launch_v2(const clskd_conv_desc& d, hipStream_t st) {
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
   ConvArgsV2 a{d};
   hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, BM), (unsigned)cdiv(d.N, BN)), dim3(NW * 64), lds, st, a);
+  note_kernel_fn((const void*)kern);
   note_kernel("conv_igemm_bf16_dma<%d,%d,%d,%d,%d,%s,%d>", BM, BK, BN, NW, S, type_name<OutT>(), DBG);
   return CLSKD_OK;
 }
@@ -440,40 +441,27 @@ int launch_conv_halo(const clskd_conv_desc& d, hipStream_t st, bool* launched);
 int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched);
 
 int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
-  static const bool no_halo = [] {  // A/B switch: CLSKD_NO_HALO=1 keeps narrow layers on the engine
-    const char* e = getenv("CLSKD_NO_HALO");
-    return e && e[0] == '1';
-  }();
+  const bool no_halo = knob(KNOB_NO_HALO) == 1;  // A/B switch: 1 keeps narrow layers on the engine
   if (!no_halo) {
     bool launched = false;
     const int rc = launch_conv_halo(d, st, &launched);
     if (rc != CLSKD_OK || launched) return rc;
   }
-  static const int dbg0 = [] {
-    const char* e = getenv("CLSKD_BF16_DEBUG_MODE");
-    return e ? atoi(e) : 0;
-  }();
-  if (dbg0 == 0) {
+  const int dbg = knob(KNOB_BF16_DEBUG_MODE);
+  {
+    const int rc = experiment_guard("CLSKD_BF16_DEBUG_MODE", dbg);
+    if (rc != CLSKD_OK) return rc;
+  }
+  if (dbg == 0) {
     bool launched = false;
     const int rc = launch_conv_gemm8(d, st, &launched);
     if (rc != CLSKD_OK || launched) return rc;
   }
-  static const int nw = [] {
-    const char* e = getenv("CLSKD_BF16_WAVES");
-    return e && e[0] == '4' ? 4 : 8;
-  }();
-  static const int stages = [] {  // experiment knob: CLSKD_BF16_STAGES=3|4
-    const char* e = getenv("CLSKD_BF16_STAGES");
-    return e && e[0] == '4' ? 4 : 3;
-  }();
-  static const int dbg = [] {  // timing experiments only: 1 = no DMA, 2 = no MFMA (wrong results)
-    const char* e = getenv("CLSKD_BF16_DEBUG_MODE");
-    return e ? atoi(e) : 0;
-  }();
-  static const int tilecfg = [] {  // A/B knob: CLSKD_BF16_TILE=128|256 forces one row-tile height
-    const char* e = getenv("CLSKD_BF16_TILE");
-    return e ? atoi(e) : 0;
-  }();
+  const int nw = knob(KNOB_BF16_WAVES) == 4 ? 4 : 8;
+  const int stages = knob(KNOB_BF16_STAGES) == 4 ? 4 : 3;  // experiment knob: 3 | 4
+  const int tilecfg = knob(KNOB_BF16_TILE);  // A/B knob: 128 | 256 forces one row-tile height
+#ifdef CLSKD_EXPERIMENTS
+  // timing experiments only: 1 = no DMA, 2 = no MFMA, ... (wrong results)
   if (dbg == 1 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<128, 64, 256, 8, 3, __bf16, 1>(d, st);
   if (dbg == 2 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<128, 64, 256, 8, 3, __bf16, 2>(d, st);
   if (dbg == 1 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 3, __bf16, 1>(d, st);
@@ -489,6 +477,7 @@ int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
   if (dbg == 8 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 4, __bf16, 8>(d, st);
   if (dbg == 6 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 32, 256, 16, 4, __bf16, 0>(d, st);
   if (dbg == 6 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 4, __bf16, 0>(d, st);
+#endif
   if (d.N > 32 && d.K % 32 == 0 && tilecfg != 128) {
     // 256-row tiles stage a third fewer bytes per FLOP (measured 1.1-1.25x faster per tile
     // worth of work) but halve the workgroup count: pick them unless the tail rounds eat the

@@ -376,12 +376,11 @@ __global__ __launch_bounds__(128) void conv_direct_coop_kernel(const DirectArgs 
   }
 }
 
-// Row-cooperative dispatch, opt-in while it is being validated (CLSKD_DIRECT_COOP=1, read per
-// launch so a test can switch it): N <= 2, no fused statistics, a (tap, segment, channel) K
+// Row-cooperative dispatch, opt-in while it is being validated (knob CLSKD_DIRECT_COOP=1;
+// tests switch it with clskd_set_knob): N <= 2, no fused statistics, a (tap, segment, channel) K
 // table whose channel runs per tap LPR = ctot / kvec is 2, 4, 8 or 16, at most 8 runs per lane.
 static bool coop_lpr(const clskd_conv_desc& d, int g, int* lpr, int* runs) {
-  const char* e = getenv("CLSKD_DIRECT_COOP");
-  const bool on = e && e[0] == '1';
+  const bool on = knob(KNOB_DIRECT_COOP) == 1;
   if (!on || d.stats || d.N > 2 || d.ntaps <= 0 || d.ctot % g) return false;
   const int L = d.ctot / g;
   if (L != 2 && L != 4 && L != 8 && L != 16) return false;
@@ -397,12 +396,15 @@ static void launch_coop_r(const clskd_conv_desc& d, hipStream_t st) {
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
   const size_t lds = (size_t)(d.K / G) * 16;
   DirectArgs a{d};
-  if (d.out_dtype == CLSKD_BF16)
+  if (d.out_dtype == CLSKD_BF16) {
     hipLaunchKernelGGL((conv_direct_coop_kernel<2, G, InT, __bf16, LPR, R>),
                        dim3((unsigned)cdiv(M, 128)), dim3(128), lds, st, a);
-  else
+    note_kernel_fn((const void*)conv_direct_coop_kernel<2, G, InT, __bf16, LPR, R>);
+  } else {
     hipLaunchKernelGGL((conv_direct_coop_kernel<2, G, InT, float, LPR, R>),
                        dim3((unsigned)cdiv(M, 128)), dim3(128), lds, st, a);
+    note_kernel_fn((const void*)conv_direct_coop_kernel<2, G, InT, float, LPR, R>);
+  }
   note_kernel("conv_direct_coop_kernel<2,%d,%s,%s,%d,%d>", G, type_name<InT>(),
               d.out_dtype == CLSKD_BF16 ? "bf16" : "float", LPR, R);
 }
@@ -445,12 +447,15 @@ static void launch_np(const clskd_conv_desc& d, hipStream_t st) {
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
   const size_t lds = direct_lds(d, NP, G);
   DirectArgs a{d};
-  if (d.out_dtype == CLSKD_BF16)
+  if (d.out_dtype == CLSKD_BF16) {
     hipLaunchKernelGGL((conv_direct_kernel<NP, G, InT, __bf16>), dim3((unsigned)cdiv(M, 128)),
                        dim3(128), lds, st, a);
-  else
+    note_kernel_fn((const void*)conv_direct_kernel<NP, G, InT, __bf16>);
+  } else {
     hipLaunchKernelGGL((conv_direct_kernel<NP, G, InT, float>), dim3((unsigned)cdiv(M, 128)),
                        dim3(128), lds, st, a);
+    note_kernel_fn((const void*)conv_direct_kernel<NP, G, InT, float>);
+  }
   note_kernel("conv_direct_kernel<%d,%d,%s,%s>", NP, G, type_name<InT>(),
               d.out_dtype == CLSKD_BF16 ? "bf16" : "float");
 }

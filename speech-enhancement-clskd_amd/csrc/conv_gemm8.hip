@@ -537,12 +537,12 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   // one tile per workgroup when they all fit; otherwise whole XCD groups of workgroups for the
   // contiguous-run tile deal
   // CLSKD_G8_GRID caps the workgroup count (leaves CUs to concurrent streams; A/B knob)
-  const char* ge = getenv("CLSKD_G8_GRID");
-  const int cap = ge ? atoi(ge) : ncu;
+  const int cap = knob(KNOB_G8_GRID) > 0 ? knob(KNOB_G8_GRID) : ncu;
   const int ncap = cap > 0 && cap < ncu ? cap : ncu;
   const int grid = ntiles <= ncap ? (int)ntiles : (ncap >= 8 ? (ncap & ~7) : ncap);
   ConvArgsG8 a{d, (int)n_mt, (int)ntiles};
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NWV * 64), lds, st, a);
+  note_kernel_fn((const void*)kern);
   note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d>", BM, BN, WM, BK, NS, PHI, type_name<OutT>(), DBG, PF,
               NWV, EB);
   return CLSKD_OK;
@@ -553,13 +553,17 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
 // selects timing-experiment variants (bf16 outputs only); read per launch (tests switch it).
 int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) {
   *launched = false;
-  const char* env = getenv("CLSKD_G8");
-  const int mode = env ? atoi(env) : 1;
+  const int mode = knob(KNOB_G8);
+  if (mode >= 10) {
+    const int rc = experiment_guard("CLSKD_G8", mode);
+    if (rc != CLSKD_OK) return rc;
+  }
   if (mode == 0 || d.N <= 64 || d.K % 64 != 0 || d.nseg > 2 || (int64_t)d.B * d.Fo * d.To >= ((int64_t)1 << 31) ||
       (int64_t)d.Fo * d.stride_f >= 32768 || (int64_t)d.To * d.stride_t >= 32768)  // 16-bit row origins
     return CLSKD_OK;
   const bool f32 = d.out_dtype == CLSKD_F32;
   *launched = true;
+#ifdef CLSKD_EXPERIMENTS
   if (mode >= 10 && !f32) {
     const int cfg = mode / 10, dbg = mode % 10;
 #define G8X(BM_, BN_, WM_, BK_, NS_, PHI_)                                    \
@@ -607,6 +611,7 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
     }
 #undef G8X
   }
+#endif
   // default: BK 64, two stages, the K-tile boundary before the last substep (EB; 3-5 % on the
   // N = 256 layers against the boundary after it, CLSKD_G8=10)
   if (d.N <= 128) {

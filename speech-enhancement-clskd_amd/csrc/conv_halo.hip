@@ -162,7 +162,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const HaloArgs a) {
   }
   // loop constants (laundered: never re-loaded from the kernarg segment inside the loop)
   const int nchunk = sconst(a.nchunk), ntb = sconst(a.ntb), nfb = sconst(a.nfb);
-  const int ntaps = sconst(d.ntaps), NGH = sconst(a.NGH);
+  const int NGH = sconst(a.NGH);
   const int Fo = sconst(d.Fo), To = sconst(d.To), sfr = sconst(d.stride_f);
   const int dfmin = sconst(a.dfmin), dtmin = sconst(a.dtmin);
   const int64_t oB = vconst64(d.oB), oF = vconst64(d.oF), oT = vconst64(d.oT);
@@ -478,8 +478,7 @@ static int launch_halo_planned(const HaloArgs& a, size_t lds, hipStream_t st, bo
     return v > 0 ? v : 256;
   }();
   // CLSKD_HALO_GRID caps the workgroup count (leaves CUs to concurrent streams; A/B knob)
-  const char* ge = getenv("CLSKD_HALO_GRID");
-  const int cap = ge ? atoi(ge) : ncu;
+  const int cap = knob(KNOB_HALO_GRID) > 0 ? knob(KNOB_HALO_GRID) : ncu;
   const int ncap = cap > 0 && cap < ncu ? cap : ncu;
   const int grid = a.ntiles < ncap ? a.ntiles : ncap;
   if (d.stats && grid > a.nblk128) return CLSKD_OK;  // (never for eligible shapes)
@@ -490,6 +489,7 @@ static int launch_halo_planned(const HaloArgs& a, size_t lds, hipStream_t st, bo
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,      \
                               160 * 1024);                                                     \
     hipLaunchKernelGGL(k, dim3(grid), dim3(512), lds, st, a);                                  \
+    note_kernel_fn((const void*)k);                                                            \
     note_kernel("conv_halo_kernel<%d,%s,%d>", BN_, type_name<O_>(), NT_);                      \
   } while (0)
 #define HALO_NT(NT_)                                                                           \

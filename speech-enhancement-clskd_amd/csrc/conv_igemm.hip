@@ -387,15 +387,13 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
   CLSKD_CHECK_SHAPE(!d.vec4 || ctab_bytes <= 32 * 1024, "conv2d(f32): K=%d too long for the chunk table", d.K);
   // 8-wave 256-row tiles (A/B knob CLSKD_F32_WAVES=4|8): half the B staging per FLOP and two
   // waves per SIMD to hide the gather latency
-  static const int nw = [] {
-    const char* e = getenv("CLSKD_F32_WAVES");
-    return e && e[0] == '8' ? 8 : 4;
-  }();
+  const int nw = knob(KNOB_F32_WAVES) == 8 ? 8 : 4;
 #define LAUNCH(BN_, V_, O_, NW_)                                                             \
   do {                                                                                       \
     hipLaunchKernelGGL((conv_igemm_f32<BN_, V_, O_, NW_>),                                    \
                        dim3((unsigned)cdiv(M, 32 * NW_), (unsigned)cdiv(d.N, BN_)),           \
                        dim3(NW_ * 64), (V_) ? ctab_bytes : 0, st, a);                        \
+    note_kernel_fn((const void*)conv_igemm_f32<BN_, V_, O_, NW_>);                           \
     note_kernel("conv_igemm_f32<%d,%s,%s,%d>", BN_, (V_) ? "true" : "false",                  \
                 type_name<O_>(), NW_);                                                       \
   } while (0)

@@ -148,10 +148,7 @@ __global__ __launch_bounds__(256, 4) void conv_pointwise_kernel(const clskd_conv
 }
 
 static bool pointwise_ok(const clskd_conv_desc& d) {
-  static const bool off = [] {  // A/B switch: CLSKD_NO_POINTWISE=1 keeps 1x1 lifts on the engine
-    const char* e = getenv("CLSKD_NO_POINTWISE");
-    return e && e[0] == '1';
-  }();
+  const bool off = knob(KNOB_NO_POINTWISE) == 1;  // A/B switch: 1 keeps 1x1 lifts on the engine
   if (off) return false;
   if (d.compute != CLSKD_F32 || d.in_dtype != CLSKD_F32 || d.wlayout != CLSKD_WLAYOUT_NK ||
       d.accumulate)
@@ -183,9 +180,11 @@ static void launch_pw(const clskd_conv_desc& d, hipStream_t st) {
   const dim3 grid((unsigned)cdiv(M, 128));
   if (d.out_dtype == CLSKD_BF16) {
     hipLaunchKernelGGL((conv_pointwise_kernel<N, C, __bf16>), grid, dim3(256), 0, st, d);
+    note_kernel_fn((const void*)conv_pointwise_kernel<N, C, __bf16>);
     note_kernel("conv_pointwise_kernel<%d,%d,bf16>", N, C);
   } else {
     hipLaunchKernelGGL((conv_pointwise_kernel<N, C, float>), grid, dim3(256), 0, st, d);
+    note_kernel_fn((const void*)conv_pointwise_kernel<N, C, float>);
     note_kernel("conv_pointwise_kernel<%d,%d,float>", N, C);
   }
 }

@@ -1,0 +1,416 @@
+// Step executor: replays a captured hipGraph of one training / fwd+loss step from C++ on several
+// HIP streams.
+//
+// Why: the C2 step is ~400 launches on four streams.  Launched from Python the host needs 4-5 ms
+// per step for them (descriptor building, allocator calls, ctypes), about the device time, so the
+// step turns host-bound and run-to-run spread follows the host.  hipGraphLaunch of the captured
+// step costs 0.8 ms of host time, but ROCm's graph executor runs the branches one after another
+// (7.3 ms per step against 5.6 ms eager on four streams, measured on MI355X with and without
+// packet capture and forced graph queues).  This executor keeps both: the graph's nodes are
+// re-launched with their captured arguments (hipLaunchKernel: no Python, no descriptor work),
+// distributed over `nstreams` streams along the graph's dependency edges, with one event
+// record / wait per cross-stream edge that is not already implied by an earlier wait (vector
+// clocks, resolved once at creation).  Stream 0 is the caller's stream at launch time: the
+// other streams fork from it at the start and are joined back into it at the end, so a launch
+// is stream-ordered like any other library call.
+//
+// The graph is borrowed: the kernels' captured arguments live in its nodes, and the buffers they
+// point to in the capture's memory pool, so the caller keeps both alive while the executor is
+// used (clskd.graph.StepExecutor owns the torch CUDAGraph for this).
+#include <stdint.h>
+
+#include <algorithm>
+#include <queue>
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+enum OpKind : uint8_t { OP_KERNEL, OP_MEMSET, OP_MEMCPY, OP_WAIT, OP_RECORD };
+
+struct Op {
+  OpKind kind;
+  uint8_t stream;
+  int32_t idx;  // kernel / memset / memcpy slot, or event slot
+};
+
+struct KNode {
+  const void* func;
+  dim3 grid, block;
+  void** args;
+  unsigned shmem;
+};
+
+}  // namespace
+
+struct clskd_exec {
+  hipGraph_t graph = nullptr;
+  int nstreams = 0;
+  std::vector<hipStream_t> own;  // streams 1..nstreams-1 (stream 0 = caller's)
+  std::vector<hipEvent_t> events;
+  std::vector<KNode> kernels;
+  std::vector<hipMemsetParams> memsets;
+  std::vector<hipMemcpy3DParms> memcpys;
+  std::vector<Op> program;
+  int32_t n_nodes = 0, n_waits = 0, n_records = 0, n_empty = 0;
+  int32_t per_stream[8] = {0};
+  // optional live timing of one kernel (bench: the dominant instance): an event pair around
+  // each of its launches, on its stream
+  std::vector<char> timed;  // per kernel slot
+  std::vector<hipEvent_t> tev;
+  int32_t t_used = 0;
+};
+
+using namespace clskd;
+
+static int hip_fail(const char* what, hipError_t e) {
+  set_error("exec: %s: %s", what, hipGetErrorString(e));
+  return CLSKD_E_HIP;
+}
+
+extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, clskd_exec** out) {
+  CLSKD_CHECK_ARG(hip_graph && out, "exec_create: null graph or output");
+  CLSKD_CHECK_ARG(nstreams >= 1 && nstreams <= 8, "exec_create: nstreams %d outside [1, 8]", nstreams);
+  *out = nullptr;
+  hipGraph_t g = reinterpret_cast<hipGraph_t>(hip_graph);
+  size_t n = 0;
+  hipError_t e = hipGraphGetNodes(g, nullptr, &n);
+  if (e != hipSuccess) return hip_fail("hipGraphGetNodes", e);
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n) {
+    e = hipGraphGetNodes(g, nodes.data(), &n);
+    if (e != hipSuccess) return hip_fail("hipGraphGetNodes", e);
+  }
+  std::unordered_map<hipGraphNode_t, int> index;
+  index.reserve(n * 2);
+  for (size_t i = 0; i < n; ++i) index[nodes[i]] = (int)i;
+  size_t ne = 0;
+  e = hipGraphGetEdges(g, nullptr, nullptr, &ne);
+  if (e != hipSuccess) return hip_fail("hipGraphGetEdges", e);
+  std::vector<hipGraphNode_t> from(ne), to(ne);
+  if (ne) {
+    e = hipGraphGetEdges(g, from.data(), to.data(), &ne);
+    if (e != hipSuccess) return hip_fail("hipGraphGetEdges", e);
+  }
+  std::vector<std::vector<int>> preds(n), succs(n);
+  std::vector<int> indeg(n, 0);
+  for (size_t k = 0; k < ne; ++k) {
+    const int a = index.at(from[k]), b = index.at(to[k]);
+    preds[b].push_back(a);
+    succs[a].push_back(b);
+    ++indeg[b];
+  }
+  // topological order, ties broken by node order (the capture order, i.e. the host's enqueue
+  // order, which the schedule was tuned for)
+  std::priority_queue<int, std::vector<int>, std::greater<int>> ready;
+  for (size_t i = 0; i < n; ++i)
+    if (!indeg[i]) ready.push((int)i);
+  std::vector<int> topo;
+  topo.reserve(n);
+  while (!ready.empty()) {
+    const int v = ready.top();
+    ready.pop();
+    topo.push_back(v);
+    for (int s : succs[v])
+      if (--indeg[s] == 0) ready.push(s);
+  }
+  CLSKD_CHECK_ARG(topo.size() == n, "exec_create: graph has a cycle");
+
+  auto* ex = new clskd_exec();
+  ex->graph = g;
+  ex->nstreams = nstreams;
+  ex->n_nodes = (int32_t)n;
+  std::vector<int> type(n, -1), slot(n, -1);
+  for (size_t i = 0; i < n; ++i) {
+    hipGraphNodeType t;
+    e = hipGraphNodeGetType(nodes[i], &t);
+    if (e != hipSuccess) {
+      delete ex;
+      return hip_fail("hipGraphNodeGetType", e);
+    }
+    type[i] = (int)t;
+    if (t == hipGraphNodeTypeKernel) {
+      hipKernelNodeParams p{};
+      e = hipGraphKernelNodeGetParams(nodes[i], &p);
+      if (e != hipSuccess) {
+        delete ex;
+        return hip_fail("hipGraphKernelNodeGetParams", e);
+      }
+      if (!p.func || (p.extra && !p.kernelParams)) {
+        delete ex;
+        set_error("exec_create: kernel node %zu has no host function or uses 'extra' arguments", i);
+        return CLSKD_E_ARG;
+      }
+      slot[i] = (int)ex->kernels.size();
+      ex->kernels.push_back(KNode{p.func, p.gridDim, p.blockDim, p.kernelParams, p.sharedMemBytes});
+    } else if (t == hipGraphNodeTypeMemset) {
+      hipMemsetParams p{};
+      e = hipGraphMemsetNodeGetParams(nodes[i], &p);
+      if (e != hipSuccess) {
+        delete ex;
+        return hip_fail("hipGraphMemsetNodeGetParams", e);
+      }
+      if (!(p.elementSize == 1 || p.elementSize == 2 || p.elementSize == 4) ||
+          (p.height > 1 && p.elementSize != 1)) {
+        delete ex;
+        set_error("exec_create: memset node %zu: element size %u, height %zu not supported", i,
+                  p.elementSize, p.height);
+        return CLSKD_E_ARG;
+      }
+      slot[i] = (int)ex->memsets.size();
+      ex->memsets.push_back(p);
+    } else if (t == hipGraphNodeTypeMemcpy) {
+      hipMemcpy3DParms p{};
+      e = hipGraphMemcpyNodeGetParams(nodes[i], &p);
+      if (e != hipSuccess) {
+        delete ex;
+        return hip_fail("hipGraphMemcpyNodeGetParams", e);
+      }
+      slot[i] = (int)ex->memcpys.size();
+      ex->memcpys.push_back(p);
+    } else if (t == hipGraphNodeTypeEmpty) {
+      ++ex->n_empty;
+    } else {
+      delete ex;
+      set_error("exec_create: node %zu has type %d (only kernel, memset, memcpy and empty nodes "
+                "are replayed)", i, (int)t);
+      return CLSKD_E_ARG;
+    }
+  }
+
+  // real dependencies: an empty node passes its own dependencies through
+  std::vector<std::vector<int>> deps(n);
+  for (int v : topo) {
+    std::vector<int> d;
+    for (int u : preds[v]) {
+      if (type[u] == hipGraphNodeTypeEmpty)
+        d.insert(d.end(), deps[u].begin(), deps[u].end());
+      else
+        d.push_back(u);
+    }
+    std::sort(d.begin(), d.end());
+    d.erase(std::unique(d.begin(), d.end()), d.end());
+    deps[v] = std::move(d);
+  }
+
+  // stream assignment + redundant-wait elimination (vector clocks over topological positions)
+  const int S = nstreams;
+  std::vector<int> pos(n, -1), stream_of(n, -1);
+  for (size_t k = 0; k < topo.size(); ++k) pos[topo[k]] = (int)k;
+  std::vector<int> tail(S, -1);                                  // last node on each stream
+  std::vector<std::vector<int>> clock(S, std::vector<int>(S, -1));  // clock[s][t]: pos known done
+  std::vector<std::vector<int>> nclock(n);
+  std::vector<char> needs_event(n, 0);
+  struct Pending {
+    int v, s;
+    std::vector<int> waits;  // nodes whose events stream s waits for before v
+  };
+  std::vector<Pending> plan;
+  plan.reserve(n);
+  for (int v : topo) {
+    if (type[v] == hipGraphNodeTypeEmpty) continue;
+    int best = -1, bs = -1;
+    for (int s = 0; s < S; ++s)
+      if (tail[s] >= 0 && std::binary_search(deps[v].begin(), deps[v].end(), tail[s]) &&
+          pos[tail[s]] > best) {
+        best = pos[tail[s]];
+        bs = s;
+      }
+    if (bs < 0) {  // no dependency ends a stream: the stream whose work is oldest
+      int oldest = 1 << 30;
+      for (int s = 0; s < S; ++s) {
+        const int p = tail[s] < 0 ? -1 : pos[tail[s]];
+        if (p < oldest) {
+          oldest = p;
+          bs = s;
+        }
+      }
+    }
+    Pending pd{v, bs, {}};
+    std::vector<int>& c = clock[bs];
+    for (int u : deps[v]) {
+      const int su = stream_of[u];
+      if (su == bs || c[su] >= pos[u]) continue;
+      pd.waits.push_back(u);
+      needs_event[u] = 1;
+      const std::vector<int>& cu = nclock[u];
+      for (int t = 0; t < S; ++t) c[t] = std::max(c[t], cu[t]);
+    }
+    c[bs] = pos[v];
+    nclock[v] = c;
+    stream_of[v] = bs;
+    tail[bs] = v;
+    ex->per_stream[bs]++;
+    plan.push_back(std::move(pd));
+  }
+
+  // events: one per node with a cross-stream consumer, plus fork and one join per side stream
+  std::vector<int> ev_of(n, -1);
+  int nev = 0;
+  for (size_t i = 0; i < n; ++i)
+    if (needs_event[i]) ev_of[i] = nev++;
+  const int ev_fork = nev++;
+  const int ev_join0 = nev;
+  nev += S - 1;
+  ex->events.resize(nev, nullptr);
+  for (int k = 0; k < nev; ++k) {
+    e = hipEventCreateWithFlags(&ex->events[k], hipEventDisableTiming);
+    if (e != hipSuccess) {
+      for (int j = 0; j < k; ++j) (void)hipEventDestroy(ex->events[j]);
+      delete ex;
+      return hip_fail("hipEventCreateWithFlags", e);
+    }
+  }
+  ex->own.resize(S > 1 ? S - 1 : 0, nullptr);
+  for (int s = 1; s < S; ++s) {
+    e = hipStreamCreateWithFlags(&ex->own[s - 1], hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      clskd_exec_destroy(ex);
+      return hip_fail("hipStreamCreateWithFlags", e);
+    }
+  }
+  // program: fork, the plan in topological order (waits, the node, its record), join
+  std::vector<char> used(S, 0);
+  for (const Pending& pd : plan) used[pd.s] = 1;
+  if (S > 1) {
+    ex->program.push_back(Op{OP_RECORD, 0, ev_fork});
+    for (int s = 1; s < S; ++s)
+      if (used[s]) ex->program.push_back(Op{OP_WAIT, (uint8_t)s, ev_fork});
+  }
+  for (const Pending& pd : plan) {
+    for (int u : pd.waits) {
+      ex->program.push_back(Op{OP_WAIT, (uint8_t)pd.s, ev_of[u]});
+      ++ex->n_waits;
+    }
+    const int t = type[pd.v];
+    const OpKind k = t == hipGraphNodeTypeKernel ? OP_KERNEL : t == hipGraphNodeTypeMemset ? OP_MEMSET : OP_MEMCPY;
+    ex->program.push_back(Op{k, (uint8_t)pd.s, slot[pd.v]});
+    if (needs_event[pd.v]) {
+      ex->program.push_back(Op{OP_RECORD, (uint8_t)pd.s, ev_of[pd.v]});
+      ++ex->n_records;
+    }
+  }
+  for (int s = 1; s < S; ++s)
+    if (used[s]) {
+      ex->program.push_back(Op{OP_RECORD, (uint8_t)s, ev_join0 + s - 1});
+      ex->program.push_back(Op{OP_WAIT, 0, ev_join0 + s - 1});
+    }
+  *out = ex;
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_exec_launch(clskd_exec* ex, void* stream) {
+  CLSKD_CHECK_ARG(ex, "exec_launch: null executor");
+  hipStream_t st[8];
+  st[0] = as_stream(stream);
+  for (int s = 1; s < ex->nstreams; ++s) st[s] = ex->own[s - 1];
+  for (const Op& op : ex->program) {
+    hipError_t e = hipSuccess;
+    const hipStream_t s = st[op.stream];
+    switch (op.kind) {
+      case OP_KERNEL: {
+        const KNode& k = ex->kernels[op.idx];
+        const bool tm = !ex->timed.empty() && ex->timed[op.idx] && 2 * ex->t_used + 1 < (int)ex->tev.size();
+        if (tm) (void)hipEventRecord(ex->tev[2 * ex->t_used], s);
+        e = hipLaunchKernel(k.func, k.grid, k.block, k.args, k.shmem, s);
+        if (tm) (void)hipEventRecord(ex->tev[2 * ex->t_used++ + 1], s);
+        break;
+      }
+      case OP_MEMSET: {
+        const hipMemsetParams& p = ex->memsets[op.idx];
+        if (p.height > 1)
+          e = hipMemset2DAsync(p.dst, p.pitch, (int)p.value, p.width, p.height, s);
+        else if (p.elementSize == 4)
+          e = hipMemsetD32Async((hipDeviceptr_t)p.dst, (int)p.value, p.width, s);
+        else if (p.elementSize == 2)
+          e = hipMemsetD16Async((hipDeviceptr_t)p.dst, (unsigned short)p.value, p.width, s);
+        else
+          e = hipMemsetD8Async((hipDeviceptr_t)p.dst, (unsigned char)p.value, p.width, s);
+        break;
+      }
+      case OP_MEMCPY:
+        e = hipMemcpy3DAsync(&ex->memcpys[op.idx], s);
+        break;
+      case OP_WAIT:
+        e = hipStreamWaitEvent(s, ex->events[op.idx], 0);
+        break;
+      case OP_RECORD:
+        e = hipEventRecord(ex->events[op.idx], s);
+        break;
+    }
+    if (e != hipSuccess) return hip_fail("launch", e);
+  }
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_exec_info(const clskd_exec* ex, int32_t* info, int32_t n) {
+  CLSKD_CHECK_ARG(ex && info && n >= 8, "exec_info: needs 8 output slots");
+  info[0] = ex->n_nodes;
+  info[1] = (int32_t)ex->kernels.size();
+  info[2] = (int32_t)ex->memsets.size();
+  info[3] = (int32_t)ex->memcpys.size();
+  info[4] = ex->n_empty;
+  info[5] = ex->n_waits;
+  info[6] = ex->n_records;
+  info[7] = (int32_t)ex->program.size();
+  for (int s = 0; s < 8 && 8 + s < n; ++s) info[8 + s] = ex->per_stream[s];
+  return CLSKD_OK;
+}
+
+static void drop_timing(clskd_exec* ex) {
+  for (hipEvent_t ev : ex->tev) (void)hipEventDestroy(ev);
+  ex->tev.clear();
+  ex->timed.clear();
+  ex->t_used = 0;
+}
+
+extern "C" int clskd_exec_profile(clskd_exec* ex, const void* fn, int32_t max_launches) {
+  CLSKD_CHECK_ARG(ex, "exec_profile: null executor");
+  drop_timing(ex);
+  if (!fn || max_launches <= 0) return CLSKD_OK;
+  ex->timed.assign(ex->kernels.size(), 0);
+  int hits = 0;
+  for (size_t i = 0; i < ex->kernels.size(); ++i)
+    if (ex->kernels[i].func == fn) ex->timed[i] = 1, ++hits;
+  if (!hits) {
+    drop_timing(ex);
+    set_error("exec_profile: no kernel node launches that function");
+    return CLSKD_E_ARG;
+  }
+  ex->tev.resize(2 * (size_t)max_launches, nullptr);
+  for (auto& ev : ex->tev) {
+    const hipError_t e = hipEventCreate(&ev);
+    if (e != hipSuccess) {
+      ev = nullptr;
+      drop_timing(ex);
+      return hip_fail("hipEventCreate", e);
+    }
+  }
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_exec_profile_read(clskd_exec* ex, double* total_ms, int32_t* count) {
+  CLSKD_CHECK_ARG(ex && total_ms && count, "exec_profile_read: null argument");
+  double tot = 0;
+  for (int i = 0; i < ex->t_used; ++i) {
+    float ms = 0.f;
+    const hipError_t e = hipEventElapsedTime(&ms, ex->tev[2 * i], ex->tev[2 * i + 1]);
+    if (e != hipSuccess) return hip_fail("hipEventElapsedTime", e);
+    tot += ms;
+  }
+  *total_ms = tot;
+  *count = ex->t_used;
+  return CLSKD_OK;
+}
+
+extern "C" void clskd_exec_destroy(clskd_exec* ex) {
+  if (!ex) return;
+  drop_timing(ex);
+  for (hipEvent_t ev : ex->events)
+    if (ev) (void)hipEventDestroy(ev);
+  for (hipStream_t s : ex->own)
+    if (s) (void)hipStreamDestroy(s);
+  delete ex;
+}

@@ -244,8 +244,7 @@ inline unsigned grid_for(int64_t n) { return (unsigned)std::min<int64_t>(cdiv(n,
 // per split.  The [S][N][K] partials are written once and re-read by wgrad_reduce_kernel, so
 // S trades occupancy against partial traffic.
 inline int wgrad_target() {
-  const char* e = getenv("CLSKD_WGRAD_WG");
-  const int v = e ? atoi(e) : 4096;
+  const int v = knob(KNOB_WGRAD_WG);
   return v >= 64 ? v : 4096;
 }
 inline void wgrad_plan(const clskd_conv_desc& d, int& S, int64_t& rps) {

@@ -452,15 +452,19 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
   // 772 with 8 — twice the reduction work — and 953 with 2, whose 256 weights per lane spill
   // to AGPRs); H = 32 -> 8 (281 ns/step vs 297 / 312 with 4 / 2: a latency-bound chain, more
   // waves hide more of it).  A/B knobs CLSKD_LSTM_NKS (H=128) and CLSKD_LSTM_NKS32 (H=32).
-  static const int nks128 = [] {
-    const char* e = getenv("CLSKD_LSTM_NKS");
-    const int v = e ? atoi(e) : 4;
+  const int nks128 = [] {
+    const int v = knob(KNOB_LSTM_NKS);
     return (v == 2 || v == 8) ? v : 4;
   }();
   // H = 32: CLSKD_LSTM_NKS32 = 2 | 4 | 8 selects the k-sliced multi-wave kernel, 1 (default)
-  // the single-wave kernel (lstm_wave_kernel)
-  const char* e32 = getenv("CLSKD_LSTM_NKS32");
-  const int nks32 = e32 ? atoi(e32) : 1;
+  // the single-wave kernel (lstm_wave_kernel: 245 ns/step against 281 for the 8-slice kernel)
+  const int nks32 = knob(KNOB_LSTM_NKS32);
+  {
+    const int rc = experiment_guard("CLSKD_LSTM32_TDIV", H == 32 ? knob(KNOB_LSTM32_TDIV) : 0);
+    if (rc != CLSKD_OK) return rc;
+    const int rc2 = experiment_guard("CLSKD_LSTM128_TDIV", H == 128 ? knob(KNOB_LSTM128_TDIV) : 0);
+    if (rc2 != CLSKD_OK) return rc2;
+  }
 #define LSTM_LAUNCH(H_, NKS_) \
   hipLaunchKernelGGL((lstm_recurrent_kernel<H_, NKS_>), grid, dim3(NKS_ * H_), 0, st, gx, gx_ws, \
                      gx_seq, gx_t, whh, T, out, o_ws, o_seq, o_t)
@@ -469,7 +473,9 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
       LSTM_LAUNCH(16, 4);
       break;
     case 32:
-      if (const char* td = getenv("CLSKD_LSTM32_TDIV")) T = max(1, T / max(1, atoi(td)));  // timing only
+#ifdef CLSKD_EXPERIMENTS
+      if (const int td = knob(KNOB_LSTM32_TDIV)) T = max(1, T / max(1, td));  // timing only
+#endif
       if (nks32 == 4) LSTM_LAUNCH(32, 4);
       else if (nks32 == 2) LSTM_LAUNCH(32, 2);
       else if (nks32 == 8) LSTM_LAUNCH(32, 8);
@@ -480,8 +486,10 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
       LSTM_LAUNCH(64, 4);
       break;
     case 128:
+#ifdef CLSKD_EXPERIMENTS
       // timing experiment only (wrong results): CLSKD_LSTM128_TDIV = d runs T / d steps
-      if (const char* td = getenv("CLSKD_LSTM128_TDIV")) T = max(1, T / max(1, atoi(td)));
+      if (const int td = knob(KNOB_LSTM128_TDIV)) T = max(1, T / max(1, td));
+#endif
       if (nks128 == 8) LSTM_LAUNCH(128, 8);
       else if (nks128 == 4) LSTM_LAUNCH(128, 4);
       else LSTM_LAUNCH(128, 2);

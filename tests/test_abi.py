@@ -146,3 +146,27 @@ def test_gram_chunk_and_bn_bwd_alignment_validation_without_gpu():
     rc = lib.clskd_bn_bwd(f, f, 1024, 64, f, f, f, f, 1e-5, None, None, f + 8, 16, None, None,
                           None, f, 0, 0, _lib.F32, None)
     assert rc < 0 and b"16-byte aligned" in lib.clskd_last_error()
+
+
+def test_dispatch_knobs_and_experiment_guard_without_gpu():
+    """Dispatch knobs are read once and switched through clskd_set_knob; unknown names are
+    rejected.  The product library has no timing-only modes: selecting one makes the affected
+    entry point fail with CLSKD_E_ARG before any launch instead of computing a wrong result
+    (CLSKD_LSTM*_TDIV / CLSKD_G8 >= 10 / CLSKD_BF16_DEBUG_MODE)."""
+    lib = _lib.load(require_gpu=False)
+    assert lib.clskd_experiments_build() == 0
+    v = ctypes.c_int32(-1)
+    assert lib.clskd_get_knob(b"CLSKD_LSTM_NKS32", ctypes.byref(v)) == 0 and v.value == 1
+    assert lib.clskd_set_knob(b"CLSKD_NO_SUCH_KNOB", 1) == -4
+    assert b"unknown knob" in lib.clskd_last_error()
+    prev = _lib.set_knob("CLSKD_LSTM_NKS32", 8)
+    assert prev == 1 and lib.clskd_get_knob(b"CLSKD_LSTM_NKS32", ctypes.byref(v)) == 0 and v.value == 8
+    _lib.set_knob("CLSKD_LSTM_NKS32", prev)
+    fake = 1 << 20  # 16-byte aligned, never dereferenced
+    for name, H in (("CLSKD_LSTM128_TDIV", 128), ("CLSKD_LSTM32_TDIV", 32)):
+        prev = _lib.set_knob(name, 2)
+        try:
+            rc = lib.clskd_lstm_recurrent(fake, 0, 0, 0, fake, 1, 1, 8, H, fake, 0, 0, 0, None)
+        finally:
+            _lib.set_knob(name, prev)
+        assert rc == -4 and b"CLSKD_EXPERIMENTS" in lib.clskd_last_error(), (name, rc)

@@ -1,0 +1,124 @@
+"""The benched C2 configuration against the CPU oracle at full size.
+
+bench.py runs KnowledgeDistillation.training_step (distill.py:72-148) at B=16 x 64000 samples with
+precision='mixed': the frozen teacher and the ReviewKD fusions on bf16 MFMA operands with bf16
+feature storage, the student in fp32.  This test runs exactly that step and compares it with
+oracle/ref_cpu.clskd_step (fp32 forward, fp64 SPKD Grams — the exact loss of the oracle's
+features):
+
+  * student waveform RMS <= 1e-4 and SI-SNR within 0.01 dB (the student is fp32 end to end);
+  * the MRSTFT base loss within 1e-4 relative;
+  * every bf16 feature tap within the precision contract rho_max (row-wise relative L2 error
+    against the oracle's fp32 feature);
+  * every one of the 14 SPKD terms within the perturbation bound of tests/spkd_bound.py
+    evaluated at the measured row errors (a rigorous bound: Cauchy-Schwarz on the Gram, exact
+    row-L1-normalisation algebra, no linearisation), and within REL_SPKD of the exact term.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from spkd_bound import _gram, row_rel_err, spkd_bound, spkd_term
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+torch.set_num_threads(min(16, os.cpu_count() or 1))
+
+# precision contract of the bf16 feature path: row-wise relative L2 error of a bf16 tap against
+# the fp32 oracle feature (bf16 unit roundoff 2^-9 per rounding, growing with the
+# ~15 layers of bf16 GEMMs between the spectrum and the deepest tap)
+RHO_MAX = 3e-2
+# each SPKD term of the mixed step against the exact (fp64-Gram) term of the oracle's features
+REL_SPKD = 5e-2
+
+
+def _nchw_tap(x):
+    from clskd import ops
+    if isinstance(x, ops.DeferredBN):
+        x = x.materialize()
+    return x.permute(0, 3, 1, 2)
+
+
+@pytest.mark.timeout(600)
+def test_c2_mixed_full_batch_against_oracle():
+    from clskd import config as cfg
+    from clskd.data import synthetic_pairs
+    from clskd.distill import KnowledgeDistillation
+    from clskd.model import DCCRN
+    from clskd.tools_for_loss import si_snr
+    from clskd.weights import ABF_SEED, STUDENT_SEED, TEACHER_SEED, apply_recipe, recipe_state_dict
+    from oracle import ref_cpu as R
+
+    B, L = 16, 64000
+    noisy, clean = synthetic_pairs(B, L, seed=6)
+    teacher = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.TEACHER), TEACHER_SEED)
+    student = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.STUDENT), STUDENT_SEED)
+    kd = KnowledgeDistillation(teacher, student, abf_reinit="once", precision="mixed").to(DEV).train()
+    apply_recipe(kd.review_encoder, ABF_SEED, "encoder.")
+    apply_recipe(kd.review_decoder, ABF_SEED, "decoder.")
+    X, y = torch.from_numpy(noisy).to(DEV), torch.from_numpy(clean).to(DEV)
+    out = kd.training_step((X, y), 0, return_parts=True)
+    torch.cuda.synchronize()
+
+    pt = R.to_torch_params(recipe_state_dict(cfg.dccrn_param_shapes(**cfg.TEACHER), TEACHER_SEED))
+    ps = R.to_torch_params(recipe_state_dict(cfg.dccrn_param_shapes(**cfg.STUDENT), STUDENT_SEED))
+    pa = R.to_torch_params(recipe_state_dict(
+        {**cfg.review_param_shapes("encoder"), **cfg.review_param_shapes("decoder")}, ABF_SEED))
+    with torch.no_grad():
+        ref = R.clskd_step(pt, ps, pa, torch.from_numpy(noisy), torch.from_numpy(clean),
+                           gram_dtype=torch.float64)
+
+    # ---- the student: fp32 end to end
+    wav = out["student_wav"].double().cpu().numpy()
+    rwav = ref["student_wav"].double().numpy()
+    wav_rms = float(np.sqrt(np.mean((wav - rwav) ** 2)))
+    d_sisnr = abs(si_snr(out["student_wav"], y).item()
+                  - R.si_snr(ref["student_wav"], torch.from_numpy(clean)).item())
+    print(f"student waveform RMS {wav_rms:.2e}, SI-SNR delta {d_sisnr:.2e} dB")
+    assert wav_rms <= 1e-4 and d_sisnr <= 0.01
+    assert abs(out["base"].item() - ref["base"].item()) <= 1e-4 * abs(ref["base"].item())
+
+    # ---- the 14 SPKD pairs: (hip student-side, hip teacher-side, oracle student, oracle teacher)
+    tf = out["t"]
+    s_enc, s_dec = out["s_enc"], out["s_dec"]
+    t_taps = ref["t_taps"]
+    hip_t_dec = [tf["dec_in"]] + list(tf["dec"][:5])
+    pairs = []
+    for k in range(6):
+        pairs.append((f"enc{k}", _nchw_tap(s_enc[k]), _nchw_tap(tf["enc"][k]),
+                      ref["s_enc"][k], t_taps["encoder"][k], ref["enc"][k].item(), out["enc"][k].item()))
+    for k in range(6):
+        pairs.append((f"dec{k}", _nchw_tap(s_dec[k]), _nchw_tap(hip_t_dec[k]),
+                      ref["s_dec"][k], t_taps["decoder"][k], ref["dec"][k].item(), out["dec"][k].item()))
+    sr, si = DCCRN.clstm_from_dec_in(out["s"]["dec_in"])
+    tr, ti = DCCRN.clstm_from_dec_in(tf["dec_in"])
+    pairs.append(("clstm_real", sr.transpose(0, 1), tr.transpose(0, 1), ref["s_taps"]["clstm_real"],
+                  t_taps["clstm_real"], ref["clstm_real"].item(), out["clstm_real"].item()))
+    pairs.append(("clstm_img", si.transpose(0, 1), ti.transpose(0, 1), ref["s_taps"]["clstm_img"],
+                  t_taps["clstm_img"], ref["clstm_img"].item(), out["clstm_img"].item()))
+    failures = []
+    for name, hs, ht, rs, rt, exact, got in pairs:
+        hs = hs.float().cpu().numpy()
+        ht = ht.float().cpu().numpy()
+        rs = rs.numpy()
+        rt = rt.numpy()
+        assert hs.shape == rs.shape and ht.shape == rt.shape, (name, hs.shape, rs.shape, ht.shape, rt.shape)
+        rho_s, rho_t = row_rel_err(hs, rs), row_rel_err(ht, rt)
+        Gs, Gt = _gram(rs), _gram(rt)
+        L_exact = spkd_term(Gs, Gt)
+        bnd = spkd_bound(Gs, Gt, rho_s, rho_t)
+        dev = abs(got - L_exact)
+        print(f"{name:10s} exact {L_exact:.6e} oracle-fp64 {exact:.6e} mixed {got:.6e} "
+              f"rel {dev / L_exact:.2e} | rho_s max {rho_s.max():.2e} rho_t max {rho_t.max():.2e} "
+              f"| bound {bnd:.2e} ({bnd / L_exact:.2e} rel)")
+        assert abs(exact - L_exact) <= 1e-6 * L_exact, name  # same exact value, two evaluations
+        if max(rho_s.max(), rho_t.max()) > RHO_MAX:
+            failures.append(f"{name}: feature error {max(rho_s.max(), rho_t.max()):.2e} > {RHO_MAX}")
+        if dev > bnd:
+            failures.append(f"{name}: |mixed - exact| {dev:.3e} above the perturbation bound {bnd:.3e}")
+        if dev > REL_SPKD * L_exact:
+            failures.append(f"{name}: relative deviation {dev / L_exact:.3e} > {REL_SPKD}")
+    assert not failures, failures

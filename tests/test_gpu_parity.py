@@ -110,15 +110,11 @@ def test_conv_direct_coop_last_layer(dt, C1, C2, N, ntap_f, lpr):
     assert ops.direct_ok(N, wp.shape[1])
     out = torch.empty(B, F, T, N, device=DEV, dtype=torch.float32)
     segs = [ops.seg_bftc(x.to(DEV)) for x in segs_h]
-    prev = os.environ.get("CLSKD_DIRECT_COOP")
-    os.environ["CLSKD_DIRECT_COOP"] = "1"  # opt-in dispatch, read per launch
+    prev = _lib.set_knob("CLSKD_DIRECT_COOP", 1)  # opt-in dispatch (library knob)
     try:
         ops.conv(segs, taps, B, F, T, N, wp, bias.to(DEV), out, ops.OutMap(F * T * N, T * N, N))
     finally:
-        if prev is None:
-            del os.environ["CLSKD_DIRECT_COOP"]
-        else:
-            os.environ["CLSKD_DIRECT_COOP"] = prev
+        _lib.set_knob("CLSKD_DIRECT_COOP", prev)
     torch.cuda.synchronize()
     name = _lib.load().clskd_conv_last_kernel().decode()
     assert re.fullmatch(rf"conv_direct_coop_kernel<{N if N > 1 else 2},\d,\w+,float,{lpr},\d>",
@@ -602,12 +598,15 @@ def test_clskd_step_mixed_precision():
     assert abs(out["loss"].item() - ref["loss"].item()) <= 2e-3 * ref["loss"].item()
 
 
-def test_step_graph_matches_eager():
-    """clskd.graph.StepGraph (hipGraph capture of the whole step, two streams) replays bitwise
-    what the eager step computes: loss, SPKD terms, student waveform and BN running statistics,
-    over two different batches; a changed student parameter triggers a re-capture."""
+@pytest.mark.parametrize("launch", ["graph", "exec"])
+def test_step_graph_matches_eager(launch):
+    """clskd.graph.StepGraph (hipGraph capture of the whole step, four streams; replayed by
+    hipGraphLaunch) and clskd.graph.StepExecutor (the same capture replayed by the library's C++
+    multi-stream executor, clskd_exec_launch) reproduce bitwise what the eager step computes:
+    loss, SPKD terms, student waveform and BN running statistics, over two different batches; a
+    changed student parameter triggers a re-capture."""
     from clskd.data import synthetic_pairs
-    from clskd.graph import StepGraph
+    from clskd.graph import StepExecutor, StepGraph
     batches = []
     for seed in (11, 12, 13):
         n, c = synthetic_pairs(4, 32000, seed=seed)
@@ -617,7 +616,11 @@ def test_step_graph_matches_eager():
     for X, y in batches[:2]:
         o = kd_e.training_step((X, y), 0, return_parts=True)
         ref.append((o["loss"].item(), o["spkd"].clone(), o["student_wav"].clone()))
-    g = StepGraph(kd_g, *batches[0])
+    g = (StepGraph if launch == "graph" else StepExecutor)(kd_g, *batches[0])
+    if launch == "exec":
+        print("executor:", g.info)
+        assert g.info["kernels"] > 100 and sum(g.info["per_stream"]) == g.info["nodes"] - g.info["empty"]
+        assert min(g.info["per_stream"]) > 0  # the branches run on all four streams
     for (X, y), (l, sp, wav) in zip(batches[:2], ref):
         assert g(X, y).item() == l
         assert torch.equal(g.out["spkd"], sp)
@@ -632,19 +635,20 @@ def test_step_graph_matches_eager():
     assert g(X, y).item() == l3 and g.captures == 2
 
 
-def test_step_graph_redraws_abf_each_replay():
+@pytest.mark.parametrize("launch", ["graph", "exec"])
+def test_step_graph_redraws_abf_each_replay(launch):
     """abf_reinit='step': the ABF re-initialisation (kaiming_uniform, framework.py:194-195) is
     recorded into the graph and re-drawn on every replay (graph-safe Philox offsets): SPKD
     ReviewKD terms change between replays of the same batch while the student waveform and the
     clstm terms (no ABF on their path) do not."""
     from clskd.data import synthetic_pairs
     from clskd.distill import KnowledgeDistillation
-    from clskd.graph import StepGraph
+    from clskd.graph import StepExecutor, StepGraph
     n, c = synthetic_pairs(4, 32000, seed=21)
     X, y = torch.from_numpy(n).to(DEV), torch.from_numpy(c).to(DEV)
     kd = KnowledgeDistillation(_models("teacher").train(), _models("student").train(),
                                abf_reinit="step", precision="mixed").to(DEV)
-    g = StepGraph(kd, X, y)
+    g = (StepGraph if launch == "graph" else StepExecutor)(kd, X, y)
     outs = []
     for _ in range(2):
         g(X, y)
@@ -759,13 +763,22 @@ def test_conv_gemm8_against_torch(case):
 
 
 @pytest.mark.parametrize("variant", ["1", "8"])
-def test_lstm_recurrence_against_torch(variant, monkeypatch):
+def test_lstm_recurrence_against_torch(variant):
     """Complex-LSTM recurrence (tools_for_model.py:159-174, nn.LSTM gates i, f, g, o, zero
     state) at the student's H = 32: the single-wave kernel (CLSKD_LSTM_NKS32=1, default) and the
     8-slice multi-wave kernel, vs a torch fp64 recurrence on the same gate inputs.  Tolerance
     2e-5 (v_exp / v_rcp gate activations, fp32 state)."""
     from clskd import ops
-    monkeypatch.setenv("CLSKD_LSTM_NKS32", variant)
+    from clskd import _lib
+    prev = _lib.set_knob("CLSKD_LSTM_NKS32", int(variant))
+    try:
+        _lstm_recurrence_check()
+    finally:
+        _lib.set_knob("CLSKD_LSTM_NKS32", prev)
+
+
+def _lstm_recurrence_check():
+    from clskd import ops
     g = torch.Generator().manual_seed(3)
     nws, nseq, T, H = 2, 5, 37, 32
     gx = torch.randn(nseq, T, nws * 4 * H, generator=g)

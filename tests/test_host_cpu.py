@@ -1,0 +1,82 @@
+"""Host-side logic of the Python drop-in layer that needs no GPU: caches and bookkeeping."""
+import gc
+
+import torch
+
+
+class _FakeWeight:
+    """Stands in for a device tensor: same storage address and version for two distinct objects
+    (what the allocator can hand a new model after an old one is freed)."""
+
+    def __init__(self, ptr, version=0):
+        self._ptr, self._version = ptr, version
+
+    def data_ptr(self):
+        return self._ptr
+
+
+def test_tw_cache_rebuilds_for_a_new_source_identity():
+    """backward._tw (transposed-weight cache): a source with the same data_ptr and _version but a
+    new object identity must rebuild (the round-2 stale-entry flake), an in-place update
+    (version bump) must rebuild, the same object must hit; dead sources are swept and the cache
+    is bounded."""
+    from clskd import backward as bw
+    bw._TW.clear()
+    calls = []
+
+    def build(tag):
+        def f():
+            calls.append(tag)
+            return torch.full((2,), float(len(calls)))
+        return f
+
+    key = ("abf", 1234, "conv2")
+    a = _FakeWeight(0x1000)
+    w1 = bw._tw(key, a, build("a"))
+    assert bw._tw(key, a, build("a-again")) is w1 and calls == ["a"]
+    b = _FakeWeight(0x1000)  # same address and version, different object
+    w2 = bw._tw(key, b, build("b"))
+    assert calls == ["a", "b"] and w2 is not w1
+    b._version += 1  # in-place update of the source
+    bw._tw(key, b, build("b-v1"))
+    assert calls[-1] == "b-v1"
+    # dead sources are swept on insert
+    c = _FakeWeight(0x2000)
+    bw._tw(("other", 1), c, build("c"))
+    del c
+    gc.collect()
+    d = _FakeWeight(0x3000)
+    bw._tw(("third", 1), d, build("d"))
+    assert ("other", 1) not in bw._TW
+    # bounded
+    keep = [_FakeWeight(0x4000 + i) for i in range(bw._TW_MAX + 10)]
+    for i, src in enumerate(keep):
+        bw._tw(("many", i), src, lambda: torch.zeros(1))
+    assert len(bw._TW) <= bw._TW_MAX
+    bw._TW.clear()
+
+
+def test_spkd_perturbation_bound_holds():
+    """tests/spkd_bound.py: the bound on an SPKD term's change under row-wise relative feature
+    errors rho holds for random and for aligned (worst-direction) perturbations.  (It is a
+    worst-case bound: for random error directions the observed change is ~sqrt(K) smaller.)"""
+    import numpy as np
+    from spkd_bound import _gram, row_rel_err, spkd_bound, spkd_term
+    rng = np.random.default_rng(0)
+    B, K = 16, 4000
+    for trial in range(20):
+        base = rng.standard_normal(K)
+        zt = np.maximum(0.6 * base + rng.standard_normal((B, K)), 0) + 0.05 * rng.standard_normal((B, K))
+        zs = np.maximum(0.5 * base + rng.standard_normal((B, K)), 0)
+        rho_t = 10 ** rng.uniform(-4, -1.5, B)
+        rho_s = 10 ** rng.uniform(-5, -2, B)
+        L0 = spkd_term(_gram(zs), _gram(zt))
+        for aligned in (False, True):
+            et = rng.standard_normal((B, K)) if not aligned else zt * np.sign(rng.standard_normal((B, 1)))
+            es = rng.standard_normal((B, K)) if not aligned else -zs
+            et *= (rho_t * np.linalg.norm(zt, axis=1) / np.linalg.norm(et, axis=1))[:, None]
+            es *= (rho_s * np.linalg.norm(zs, axis=1) / np.linalg.norm(es, axis=1))[:, None]
+            np.testing.assert_allclose(row_rel_err(zt + et, zt), rho_t, rtol=1e-9)
+            L1 = spkd_term(_gram(zs + es), _gram(zt + et))
+            bnd = spkd_bound(_gram(zs), _gram(zt), rho_s, rho_t)
+            assert abs(L1 - L0) <= bnd, (trial, aligned, abs(L1 - L0), bnd)

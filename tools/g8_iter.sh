@@ -1,4 +1,6 @@
 #!/bin/bash
+# timing-only engine modes need the experiments build: CLSKD_EXPERIMENTS=1 python -m clskd.build (run on the CPU first)
+export CLSKD_LIB=exp
 # conv_gemm8 iteration: engine parity tests (with CLSKD_G8=$TMODE), then the single-layer
 # microbenchmark over the modes in $MODES (CLSKD_G8 = 10*cfg + dbg; 0 = the older engine).
 set -e

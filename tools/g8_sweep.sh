@@ -1,4 +1,6 @@
 #!/bin/bash
+# timing-only engine modes need the experiments build: CLSKD_EXPERIMENTS=1 python -m clskd.build (run on the CPU first)
+export CLSKD_LIB=exp
 # conv_gemm8 configuration / ablation sweep (CLSKD_G8=<cfg*10+dbg>) on the wide teacher layers.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,4 +1,6 @@
 #!/bin/bash
+# timing-only engine modes need the experiments build: CLSKD_EXPERIMENTS=1 python -m clskd.build (run on the CPU first)
+export CLSKD_LIB=exp
 # PMC passes over the conv_gemm8 microbenchmark (one layer, CLSKD_G8 modes in $MODES); each
 # pass its own rocprofv3 run (gfx950 per-block slot limits), kernel-trace only.
 set -e
