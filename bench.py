@@ -35,6 +35,7 @@ METRIC_SPKD = "frames/sec/GPU DCCRN SPKD-output fwd+loss (distill_SPKD.py) @16k 
 B_SPKD = 32  # config C4: batch 32 x 4 s
 PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (f32-in MFMA), dense
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
+PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 B_PER_GPU = 16
 NBATCH = 4
 TRAFFIC_FILE = "r2_pmc_traffic.json"  # written by tools/pmc_traffic.py
@@ -187,10 +188,11 @@ def run_c1(args, dev):
                        gpu_eager_ms=round(float(np.median(eager)) * 1e3, 4),
                        gpu_frames_per_s=round(frames / lat, 1),
                        cpu_ms=round(cpu[usable] * 1e3, 3), cpu_1thread_ms=round(cpu[1] * 1e3, 3),
-                       cpu_frames_per_s=round(frames / cpu[usable], 1),
-                       gpu_over_cpu=round(cpu[usable] / lat, 1),
+                       cpu_frames_per_s=round(frames / min(cpu.values()), 1),
+                       gpu_over_cpu=round(min(cpu.values()) / lat, 1),
                        kernels=cc.info["kernels"], wav_rms_vs_oracle=rms)
     main_leg = legs[16000]
+    best_cpu_ms, best_threads = min((main_leg["cpu_ms"], usable), (main_leg["cpu_1thread_ms"], 1))
     mflop = 7.6e6 * main_leg["frames"]  # SURVEY.md §8 d: 3.79 MMAC/frame
     out = {
         "metric": METRIC_C1, "value": main_leg["gpu_frames_per_s"], "unit": "frames/s",
@@ -207,11 +209,14 @@ def run_c1(args, dev):
                      "traffic": None,
                      "note": "one 1 s clip is ~70 dependent small launches: the forward is bound by "
                              "launch latency and the 163-step LSTM recurrence, not by MFMA or HBM"},
-        "cpu_baseline": {"value": main_leg["cpu_frames_per_s"], "unit": "frames/s", "cores": usable,
+        "cpu_baseline": {"value": round(main_leg["frames"] / (best_cpu_ms * 1e-3), 1),
+                         "unit": "frames/s", "cores": best_threads,
                          "kind": "port", "cpu_model": model, "host_cpus": total,
                          "sample": "oracle/ref_cpu.dccrn_forward(train=False), B=1 x 16000 samples, "
-                                   f"3 warm-ups + median of 10, fp32, {usable} threads "
-                                   f"(1 thread: {main_leg['cpu_1thread_ms']} ms)"},
+                                   f"3 warm-ups + median of 10, fp32; {usable} threads "
+                                   f"{main_leg['cpu_ms']} ms, 1 thread {main_leg['cpu_1thread_ms']} ms "
+                                   "(the faster one is the value: a 1 s clip is too small to "
+                                   "spread over many cores)"},
     }
     print(json.dumps(out))
 
@@ -242,10 +247,15 @@ def main():
     ap.add_argument("--c1", action="store_true",
                     help="config C1: the student's eval forward at batch 1 (16000 and 8000 "
                          "samples) as a latency, GPU (eager and executor) beside the CPU oracle")
-    ap.add_argument("--precision", default="mixed", choices=["mixed", "fp32"],
-                    help="mixed: teacher + ReviewKD GEMMs on bf16 MFMA operands (fp32 accumulate), "
-                         "student fp32; fp32: every GEMM on exact-f32 MFMA")
+    ap.add_argument("--precision", default=None, choices=["mixed", "fp16", "fp32"],
+                    help="mixed (C2/C3 default): teacher + ReviewKD GEMMs on bf16 MFMA operands (fp32 "
+                         "accumulate), student fp32; fp16 (C4 default, --spkd only): the teacher on "
+                         "IEEE-half operands and fp16 storage; fp32: every GEMM on exact-f32 MFMA")
     args = ap.parse_args()
+    if args.precision is None:
+        args.precision = "fp16" if args.spkd else "mixed"
+    if args.precision == "fp16" and not args.spkd:
+        raise SystemExit("--precision fp16 is the C4 (--spkd) teacher mode")
 
     from clskd import dist as cdist
     rank, world, local_rank = cdist.env_rank()
@@ -376,6 +386,26 @@ def main():
         census, census_steps = ktimes, args.steps
     el = cdist.max_over_ranks(el, dev)
     loss_v = float(loss.item())
+    quality = None
+    if not args.train and not args.spkd and args.precision == "mixed":
+        # quality gate of the metric ("SI-SNR parity ±0.01 dB"): the timed step's student
+        # waveform vs the all-fp32 step on the same batch (after the timed region)
+        from clskd.tools_for_loss import si_snr
+        last = (args.steps - 1) % NBATCH
+        src = executor.out if args.launch == "exec" else (graph.out if args.graph else kd.last)
+        wav_m = src["student_wav"].clone()
+        with torch.no_grad():
+            kd.set_precision("fp32")
+            o32 = kd.training_step((Xs[last], Ys[last]), 0, return_parts=True)
+            kd.set_precision(args.precision)
+            s_m = si_snr(wav_m, Ys[last]).item()
+            s_32 = si_snr(o32["student_wav"], Ys[last]).item()
+            wav_rms = float((wav_m - o32["student_wav"]).pow(2).mean().sqrt())
+        quality = dict(si_snr_db=round(s_m, 6), si_snr_fp32_step_db=round(s_32, 6),
+                       si_snr_delta_db=abs(s_m - s_32), student_wav_rms_vs_fp32_step=wav_rms,
+                       loss=round(loss_v, 6), loss_fp32_step=round(float(o32["loss"].item()), 6),
+                       note="timed batch (last step) vs the all-fp32 step on the same batch; the "
+                            "oracle-pinned full-size check is tests/test_gpu_c2_mixed.py")
 
     if rank == 0:
         frames = world * bsz * T * args.steps
@@ -385,8 +415,22 @@ def main():
         conv_total_fl = sum(v[2] for v in census.values())
         avg_ms = ms / n_l
         achieved = flops / n_l / (avg_ms * 1e-3) / 1e12
-        bf16_ops = name.startswith(("conv_igemm_bf16", "conv_halo_kernel", "conv_gemm8"))
-        peak = PEAK_BF16_MFMA_TFLOPS if bf16_ops else PEAK_F32_MFMA_TFLOPS
+        def _peak(kname):
+            # 16-bit MFMA engines (bf16 / f16 operands, fp32 or 16-bit outputs)
+            lowp = kname.startswith(("conv_igemm_bf16", "conv_halo_kernel", "conv_gemm8"))
+            return PEAK_BF16_MFMA_TFLOPS if lowp else PEAK_F32_MFMA_TFLOPS
+
+        def _bytes(kname):  # compulsory bytes per launch (census: input + weights + output once)
+            nb = ops.KernelTimer.nbytes.get(kname)
+            return nb[1] / nb[0] if nb else None
+
+        peak = _peak(name)
+        byt = _bytes(name)
+        # roofline: MFMA-bound when the launch's arithmetic intensity (FLOP per compulsory byte)
+        # is above the ridge peak_flops / HBM peak, HBM-bound below it
+        intensity = flops / n_l / byt if byt else None
+        ridge = peak * 1e12 / (PEAK_HBM_GBPS * 1e9)
+        hbm_bound = intensity is not None and intensity < ridge
         traffic, traffic_src = None, None
         tpath = os.path.join(REPO, "profiles", TRAFFIC_FILE)
         if os.path.exists(tpath) and not args.spkd:  # the PMC passes profile the C2 leg
@@ -394,9 +438,18 @@ def main():
             if tk is not None:
                 traffic = round(tk["hbm_bytes_per_launch"])
                 traffic_src = f"profiles/{TRAFFIC_FILE} (PMC FETCH_SIZE x2 + WRITE_SIZE, per launch)"
-        roof = dict(bound="mfma", kernel=name, achieved=round(achieved, 2),
-                    peak=peak, unit="TFLOP/s",
-                    frac=round(achieved / peak, 4), traffic=traffic, traffic_source=traffic_src,
+        if hbm_bound:
+            ach_bw = byt / (avg_ms * 1e-3) / 1e9
+            roof = dict(bound="hbm", kernel=name, achieved=round(ach_bw, 1), peak=PEAK_HBM_GBPS,
+                        unit="GB/s", frac=round(ach_bw / PEAK_HBM_GBPS, 4),
+                        achieved_tflops=round(achieved, 2))
+        else:
+            roof = dict(bound="mfma", kernel=name, achieved=round(achieved, 2), peak=peak,
+                        unit="TFLOP/s", frac=round(achieved / peak, 4))
+        roof.update(traffic=traffic, traffic_source=traffic_src,
+                    algorithmic_bytes_per_launch=round(byt) if byt else None,
+                    arithmetic_intensity_flop_per_byte=round(intensity, 1) if intensity else None,
+                    ridge_flop_per_byte=round(ridge, 1),
                     launches_per_step=n_l // args.steps, timing=timing,
                     avg_launch_us=round(avg_ms * 1e3, 2),
                     algorithmic_gflop_per_launch=round(flops / n_l / 1e9, 3),
@@ -412,7 +465,11 @@ def main():
                         tflops=round(conv_total_fl / (conv_total_ms * 1e-3) / 1e12, 2),
                         per_kernel={k: dict(launches_per_step=v[0] // census_steps,
                                             avg_us=round(v[1] / v[0] * 1e3, 1),
-                                            tflops=round(v[2] / (v[1] * 1e-3) / 1e12, 1))
+                                            tflops=round(v[2] / (v[1] * 1e-3) / 1e12, 1),
+                                            compulsory_gbps=(round(_bytes(k) * v[0] / (v[1] * 1e-3) / 1e9, 1)
+                                                             if _bytes(k) else None),
+                                            bound=("hbm" if _bytes(k) and v[2] / v[0] / _bytes(k) <
+                                                   _peak(k) * 1e12 / (PEAK_HBM_GBPS * 1e9) else "mfma"))
                                     for k, v in sorted(census.items(), key=lambda kv: -kv[1][1])}))
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not args.train and not args.spkd:
@@ -440,7 +497,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if args.precision == "mixed" else "fp32",
+            "dtype": {"mixed": "bf16", "fp16": "fp16"}.get(args.precision, "fp32"),
             "data": "synthetic (seeded 16 kHz enveloped-sinusoid clean + noise at 0-10 dB SNR; "
                     "recipe weights, SURVEY.md §8 d)",
             "config": {"workload": workload,
@@ -460,10 +517,15 @@ def main():
                        "precision": ("teacher GEMMs bf16 MFMA operands / fp32 accumulate; "
                                      "student, STFT/iSTFT, LSTM recurrence, BN, losses fp32")
                        if (args.spkd and args.precision == "mixed") else
+                                    ("teacher GEMMs fp16 MFMA operands (v_mfma_f32_32x32x16_f16) / "
+                                     "fp32 accumulate, fp16 teacher features; student, STFT/iSTFT, "
+                                     "LSTM recurrence, BN, losses fp32")
+                       if args.precision == "fp16" else
                                     ("teacher+ReviewKD GEMMs bf16 MFMA operands / fp32 accumulate; "
                                      "student, STFT/iSTFT, LSTM recurrence, BN, losses fp32")
                        if args.precision == "mixed" else "fp32 MFMA everywhere"},
             "roofline": roof,
+            "quality": quality,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

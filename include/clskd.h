@@ -33,7 +33,10 @@ typedef enum {
   CLSKD_E_ARG = -4
 } clskd_status;
 
-typedef enum { CLSKD_F32 = 0, CLSKD_BF16 = 1 } clskd_compute;
+/* storage / MFMA operand types.  CLSKD_F16 (IEEE half) is the operand type of configuration C4
+ * (distill_SPKD.py at fp16): the conv engines, BN and STFT-side kernels of a DCCRN forward
+ * take it wherever they take bf16. */
+typedef enum { CLSKD_F32 = 0, CLSKD_BF16 = 1, CLSKD_F16 = 2 } clskd_compute;
 
 const char* clskd_last_error(void);
 int clskd_version(void);
@@ -95,16 +98,16 @@ typedef struct {
   const clskd_ktab_entry* ktab; /* device, K entries */
   const uint8_t* kseg;          /* device, K entries: segment index of each k */
   int32_t vec4;                 /* 1: every aligned group of 4 k's is 4 contiguous channels */
-  const void* weight;  /* device [N][K] packed, fp32 (compute F32) or bf16 (compute BF16) */
+  const void* weight;  /* device [N][K] packed, fp32 (compute F32) or bf16 / f16 (compute BF16 / F16) */
   const float* bias;   /* device [N] or NULL */
   /* output address: out + b*oB + (fo*of_mul+of_add)*oF + to*oT + (n/nlo)*oNhi + (n%nlo)*oNlo */
   void* out;
   int64_t oB, oF, oT, oNhi, oNlo;
   int32_t nlo, of_mul, of_add;
   int32_t compute;   /* clskd_compute: MFMA operand type */
-  int32_t in_dtype;  /* CLSKD_F32 / CLSKD_BF16 storage of every segment (bf16 <=> bf16 compute;
+  int32_t in_dtype;  /* CLSKD_F32 / CLSKD_BF16 / CLSKD_F16 storage of every segment (= compute;
                         bf16 needs segment channel runs of 8 and strides % 8) */
-  int32_t out_dtype; /* CLSKD_F32 / CLSKD_BF16 storage of `out` */
+  int32_t out_dtype; /* CLSKD_F32 / CLSKD_BF16 / CLSKD_F16 storage of `out` (16-bit outs match in_dtype) */
   double* stats;     /* optional fused BatchNorm statistics: per M-block (128 output rows) fp64
                         partials stats[blockIdx.x][N][2] = {sum, sumsq} of the biased outputs,
                         consumed by clskd_bn_finalize (nblk = number of M-blocks) */
@@ -539,13 +542,23 @@ int clskd_spkd_bn_bwd(const void* raw, int32_t dtype, int64_t sB, int64_t P, int
  * arguments on `nstreams` HIP streams along the graph's dependency edges (one event record /
  * wait per cross-stream edge not already implied; resolved once here).  Unlike hipGraphLaunch
  * the independent branches run concurrently.  Stream 0 is the launch stream: the others fork
- * from it and join back into it, so a launch is stream-ordered like any other call.  The graph is
+ * from it and join back into it, so a launch is stream-ordered like any other call.
+ * side_streams (nstreams - 1 hipStream_t, or NULL: the executor creates its own): streams the
+ * caller already uses, so the replay keeps the eager path's hardware-queue mapping (a process has
+ * few hardware queues; streams created later can share one with a busy stream).  The graph is
  * BORROWED: the caller keeps it (its nodes hold the kernels' arguments) and the memory its
  * nodes address alive while the executor exists.
  * info[0..7] = nodes, kernel nodes, memset nodes, memcpy nodes, empty nodes, cross-stream
  * waits, event records, program length; info[8..8+nstreams) = nodes per stream (n >= 8). */
 typedef struct clskd_exec clskd_exec;
-int clskd_exec_create(void* hip_graph, int32_t nstreams, clskd_exec** out);
+int clskd_exec_create(void* hip_graph, int32_t nstreams, void* const* side_streams,
+                      int32_t use_tags, clskd_exec** out);
+/* Capture-time stream tags: during the capture, after each library call the host calls
+ * clskd_exec_tag(stream, index) with the stream the call was issued on; the node(s) that call
+ * added are placed on stream `index` by a later clskd_exec_create(..., use_tags = 1), so the
+ * replay keeps the host's own chains.  clskd_exec_tag_reset clears the tags. */
+int clskd_exec_tag(void* stream, int32_t tag);
+void clskd_exec_tag_reset(void);
 int clskd_exec_launch(clskd_exec* ex, void* stream);
 int clskd_exec_info(const clskd_exec* ex, int32_t* info, int32_t n);
 void clskd_exec_destroy(clskd_exec* ex);
@@ -555,6 +568,52 @@ void clskd_exec_destroy(clskd_exec* ex);
  * synchronize) returns the summed event spans and the number of timed launches. */
 int clskd_exec_profile(clskd_exec* ex, const void* fn, int32_t max_launches);
 int clskd_exec_profile_read(clskd_exec* ex, double* total_ms, int32_t* count);
+
+/* ------------------------------------------------------------------------------------------
+ * Streaming hop (configuration C5): one 6.25 ms hop of the DCCRN eval forward for B streams as
+ * ONE launch (one workgroup per stream).
+ * Replaces: the per-hop launch sequence of the streaming driver — ConvSTFT row
+ * (tools_for_model.py:53-67), encoder (DCCRN.py:171-176), complex LSTMs with carried state
+ * (tools_for_model.py:159-174), decoder with its one-frame look-ahead per layer (DCCRN.py:201-206),
+ * mask 'E' (DCCRN.py:207-226), ConviSTFT row + overlap-add (tools_for_model.py:90-109).
+ * Weights are k-major fp32 copies [K][N] of the packed operands (encoder K order (kf*2+kt, ci);
+ * decoder per parity (tap, [input | skip] channels); LSTM input [K][8H] of both weight sets,
+ * W_hh [2][4H][H]; projections [H][P]); BatchNorm as eval [scale | shift] + PReLU slope.
+ * `state` holds per-stream rings (stride state_stride floats, zero at the start of a stream):
+ * off_* are float offsets inside one stream's state (xwin 400; spectrum [7][514]; encoder output
+ * i [7-i][128>>i][enc_cout[i]]; decoder input [2][D4][C6]; decoder output d [2][2*(D4<<d)][dec_co[d]];
+ * h, c [2 layers][2 ws][2 halves][H]; iSTFT frames [4][400]).  Hop t consumes x_in[b][100]
+ * (live = 1) or zeros (live = 0, drain) and writes wav_out[b][100]: the samples the offline
+ * forward outputs 9 hops earlier (6 decoder look-ahead frames + the 300-sample centring).
+ * Decoder output frames >= zero_from (>= 0) are zeros (the offline decoder's out-of-range frames). */
+typedef struct {
+  const float* stft_w;      /* [400][514] */
+  const float* istft_w;     /* [>=516][400] */
+  const float* window;      /* [400] */
+  const float* enc_w[6];
+  const float* enc_b[6];
+  const float* enc_coef[6]; /* [2*Co] scale | shift */
+  const float* enc_alpha[6];
+  const float* lstm_w[2];   /* [K][8H] */
+  const float* lstm_b[2];   /* [8H] */
+  const float* lstm_whh[2]; /* [2][4H][H] */
+  const float* proj_w[2];   /* [H][P] per half */
+  const float* proj_b[2];
+  const float* dec_w[6][2]; /* per parity */
+  const float* dec_b[6][2];
+  const float* dec_coef[6]; /* d < 5 */
+  const float* dec_alpha[6];
+  float* state;
+  int64_t state_stride;
+  const float* x_in;        /* [B][100] */
+  float* wav_out;           /* [B][100] */
+  int32_t B, t, live, zero_from;
+  int32_t H, D4;
+  int32_t enc_cin[6], enc_cout[6];
+  int32_t dec_ca[6], dec_cb[6], dec_co[6];
+  int32_t off_xwin, off_spec, off_enc[6], off_decin, off_dout[5], off_h, off_c, off_frames;
+} clskd_stream_hop_args;
+int clskd_stream_hop(const clskd_stream_hop_args* a, void* stream);
 
 #ifdef __cplusplus
 }

@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libclskd_hip_exp.so" if os.environ.get("CLSKD_LI
                         else "libclskd_hip.so")
 
 MAX_SEGS = 4
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 WLAYOUT_NK, WLAYOUT_DIRECT = 0, 1
 
 
@@ -60,6 +60,23 @@ class GramBwdJob(C.Structure):
                 ("shift", C.c_void_p), ("coef", C.c_void_p), ("out", C.c_void_p),
                 ("o_sB", C.c_int64), ("o_Ctot", C.c_int32), ("o_c0", C.c_int32),
                 ("accumulate", C.c_int32), ("reserved", C.c_int32)]
+
+
+class StreamHopArgs(C.Structure):
+    _fields_ = [("stft_w", C.c_void_p), ("istft_w", C.c_void_p), ("window", C.c_void_p),
+                ("enc_w", C.c_void_p * 6), ("enc_b", C.c_void_p * 6), ("enc_coef", C.c_void_p * 6),
+                ("enc_alpha", C.c_void_p * 6), ("lstm_w", C.c_void_p * 2), ("lstm_b", C.c_void_p * 2),
+                ("lstm_whh", C.c_void_p * 2), ("proj_w", C.c_void_p * 2), ("proj_b", C.c_void_p * 2),
+                ("dec_w", (C.c_void_p * 2) * 6), ("dec_b", (C.c_void_p * 2) * 6),
+                ("dec_coef", C.c_void_p * 6), ("dec_alpha", C.c_void_p * 6),
+                ("state", C.c_void_p), ("state_stride", C.c_int64), ("x_in", C.c_void_p),
+                ("wav_out", C.c_void_p), ("B", C.c_int32), ("t", C.c_int32), ("live", C.c_int32),
+                ("zero_from", C.c_int32), ("H", C.c_int32), ("D4", C.c_int32),
+                ("enc_cin", C.c_int32 * 6), ("enc_cout", C.c_int32 * 6), ("dec_ca", C.c_int32 * 6),
+                ("dec_cb", C.c_int32 * 6), ("dec_co", C.c_int32 * 6), ("off_xwin", C.c_int32),
+                ("off_spec", C.c_int32), ("off_enc", C.c_int32 * 6), ("off_decin", C.c_int32),
+                ("off_dout", C.c_int32 * 5), ("off_h", C.c_int32), ("off_c", C.c_int32),
+                ("off_frames", C.c_int32)]
 
 
 assert C.sizeof(KtabEntry) == 8
@@ -146,12 +163,15 @@ SIGNATURES = {
                                       C.POINTER(C.c_void_p), C.POINTER(C.c_int32), _i32, _i32,
                                       _i32, _f32, _p, _p]),
     "clskd_gram_bwd": (_i32, [_p, _i32, _i32, _p]),
-    "clskd_exec_create": (_i32, [_p, _i32, C.POINTER(C.c_void_p)]),
+    "clskd_exec_create": (_i32, [_p, _i32, C.POINTER(C.c_void_p), _i32, C.POINTER(C.c_void_p)]),
+    "clskd_exec_tag": (_i32, [_p, _i32]),
+    "clskd_exec_tag_reset": (None, []),
     "clskd_exec_launch": (_i32, [_p, _p]),
     "clskd_exec_info": (_i32, [_p, C.POINTER(C.c_int32), _i32]),
     "clskd_exec_destroy": (None, [_p]),
     "clskd_exec_profile": (_i32, [_p, _p, _i32]),
     "clskd_exec_profile_read": (_i32, [_p, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
+    "clskd_stream_hop": (_i32, [C.POINTER(StreamHopArgs), _p]),
     "clskd_spkd_bn_bwd": (_i32, [_p, _i32, _i64, _i64, _i32, _i32, _p, _p, _p, _p, _p, _f32, _p, _p,
                                  _i32, _p, _p, _p, _i32, _p]),
 }
@@ -201,7 +221,14 @@ def set_knob(name, value):
     return prev.value
 
 
+# capture-time stream tagging (clskd.graph.StepExecutor): a callable run after every library
+# call while a step is being captured
+TAG_HOOK = None
+
+
 def check(rc, what=""):
+    if TAG_HOOK is not None:
+        TAG_HOOK()
     if rc != 0:
         msg = _LIB.clskd_last_error().decode() if _LIB is not None else ""
         raise RuntimeError(f"clskd {what} failed ({rc}): {msg}")

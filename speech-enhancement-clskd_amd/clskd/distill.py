@@ -55,7 +55,7 @@ _TEACHER_FIRST = os.environ.get("CLSKD_TEACHER_FIRST", "1") == "1"
 _RKD_FORK = os.environ.get("CLSKD_RKD_FORK", "1") == "1"
 
 
-_SERIAL = False
+_SERIAL = os.environ.get("CLSKD_SERIAL_STREAMS") == "1"  # diagnostic: the whole step on one stream
 
 
 class serialized_streams:
@@ -484,11 +484,12 @@ class SPKDDistillation(nn.Module):
     def set_precision(self, precision):
         """As KnowledgeDistillation.set_precision: "mixed" runs the frozen teacher (no_grad in
         distill_SPKD.py:75-76; its waveform only feeds the SPKD Gram) on bf16 MFMA operands with
-        fp32 accumulation; the student stays fp32."""
-        if precision not in ("fp32", "mixed"):
+        fp32 accumulation; "fp16" the same on IEEE-half operands and fp16 feature storage
+        (configuration C4 of BASELINE.json: "batch=32 x 4 s fp16"); the student stays fp32."""
+        if precision not in ("fp32", "mixed", "fp16"):
             raise ValueError(precision)
         self.precision = precision
-        self.teacher.compute = "bf16" if precision == "mixed" else "fp32"
+        self.teacher.compute = {"mixed": "bf16", "fp16": "fp16"}.get(precision, "fp32")
         self.student.compute = "fp32"
         return self
 

@@ -17,6 +17,8 @@ Usage::
     loss = step(X_next, y_next)         # copy into the static inputs, replay
     parts = step.out                    # static output dict (overwritten by the next replay)
 """
+import os
+
 import torch
 
 from .distill import KnowledgeDistillation
@@ -59,6 +61,13 @@ class StepGraph:
     def _capture(self):
         self._release()
         dev = self.X.device
+        # the step's side streams exist before any helper stream: HIP hands a process's few
+        # hardware queues (GPU_MAX_HW_QUEUES = 4) to streams in creation order, and the eager
+        # schedule's four streams must not share one (measured: a shared queue serialises two
+        # of the replayed branches, 6.5 vs 5.6 ms per C2 step)
+        from .distill import _side_stream
+        for w in (0, 1, 2):
+            _side_stream(dev, w)
         cur = torch.cuda.current_stream(dev)
         # warm-up populates K tables and packed weights outside the graph; BN running statistics
         # are restored afterwards so capture leaves the model state as it found it
@@ -75,14 +84,21 @@ class StepGraph:
                 b.copy_(v)
         self.graph = None
         g = torch.cuda.CUDAGraph(keep_graph=True) if self.keep_graph else torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.out = self.kd.training_step((self.X, self.y), return_parts=True)
+        self._tagging(True)
+        try:
+            with torch.cuda.graph(g):
+                self.out = self.kd.training_step((self.X, self.y), return_parts=True)
+        finally:
+            self._tagging(False)
         self.graph = g
         self.sig = self._sig()
         self.captures += 1
         self._after_capture()
 
     def _after_capture(self):
+        pass
+
+    def _tagging(self, on):
         pass
 
     def _release(self):
@@ -116,18 +132,49 @@ class StepExecutor(StepGraph):
 
     keep_graph = True
 
-    def __init__(self, kd, X, y, warmup=1, nstreams=4):
+    def __init__(self, kd, X, y, warmup=1, nstreams=None):
+        if nstreams is None:  # diagnostic override: CLSKD_EXEC_STREAMS (1 = serial replay)
+            nstreams = int(os.environ.get("CLSKD_EXEC_STREAMS", "4"))
         self.nstreams = nstreams
         self._ex = None
         super().__init__(kd, X, y, warmup)
 
+    def _tagging(self, on):
+        """While capturing: after every library call report its stream (index 0 = the capture
+        stream, 1/2/3 = the step's student / ReviewKD-encoder / teacher streams) so the
+        executor replays each node on the stream the schedule put it on."""
+        from . import _lib
+        from .distill import _side_stream
+        lib = _lib.load()
+        if not on:
+            _lib.TAG_HOOK = None
+            return
+        lib.clskd_exec_tag_reset()
+        dev = self.X.device
+        idx = {_side_stream(dev, w).cuda_stream: i + 1 for i, w in enumerate((0, 1, 2))}
+        raw = _lib.stream_ptr
+
+        def hook():
+            s = raw()
+            lib.clskd_exec_tag(s, idx.get(s, 0))
+
+        _lib.TAG_HOOK = hook
+
     def _after_capture(self):
         import ctypes as C
         from . import _lib
+        from .distill import _side_stream
         lib = _lib.load()
         h = C.c_void_p()
+        # the step's own side streams (student, ReviewKD-encoder, teacher): same hardware queues
+        dev = self.X.device
+        side = (C.c_void_p * 3)(*[_side_stream(dev, w).cuda_stream for w in (0, 1, 2)])
+        own = os.environ.get("CLSKD_EXEC_OWN_STREAMS") == "1"  # A/B: the executor's own streams
+        tags = os.environ.get("CLSKD_EXEC_TAGS", "1") == "1"  # A/B: capture-time stream tags
         _lib.check(lib.clskd_exec_create(C.c_void_p(self.graph.raw_cuda_graph()), self.nstreams,
-                                         C.byref(h)), "exec_create")
+                                         side if (self.nstreams == 4 and not own) else None,
+                                         1 if tags else 0, C.byref(h)),
+                   "exec_create")
         self._ex = h
         info = (C.c_int32 * 16)()
         _lib.check(lib.clskd_exec_info(h, info, 16), "exec_info")
@@ -183,8 +230,8 @@ class CapturedCall:
             self.out = fn(*self.inputs)
         lib = _lib.load()
         h = C.c_void_p()
-        _lib.check(lib.clskd_exec_create(C.c_void_p(self.graph.raw_cuda_graph()), nstreams,
-                                         C.byref(h)), "exec_create")
+        _lib.check(lib.clskd_exec_create(C.c_void_p(self.graph.raw_cuda_graph()), nstreams, None,
+                                         0, C.byref(h)), "exec_create")
         self._ex = h
         info = (C.c_int32 * 16)()
         _lib.check(lib.clskd_exec_info(h, info, 16), "exec_info")

@@ -198,7 +198,7 @@ class DCCRN(nn.Module):
             self.decoder.append(nn.Sequential(*mods))
         self._wcache = {}
         self._tap_sinks = []
-        # MFMA operand type of the large GEMMs: "fp32" (exact-f32 MFMA) or "bf16" (bf16 operands,
+        # MFMA operand type of the large GEMMs: "fp32" (exact-f32 MFMA), "bf16" / "fp16" (16-bit operands,
         # fp32 accumulation).  STFT/iSTFT framing GEMMs always run fp32.
         self.compute = "fp32"
 
@@ -225,13 +225,13 @@ class DCCRN(nn.Module):
     @staticmethod
     def _cmp(segs, K=None):
         """MFMA operand type of one GEMM = storage type of its input segments."""
-        return "bf16" if segs[0].tensor.dtype == torch.bfloat16 else "fp32"
+        return {torch.bfloat16: "bf16", torch.float16: "fp16"}.get(segs[0].tensor.dtype, "fp32")
 
     @property
     def act_dtype(self):
         """Storage of the BFTC activations: bf16 when the model computes in bf16 (the frozen
         teacher in precision='mixed'), fp32 otherwise."""
-        return torch.bfloat16 if self.compute == "bf16" else torch.float32
+        return {"bf16": torch.bfloat16, "fp16": torch.float16}.get(self.compute, torch.float32)
 
     def _packed(self, key, params, build):
         ent = self._wcache.get(key)

@@ -31,6 +31,7 @@ class KernelTimer:
     records = []
     only = None  # optional kernel-instance name: time just that kernel's launches
     fns = {}  # kernel-instance name -> host function (clskd_exec_profile key)
+    nbytes = {}  # kernel-instance name -> [launches, summed compulsory bytes]
 
     @classmethod
     def start(cls, only=None):
@@ -91,7 +92,7 @@ def direct_weight(wpacked):
         return ent[1]
     N, Kp = wpacked.shape
     NP = direct_np(N)
-    if wpacked.dtype == torch.bfloat16:
+    if wpacked.dtype in (torch.bfloat16, torch.float16):
         wd = wpacked.new_zeros(Kp // 2, NP, 2)
         wd[:, :N, :] = wpacked.view(N, Kp // 2, 2).permute(1, 0, 2)
     else:
@@ -170,28 +171,32 @@ def _ktab(geoms, taps, device_index, bk=BK):
 
 def pack_weight(w, K, compute="fp32"):
     """w: [N, ntaps, Cin] (K order tap-major, channel-minor) -> [N, Kp] contiguous, zero pad.
-    fp32: Kp multiple of 16, float32; bf16: Kp multiple of 64, bfloat16 (RNE)."""
+    fp32: Kp multiple of 16, float32; bf16 / fp16: Kp multiple of 64, bfloat16 / float16 (RNE)."""
     N = w.shape[0]
     w = w.reshape(N, -1).float()
     assert w.shape[1] == K, (w.shape, K)
-    bk = BK_BF16 if compute == "bf16" else BK
+    bk = BK_BF16 if compute in ("bf16", "fp16") else BK
     Kp = -(-K // bk) * bk
     if Kp != K:
         w = torch.cat([w, w.new_zeros(N, Kp - K)], 1)
     if compute == "bf16":
         return w.to(torch.bfloat16).contiguous()
+    if compute == "fp16":
+        return w.to(torch.float16).contiguous()
     # always a fresh, 16-B-aligned tensor: never a view aliasing the parameter storage (which
     # may sit at any offset of a flat parameter buffer, clskd.train.FlatParams)
     return w.clone(memory_format=torch.contiguous_format)
 
 
 def _dt(t):
-    """clskd storage-type code of a tensor (0 = fp32, 1 = bf16)."""
+    """clskd storage-type code of a tensor (0 = fp32, 1 = bf16, 2 = fp16)."""
     if t.dtype == torch.float32:
         return _lib.F32
     if t.dtype == torch.bfloat16:
         return _lib.BF16
-    raise TypeError(f"clskd kernels take float32 or bfloat16 tensors, got {t.dtype}")
+    if t.dtype == torch.float16:
+        return _lib.F16
+    raise TypeError(f"clskd kernels take float32, bfloat16 or float16 tensors, got {t.dtype}")
 
 
 def seg_addr(s):
@@ -223,7 +228,8 @@ def conv_mblocks(B, Fo, To):
 
 class _ConvPlan:
     """Launch descriptor of one conv signature, built once; per call only the pointers change."""
-    __slots__ = ("desc", "segs", "nseg", "direct", "name", "fn", "flops", "shape", "nstats", "osize")
+    __slots__ = ("desc", "segs", "nseg", "direct", "name", "fn", "flops", "bytes", "shape", "nstats",
+                 "osize")
 
 
 _CONV_PLANS = {}
@@ -234,10 +240,11 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
     in_dt = {_dt(s.tensor) for s in segs}
     assert len(in_dt) == 1, "all segments of one conv share a storage type"
     in_dt = in_dt.pop()
-    bf16 = in_dt == _lib.BF16
+    bf16 = in_dt in (_lib.BF16, _lib.F16)  # 16-bit MFMA operands (bf16, or fp16 for C4)
     kt, ks, K, Kp, vec4 = _ktab(geoms, taps, out.device.index or 0, BK_BF16 if bf16 else BK)
     assert wpacked.shape == (N, Kp) and wpacked.is_contiguous(), (wpacked.shape, N, Kp)
-    assert wpacked.dtype == (torch.bfloat16 if bf16 else torch.float32), wpacked.dtype
+    assert wpacked.dtype == {_lib.BF16: torch.bfloat16, _lib.F16: torch.float16}.get(
+        in_dt, torch.float32), wpacked.dtype
     for s in segs:
         if seg_addr(s) % 16 != 0:
             vec4 = False
@@ -266,7 +273,7 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
     d.oB, d.oF, d.oT, d.oNhi, d.oNlo = omap.oB, omap.oF, omap.oT, omap.oNhi, omap.oNlo
     d.nlo = min(omap.nlo, 1 << 30)
     d.of_mul, d.of_add = omap.of_mul, omap.of_add
-    d.compute = _lib.BF16 if bf16 else _lib.F32
+    d.compute = in_dt
     d.in_dtype = in_dt
     d.out_dtype = _dt(out)
     d.kvec = kvec
@@ -286,7 +293,12 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
     pl.name = None  # kernel instance the library dispatches to (read after the first launch)
     pl.fn = None  # its host function (the executor times launches by it)
     pl.flops = 2.0 * B * Fo * To * N * K
-    pl.shape = (B * Fo * To, N, K, "bf16" if bf16 else "f32")
+    # compulsory (algorithmic) bytes of one launch: every input element once, the weights once,
+    # every output element once — the HBM roofline's traffic floor
+    esz = {_lib.BF16: 2, _lib.F16: 2}.get(in_dt, 4)
+    pl.bytes = float(sum(B * g.F * g.T * g.C for g in geoms) * esz + N * K * esz
+                     + B * Fo * To * N * out.element_size())
+    pl.shape = (B * Fo * To, N, K, {_lib.BF16: "bf16", _lib.F16: "f16"}.get(in_dt, "f32"))
     pl.nstats = conv_mblocks(B, Fo, To) * N * 2
     pl.osize = out.element_size()
     _CONV_PLANS[key] = pl
@@ -343,6 +355,9 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
             pl.fn = L.clskd_conv_last_kernel_fn()
         KernelTimer.records.append((pl.name, pl.flops, e0, e1, pl.shape))
         KernelTimer.fns[pl.name] = pl.fn
+        nb = KernelTimer.nbytes.setdefault(pl.name, [0, 0.0])
+        nb[0] += 1
+        nb[1] += pl.bytes
     else:
         check(L.clskd_conv2d_fwd(d, _stream()), "conv2d")
         if pl.name is None:

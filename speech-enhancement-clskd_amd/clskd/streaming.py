@@ -270,3 +270,97 @@ class StreamingDCCRN:
             self._hop(live_in=False, zero_from=T)
             outs.append(self.wav_out.clone())
         return torch.cat(outs, 1)[:, :L]
+
+
+class FusedStreamingDCCRN(StreamingDCCRN):
+    """The same hop as StreamingDCCRN, as ONE launch per hop (clskd_stream_hop,
+    csrc/stream_hop.hip): one workgroup per stream walks the ConvSTFT row, encoder, complex
+    LSTMs, projection, decoder, mask 'E', iSTFT row and overlap-add with each layer's current
+    frame in LDS and the frames the causal convolutions / decoder look-ahead need in per-stream
+    rings.  Same step() / process() contract and latency (9 hops); the ~70-launch hop becomes one
+    launch, so the hop is no longer bound by launch and dependency latency.  Weights are the
+    offline forward's packed fp32 operands transposed k-major (built once; re-create the object
+    after changing the model's parameters)."""
+
+    def __init__(self, model, batch):
+        super().__init__(model, batch, graph=False)
+        m, B, dev = self.m, self.B, self.dev
+        from . import _lib
+        nl, H, D4 = self.nl, self.H, self.D4
+        if nl != 6 or m.hidden_layers != 2:
+            raise NotImplementedError("the fused hop is built for the 6-layer, 2-LSTM DCCRN")
+        kn = m.kernel_num
+        C6 = kn[-1]
+        keep = []
+
+        def kmaj(w):  # packed [N][Kp] -> k-major [Kp][N]
+            t = w.float().t().contiguous()
+            keep.append(t)
+            return t.data_ptr()
+
+        def p(t):
+            keep.append(t)
+            return t.data_ptr()
+
+        a = _lib.StreamHopArgs()
+        a.stft_w = kmaj(m._stft_w())
+        winv, window = m._istft_w()
+        a.istft_w, a.window = kmaj(winv), p(window)
+        for i in range(nl):
+            wp, bias = m._enc_w(i, "fp32")
+            a.enc_w[i], a.enc_b[i] = kmaj(wp), p(bias)
+            a.enc_coef[i], a.enc_alpha[i] = p(self.ebn[i]), p(m.encoder[i][2].weight.detach().float())
+            a.enc_cin[i], a.enc_cout[i] = kn[i], kn[i + 1]
+        for li in range(2):
+            packs = m._lstm_w(li, "fp32")
+            a.lstm_w[li], a.lstm_b[li], a.lstm_whh[li] = kmaj(packs[0]), p(packs[1]), p(packs[2])
+            if li == 1:
+                for half in range(2):
+                    a.proj_w[half], a.proj_b[half] = kmaj(packs[3 + 2 * half]), p(packs[4 + 2 * half])
+        for d in range(nl):
+            for parity in (0, 1):
+                wp, bias = m._dec_w(d, parity, "fp32")
+                a.dec_w[d][parity], a.dec_b[d][parity] = kmaj(wp), p(bias)
+            if d < nl - 1:
+                a.dec_coef[d], a.dec_alpha[d] = p(self.dbn[d]), p(m.decoder[d][2].weight.detach().float())
+            a.dec_ca[d] = C6 if d == 0 else self.Co[d - 1]
+            a.dec_cb[d] = kn[nl - d]
+            a.dec_co[d] = self.Co[d]
+        a.H, a.D4, a.B = H, D4, B
+        # per-stream state layout (floats)
+        off = 0
+
+        def take(n):
+            nonlocal off
+            o = off
+            off += (n + 3) // 4 * 4
+            return o
+
+        a.off_xwin = take(WIN)
+        a.off_spec = take(7 * 514)
+        for i in range(nl):
+            a.off_enc[i] = take((7 - i) * (128 >> i) * kn[i + 1])
+        a.off_decin = take(2 * D4 * C6)
+        for d in range(nl - 1):
+            a.off_dout[d] = take(2 * 2 * self.Fd[d] * self.Co[d])
+        a.off_h = take(2 * 4 * H)
+        a.off_c = take(2 * 4 * H)
+        a.off_frames = take(4 * WIN)
+        a.state_stride = off
+        self.fstate = torch.zeros(B, off, device=dev, dtype=torch.float32)
+        a.state = self.fstate.data_ptr()
+        a.x_in, a.wav_out = self.x_in.data_ptr(), self.wav_out.data_ptr()
+        self._args, self._keep = a, keep
+
+    def _hop(self, live_in=True, zero_from=None):
+        a = self._args
+        a.t, a.live = self.t, int(live_in)
+        a.zero_from = -1 if zero_from is None else int(zero_from)
+        ops.check(ops.lib().clskd_stream_hop(a, ops._stream()), "stream_hop")
+        self.t += 1
+
+    def step(self, x_hop):
+        self.x_in.copy_(x_hop)
+        self._hop()
+        self.steps_run += 1
+        return self.wav_out.clone() if self.t - 1 - LOOKAHEAD >= 3 else None

@@ -20,7 +20,7 @@ void note_kernel_fn(const void* fn);
 enum KnobId {
   KNOB_G8, KNOB_G8_GRID, KNOB_HALO_GRID, KNOB_DIRECT_COOP, KNOB_LSTM_NKS, KNOB_LSTM_NKS32,
   KNOB_WGRAD_WG, KNOB_NO_HALO, KNOB_BF16_WAVES, KNOB_BF16_STAGES, KNOB_BF16_TILE,
-  KNOB_NO_POINTWISE, KNOB_ABF_MOMENT_DIV, KNOB_F32_WAVES,
+  KNOB_NO_POINTWISE, KNOB_ABF_MOMENT_DIV, KNOB_F32_WAVES, KNOB_EXEC_PRIO,
   // timing-only experiment modes (wrong results): -DCLSKD_EXPERIMENTS builds only
   KNOB_LSTM128_TDIV, KNOB_LSTM32_TDIV, KNOB_BF16_DEBUG_MODE,
   KNOB_COUNT
@@ -32,6 +32,11 @@ int experiment_guard(const char* what, int value);
 template <typename T> inline const char* type_name();
 template <> inline const char* type_name<float>() { return "float"; }
 template <> inline const char* type_name<__bf16>() { return "bf16"; }
+template <> inline const char* type_name<_Float16>() { return "f16"; }
+// storage-type code of a 16-bit type (clskd_compute)
+template <typename T> constexpr int lowp_code() { return sizeof(T) == 4 ? CLSKD_F32 : CLSKD_BF16; }
+template <> constexpr int lowp_code<_Float16>() { return CLSKD_F16; }
+inline bool is_lowp(int dt) { return dt == CLSKD_BF16 || dt == CLSKD_F16; }
 
 #define CLSKD_CHECK_ARG(cond, ...)                 \
   do {                                             \
@@ -80,6 +85,12 @@ __device__ __forceinline__ f32x4 load4<__bf16>(const __bf16* p) {
   const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
   return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
+template <>
+__device__ __forceinline__ f32x4 load4<_Float16>(const _Float16* p) {
+  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+  const f16x4 v = *reinterpret_cast<const f16x4*>(p);
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
 template <typename T>
 __device__ __forceinline__ void store4(T* p, f32x4 v);
 template <>
@@ -94,6 +105,21 @@ __device__ __forceinline__ void store4<__bf16>(__bf16* p, f32x4 v) {
   o[2] = (__bf16)v[2];
   o[3] = (__bf16)v[3];
   *reinterpret_cast<bf16x4*>(p) = o;
+}
+
+// one v_mfma_f32_32x32x16 on 16-bit operands held as any 16-byte vector (8 lanes of bf16 or
+// IEEE half bits): InT selects the bf16 or the f16 instruction (same rate on gfx950)
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+template <typename InT, typename V>
+__device__ __forceinline__ f32x16 mfma16(const V& a, const V& b, const f32x16& c) {
+  static_assert(sizeof(V) == 16, "8 x 16-bit operand lanes");
+  if constexpr (__is_same(InT, _Float16))
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a),
+                                                  __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                   __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

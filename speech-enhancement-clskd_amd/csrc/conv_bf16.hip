@@ -457,6 +457,11 @@ int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
     const int rc = launch_conv_gemm8(d, st, &launched);
     if (rc != CLSKD_OK || launched) return rc;
   }
+  // the LDS-DMA engine below is bf16 only: an f16 layer that neither the halo kernel nor the
+  // persistent engine takes is an error, never a silent bf16 computation
+  CLSKD_CHECK_ARG(d.in_dtype == CLSKD_BF16,
+                  "conv2d(f16): N=%d K=%d nseg=%d fits neither the halo kernel nor conv_gemm8", d.N,
+                  d.K, d.nseg);
   const int nw = knob(KNOB_BF16_WAVES) == 4 ? 4 : 8;
   const int stages = knob(KNOB_BF16_STAGES) == 4 ? 4 : 3;  // experiment knob: 3 | 4
   const int tilecfg = knob(KNOB_BF16_TILE);  // A/B knob: 128 | 256 forces one row-tile height

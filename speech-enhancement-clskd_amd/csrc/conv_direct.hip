@@ -35,6 +35,11 @@ template <> struct VecOf<float, 2> { typedef f32x2d T; };
 template <> struct VecOf<__bf16, 8> { typedef bf16x8d T; };
 template <> struct VecOf<__bf16, 4> { typedef __bf16 T __attribute__((ext_vector_type(4))); };
 template <> struct VecOf<__bf16, 2> { typedef __bf16 T __attribute__((ext_vector_type(2))); };
+typedef _Float16 f16x8d __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2d __attribute__((ext_vector_type(2)));
+template <> struct VecOf<_Float16, 8> { typedef f16x8d T; };
+template <> struct VecOf<_Float16, 4> { typedef _Float16 T __attribute__((ext_vector_type(4))); };
+template <> struct VecOf<_Float16, 2> { typedef f16x2d T; };
 
 typedef __bf16 bf16x2d __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4d __attribute__((ext_vector_type(4)));
@@ -45,13 +50,26 @@ typedef const __attribute__((address_space(4))) float* cf32p;
 template <int G, typename InT>
 struct XRun;  // one run of G input channels as loaded
 template <> struct XRun<8, __bf16> { bf16x8d v; };  // 8 bf16 = 4 packed pairs
+template <> struct XRun<8, _Float16> { f16x8d v; };  // 8 IEEE halves = 4 packed pairs
+
+// acc += x[2I] * w.lo + x[2I+1] * w.hi (fp32 accumulate): v_dot2c_f32_bf16 / v_dot2_f32_f16,
+// the weight pair as one 32-bit (SGPR) word
+template <int I, typename V>
+__device__ __forceinline__ float dot2_pair(const V& x, uint32_t wbits, float a) {
+  if constexpr (__is_same(V, f16x8d))
+    return __builtin_amdgcn_fdot2(__builtin_shufflevector(x, x, 2 * I, 2 * I + 1),
+                                  __builtin_bit_cast(f16x2d, wbits), a, false);
+  else
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(x, x, 2 * I, 2 * I + 1),
+                                           __builtin_bit_cast(bf16x2d, wbits), a, false);
+}
 template <> struct XRun<4, float> { f32x4 v; };
 template <> struct XRun<2, float> { f32x2d v; };
 template <> struct XRun<1, float> { float v; };
 
 template <int G, typename InT>
 __device__ __forceinline__ void zero_run(XRun<G, InT>& x) {
-  if constexpr (G == 8) x.v = bf16x8d{};
+  if constexpr (G == 8) x.v = decltype(x.v){};
   else if constexpr (G == 4) x.v = f32x4{0.f, 0.f, 0.f, 0.f};
   else if constexpr (G == 2) x.v = f32x2d{0.f, 0.f};
   else x.v = 0.f;
@@ -117,7 +135,7 @@ __global__ __launch_bounds__(128) void conv_direct_kernel(const DirectArgs args)
       typedef uint32_t u4 __attribute__((ext_vector_type(4)));
       u4 w = __builtin_bit_cast(u4, x.v);
       w = ok ? w : u4{0u, 0u, 0u, 0u};
-      x.v = __builtin_bit_cast(bf16x8d, w);
+      x.v = __builtin_bit_cast(decltype(x.v), w);
     } else if constexpr (G == 1) {
       x.v = ok ? x.v : 0.f;
     } else {
@@ -140,14 +158,10 @@ __global__ __launch_bounds__(128) void conv_direct_kernel(const DirectArgs args)
         // direct layout [K/2][NP] u32 pairs: this run's 4*NP words are contiguous
         const cu32p wp = wrun_u + n;
         float a = acc[n];
-        a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(xc.v, xc.v, 0, 1),
-                                            __builtin_bit_cast(bf16x2d, wp[0]), a, false);
-        a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(xc.v, xc.v, 2, 3),
-                                            __builtin_bit_cast(bf16x2d, wp[NP]), a, false);
-        a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(xc.v, xc.v, 4, 5),
-                                            __builtin_bit_cast(bf16x2d, wp[2 * NP]), a, false);
-        a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(xc.v, xc.v, 6, 7),
-                                            __builtin_bit_cast(bf16x2d, wp[3 * NP]), a, false);
+        a = dot2_pair<0>(xc.v, wp[0], a);
+        a = dot2_pair<1>(xc.v, wp[NP], a);
+        a = dot2_pair<2>(xc.v, wp[2 * NP], a);
+        a = dot2_pair<3>(xc.v, wp[3 * NP], a);
         acc[n] = a;
       } else {
         // direct layout [K][NP] fp32: this run's G*NP weights are contiguous
@@ -322,7 +336,7 @@ __global__ __launch_bounds__(128) void conv_direct_coop_kernel(const DirectArgs 
         typedef uint32_t u4 __attribute__((ext_vector_type(4)));
         u4 wv = __builtin_bit_cast(u4, x[r].v);
         wv = ok ? wv : u4{0u, 0u, 0u, 0u};
-        x[r].v = __builtin_bit_cast(bf16x8d, wv);
+        x[r].v = __builtin_bit_cast(decltype(x[r].v), wv);
       } else if constexpr (G == 1) {
         x[r].v = ok ? x[r].v : 0.f;
       } else {
@@ -339,14 +353,10 @@ __global__ __launch_bounds__(128) void conv_direct_coop_kernel(const DirectArgs 
       for (int n = 0; n < NP; ++n) {
         if constexpr (G == 8) {
           float a = acc[n];
-          a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(x[r].v, x[r].v, 0, 1),
-                                              __builtin_bit_cast(bf16x2d, w[r][0 * NP + n]), a, false);
-          a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(x[r].v, x[r].v, 2, 3),
-                                              __builtin_bit_cast(bf16x2d, w[r][1 * NP + n]), a, false);
-          a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(x[r].v, x[r].v, 4, 5),
-                                              __builtin_bit_cast(bf16x2d, w[r][2 * NP + n]), a, false);
-          a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(x[r].v, x[r].v, 6, 7),
-                                              __builtin_bit_cast(bf16x2d, w[r][3 * NP + n]), a, false);
+          a = dot2_pair<0>(x[r].v, w[r][0 * NP + n], a);
+          a = dot2_pair<1>(x[r].v, w[r][1 * NP + n], a);
+          a = dot2_pair<2>(x[r].v, w[r][2 * NP + n], a);
+          a = dot2_pair<3>(x[r].v, w[r][3 * NP + n], a);
           acc[n] = a;
         } else if constexpr (G == 1) {
           acc[n] = fmaf(x[r].v, __uint_as_float(w[r][n]), acc[n]);
@@ -396,7 +406,11 @@ static void launch_coop_r(const clskd_conv_desc& d, hipStream_t st) {
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
   const size_t lds = (size_t)(d.K / G) * 16;
   DirectArgs a{d};
-  if (d.out_dtype == CLSKD_BF16) {
+  if (d.out_dtype == CLSKD_F16) {
+    hipLaunchKernelGGL((conv_direct_coop_kernel<2, G, InT, _Float16, LPR, R>),
+                       dim3((unsigned)cdiv(M, 128)), dim3(128), lds, st, a);
+    note_kernel_fn((const void*)conv_direct_coop_kernel<2, G, InT, _Float16, LPR, R>);
+  } else if (d.out_dtype == CLSKD_BF16) {
     hipLaunchKernelGGL((conv_direct_coop_kernel<2, G, InT, __bf16, LPR, R>),
                        dim3((unsigned)cdiv(M, 128)), dim3(128), lds, st, a);
     note_kernel_fn((const void*)conv_direct_coop_kernel<2, G, InT, __bf16, LPR, R>);
@@ -406,7 +420,7 @@ static void launch_coop_r(const clskd_conv_desc& d, hipStream_t st) {
     note_kernel_fn((const void*)conv_direct_coop_kernel<2, G, InT, float, LPR, R>);
   }
   note_kernel("conv_direct_coop_kernel<2,%d,%s,%s,%d,%d>", G, type_name<InT>(),
-              d.out_dtype == CLSKD_BF16 ? "bf16" : "float", LPR, R);
+              d.out_dtype == CLSKD_BF16 ? "bf16" : d.out_dtype == CLSKD_F16 ? "f16" : "float", LPR, R);
 }
 
 template <int G, typename InT, int LPR>
@@ -447,7 +461,11 @@ static void launch_np(const clskd_conv_desc& d, hipStream_t st) {
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
   const size_t lds = direct_lds(d, NP, G);
   DirectArgs a{d};
-  if (d.out_dtype == CLSKD_BF16) {
+  if (d.out_dtype == CLSKD_F16) {
+    hipLaunchKernelGGL((conv_direct_kernel<NP, G, InT, _Float16>), dim3((unsigned)cdiv(M, 128)),
+                       dim3(128), lds, st, a);
+    note_kernel_fn((const void*)conv_direct_kernel<NP, G, InT, _Float16>);
+  } else if (d.out_dtype == CLSKD_BF16) {
     hipLaunchKernelGGL((conv_direct_kernel<NP, G, InT, __bf16>), dim3((unsigned)cdiv(M, 128)),
                        dim3(128), lds, st, a);
     note_kernel_fn((const void*)conv_direct_kernel<NP, G, InT, __bf16>);
@@ -457,7 +475,7 @@ static void launch_np(const clskd_conv_desc& d, hipStream_t st) {
     note_kernel_fn((const void*)conv_direct_kernel<NP, G, InT, float>);
   }
   note_kernel("conv_direct_kernel<%d,%d,%s,%s>", NP, G, type_name<InT>(),
-              d.out_dtype == CLSKD_BF16 ? "bf16" : "float");
+              d.out_dtype == CLSKD_BF16 ? "bf16" : d.out_dtype == CLSKD_F16 ? "f16" : "float");
 }
 
 template <int G, typename InT>
@@ -475,7 +493,7 @@ int launch_conv_direct(const clskd_conv_desc& d, hipStream_t st) {
                     d.N, d.K);
   CLSKD_CHECK_ARG(((uintptr_t)d.weight & 15) == 0, "conv2d(direct): weight must be 16-byte aligned");
   int g = d.kvec;
-  if (g == 0) g = d.in_dtype == CLSKD_BF16 ? 8 : (d.vec4 ? 4 : 1);
+  if (g == 0) g = is_lowp(d.in_dtype) ? 8 : (d.vec4 ? 4 : 1);
   CLSKD_CHECK_SHAPE(d.K % g == 0, "conv2d(direct): K=%d not a multiple of kvec %d", d.K, g);
   int lpr = 0, runs = 0;
   const bool coop = coop_lpr(d, g, &lpr, &runs);
@@ -483,6 +501,10 @@ int launch_conv_direct(const clskd_conv_desc& d, hipStream_t st) {
     CLSKD_CHECK_SHAPE(g == 8, "conv2d(direct): bf16 segments need kvec 8");
     if (coop) launch_coop<8, __bf16>(d, lpr, runs, st);
     else launch_g<8, __bf16>(d, st);
+  } else if (d.in_dtype == CLSKD_F16) {
+    CLSKD_CHECK_SHAPE(g == 8, "conv2d(direct): f16 segments need kvec 8");
+    if (coop) launch_coop<8, _Float16>(d, lpr, runs, st);
+    else launch_g<8, _Float16>(d, st);
   } else {
     for (int s = 0; s < d.nseg; ++s) {
       const clskd_seg& sg = d.seg[s];

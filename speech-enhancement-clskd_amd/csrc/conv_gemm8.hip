@@ -106,7 +106,7 @@ struct ConvArgsG8 {
 // 6 = s_setprio 1 around each substep's MFMA cluster, 7 = static priority 1 for waves 4-7, 8 = both;
 // 9 = no DMA wait inside the stream (timing only: DMA latency vs issue cost).
 template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8,
-          int EB = 0>
+          int EB = 0, typename InT = __bf16>
 __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 args) {
   using namespace g8;
   const clskd_conv_desc& d = args.d;
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int jj = 0; jj < FN; ++jj)
-          acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[jj], acc[i][jj], 0, 0, 0);
+          acc[i][jj] = mfma16<InT>(af[i], bfr[jj], acc[i][jj]);
       if constexpr (DBG == 6 || DBG == 8) __builtin_amdgcn_s_setprio(0);
     } else {
 #pragma unroll
@@ -510,7 +510,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
 }
 
 template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8,
-          int EB = 0>
+          int EB = 0, typename InT = __bf16>
 static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   using namespace g8;
   constexpr int SB = (BM + BN) * 2 * BK;
@@ -520,7 +520,7 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
     set_error("conv2d(bf16 g8): K=%d N=%d needs %zu B of LDS", d.K, d.N, lds);
     return CLSKD_E_SHAPE;
   }
-  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG, PF, NWV, EB>;
+  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG, PF, NWV, EB, InT>;
   static bool attr_set = false;  // per instantiation
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -543,8 +543,12 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   ConvArgsG8 a{d, (int)n_mt, (int)ntiles};
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NWV * 64), lds, st, a);
   note_kernel_fn((const void*)kern);
-  note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d>", BM, BN, WM, BK, NS, PHI, type_name<OutT>(), DBG, PF,
-              NWV, EB);
+  if constexpr (__is_same(InT, _Float16))
+    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d,f16>", BM, BN, WM, BK, NS, PHI,
+                type_name<OutT>(), DBG, PF, NWV, EB);
+  else
+    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d>", BM, BN, WM, BK, NS, PHI,
+                type_name<OutT>(), DBG, PF, NWV, EB);
   return CLSKD_OK;
 }
 
@@ -564,7 +568,7 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
   const bool f32 = d.out_dtype == CLSKD_F32;
   *launched = true;
 #ifdef CLSKD_EXPERIMENTS
-  if (mode >= 10 && !f32) {
+  if (mode >= 10 && !f32 && d.in_dtype == CLSKD_BF16) {
     const int cfg = mode / 10, dbg = mode % 10;
 #define G8X(BM_, BN_, WM_, BK_, NS_, PHI_)                                    \
   switch (dbg) {                                                              \
@@ -614,6 +618,13 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
 #endif
   // default: BK 64, two stages, the K-tile boundary before the last substep (EB; 3-5 % on the
   // N = 256 layers against the boundary after it, CLSKD_G8=10)
+  if (d.in_dtype == CLSKD_F16) {  // C4: IEEE-half operands (v_mfma_f32_32x32x16_f16)
+    if (d.N <= 128)
+      return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float, 0, 1, 8, 1, _Float16>(d, st)
+                 : launch_g8<256, 128, 4, 64, 2, 2, _Float16, 0, 1, 8, 1, _Float16>(d, st);
+    return f32 ? launch_g8<256, 256, 2, 64, 2, 2, float, 0, 1, 8, 1, _Float16>(d, st)
+               : launch_g8<256, 256, 2, 64, 2, 2, _Float16, 0, 1, 8, 1, _Float16>(d, st);
+  }
   if (d.N <= 128) {
     return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float, 0, 1, 8, 1>(d, st)
                : launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 1, 8, 1>(d, st);

@@ -95,7 +95,7 @@ __device__ __forceinline__ int64_t vconst64(int64_t v) {
   return v;
 }
 
-template <int BN, typename OutT, int NTAPS>
+template <int BN, typename OutT, int NTAPS, typename InT = __bf16>
 __global__ __launch_bounds__(512) void conv_halo_kernel(const HaloArgs a) {
   constexpr int DBG = 0;
   using namespace halo;
@@ -304,8 +304,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const HaloArgs a) {
           const int q = ((t & 1) * 2 + k16) % NS;
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb)
-            acc[q][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[t & 1][k16], bw[t & 1][k16][nb],
-                                                                  acc[q][nb], 0, 0, 0);
+            acc[q][nb] = mfma16<InT>(af[t & 1][k16], bw[t & 1][k16][nb], acc[q][nb]);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -375,7 +374,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const HaloArgs a) {
 // Plan + eligibility (host).  Returns false (engine path) when the layer does not fit.
 static bool halo_plan(const clskd_conv_desc& d, HaloArgs& a, size_t& lds) {
   using namespace halo;
-  if (d.in_dtype != CLSKD_BF16 || d.N > 64 || d.ntaps < 1 || d.ntaps > 16 || d.stride_t != 1)
+  if (!is_lowp(d.in_dtype) || d.N > 64 || d.ntaps < 1 || d.ntaps > 16 || d.stride_t != 1)
     return false;
   if (d.stride_f < 1 || d.stride_f > 2 || d.ctot < CW) return false;
   a.d = d;
@@ -444,7 +443,7 @@ int launch_conv_halo(const clskd_conv_desc& d, hipStream_t st, bool* launched) {
   size_t lds = 0;
   *launched = false;
   if (halo_plan(d, a, lds)) return launch_halo_planned(a, lds, st, launched);
-  if (d.N <= 32 || d.N > 64 || d.nlo < d.N || d.in_dtype != CLSKD_BF16) return CLSKD_OK;
+  if (d.N <= 32 || d.N > 64 || d.nlo < d.N || !is_lowp(d.in_dtype)) return CLSKD_OK;
   HaloArgs a2;
   size_t lds2 = 0;
   clskd_conv_desc d1 = d, d2 = d;
@@ -483,22 +482,29 @@ static int launch_halo_planned(const HaloArgs& a, size_t lds, hipStream_t st, bo
   const int grid = a.ntiles < ncap ? a.ntiles : ncap;
   if (d.stats && grid > a.nblk128) return CLSKD_OK;  // (never for eligible shapes)
   const bool f32out = d.out_dtype == CLSKD_F32;
-#define HALO_LAUNCH(BN_, O_, NT_)                                                              \
+#define HALO_LAUNCH(BN_, O_, NT_, I_)                                                          \
   do {                                                                                         \
-    auto k = conv_halo_kernel<BN_, O_, NT_>;                                                   \
+    auto k = conv_halo_kernel<BN_, O_, NT_, I_>;                                               \
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,      \
                               160 * 1024);                                                     \
     hipLaunchKernelGGL(k, dim3(grid), dim3(512), lds, st, a);                                  \
     note_kernel_fn((const void*)k);                                                            \
-    note_kernel("conv_halo_kernel<%d,%s,%d>", BN_, type_name<O_>(), NT_);                      \
+    if (__is_same(I_, _Float16))                                                               \
+      note_kernel("conv_halo_kernel<%d,%s,%d,f16>", BN_, type_name<O_>(), NT_);                \
+    else                                                                                       \
+      note_kernel("conv_halo_kernel<%d,%s,%d>", BN_, type_name<O_>(), NT_);                    \
+  } while (0)
+#define HALO_NI(NT_, I_)                                                                       \
+  do {                                                                                         \
+    if (d.N <= 32) {                                                                           \
+      if (f32out) HALO_LAUNCH(32, float, NT_, I_); else HALO_LAUNCH(32, I_, NT_, I_);          \
+    } else {                                                                                   \
+      if (f32out) HALO_LAUNCH(64, float, NT_, I_); else HALO_LAUNCH(64, I_, NT_, I_);          \
+    }                                                                                          \
   } while (0)
 #define HALO_NT(NT_)                                                                           \
   do {                                                                                         \
-    if (d.N <= 32) {                                                                           \
-      if (f32out) HALO_LAUNCH(32, float, NT_); else HALO_LAUNCH(32, __bf16, NT_);              \
-    } else {                                                                                   \
-      if (f32out) HALO_LAUNCH(64, float, NT_); else HALO_LAUNCH(64, __bf16, NT_);              \
-    }                                                                                          \
+    if (d.in_dtype == CLSKD_F16) HALO_NI(NT_, _Float16); else HALO_NI(NT_, __bf16);            \
   } while (0)
   switch (d.ntaps) {
     case 4: HALO_NT(4); break;
@@ -508,6 +514,7 @@ static int launch_halo_planned(const HaloArgs& a, size_t lds, hipStream_t st, bo
     default: return CLSKD_OK;  // not a built tap count: engine path
   }
 #undef HALO_NT
+#undef HALO_NI
 #undef HALO_LAUNCH
   *launched = true;
   return CLSKD_OK;

@@ -324,25 +324,29 @@ using namespace clskd;
 extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
   CLSKD_CHECK_ARG(dp != nullptr, "conv2d: null descriptor");
   const clskd_conv_desc& d = *dp;
-  CLSKD_CHECK_ARG(d.compute == CLSKD_F32 || d.compute == CLSKD_BF16, "conv2d: unknown compute %d",
-                  d.compute);
+  CLSKD_CHECK_ARG(d.compute == CLSKD_F32 || d.compute == CLSKD_BF16 || d.compute == CLSKD_F16,
+                  "conv2d: unknown compute %d", d.compute);
   CLSKD_CHECK_SHAPE(d.B > 0 && d.Fo > 0 && d.To > 0 && d.N > 0 && d.K > 0, "conv2d: empty shape");
-  const int kmul = d.compute == CLSKD_BF16 ? 64 : BK;
+  const bool lowp = is_lowp(d.compute);
+  const int kmul = lowp ? 64 : BK;
   CLSKD_CHECK_SHAPE(d.K % kmul == 0, "conv2d: K=%d must be padded to a multiple of %d", d.K, kmul);
-  CLSKD_CHECK_SHAPE(d.compute != CLSKD_BF16 || d.K <= 8192, "conv2d(bf16): K=%d > 8192", d.K);
-  CLSKD_CHECK_ARG((d.in_dtype == CLSKD_BF16) == (d.compute == CLSKD_BF16),
-                  "conv2d: bf16 MFMA operands come from bf16 activations (in_dtype) only");
-  CLSKD_CHECK_ARG(d.out_dtype == CLSKD_F32 || d.out_dtype == CLSKD_BF16, "conv2d: out_dtype");
+  CLSKD_CHECK_SHAPE(!lowp || d.K <= 8192, "conv2d(bf16/f16): K=%d > 8192", d.K);
+  CLSKD_CHECK_ARG(d.in_dtype == d.compute,
+                  "conv2d: 16-bit MFMA operands come from activations of that type (in_dtype)");
+  CLSKD_CHECK_ARG(d.out_dtype == CLSKD_F32 || d.out_dtype == CLSKD_BF16 || d.out_dtype == CLSKD_F16,
+                  "conv2d: out_dtype");
+  CLSKD_CHECK_ARG(!is_lowp(d.out_dtype) || !lowp || d.out_dtype == d.in_dtype,
+                  "conv2d: a 16-bit output of a 16-bit GEMM has the input's type");
   CLSKD_CHECK_SHAPE(d.nseg >= 1 && d.nseg <= CLSKD_MAX_SEGS, "conv2d: nseg=%d", d.nseg);
   CLSKD_CHECK_ARG(d.weight && d.out && d.ktab && d.kseg, "conv2d: null pointer");
   CLSKD_CHECK_SHAPE(d.nlo >= 1, "conv2d: nlo must be >= 1");
   CLSKD_CHECK_ARG(((uintptr_t)d.weight & 15) == 0, "conv2d: weight must be 16-byte aligned");
   for (int s = 0; s < d.nseg; ++s) CLSKD_CHECK_ARG(d.seg[s].ptr != nullptr, "conv2d: null segment %d", s);
-  if (d.in_dtype == CLSKD_BF16) {
+  if (is_lowp(d.in_dtype)) {
     for (int s = 0; s < d.nseg; ++s) {
       const clskd_seg& g = d.seg[s];
       CLSKD_CHECK_ARG(((uintptr_t)g.ptr & 15) == 0 && g.sB % 8 == 0 && g.sF % 8 == 0 && g.sT % 8 == 0,
-                      "conv2d(bf16): segment %d must be 16-byte aligned with strides %% 8", s);
+                      "conv2d(bf16/f16): segment %d must be 16-byte aligned with strides %% 8", s);
     }
   } else if (d.vec4) {
     for (int s = 0; s < d.nseg; ++s) {
@@ -367,7 +371,7 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
     CLSKD_LAUNCH_CHECK("conv2d_direct");
     return CLSKD_OK;
   }
-  if (d.compute == CLSKD_BF16) {
+  if (lowp) {
     const int rc = launch_conv_bf16(d, st);
     if (rc != CLSKD_OK) return rc;
     CLSKD_LAUNCH_CHECK("conv2d_bf16");
@@ -399,8 +403,12 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
   } while (0)
 #define LAUNCH_NW(BN_, V_, O_) \
   do { if (nw == 8) LAUNCH(BN_, V_, O_, 8); else LAUNCH(BN_, V_, O_, 4); } while (0)
-#define LAUNCH_O(BN_, V_) \
-  do { if (d.out_dtype == CLSKD_BF16) LAUNCH_NW(BN_, V_, __bf16); else LAUNCH_NW(BN_, V_, float); } while (0)
+#define LAUNCH_O(BN_, V_)                                                   \
+  do {                                                                      \
+    if (d.out_dtype == CLSKD_BF16) LAUNCH_NW(BN_, V_, __bf16);              \
+    else if (d.out_dtype == CLSKD_F16) LAUNCH_NW(BN_, V_, _Float16);        \
+    else LAUNCH_NW(BN_, V_, float);                                         \
+  } while (0)
   if (d.N <= 32) {
     if (d.vec4) LAUNCH_O(32, true); else LAUNCH_O(32, false);
   } else if (d.N <= 64) {

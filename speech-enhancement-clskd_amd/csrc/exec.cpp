@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <mutex>
 #include <queue>
 #include <unordered_map>
 #include <vector>
@@ -49,6 +50,7 @@ struct clskd_exec {
   hipGraph_t graph = nullptr;
   int nstreams = 0;
   std::vector<hipStream_t> own;  // streams 1..nstreams-1 (stream 0 = caller's)
+  bool owns_streams = true;      // false: borrowed from the caller (clskd_exec_create)
   std::vector<hipEvent_t> events;
   std::vector<KNode> kernels;
   std::vector<hipMemsetParams> memsets;
@@ -70,7 +72,33 @@ static int hip_fail(const char* what, hipError_t e) {
   return CLSKD_E_HIP;
 }
 
-extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, clskd_exec** out) {
+// Capture-time stream tags: after each library call during a capture, the host reports which
+// of its streams the call ran on; the capture's current dependency set of that stream is then
+// exactly the node(s) just added, which get the tag.  exec_create places tagged nodes on the
+// stream of that index, so the replay keeps the eager schedule's chains (one node per stream
+// position) instead of a reconstructed chain cover.
+static std::mutex g_tag_mu;
+static std::unordered_map<hipGraphNode_t, int> g_tags;
+
+extern "C" void clskd_exec_tag_reset(void) {
+  std::lock_guard<std::mutex> lk(g_tag_mu);
+  g_tags.clear();
+}
+
+extern "C" int clskd_exec_tag(void* stream, int32_t tag) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  const hipGraphNode_t* deps = nullptr;
+  size_t nd = 0;
+  const hipError_t e = hipStreamGetCaptureInfo_v2(as_stream(stream), &st, nullptr, nullptr, &deps, &nd);
+  if (e != hipSuccess) return hip_fail("hipStreamGetCaptureInfo_v2", e);
+  if (st != hipStreamCaptureStatusActive) return CLSKD_OK;
+  std::lock_guard<std::mutex> lk(g_tag_mu);
+  for (size_t i = 0; i < nd; ++i) g_tags.emplace(deps[i], tag);  // first report wins
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, void* const* side_streams,
+                                 int32_t use_tags, clskd_exec** out) {
   CLSKD_CHECK_ARG(hip_graph && out, "exec_create: null graph or output");
   CLSKD_CHECK_ARG(nstreams >= 1 && nstreams <= 8, "exec_create: nstreams %d outside [1, 8]", nstreams);
   *out = nullptr;
@@ -195,6 +223,25 @@ extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, clskd_exec**
     deps[v] = std::move(d);
   }
 
+  // capture-time stream tags (clskd_exec_tag); an untagged node (e.g. the first kernel of a
+  // multi-launch call) inherits the tag of a tagged successor that depends on it directly
+  std::vector<int> tag(n, -1);
+  if (use_tags) {
+    std::lock_guard<std::mutex> lk(g_tag_mu);
+    for (size_t i = 0; i < n; ++i) {
+      auto it = g_tags.find(nodes[i]);
+      if (it != g_tags.end() && it->second >= 0 && it->second < nstreams) tag[i] = it->second;
+    }
+  }
+  for (auto it = topo.rbegin(); it != topo.rend(); ++it) {
+    const int u = *it;
+    if (tag[u] >= 0) continue;
+    for (int v : succs[u])
+      if (tag[v] >= 0) {
+        tag[u] = tag[v];
+        break;
+      }
+  }
   // stream assignment + redundant-wait elimination (vector clocks over topological positions)
   const int S = nstreams;
   std::vector<int> pos(n, -1), stream_of(n, -1);
@@ -211,14 +258,30 @@ extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, clskd_exec**
   plan.reserve(n);
   for (int v : topo) {
     if (type[v] == hipGraphNodeTypeEmpty) continue;
-    int best = -1, bs = -1;
-    for (int s = 0; s < S; ++s)
-      if (tail[s] >= 0 && std::binary_search(deps[v].begin(), deps[v].end(), tail[s]) &&
-          pos[tail[s]] > best) {
-        best = pos[tail[s]];
-        bs = s;
+    // dependency clock of v: per stream, the last position v depends on (directly or not)
+    std::vector<int> dc(S, -1);
+    for (int u : deps[v]) {
+      const std::vector<int>& cu = nclock[u];
+      for (int t = 0; t < S; ++t) dc[t] = std::max(dc[t], cu[t]);
+    }
+    // a stream is free for v when v already depends on all its work (no false serialisation);
+    // among free streams prefer one whose tail is a direct dependency (continue that chain),
+    // the most recent first; with none free, the stream whose work is oldest
+    int bs = tag[v];  // the stream the eager schedule ran it on, when tagged at capture
+    if (bs < 0) {
+      int best = -2;
+      for (int s = 0; s < S; ++s) {
+        const int tp = tail[s] < 0 ? -1 : pos[tail[s]];
+        if (tp > dc[s]) continue;
+        const bool direct = tail[s] >= 0 && std::binary_search(deps[v].begin(), deps[v].end(), tail[s]);
+        const int score = direct ? (1 << 20) + tp : tp;
+        if (score > best) {
+          best = score;
+          bs = s;
+        }
       }
-    if (bs < 0) {  // no dependency ends a stream: the stream whose work is oldest
+    }
+    if (bs < 0) {
       int oldest = 1 << 30;
       for (int s = 0; s < S; ++s) {
         const int p = tail[s] < 0 ? -1 : pos[tail[s]];
@@ -264,8 +327,19 @@ extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, clskd_exec**
     }
   }
   ex->own.resize(S > 1 ? S - 1 : 0, nullptr);
+  ex->owns_streams = side_streams == nullptr;
   for (int s = 1; s < S; ++s) {
-    e = hipStreamCreateWithFlags(&ex->own[s - 1], hipStreamNonBlocking);
+    if (side_streams) {  // the caller's streams: the same hardware-queue mapping as its eager path
+      ex->own[s - 1] = as_stream(side_streams[s - 1]);
+      continue;
+    }
+    // knob CLSKD_EXEC_PRIO: bit s = create stream s at the highest priority (A/B)
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if ((knob(KNOB_EXEC_PRIO) >> s) & 1)
+      e = hipStreamCreateWithPriority(&ex->own[s - 1], hipStreamNonBlocking, hi);
+    else
+      e = hipStreamCreateWithFlags(&ex->own[s - 1], hipStreamNonBlocking);
     if (e != hipSuccess) {
       clskd_exec_destroy(ex);
       return hip_fail("hipStreamCreateWithFlags", e);
@@ -410,7 +484,8 @@ extern "C" void clskd_exec_destroy(clskd_exec* ex) {
   drop_timing(ex);
   for (hipEvent_t ev : ex->events)
     if (ev) (void)hipEventDestroy(ev);
-  for (hipStream_t s : ex->own)
-    if (s) (void)hipStreamDestroy(s);
+  if (ex->owns_streams)
+    for (hipStream_t s : ex->own)
+      if (s) (void)hipStreamDestroy(s);
   delete ex;
 }

@@ -130,6 +130,22 @@ struct Vec8<__bf16> {
   }
 };
 
+template <>
+struct Vec8<_Float16> {
+  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+  __device__ static void load(const _Float16* p, float (&v)[8]) {
+    const f16x8 a = *reinterpret_cast<const f16x8*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)a[j];
+  }
+  __device__ static void store(_Float16* p, const float (&v)[8]) {
+    f16x8 a;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = (_Float16)v[j];
+    *reinterpret_cast<f16x8*>(p) = a;
+  }
+};
+
 // y = x*scale[c] + shift[c] (+ PReLU).  8 channels per thread; with C/8 dividing the grid
 // stride each thread keeps one channel group, so scale/shift stay in registers.
 template <typename T>
@@ -465,11 +481,14 @@ extern "C" int clskd_bn_stats_partial(const void* x, int64_t rows, int32_t C, do
   CLSKD_CHECK_SHAPE(rows > 0 && C >= 4 && C % 4 == 0 && C <= 1024, "bn_stats: bad C=%d", C);
   CLSKD_CHECK_SHAPE(nblk >= 1, "bn_stats: nblk");
   CLSKD_CHECK_ARG(((uintptr_t)x & 15) == 0, "bn_stats: x must be 16-byte aligned");
-  CLSKD_CHECK_ARG(dtype == CLSKD_F32 || dtype == CLSKD_BF16, "bn_stats: dtype");
+  CLSKD_CHECK_ARG(dtype == CLSKD_F32 || dtype == CLSKD_BF16 || dtype == CLSKD_F16, "bn_stats: dtype");
   const int64_t rpb = cdiv(rows, nblk);
   if (dtype == CLSKD_BF16)
     hipLaunchKernelGGL(bn_stats_partial_kernel<__bf16>, dim3(nblk), dim3(256), 0, as_stream(stream),
                        (const __bf16*)x, rows, C, rpb, partial);
+  else if (dtype == CLSKD_F16)
+    hipLaunchKernelGGL(bn_stats_partial_kernel<_Float16>, dim3(nblk), dim3(256), 0, as_stream(stream),
+                       (const _Float16*)x, rows, C, rpb, partial);
   else
     hipLaunchKernelGGL(bn_stats_partial_kernel<float>, dim3(nblk), dim3(256), 0, as_stream(stream),
                        (const float*)x, rows, C, rpb, partial);
@@ -520,7 +539,7 @@ static int bn_apply_impl(const void* x, void* y, int64_t rows, int32_t C, const 
   CLSKD_CHECK_ARG(x && y && scale && shift, "bn_apply: null pointer");
   CLSKD_CHECK_SHAPE(C % 8 == 0 && rows > 0, "bn_apply: C=%d must be a multiple of 8", C);
   CLSKD_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0, "bn_apply: alignment");
-  CLSKD_CHECK_ARG(dtype == CLSKD_F32 || dtype == CLSKD_BF16, "bn_apply: dtype");
+  CLSKD_CHECK_ARG(dtype == CLSKD_F32 || dtype == CLSKD_BF16 || dtype == CLSKD_F16, "bn_apply: dtype");
   const int64_t items = rows * C / 8;
   const int CG = C / 8;
   // grid a multiple of CG-friendly size: 256 threads/block, stride = 256*grid
@@ -529,6 +548,9 @@ static int bn_apply_impl(const void* x, void* y, int64_t rows, int32_t C, const 
   if (dtype == CLSKD_BF16)
     hipLaunchKernelGGL(bn_apply_kernel<__bf16>, dim3((unsigned)g), dim3(256), 0, as_stream(stream),
                        (const __bf16*)x, (__bf16*)y, items, CG, scale, shift, alpha, split);
+  else if (dtype == CLSKD_F16)
+    hipLaunchKernelGGL(bn_apply_kernel<_Float16>, dim3((unsigned)g), dim3(256), 0, as_stream(stream),
+                       (const _Float16*)x, (_Float16*)y, items, CG, scale, shift, alpha, split);
   else
     hipLaunchKernelGGL(bn_apply_kernel<float>, dim3((unsigned)g), dim3(256), 0, as_stream(stream),
                        (const float*)x, (float*)y, items, CG, scale, shift, alpha, split);

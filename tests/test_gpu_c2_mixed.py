@@ -28,11 +28,14 @@ DEV = "cuda"
 torch.set_num_threads(min(16, os.cpu_count() or 1))
 
 # precision contract of the bf16 feature path: row-wise relative L2 error of a bf16 tap against
-# the fp32 oracle feature (bf16 unit roundoff 2^-9 per rounding, growing with the
-# ~15 layers of bf16 GEMMs between the spectrum and the deepest tap)
-RHO_MAX = 3e-2
-# each SPKD term of the mixed step against the exact (fp64-Gram) term of the oracle's features
-REL_SPKD = 5e-2
+# the fp32 oracle feature (bf16 unit roundoff 2^-9 = 2e-3 per rounding, growing
+# with the bf16 GEMMs between the spectrum and the tap; measured on MI355X: student-side
+# (ReviewKD) taps <= 3.9e-3, teacher taps <= 9.2e-3, student clstm taps 5.6e-7 (fp32))
+RHO_MAX = 1.5e-2
+# each SPKD term of the mixed step against the exact (fp64-Gram) term of the oracle's features.
+# Measured <= 1.2e-3 — the size of the reference's OWN fp32 error on these terms (its fp32 Gram
+# over K ~ 2.6M is ~1e-3 off the exact value); 5e-3 leaves a 4x margin.
+REL_SPKD = 5e-3
 
 
 def _nchw_tap(x):

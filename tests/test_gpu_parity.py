@@ -123,7 +123,7 @@ def test_conv_direct_coop_last_layer(dt, C1, C2, N, ntap_f, lpr):
                                rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("dt", ["f32", "bf16", "fp16"])
 @pytest.mark.parametrize("C1,C2,N", [(2, 0, 8), (2, 0, 16), (8, 8, 2), (16, 16, 2), (6, 0, 4),
                                      (6, 2, 3), (3, 0, 1), (1, 0, 16), (2, 0, 32), (3, 0, 32)])
 def test_conv_direct_against_torch_and_engine(dt, C1, C2, N):
@@ -132,11 +132,11 @@ def test_conv_direct_against_torch_and_engine(dt, C1, C2, N):
     MFMA engines on the same descriptor (CLSKD_WLAYOUT_NK).  Tolerance: 1e-5 relative (fp32
     accumulation orders differ)."""
     from clskd import ops
-    if dt == "bf16" and (C1 % 8 or C2 % 8):
-        pytest.skip("bf16 segments need channel runs of 8")
+    if dt != "f32" and (C1 % 8 or C2 % 8):
+        pytest.skip("16-bit segments need channel runs of 8")
     g = torch.Generator().manual_seed(C1 * 100 + C2 * 10 + N)
     B, F, T = 3, 33, 29
-    tdt = torch.bfloat16 if dt == "bf16" else torch.float32
+    tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(dt, torch.float32)
     segs_h = [torch.randn(B, F, T, C1, generator=g).to(tdt)]
     if C2:
         segs_h.append(torch.randn(B, F, T, C2, generator=g).to(tdt))
@@ -147,7 +147,7 @@ def test_conv_direct_against_torch_and_engine(dt, C1, C2, N):
     Fo = (F + 4 - 5) // 2 + 1
     To = T
     wk = w.permute(0, 2, 3, 1).reshape(N, 10, Cin)
-    wp = ops.pack_weight(wk.to(DEV), 10 * Cin, "bf16" if dt == "bf16" else "fp32")
+    wp = ops.pack_weight(wk.to(DEV), 10 * Cin, dt if dt != "f32" else "fp32")
     wq = wp[:, :10 * Cin].float().cpu().reshape(N, 5, 2, Cin).permute(0, 3, 1, 2).double()
     xin = torch.cat([x.double() for x in segs_h], 3).permute(0, 3, 1, 2)
     ref = torch.nn.functional.conv2d(torch.nn.functional.pad(xin, (1, 0, 2, 2)), wq, bias.double(),
@@ -222,8 +222,13 @@ HALO_CASES = {
 }
 
 
+_LP = {"bf16": torch.bfloat16, "fp16": torch.float16}
+_LP_TOL = {"bf16": 8e-3, "fp16": 2e-3}  # 16-bit output rounding (unit roundoff 2^-9 / 2^-12)
+
+
+@pytest.mark.parametrize("lp", ["bf16", "fp16"])
 @pytest.mark.parametrize("case", sorted(HALO_CASES))
-def test_conv_halo_kernel_against_torch(case):
+def test_conv_halo_kernel_against_torch(case, lp):
     """Halo-tiled narrow bf16 conv (weights resident in LDS, input halo reused across taps):
     shapes the dispatcher routes there (N <= 64, channel runs of 32) incl. two segments, stride-2
     F and an interleaved (polyphase) output map, fused BN statistics; vs torch fp64 on the same
@@ -232,12 +237,12 @@ def test_conv_halo_kernel_against_torch(case):
     segc, N, taps, sf, Fi, Fo, of_mul, of_add, out_bf16 = HALO_CASES[case]
     g = torch.Generator().manual_seed(len(case) * 7 + N)
     B, T = 3, 100
-    segs_h = [torch.randn(B, Fi, T, c, generator=g).to(torch.bfloat16) for c in segc]
+    segs_h = [torch.randn(B, Fi, T, c, generator=g).to(_LP[lp]) for c in segc]
     Cin = sum(segc)
     K = len(taps) * Cin
     w = torch.randn(N, len(taps), Cin, generator=g) * 0.05
     bias = torch.randn(N, generator=g)
-    wp = ops.pack_weight(w.to(DEV), K, "bf16")
+    wp = ops.pack_weight(w.to(DEV), K, lp)
     assert not ops.direct_ok(N, wp.shape[1])
     wq = wp[:, :K].float().cpu().double().view(N, len(taps), Cin)
     x = torch.cat([s.double() for s in segs_h], 3)  # [B, Fi, T, Cin]
@@ -252,14 +257,15 @@ def test_conv_halo_kernel_against_torch(case):
             x[:, fi[vf][:, None], tt[vt][None, :]]
         ref += torch.einsum("bftc,nc->bftn", sub, wq[:, ti])
     Fout = Fo * of_mul
-    out = torch.zeros(B, Fout, T, N, device=DEV, dtype=torch.bfloat16 if out_bf16 else torch.float32)
+    out = torch.zeros(B, Fout, T, N, device=DEV, dtype=_LP[lp] if out_bf16 else torch.float32)
     nblk = ops.conv_mblocks(B, Fo, T)
     st = torch.full((nblk * N * 2,), float("nan"), device=DEV, dtype=torch.float64)
     ops.conv([ops.seg_bftc(s.to(DEV)) for s in segs_h], taps, B, Fo, T, N, wp, bias.to(DEV), out,
              ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add), stride_f=sf, stats=st)
-    assert ops.conv_kernel_of_last_launch().startswith("conv_halo_kernel"), ops.conv_kernel_of_last_launch()
+    kname = ops.conv_kernel_of_last_launch()
+    assert kname.startswith("conv_halo_kernel") and (kname.endswith(",f16>") == (lp == "fp16")), kname
     o = out.double().cpu()[:, of_add::of_mul]
-    tol = 8e-3 if out_bf16 else 1e-4
+    tol = _LP_TOL[lp] if out_bf16 else 1e-4
     np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=tol, atol=tol)
     if of_mul > 1:  # the other parity's rows are untouched
         assert torch.all(out.double().cpu()[:, (of_add + 1) % of_mul::of_mul] == 0)
@@ -714,8 +720,9 @@ G8_CASES = {
 }
 
 
+@pytest.mark.parametrize("lp", ["bf16", "fp16"])
 @pytest.mark.parametrize("case", sorted(G8_CASES))
-def test_conv_gemm8_against_torch(case):
+def test_conv_gemm8_against_torch(case, lp):
     """Phase-interleaved 8-wave bf16 GEMM engine (conv_gemm8.hip; N > 64): im2col 5x2 stride-2,
     two-segment polyphase decoder layers with an interleaved output map, ABF 3x3, and pointwise
     layers with 1-3 K-tiles (pipeline prologue/drain edge cases), fused BN statistics, M not a
@@ -725,12 +732,12 @@ def test_conv_gemm8_against_torch(case):
     segc, N, taps, sf, Fi, Fo, of_mul, of_add, out_bf16 = G8_CASES[case]
     g = torch.Generator().manual_seed(len(case) * 13 + N)
     B, T = 3, 97
-    segs_h = [torch.randn(B, Fi, T, c, generator=g).to(torch.bfloat16) for c in segc]
+    segs_h = [torch.randn(B, Fi, T, c, generator=g).to(_LP[lp]) for c in segc]
     Cin = sum(segc)
     K = len(taps) * Cin
     w = torch.randn(N, len(taps), Cin, generator=g) * (0.5 / K ** 0.5)
     bias = torch.randn(N, generator=g)
-    wp = ops.pack_weight(w.to(DEV), K, "bf16")
+    wp = ops.pack_weight(w.to(DEV), K, lp)
     wq = wp[:, :K].float().cpu().double().view(N, len(taps), Cin)
     x = torch.cat([s.double() for s in segs_h], 3)
     ref = bias.double().view(1, 1, 1, N).expand(B, Fo, T, N).clone()
@@ -744,14 +751,15 @@ def test_conv_gemm8_against_torch(case):
             x[:, fi[vf][:, None], tt[vt][None, :]]
         ref += torch.einsum("bftc,nc->bftn", sub, wq[:, ti])
     Fout = Fo * of_mul
-    out = torch.zeros(B, Fout, T, N, device=DEV, dtype=torch.bfloat16 if out_bf16 else torch.float32)
+    out = torch.zeros(B, Fout, T, N, device=DEV, dtype=_LP[lp] if out_bf16 else torch.float32)
     nblk = ops.conv_mblocks(B, Fo, T)
     st = torch.full((nblk * N * 2,), float("nan"), device=DEV, dtype=torch.float64)
     ops.conv([ops.seg_bftc(s.to(DEV)) for s in segs_h], taps, B, Fo, T, N, wp, bias.to(DEV), out,
              ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add), stride_f=sf, stats=st)
-    assert ops.conv_kernel_of_last_launch().startswith("conv_gemm8"), ops.conv_kernel_of_last_launch()
+    kname = ops.conv_kernel_of_last_launch()
+    assert kname.startswith("conv_gemm8") and (kname.endswith(",f16>") == (lp == "fp16")), kname
     o = out.double().cpu()[:, of_add::of_mul]
-    tol = 8e-3 if out_bf16 else 1e-4
+    tol = _LP_TOL[lp] if out_bf16 else 1e-4
     np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=tol, atol=tol)
     if of_mul > 1:
         assert torch.all(out.double().cpu()[:, (of_add + 1) % of_mul::of_mul] == 0)
