@@ -568,6 +568,11 @@ void clskd_exec_destroy(clskd_exec* ex);
  * synchronize) returns the summed event spans and the number of timed launches. */
 int clskd_exec_profile(clskd_exec* ex, const void* fn, int32_t max_launches);
 int clskd_exec_profile_read(clskd_exec* ex, double* total_ms, int32_t* count);
+/* Per-stream milestones (diagnostic): with marks on, every launch records a timing event before
+ * the fork and at each stream's tail; clskd_exec_marks_read (after a synchronize) returns per
+ * stream the mean tail time after the fork in ms over the last <= 64 launches (n >= nstreams). */
+int clskd_exec_marks(clskd_exec* ex, int32_t on);
+int clskd_exec_marks_read(clskd_exec* ex, float* out, int32_t n);
 
 /* ------------------------------------------------------------------------------------------
  * Streaming hop (configuration C5): one 6.25 ms hop of the DCCRN eval forward for B streams as

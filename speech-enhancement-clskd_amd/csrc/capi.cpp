@@ -39,7 +39,8 @@ static const KnobDef kKnobs[KNOB_COUNT] = {
     {"CLSKD_DIRECT_COOP", 0}, {"CLSKD_LSTM_NKS", 4},     {"CLSKD_LSTM_NKS32", 1},
     {"CLSKD_WGRAD_WG", 4096}, {"CLSKD_NO_HALO", 0},      {"CLSKD_BF16_WAVES", 8},
     {"CLSKD_BF16_STAGES", 3}, {"CLSKD_BF16_TILE", 0},    {"CLSKD_NO_POINTWISE", 0},
-    {"CLSKD_ABF_MOMENT_DIV", 1}, {"CLSKD_F32_WAVES", 4}, {"CLSKD_EXEC_PRIO", 0},
+    {"CLSKD_ABF_MOMENT_DIV", 1}, {"CLSKD_F32_WAVES", 4}, {"CLSKD_EXEC_PRIO", 0}, {"CLSKD_EXEC_GATE", 0},
+    {"CLSKD_EXEC_PACE_NS", 0},
     {"CLSKD_LSTM128_TDIV", 0},
     {"CLSKD_LSTM32_TDIV", 0}, {"CLSKD_BF16_DEBUG_MODE", 0},
 };

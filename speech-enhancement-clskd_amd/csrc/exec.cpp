@@ -18,6 +18,7 @@
 // point to in the capture's memory pool, so the caller keeps both alive while the executor is
 // used (clskd.graph.StepExecutor owns the torch CUDAGraph for this).
 #include <stdint.h>
+#include <time.h>
 
 #include <algorithm>
 #include <mutex>
@@ -63,6 +64,11 @@ struct clskd_exec {
   std::vector<char> timed;  // per kernel slot
   std::vector<hipEvent_t> tev;
   int32_t t_used = 0;
+  // optional per-stream milestones: a timing event before the fork and at every stream's tail,
+  // per launch in a ring of MK launches (diagnostic: which branch ends when)
+  static constexpr int MK = 64;
+  std::vector<hipEvent_t> mk;  // [MK][1 + nstreams]
+  int32_t mk_n = 0;
 };
 
 using namespace clskd;
@@ -308,6 +314,21 @@ extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, void* const*
     ex->per_stream[bs]++;
     plan.push_back(std::move(pd));
   }
+  // scheduling gate (knob CLSKD_EXEC_GATE = s*100000 + g*10000 + k, A/B): stream s's first node
+  // additionally waits for the k-th node of stream g — a head start for a critical chain that the
+  // replay, which issues the whole step at once, does not otherwise give it
+  if (const int gate = knob(KNOB_EXEC_GATE)) {
+    const int gs = gate / 100000, gg = (gate / 10000) % 10, gk = gate % 10000;
+    int first = -1, seen = 0, gu = -1;
+    for (size_t i = 0; i < plan.size(); ++i) {
+      if (plan[i].s == gg && gu < 0 && ++seen == gk) gu = plan[i].v;
+      if (plan[i].s == gs && first < 0) first = (int)i;
+    }
+    if (gs < S && gg < S && gs != gg && first >= 0 && gu >= 0 && pos[gu] < pos[plan[first].v]) {
+      plan[first].waits.push_back(gu);
+      needs_event[gu] = 1;
+    }
+  }
 
   // events: one per node with a cross-stream consumer, plus fork and one join per side stream
   std::vector<int> ev_of(n, -1);
@@ -375,11 +396,24 @@ extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, void* const*
   return CLSKD_OK;
 }
 
+static inline void pace(int ns) {  // diagnostic host pacing (knob CLSKD_EXEC_PACE_NS)
+  if (ns <= 0) return;
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  do {
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+  } while ((t1.tv_sec - t0.tv_sec) * 1000000000LL + (t1.tv_nsec - t0.tv_nsec) < ns);
+}
+
 extern "C" int clskd_exec_launch(clskd_exec* ex, void* stream) {
   CLSKD_CHECK_ARG(ex, "exec_launch: null executor");
+  const int pace_ns = knob(KNOB_EXEC_PACE_NS);
   hipStream_t st[8];
   st[0] = as_stream(stream);
   for (int s = 1; s < ex->nstreams; ++s) st[s] = ex->own[s - 1];
+  const int S1 = ex->nstreams + 1;
+  hipEvent_t* mk = ex->mk.empty() ? nullptr : &ex->mk[(size_t)(ex->mk_n % clskd_exec::MK) * S1];
+  if (mk) (void)hipEventRecord(mk[0], st[0]);
   for (const Op& op : ex->program) {
     hipError_t e = hipSuccess;
     const hipStream_t s = st[op.stream];
@@ -390,6 +424,7 @@ extern "C" int clskd_exec_launch(clskd_exec* ex, void* stream) {
         if (tm) (void)hipEventRecord(ex->tev[2 * ex->t_used], s);
         e = hipLaunchKernel(k.func, k.grid, k.block, k.args, k.shmem, s);
         if (tm) (void)hipEventRecord(ex->tev[2 * ex->t_used++ + 1], s);
+        pace(pace_ns);
         break;
       }
       case OP_MEMSET: {
@@ -415,6 +450,41 @@ extern "C" int clskd_exec_launch(clskd_exec* ex, void* stream) {
         break;
     }
     if (e != hipSuccess) return hip_fail("launch", e);
+  }
+  if (mk) {
+    for (int s = ex->nstreams - 1; s >= 0; --s) (void)hipEventRecord(mk[1 + s], st[s]);
+    ++ex->mk_n;
+  }
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_exec_marks(clskd_exec* ex, int32_t on) {
+  CLSKD_CHECK_ARG(ex, "exec_marks: null executor");
+  for (hipEvent_t ev : ex->mk) (void)hipEventDestroy(ev);
+  ex->mk.clear();
+  ex->mk_n = 0;
+  if (!on) return CLSKD_OK;
+  ex->mk.resize((size_t)clskd_exec::MK * (ex->nstreams + 1), nullptr);
+  for (auto& ev : ex->mk) {
+    const hipError_t e = hipEventCreate(&ev);
+    if (e != hipSuccess) return hip_fail("hipEventCreate", e);
+  }
+  return CLSKD_OK;
+}
+
+// out[s] = mean over the recorded launches (at most the last MK) of (tail of stream s - fork), ms
+extern "C" int clskd_exec_marks_read(clskd_exec* ex, float* out, int32_t n) {
+  CLSKD_CHECK_ARG(ex && out && n >= ex->nstreams && !ex->mk.empty(), "exec_marks_read: arguments");
+  const int S1 = ex->nstreams + 1, cnt = ex->mk_n < clskd_exec::MK ? ex->mk_n : clskd_exec::MK;
+  for (int s = 0; s < ex->nstreams; ++s) {
+    double acc = 0;
+    for (int i = 0; i < cnt; ++i) {
+      float ms = 0.f;
+      const hipError_t e = hipEventElapsedTime(&ms, ex->mk[(size_t)i * S1], ex->mk[(size_t)i * S1 + 1 + s]);
+      if (e != hipSuccess) return hip_fail("hipEventElapsedTime", e);
+      acc += ms;
+    }
+    out[s] = cnt ? (float)(acc / cnt) : 0.f;
   }
   return CLSKD_OK;
 }
@@ -482,6 +552,7 @@ extern "C" int clskd_exec_profile_read(clskd_exec* ex, double* total_ms, int32_t
 extern "C" void clskd_exec_destroy(clskd_exec* ex) {
   if (!ex) return;
   drop_timing(ex);
+  for (hipEvent_t ev : ex->mk) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : ex->events)
     if (ev) (void)hipEventDestroy(ev);
   if (ex->owns_streams)

@@ -22,9 +22,11 @@
 namespace clskd {
 namespace shop {
 
-constexpr int NT = 256;    // threads per stream workgroup
-constexpr int MAXR = 8;    // output rows per thread and channel
+constexpr int NT = 512;    // threads per stream workgroup (8 waves: two per SIMD)
+constexpr int MAXR = 4;    // output rows per thread and channel
 constexpr int HOP = 100, WIN = 400, NBIN = 514, LDEST = 516;
+constexpr int WCH = 8192;  // floats per LDS weight chunk (32 KB; two chunks double-buffered)
+constexpr int PER = WCH / 4 / NT;  // float4 loads per thread per chunk
 
 __device__ __forceinline__ int ring(int f, int D) { return ((f % D) + D) % D; }
 
@@ -35,45 +37,94 @@ __device__ __forceinline__ float tanh_f(float x) {
   return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * 2.8853900817779268f));
 }
 
+// Rows [0, K) of a k-major weight matrix Wt [K][N] (fp32; storage padded to whole float4s)
+// stream through LDS in chunks of kc rows (kc * N <= WCH, kc a multiple of 4): chunk c + 1 is
+// loaded into registers (PER float4 per thread, all in flight at once) while chunk c is
+// consumed from LDS, so a hop pays the L2 latency once per 32 KB instead of once per weight.
+// compute(w, k0, kn): w = LDS rows k0 .. k0 + kn - 1 ([kn][N]).  Ends with a barrier.
+template <class F>
+__device__ void wstream(const float* __restrict__ Wt, int K, int N, float* wbuf, F&& compute) {
+  const int tid = threadIdx.x;
+  int kc = (WCH / N) & ~3;
+  if (kc < 4) kc = 4;
+  const int nch = (K + kc - 1) / kc;
+  f32x4 r[PER];
+  auto gload = [&](int c) {
+    const int rows = min(kc, K - c * kc);
+    const int n4 = (rows * N + 3) / 4;
+    const f32x4* src = reinterpret_cast<const f32x4*>(Wt + (size_t)c * kc * N);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = tid + i * NT;
+      r[i] = idx < n4 ? src[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto sstore = [&](int buf) {
+    f32x4* dst = reinterpret_cast<f32x4*>(wbuf + buf * WCH);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) dst[tid + i * NT] = r[i];
+  };
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) gload(c + 1);
+    compute(wbuf + (c & 1) * WCH, c * kc, min(kc, K - c * kc));
+    if (c + 1 < nch) sstore((c + 1) & 1);
+    __syncthreads();
+  }
+}
+
 // out[(fo*of_mul + of_add)][co] = act(bias[co] + sum_taps sum_c Wt[(tap*Ci + c)*Co + co] *
 // win[slot(tap)][fo*sf + dF(tap)][c]) for fo < Fo; win = LDS [2][F][Ci] (slot 0 = older frame);
-// out-of-range input rows read `zrow` (Ci zeros in LDS).  mode 0: none, 1: BN (coef) + PReLU.
+// out-of-range input rows read `zrow` (Ci zeros in LDS).  coef: BN [scale | shift] + PReLU.
 __device__ void conv_layer(const float* win, int F, int Ci, int ntap, const int* tdf, const int* tsl,
                            int sf, int Fo, int Co, int of_mul, int of_add, const float* __restrict__ Wt,
                            const float* __restrict__ bias, const float* __restrict__ coef,
-                           const float* __restrict__ alpha, float* out, const float* zrow, bool zero) {
+                           const float* __restrict__ alpha, float* out, const float* zrow, bool zero,
+                           float* wbuf) {
   const int tid = threadIdx.x;
   const int co = tid % Co, g = tid / Co, G = NT / Co;
   const int R = (Fo + G - 1) / G;
-  if (g >= G) return;
+  const bool act = g < G;
   if (zero) {
-    for (int r = 0; r < R; ++r) {
-      const int fo = g + G * r;
-      if (fo < Fo) out[(fo * of_mul + of_add) * Co + co] = 0.f;
-    }
+    if (act)
+      for (int r = 0; r < R; ++r) {
+        const int fo = g + G * r;
+        if (fo < Fo) out[(fo * of_mul + of_add) * Co + co] = 0.f;
+      }
     return;
   }
-  const float b0 = bias ? bias[co] : 0.f;
+  const float b0 = (act && bias) ? bias[co] : 0.f;
   float acc[MAXR];
 #pragma unroll
   for (int r = 0; r < MAXR; ++r) acc[r] = b0;
-  for (int j = 0; j < ntap; ++j) {
+  wstream(Wt, ntap * Ci, Co, wbuf, [&](const float* w, int k0, int kn) {
+    if (!act) return;
+    int j = k0 / Ci, c = k0 - j * Ci;
     const float* rows[MAXR];
+    auto set_rows = [&]() {
 #pragma unroll
-    for (int r = 0; r < MAXR; ++r) {
-      const int fo = g + G * r;
-      const int fi = fo * sf + tdf[j];
-      rows[r] = (r < R && fo < Fo && fi >= 0 && fi < F) ? win + ((size_t)tsl[j] * F + fi) * Ci : zrow;
-    }
-    const float* wj = Wt + (size_t)j * Ci * Co + co;
-#pragma unroll 4
-    for (int c = 0; c < Ci; ++c) {
-      const float w = wj[(size_t)c * Co];
+      for (int r = 0; r < MAXR; ++r) {
+        const int fo = g + G * r;
+        const int fi = fo * sf + tdf[j];
+        rows[r] = (r < R && fo < Fo && fi >= 0 && fi < F) ? win + ((size_t)tsl[j] * F + fi) * Ci : zrow;
+      }
+    };
+    set_rows();
+    for (int q = 0; q < kn; ++q) {
+      const float wv = w[q * Co + co];
 #pragma unroll
       for (int r = 0; r < MAXR; ++r)
-        if (r < R) acc[r] = fmaf(w, rows[r][c], acc[r]);
+        if (r < R) acc[r] = fmaf(wv, rows[r][c], acc[r]);
+      if (++c == Ci && q + 1 < kn) {
+        c = 0;
+        ++j;
+        set_rows();
+      }
     }
-  }
+  });
+  if (!act) return;
   float sc = 1.f, sh = 0.f, al = 0.f;
   if (coef) {
     sc = coef[co];
@@ -94,16 +145,30 @@ __device__ void conv_layer(const float* win, int F, int Ci, int ntap, const int*
   }
 }
 
-// y[n] = bias[n] + sum_k Wt[k*N + n] x[k] for n < N (x in LDS)
+// y[h][n] = bias[n] + sum_k Wt[k*N + n] x[h*xs + k] for n < N, h < nh (x in LDS)
 __device__ void gemv(const float* __restrict__ Wt, const float* __restrict__ bias, const float* x,
-                     int K, int N, float* y) {
-  for (int n = threadIdx.x; n < N; n += NT) {
-    float a = bias ? bias[n] : 0.f;
-    const float* w = Wt + n;
-#pragma unroll 8
-    for (int k = 0; k < K; ++k) a = fmaf(w[(size_t)k * N], x[k], a);
-    y[n] = a;
+                     int xs, int nh, int K, int N, float* y, int ys, float* wbuf) {
+  const int tid = threadIdx.x;
+  constexpr int MO = 4;  // outputs per thread: (h, n) = q, q + NT, ...
+  float acc[MO];
+  int hh[MO], nn[MO];
+#pragma unroll
+  for (int i = 0; i < MO; ++i) {
+    const int q = tid + i * NT;
+    hh[i] = q / N;
+    nn[i] = q % N;
+    acc[i] = (q < nh * N && bias) ? bias[nn[i]] : 0.f;
   }
+  wstream(Wt, K, N, wbuf, [&](const float* w, int k0, int kn) {
+    for (int kq = 0; kq < kn; ++kq) {
+#pragma unroll
+      for (int i = 0; i < MO; ++i)
+        if (tid + i * NT < nh * N) acc[i] = fmaf(w[kq * N + nn[i]], x[hh[i] * xs + k0 + kq], acc[i]);
+    }
+  });
+#pragma unroll
+  for (int i = 0; i < MO; ++i)
+    if (tid + i * NT < nh * N) y[hh[i] * ys + nn[i]] = acc[i];
 }
 
 }  // namespace shop
@@ -126,6 +191,7 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
   __shared__ float hv[2][2][64], cv[2][2][64], act[2][2][4 * 64], rin[2][64];
   __shared__ float est[LDEST];
   __shared__ float frame[WIN];
+  __shared__ __attribute__((aligned(16))) float wbuf[2 * WCH];  // weight chunks (wstream)
 
   for (int i = tid; i < 256; i += NT) zrow[i] = 0.f;
   // ---- input window: shift by one hop, append the new samples (tools_for_model.py:53-67)
@@ -138,7 +204,7 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
   float* nxt = curB;
   if (a.live) {
     // ---- ConvSTFT row of the newest window -> spectrum ring
-    gemv(a.stft_w, nullptr, xw, WIN, NBIN, spec);
+    gemv(a.stft_w, nullptr, xw, 0, 1, WIN, NBIN, spec, 0, wbuf);
     __syncthreads();
     float* sring = st + a.off_spec;
     for (int i = tid; i < NBIN; i += NT) sring[ring(t, 7) * NBIN + i] = spec[i];
@@ -169,7 +235,7 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
       }
       __syncthreads();
       shop::conv_layer(win, Fi, Ci, 10, enc_tdf, enc_tsl, 2, Fo, Co, 1, 0, a.enc_w[i], a.enc_b[i],
-                       a.enc_coef[i], a.enc_alpha[i], nxt, zrow, false);
+                       a.enc_coef[i], a.enc_alpha[i], nxt, zrow, false, wbuf);
       __syncthreads();
       float* er = st + a.off_enc[i] + (int64_t)ring(t, 7 - i) * Fo * Co;
       for (int q = tid; q < Fo * Co; q += NT) er[q] = nxt[q];
@@ -194,21 +260,19 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
         (&cv[0][0][0])[(q / H) * 64 + q % H] = cs[q];
       }
       __syncthreads();
-      for (int q = tid; q < 2 * 8 * H; q += NT) {  // gx[half][n], n < 8H (both weight sets)
-        const int half = q / (8 * H), n = q % (8 * H);
-        float s = a.lstm_b[li][n];
-        const float* w = a.lstm_w[li] + n;
-        const float* x = xin + half * K;
-#pragma unroll 8
-        for (int k = 0; k < K; ++k) s = fmaf(w[(size_t)k * 8 * H], x[k], s);
-        gx[half][n] = s;
+      // gx[half][n] (n < 8H: both weight sets side by side)
+      gemv(a.lstm_w[li], a.lstm_b[li], xin, K, 2, K, 8 * H, &gx[0][0], 8 * 64, wbuf);
+      // W_hh [2][4H][H] into LDS (one chunk)
+      {
+        const f32x4* src = reinterpret_cast<const f32x4*>(a.lstm_whh[li]);
+        for (int q = tid; q < 2 * G4 * H / 4; q += NT) reinterpret_cast<f32x4*>(wbuf)[q] = src[q];
       }
       __syncthreads();
       // gates (ws, half, g) as clskd_lstm_cell: a = gx + W_hh[ws][g] . h[ws][half]
       for (int q = tid; q < 2 * 2 * G4; q += NT) {
         const int ws = q / (2 * G4), half = (q / G4) % 2, gg = q % G4;
         float s = gx[half][ws * G4 + gg];
-        const float* w = a.lstm_whh[li] + ((int64_t)ws * G4 + gg) * H;
+        const float* w = wbuf + (ws * G4 + gg) * H;
         for (int j = 0; j < H; ++j) s = fmaf(w[j], hv[ws][half][j], s);
         act[ws][half][gg] = (gg / H) == 2 ? fmaf(2.f, sigm(2.f * s), -1.f) : sigm(s);
       }
@@ -231,12 +295,13 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
       __syncthreads();
     }
     // projection (NavieComplexLSTM r_trans / i_trans): dec_in[f][half*Ch + c], n = c*D4 + f
+    float* pj = &act[0][0][0];  // [2][Ch*D4] (the gate scratch is free now)
+    for (int half = 0; half < 2; ++half)
+      gemv(a.proj_w[half], a.proj_b[half], rin[half], 0, 1, H, Ch * D4, pj + half * Ch * D4, 0, wbuf);
+    __syncthreads();
     for (int q = tid; q < 2 * Ch * D4; q += NT) {
       const int half = q / (Ch * D4), n = q % (Ch * D4);
-      float s = a.proj_b[half][n];
-      const float* w = a.proj_w[half] + n;
-      for (int k = 0; k < H; ++k) s = fmaf(w[(size_t)k * Ch * D4], rin[half][k], s);
-      decin[(n % D4) * C6 + half * Ch + n / D4] = s;
+      decin[(n % D4) * C6 + half * Ch + n / D4] = pj[q];
     }
     __syncthreads();
   } else {
@@ -285,7 +350,8 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
         tsl[j] = 1 - (j % 2);
       }
       shop::conv_layer(win, F, Ci, nt, tdf, tsl, 1, F, Co, 2, p, a.dec_w[d][p], a.dec_b[d][p],
-                       last ? nullptr : a.dec_coef[d], last ? nullptr : a.dec_alpha[d], nxt, zrow, dead);
+                       last ? nullptr : a.dec_coef[d], last ? nullptr : a.dec_alpha[d], nxt, zrow, dead,
+                       wbuf);
     }
     __syncthreads();
     if (!last) {
@@ -320,7 +386,7 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
   }
   if (tid < 2) est[514 + tid] = 0.f;
   __syncthreads();
-  gemv(a.istft_w, nullptr, est, LDEST, WIN, frame);
+  gemv(a.istft_w, nullptr, est, 0, 1, LDEST, WIN, frame, 0, wbuf);
   __syncthreads();
   float* fr = st + a.off_frames;
   for (int i = tid; i < WIN; i += NT) fr[ring(t, 4) * WIN + i] = frame[i];
@@ -355,22 +421,24 @@ extern "C" int clskd_stream_hop(const clskd_stream_hop_args* a, void* stream) {
                     "stream_hop: H=%d D4=%d outside the built LDS budget", a->H, a->D4);
   for (int i = 0; i < 6; ++i) {
     const int Fi = 256 >> i, Co = a->enc_cout[i], Ci = a->enc_cin[i];
-    CLSKD_CHECK_SHAPE(Co >= 1 && Co <= 256 && (256 % Co) == 0, "stream_hop: enc %d Co=%d", i, Co);
+    CLSKD_CHECK_SHAPE(Co >= 1 && Co <= shop::NT && (shop::NT % Co) == 0, "stream_hop: enc %d Co=%d", i, Co);
     CLSKD_CHECK_SHAPE(2 * Fi * Ci <= 4096 && (Fi / 2) * Co <= 1024 && Ci <= 256,
                       "stream_hop: encoder %d too wide for the LDS budget", i);
-    CLSKD_CHECK_SHAPE((Fi / 2 + 256 / Co - 1) / (256 / Co) <= shop::MAXR, "stream_hop: enc %d rows", i);
+    CLSKD_CHECK_SHAPE((Fi / 2 + shop::NT / Co - 1) / (shop::NT / Co) <= shop::MAXR, "stream_hop: enc %d rows", i);
     CLSKD_CHECK_ARG(a->enc_w[i] && a->enc_b[i] && a->enc_coef[i] && a->enc_alpha[i], "stream_hop: enc %d", i);
   }
   for (int d = 0; d < 6; ++d) {
     const int F = a->D4 << d, Ci = a->dec_ca[d] + a->dec_cb[d], Co = a->dec_co[d];
-    CLSKD_CHECK_SHAPE(Co >= 1 && Co <= 256 && (256 % Co) == 0, "stream_hop: dec %d Co=%d", d, Co);
+    CLSKD_CHECK_SHAPE(Co >= 1 && Co <= shop::NT && (shop::NT % Co) == 0, "stream_hop: dec %d Co=%d", d, Co);
     CLSKD_CHECK_SHAPE(2 * F * Ci <= 4096 && 2 * F * Co <= 1024 && Ci <= 256,
                       "stream_hop: decoder %d too wide for the LDS budget", d);
-    CLSKD_CHECK_SHAPE((F + 256 / Co - 1) / (256 / Co) <= shop::MAXR, "stream_hop: dec %d rows", d);
+    CLSKD_CHECK_SHAPE((F + shop::NT / Co - 1) / (shop::NT / Co) <= shop::MAXR, "stream_hop: dec %d rows", d);
     CLSKD_CHECK_ARG(a->dec_w[d][0] && a->dec_w[d][1], "stream_hop: dec %d weights", d);
   }
-  CLSKD_CHECK_SHAPE(2 * a->D4 * (a->enc_cout[5] / 2) <= 4096 && 8 * a->H * 2 <= 1024,
-                    "stream_hop: LSTM input too wide");
+  CLSKD_CHECK_SHAPE(2 * a->D4 * (a->enc_cout[5] / 2) <= 4096 && 8 * a->H * 2 <= 1024 &&
+                        2 * 4 * a->H * a->H <= shop::WCH && 2 * 4 * a->H <= shop::MAXR * shop::NT * 4,
+                    "stream_hop: LSTM too wide for the LDS budget");
+  CLSKD_CHECK_SHAPE(514 <= 4 * shop::NT && 2 * 8 * a->H <= 4 * shop::NT, "stream_hop: gemv outputs");
   hipLaunchKernelGGL(stream_hop_kernel, dim3((unsigned)a->B), dim3(shop::NT), 0, as_stream(stream), *a);
   CLSKD_LAUNCH_CHECK("stream_hop");
   return CLSKD_OK;
