@@ -581,9 +581,12 @@ int clskd_exec_marks_read(clskd_exec* ex, float* out, int32_t n);
  * (tools_for_model.py:53-67), encoder (DCCRN.py:171-176), complex LSTMs with carried state
  * (tools_for_model.py:159-174), decoder with its one-frame look-ahead per layer (DCCRN.py:201-206),
  * mask 'E' (DCCRN.py:207-226), ConviSTFT row + overlap-add (tools_for_model.py:90-109).
- * Weights are k-major fp32 copies [K][N] of the packed operands (encoder K order (kf*2+kt, ci);
- * decoder per parity (tap, [input | skip] channels); LSTM input [K][8H] of both weight sets,
- * W_hh [2][4H][H]; projections [H][P]); BatchNorm as eval [scale | shift] + PReLU slope.
+ * Weights are fp32 copies of the packed operands in k-quad layout [K/4][N][4] (element (k, n) at
+ * ((k/4)*N + n)*4 + k%4, so a lane per output reads four k at once and a wavefront reads one
+ * contiguous run): encoder K order (kf*2+kt, ci) with encoder 0's two input channels padded to
+ * four; decoder per parity (tap, [input | skip] channels); LSTM input [K][8H] of both weight sets;
+ * W_hh as [H][2*4H] (n = ws*4H + gate row); projections [H][P]; STFT [400][514]; iSTFT
+ * [516][400].  BatchNorm as eval [scale | shift] + PReLU slope.
  * `state` holds per-stream rings (stride state_stride floats, zero at the start of a stream):
  * off_* are float offsets inside one stream's state (xwin 400; spectrum [7][514]; encoder output
  * i [7-i][128>>i][enc_cout[i]]; decoder input [2][D4][C6]; decoder output d [2][2*(D4<<d)][dec_co[d]];
@@ -592,17 +595,17 @@ int clskd_exec_marks_read(clskd_exec* ex, float* out, int32_t n);
  * forward outputs 9 hops earlier (6 decoder look-ahead frames + the 300-sample centring).
  * Decoder output frames >= zero_from (>= 0) are zeros (the offline decoder's out-of-range frames). */
 typedef struct {
-  const float* stft_w;      /* [400][514] */
-  const float* istft_w;     /* [>=516][400] */
+  const float* stft_w;      /* [100][514][4] */
+  const float* istft_w;     /* [129][400][4] */
   const float* window;      /* [400] */
   const float* enc_w[6];
   const float* enc_b[6];
   const float* enc_coef[6]; /* [2*Co] scale | shift */
   const float* enc_alpha[6];
-  const float* lstm_w[2];   /* [K][8H] */
+  const float* lstm_w[2];   /* [K/4][8H][4] */
   const float* lstm_b[2];   /* [8H] */
-  const float* lstm_whh[2]; /* [2][4H][H] */
-  const float* proj_w[2];   /* [H][P] per half */
+  const float* lstm_whh[2]; /* [H/4][8H][4] */
+  const float* proj_w[2];   /* [H/4][P][4] per half */
   const float* proj_b[2];
   const float* dec_w[6][2]; /* per parity */
   const float* dec_b[6][2];
@@ -619,6 +622,11 @@ typedef struct {
   int32_t off_xwin, off_spec, off_enc[6], off_decin, off_dout[5], off_h, off_c, off_frames;
 } clskd_stream_hop_args;
 int clskd_stream_hop(const clskd_stream_hop_args* a, void* stream);
+/* Diagnostic (-DCLSKD_EXPERIMENTS builds only; else an error): wall-clock (100 MHz) timestamps
+ * of stream 0's hop phases from the last launch — start, STFT, encoders 0-5, LSTMs 0-1,
+ * projection, decoders 0-5, mask, iSTFT, end, then per encoder layer (staged, conv done) — n <= 40
+ * values (after a synchronize). */
+int clskd_stream_hop_marks(int64_t* out, int32_t n);
 
 #ifdef __cplusplus
 }

@@ -279,8 +279,8 @@ class FusedStreamingDCCRN(StreamingDCCRN):
     frame in LDS and the frames the causal convolutions / decoder look-ahead need in per-stream
     rings.  Same step() / process() contract and latency (9 hops); the ~70-launch hop becomes one
     launch, so the hop is no longer bound by launch and dependency latency.  Weights are the
-    offline forward's packed fp32 operands transposed k-major (built once; re-create the object
-    after changing the model's parameters)."""
+    offline forward's packed fp32 operands in the kernel's k-quad layout [K/4][N][4] (built once;
+    re-create the object after changing the model's parameters)."""
 
     def __init__(self, model, batch):
         super().__init__(model, batch, graph=False)
@@ -293,8 +293,16 @@ class FusedStreamingDCCRN(StreamingDCCRN):
         C6 = kn[-1]
         keep = []
 
-        def kmaj(w):  # packed [N][Kp] -> k-major [Kp][N]
-            t = w.float().t().contiguous()
+        def q4(w, K, ci=None):
+            """packed [N][Kp] (first K columns real) -> k-quad [K/4][N][4]; ci: pad each tap's ci
+            input channels to a quad (encoder 0's (re, im))."""
+            w = w.float()[:, :K]
+            N = w.shape[0]
+            if ci is not None:
+                w = torch.nn.functional.pad(w.reshape(N, K // ci, ci), (0, 4 - ci)).reshape(N, -1)
+                K = w.shape[1]
+            assert K % 4 == 0, K
+            t = w.reshape(N, K // 4, 4).permute(1, 0, 2).contiguous()
             keep.append(t)
             return t.data_ptr()
 
@@ -303,24 +311,27 @@ class FusedStreamingDCCRN(StreamingDCCRN):
             return t.data_ptr()
 
         a = _lib.StreamHopArgs()
-        a.stft_w = kmaj(m._stft_w())
+        a.stft_w = q4(m._stft_w(), WIN)
         winv, window = m._istft_w()
-        a.istft_w, a.window = kmaj(winv), p(window)
+        a.istft_w, a.window = q4(winv, 516), p(window)
         for i in range(nl):
             wp, bias = m._enc_w(i, "fp32")
-            a.enc_w[i], a.enc_b[i] = kmaj(wp), p(bias)
+            a.enc_w[i], a.enc_b[i] = q4(wp, 10 * kn[i], ci=2 if i == 0 else None), p(bias)
             a.enc_coef[i], a.enc_alpha[i] = p(self.ebn[i]), p(m.encoder[i][2].weight.detach().float())
             a.enc_cin[i], a.enc_cout[i] = kn[i], kn[i + 1]
         for li in range(2):
             packs = m._lstm_w(li, "fp32")
-            a.lstm_w[li], a.lstm_b[li], a.lstm_whh[li] = kmaj(packs[0]), p(packs[1]), p(packs[2])
+            K = D4 * (C6 // 2) if li == 0 else H
+            whh = packs[2].float().reshape(8 * H, H)  # [2][4H][H] -> n = ws*4H + g
+            a.lstm_w[li], a.lstm_b[li], a.lstm_whh[li] = q4(packs[0], K), p(packs[1]), q4(whh, H)
             if li == 1:
                 for half in range(2):
-                    a.proj_w[half], a.proj_b[half] = kmaj(packs[3 + 2 * half]), p(packs[4 + 2 * half])
+                    a.proj_w[half], a.proj_b[half] = q4(packs[3 + 2 * half], H), p(packs[4 + 2 * half])
         for d in range(nl):
             for parity in (0, 1):
                 wp, bias = m._dec_w(d, parity, "fp32")
-                a.dec_w[d][parity], a.dec_b[d][parity] = kmaj(wp), p(bias)
+                ci = (C6 if d == 0 else self.Co[d - 1]) + kn[nl - d]
+                a.dec_w[d][parity], a.dec_b[d][parity] = q4(wp, (6 if parity == 0 else 4) * ci), p(bias)
             if d < nl - 1:
                 a.dec_coef[d], a.dec_alpha[d] = p(self.dbn[d]), p(m.decoder[d][2].weight.detach().float())
             a.dec_ca[d] = C6 if d == 0 else self.Co[d - 1]
