@@ -38,7 +38,7 @@ PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sp
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 B_PER_GPU = 16
 NBATCH = 4
-TRAFFIC_FILE = "r2_pmc_traffic.json"  # written by tools/pmc_traffic.py
+TRAFFIC_FILE = "r3_pmc_traffic.json"  # written by tools/pmc_traffic.py
 L = 64000
 
 
@@ -229,12 +229,14 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU-oracle B=16 steps (median)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--abf-reinit", default="step", choices=["step", "once"])
-    ap.add_argument("--launch", default="exec", choices=["exec", "eager", "graph"],
-                    help="exec (default, C2): capture the step once and replay it with the "
-                         "library's C++ multi-stream executor (clskd.graph.StepExecutor: no Python "
-                         "per launch, branches concurrent); eager: launch the four-stream schedule "
-                         "from Python every step; graph: hipGraphLaunch of the capture (ROCm's "
-                         "graph executor runs the branches one after another)")
+    ap.add_argument("--launch", default="eager", choices=["exec", "eager", "graph"],
+                    help="eager (default, C2): launch the four-stream schedule from Python every "
+                         "step (host enqueue ~4.1 ms under a ~5.6 ms device step: device-bound); "
+                         "exec: capture the step once and replay it with the library's C++ "
+                         "multi-stream executor (clskd.graph.StepExecutor: ~1 ms host enqueue, but "
+                         "the replayed branches all start at the fork and slow the teacher chain: "
+                         "6.4-6.5 ms device); graph: hipGraphLaunch of the capture (ROCm's graph "
+                         "executor runs the branches one after another)")
     ap.add_argument("--graph", action="store_true", help="same as --launch graph")
     ap.add_argument("--train", action="store_true",
                     help="config C3: the full training step — fwd+loss, HIP backward into the flat "

@@ -163,8 +163,8 @@ int clskd_conv_direct_ok(int32_t N, int32_t K);
 int clskd_bn_stats_partial(const void* x, int64_t rows, int32_t C, double* partial,
                            int32_t nblk, int32_t dtype, void* stream);
 /* clskd_bn_compact: level-2 reduction of [nblk][C][2] partials into [ceil(nblk/group)][C][2]
- * (fixed-order group sums; keeps clskd_bn_finalize's serial part short when the conv epilogue
- * produced one partial per 128 output rows). */
+ * (fixed-order group sums).  Optional: clskd_bn_finalize reads any nblk directly (16-B loads,
+ * eight in flight per lane), which is what the framework does — one launch per BatchNorm. */
 int clskd_bn_compact(const double* partial, int32_t nblk, int32_t C, int32_t group, double* out,
                      void* stream);
 int clskd_bn_finalize(const double* partial, int32_t nblk, int64_t rows, int32_t C,

@@ -400,12 +400,6 @@ def batch_norm_bftc(x, y, gamma, beta, running_mean, running_var, train, momentu
             nblk = L.clskd_bn_partial_blocks(rows, Cn)
             part = torch.empty(nblk * Cn * 2, device=dev, dtype=torch.float64)
             check(L.clskd_bn_stats_partial(ptr(x), rows, Cn, ptr(part), nblk, _dt(x), st), "bn_stats")
-        if nblk > 256:  # two-level: coalesced group sums across the chip, then the finalize
-            grp = 64
-            ng = -(-nblk // grp)
-            part2 = torch.empty(ng * Cn * 2, device=dev, dtype=torch.float64)
-            check(L.clskd_bn_compact(ptr(part), nblk, Cn, grp, ptr(part2), st), "bn_compact")
-            part, nblk = part2, ng
         mean_o = var_o = None
         if stats_out is not None:
             mean_o, var_o = stats_out
@@ -532,16 +526,10 @@ def abf_bn1_coef(x, w1, bn, train, stats_out=None):
 
 def bn_coef_from_partials(part, nblk, rows, C, bn, coef, stats_out=None):
     """Train-mode BatchNorm coefficients [scale | shift] into `coef` from fused {sum, sumsq}
-    partials [nblk][C][2] (clskd_bn_compact when nblk > 256, clskd_bn_finalize); updates bn's
-    running statistics once."""
+    partials [nblk][C][2] (one clskd_bn_finalize launch reads them all); updates bn's running
+    statistics once."""
     L = lib()
     st = _stream()
-    if nblk > 256:
-        grp = 64
-        ng = -(-nblk // grp)
-        part2 = torch.empty(ng * C * 2, device=part.device, dtype=torch.float64)
-        check(L.clskd_bn_compact(ptr(part), nblk, C, grp, ptr(part2), st), "bn_compact")
-        part, nblk = part2, ng
     mean_o = var_o = None
     if stats_out is not None:
         mean_o, var_o = stats_out

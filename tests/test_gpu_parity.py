@@ -441,6 +441,45 @@ def test_bn_running_stats_two_updates():
             np.testing.assert_allclose(_np(sd[k[4:]]), fx[k], rtol=1e-4, atol=1e-6, err_msg=k)
 
 
+@pytest.mark.parametrize("nblk,C", [(3, 8), (256, 64), (2048, 16), (3000, 128)])
+def test_bn_finalize_reads_all_partials(nblk, C):
+    """clskd_bn_finalize alone (no level-2 compaction launch) on up to 3000 {sum, sumsq}
+    partials: scale / shift / batch mean / var and one running-stat update vs fp64 numpy."""
+    from clskd import ops
+    g = torch.Generator().manual_seed(nblk + C)
+    rows = 1000 * nblk
+    x = torch.randn(nblk, C, 2, generator=g, dtype=torch.float64)
+    x[..., 0] *= 50.0
+    x[..., 1] = x[..., 1].abs() * 1000.0 + 2000.0
+    part = x.to(DEV)
+    gamma = torch.rand(C, generator=g).to(DEV)
+    beta = torch.randn(C, generator=g).to(DEV)
+    rm = torch.randn(C, generator=g).to(DEV)
+    rv = torch.rand(C, generator=g).to(DEV) + 0.5
+    bn = torch.nn.BatchNorm2d(C).to(DEV)
+    with torch.no_grad():
+        bn.weight.copy_(gamma)
+        bn.bias.copy_(beta)
+        bn.running_mean.copy_(rm)
+        bn.running_var.copy_(rv)
+    coef = torch.empty(2 * C, device=DEV)
+    mean_o = torch.empty(C, device=DEV)
+    var_o = torch.empty(C, device=DEV)
+    ops.bn_coef_from_partials(part.reshape(-1), nblk, rows, C, bn, coef, (mean_o, var_o))
+    torch.cuda.synchronize()
+    S, Q = x[..., 0].sum(0).numpy(), x[..., 1].sum(0).numpy()
+    mean = S / rows
+    var = np.maximum(Q / rows - mean * mean, 0.0)
+    sc = gamma.double().cpu().numpy() / np.sqrt(var + bn.eps)
+    np.testing.assert_allclose(_np(mean_o), mean, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(_np(var_o), var, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(_np(coef[:C]), sc, rtol=1e-6)
+    np.testing.assert_allclose(_np(coef[C:]), beta.double().cpu().numpy() - mean * sc, rtol=1e-5, atol=1e-5)
+    unb = var * rows / (rows - 1)
+    np.testing.assert_allclose(_np(bn.running_mean), 0.9 * rm.double().cpu().numpy() + 0.1 * mean, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(_np(bn.running_var), 0.9 * rv.double().cpu().numpy() + 0.1 * unb, rtol=1e-5, atol=1e-6)
+
+
 def test_forward_eval_golden():
     fx = golden("student_fwd_eval.npz")
     m = _models("student").eval()

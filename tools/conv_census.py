@@ -1,5 +1,10 @@
-"""Per-launch census of the conv engine over one eager CLSKD step (bench workload C2):
-kernel variant, GEMM shape (M = B*Fo*To, N, K), duration and TFLOP/s.  Diagnostic only."""
+"""Every conv launch of one C2 step (serialised on one stream: isolated durations) with its GEMM
+shape, kernel instance and time, in launch order, plus totals per instance.  Diagnostic.
+
+    python tools/conv_census.py [--precision mixed]
+"""
+import argparse
+import collections
 import os
 import sys
 
@@ -10,31 +15,35 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from clskd import ops  # noqa: E402
 from clskd.data import synthetic_pairs  # noqa: E402
+from clskd.distill import serialized_streams  # noqa: E402
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--precision", default="mixed")
+    a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    kd = bench.build_kd(dev, "step", sys.argv[1] if len(sys.argv) > 1 else "mixed")
+    kd = bench.build_kd(dev, "step", a.precision)
     n, c = synthetic_pairs(bench.B_PER_GPU, bench.L, seed=1)
     X, y = torch.from_numpy(n).to(dev), torch.from_numpy(c).to(dev)
-    for _ in range(2):
-        kd.training_step((X, y))
-    torch.cuda.synchronize()
-    # serialise the three streams so per-launch times are not inflated by overlap
-    import clskd.distill as D
-    for which in (0, 1):
-        D._SIDE[(dev.index, which)] = torch.cuda.current_stream(dev)
-    ops.KernelTimer.start()
-    kd.training_step((X, y))
-    torch.cuda.synchronize()
-    recs = ops.KernelTimer.per_launch()
-    ops.KernelTimer.stop()
-    tot = 0.0
-    print(f"{'kernel':46s} {'M':>9s} {'N':>5s} {'K':>6s} {'dt':>5s} {'us':>8s} {'TF/s':>7s}")
-    for name, (M, N, K, dt), us, tf in recs:
-        tot += us
-        print(f"{name:46s} {M:9d} {N:5d} {K:6d} {dt:>5s} {us:8.1f} {tf:7.1f}")
-    print(f"total {tot / 1e3:.3f} ms over {len(recs)} launches")
+    with torch.no_grad():
+        for _ in range(3):
+            kd.training_step((X, y))
+        torch.cuda.synchronize()
+        ops.KernelTimer.start()
+        with serialized_streams():
+            kd.training_step((X, y))
+        torch.cuda.synchronize()
+        recs = ops.KernelTimer.per_launch()
+        ops.KernelTimer.stop()
+    tot = collections.defaultdict(lambda: [0, 0.0])
+    for name, shp, us, tf in recs:
+        print(f"{us:8.1f} us {tf:7.1f} TF/s  M={shp[0]:>8} N={shp[1]:>4} K={shp[2]:>5} {shp[3]:4s}  {name}")
+        tot[name][0] += 1
+        tot[name][1] += us
+    print("totals:")
+    for k, (cnt, us) in sorted(tot.items(), key=lambda kv: -kv[1][1]):
+        print(f"{us:9.1f} us {cnt:3d} launches  {k}")
 
 
 if __name__ == "__main__":

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-end evidence on one MI355X (run via gpurun from the repo root):
 #   GPU parity tests; two PMC passes of the bench (FETCH_SIZE, WRITE_SIZE separately) joined by
-#   tools/pmc_traffic.py into profiles/r2_pmc_traffic.json (so the bench lines below carry
+#   tools/pmc_traffic.py into profiles/r3_pmc_traffic.json (so the bench lines below carry
 #   roofline.traffic for the kernel instances of THIS build); the default bench line; the C3
 #   training-step line; a rocprofv3 kernel-trace/stats pass of the bench.  Every GPU step has its
 #   own time limit; the chain stops at the first failure.
@@ -15,8 +15,8 @@ timeout -k 10 500 python -u -m pytest $R/tests -m gpu -x -v --timeout 120 --time
   timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/fetch.log 2>&1
   timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/write.log 2>&1
 )
-python3 $R/tools/pmc_traffic.py $O/fetch/run_counter_collection.csv $O/write/run_counter_collection.csv $R/profiles/r2_pmc_traffic.json > $O/traffic.txt
-cp $R/profiles/r2_pmc_traffic.json $O/r2_pmc_traffic.json
+python3 $R/tools/pmc_traffic.py $O/fetch/run_counter_collection.csv $O/write/run_counter_collection.csv $R/profiles/r3_pmc_traffic.json > $O/traffic.txt
+cp $R/profiles/r3_pmc_traffic.json $O/r3_pmc_traffic.json
 timeout -k 10 300 python $R/bench.py > $O/bench.log 2>&1
 timeout -k 10 300 python $R/bench.py --train --no-cpu-baseline > $O/bench_train.log 2>&1
 cd /tmp && export TMPDIR=/tmp
