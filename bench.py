@@ -436,7 +436,11 @@ def main():
         traffic, traffic_src = None, None
         tpath = os.path.join(REPO, "profiles", TRAFFIC_FILE)
         if os.path.exists(tpath) and not args.spkd:  # the PMC passes profile the C2 leg
-            tk = json.load(open(tpath))["kernels"].get(name)
+            kern = json.load(open(tpath))["kernels"]
+            tk = kern.get(name)
+            if tk is None:  # rocprof names carry the operand type as one more template argument
+                more = [k for k in kern if k.startswith(name[:-1] + ",") and k.count(",") == name.count(",") + 1]
+                tk = kern[more[0]] if len(more) == 1 else None
             if tk is not None:
                 traffic = round(tk["hbm_bytes_per_launch"])
                 traffic_src = f"profiles/{TRAFFIC_FILE} (PMC FETCH_SIZE x2 + WRITE_SIZE, per launch)"

@@ -123,17 +123,21 @@ def test_conv_direct_coop_last_layer(dt, C1, C2, N, ntap_f, lpr):
                                rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("dt", ["f32", "bf16", "fp16"])
-@pytest.mark.parametrize("C1,C2,N", [(2, 0, 8), (2, 0, 16), (8, 8, 2), (16, 16, 2), (6, 0, 4),
-                                     (6, 2, 3), (3, 0, 1), (1, 0, 16), (2, 0, 32), (3, 0, 32)])
+_DIRECT_SHAPES = [(2, 0, 8), (2, 0, 16), (8, 8, 2), (16, 16, 2), (6, 0, 4), (6, 2, 3), (3, 0, 1),
+                  (1, 0, 16), (2, 0, 32), (3, 0, 32)]
+
+
+# 16-bit segments need channel runs of 8 (the kernel's 16-B loads): only those shapes run in
+# bf16 / fp16, every shape in fp32
+@pytest.mark.parametrize("dt,C1,C2,N", [("f32",) + s for s in _DIRECT_SHAPES] +
+                         [(d,) + s for d in ("bf16", "fp16") for s in _DIRECT_SHAPES
+                          if s[0] % 8 == 0 and s[1] % 8 == 0])
 def test_conv_direct_against_torch_and_engine(dt, C1, C2, N):
     """Direct-convolution kernel (narrow N / short K): 2-segment 5x2 stride-(2,1) conv with fused
     BN statistics against torch (fp64 on the same bf16-rounded operands for bf16) and against the
     MFMA engines on the same descriptor (CLSKD_WLAYOUT_NK).  Tolerance: 1e-5 relative (fp32
     accumulation orders differ)."""
     from clskd import ops
-    if dt != "f32" and (C1 % 8 or C2 % 8):
-        pytest.skip("16-bit segments need channel runs of 8")
     g = torch.Generator().manual_seed(C1 * 100 + C2 * 10 + N)
     B, F, T = 3, 33, 29
     tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(dt, torch.float32)
