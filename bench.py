@@ -238,6 +238,10 @@ def main():
                          "6.4-6.5 ms device); graph: hipGraphLaunch of the capture (ROCm's graph "
                          "executor runs the branches one after another)")
     ap.add_argument("--graph", action="store_true", help="same as --launch graph")
+    ap.add_argument("--ahead", action="store_true",
+                    help="C2 eager: the teacher chain of step i+1 overlaps step i's tail "
+                         "(clskd_step teacher_ahead; measured 5.70 vs 5.76 ms: the four streams "
+                         "already share the CUs, so off by default)")
     ap.add_argument("--train", action="store_true",
                     help="config C3: the full training step — fwd+loss, HIP backward into the flat "
                          "student gradient, one RCCL all-reduce (N > 1), one Adam launch "
@@ -280,6 +284,9 @@ def main():
     args.graph = args.launch == "graph"
     bsz = B_SPKD if args.spkd else B_PER_GPU
     kd = build_kd(dev, args.abf_reinit, args.precision, spkd=args.spkd)
+    # --ahead: C2 eager steps over resident batches with the teacher chain of step i+1 overlapping
+    # step i's tail (clskd_step teacher_ahead; identical results, tests/test_gpu_parity.py)
+    kd.teacher_ahead = not args.spkd and not args.train and args.launch == "eager" and args.ahead
     # NBATCH distinct batches resident in HBM; step i consumes batch i % NBATCH
     Xs, Ys = [], []
     for k in range(NBATCH):
@@ -513,7 +520,10 @@ def main():
                        "launch": ("eager, 2 HIP streams (caller: teacher; side: student + "
                                   "MRSTFT)" if args.spkd else
                                   "eager, 4 HIP streams (caller, teacher, student, ReviewKD-"
-                                  "encoder/MRSTFT)" if args.launch == "eager" else
+                                  "encoder/MRSTFT)" + ("; teacher chain of step i+1 overlaps step "
+                                                       "i's ReviewKD/Gram/loss tail (teacher_ahead)"
+                                                       if kd.teacher_ahead else "")
+                                  if args.launch == "eager" else
                                   "C++ step executor (clskd_exec_launch): the captured step "
                                   "replayed on 4 HIP streams along its dependency edges "
                                   f"({executor.info['kernels']} kernels, "

@@ -18,6 +18,7 @@ Deliberate equivalences (documented in DESIGN.md):
     kaiming_uniform(a=1) like framework.py:194-195) or, as an explicit opt-in for parity tests
     with injected ABF weights, kept fixed (``abf_reinit='once'``).
 """
+import collections
 import os
 
 import torch
@@ -30,6 +31,9 @@ from .model import DCCRN
 
 
 _SIDE = {}
+# teacher_ahead (clskd_step): per device, the join events of the last two steps and the tensors
+# of the last two steps (kept alive until every stream that reads them has passed them)
+_AHEAD = {}
 _MARKS = None  # diagnostics (tools/stream_marks.py): list collecting (label, event) per step
 
 
@@ -235,7 +239,8 @@ class KnowledgeDistillation(nn.Module):
             params = [p for p in self.student.parameters() if p.requires_grad]
             return _CLSKDLoss.apply(self, X, y, *params)
         out = clskd_step(self.teacher, self.student, self.review_encoder, self.review_decoder,
-                         self.stft_loss, X, y, reinit=self._reinit_abf)
+                         self.stft_loss, X, y, reinit=self._reinit_abf,
+                         teacher_ahead=getattr(self, "teacher_ahead", False))
         self.last = out
         if return_parts:
             return out
@@ -272,9 +277,19 @@ class KnowledgeDistillation(nn.Module):
 
 @torch.no_grad()
 def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y, reinit=None,
-               tape=False):
+               tape=False, teacher_ahead=False):
     """One CLSKD fwd+loss step (distill.py:72-148).  Returns a dict of device tensors.
-    tape=True additionally records what clskd.backward.clskd_backward needs (result['tape'])."""
+    tape=True additionally records what clskd.backward.clskd_backward needs (result['tape']).
+
+    teacher_ahead=True (back-to-back steps over inputs already resident on the device: X and y
+    must not be written on the caller's stream between steps): the frozen teacher's chain of
+    this step — the step's critical path — does not wait for the previous step's join, only for
+    the join of the step before it, so it runs while the previous step's ReviewKD / Gram / loss
+    tail finishes.  Every other chain still starts after the previous step's join (the student's
+    BatchNorm running statistics and the ABF re-draws stay step-ordered), and each step's tensors
+    are held until two steps later, so no buffer is reused while another stream may read it.
+    The work and the results are those of the serial schedule; only the overlap changes.  Not
+    under graph capture, tapes or serialised streams."""
     if not (isinstance(teacher, DCCRN) and isinstance(student, DCCRN)):
         raise TypeError("clskd_step expects clskd.DCCRN teacher and student")
     X = X.float()
@@ -285,7 +300,21 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     B = X.shape[0]
     dev = X.device
     _mark("start", torch.cuda.current_stream(dev))
-    spec = teacher.spectrum(X)
+    capturing = torch.cuda.is_current_stream_capturing()
+    ring = _AHEAD.setdefault(dev.index, dict(joins=collections.deque(maxlen=2),
+                                             held=collections.deque(maxlen=2)))
+    ahead = teacher_ahead and not _SERIAL and not tape and not capturing and len(ring["joins"]) == 2
+    spec_ev = None
+    if ahead:
+        # the teacher chain (spectrum included) waits for the join of step i-1, not step i
+        tstream = _side_stream(dev, 2)
+        tstream.wait_event(ring["joins"][0])
+        with torch.cuda.stream(tstream):
+            spec = teacher.spectrum(X)
+        spec_ev = torch.cuda.Event()
+        spec_ev.record(tstream)
+    else:
+        spec = teacher.spectrum(X)
     # both ConvSTFTs are the fixed (win 400, hop 100, fft 512) kernel of the same window type
     s_spec = spec if teacher.win_type == student.win_type else None
     main = torch.cuda.current_stream(dev)
@@ -294,6 +323,8 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     # spec ready; the previous step's work (joined into main) is done before buffers are reused
     side.wait_stream(main)
     side2.wait_stream(main)
+    if spec_ev is not None:
+        side.wait_event(spec_ev)
     buf = torch.empty(16, dtype=torch.float32, device=dev)  # [sc, mag, spkd x 14]
     # Everything that depends on the student alone runs beside the teacher forward (main):
     #   side : student forward -> decoder-ABF re-draw -> ReviewKD decoder fusions
@@ -389,7 +420,8 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
 
     def run_teacher():
         tstream = _side_stream(dev, 2)
-        tstream.wait_stream(main)
+        if not ahead:
+            tstream.wait_stream(main)
         # the teacher's encoder-tap Grams run on the caller's stream (idle until the join) as soon
         # as the teacher encoder is done, keeping them off the teacher chain — the step's critical
         # path.  (Four streams in all: GPU_MAX_HW_QUEUES is 4; a fifth would share a hardware queue.)
@@ -443,6 +475,13 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     total = torch.empty((), dtype=torch.float32, device=dev)
     ops.sum_f32(buf[1:], total)
     _mark("main: end", main)
+    if not capturing:
+        join = torch.cuda.Event()
+        join.record(main)
+        ring["joins"].append(join)
+        # held until two steps later (teacher_ahead: the next step's teacher may still overlap
+        # this step's readers of these tensors on other streams)
+        ring["held"].append((out_s, out_t, held, rd, spec, X, y) if teacher_ahead else None)
     return dict(loss=total, base=buf[1], sc=buf[0], spkd=buf[2:], enc=buf[2:8], dec=buf[8:14],
                 clstm_real=buf[14], clstm_img=buf[15], student_wav=sf["out_wav"],
                 teacher_wav=tf["out_wav"], s_enc=ops.MaterializingList(s_enc),
