@@ -77,12 +77,11 @@ __device__ __forceinline__ void fma4(f32x2& acc, const f32x4 w, const f32x4 x) {
 // Weight quads stream from global memory straight into registers, QB float4 per lane per batch
 // (KB quads x CQ channels) and NB batches deep: batch b's loads issue NB - 1 batches before it
 // computes, and the first NB - 1 batches issue before the layer stages its input (`pre`), so the
-// staging round trip and the first weight round trips overlap.  At ~1-2 us per dependent global
-// round trip inside this kernel, a layer costs about one round trip plus its arithmetic instead of
-// one per batch.  Trip counts are uniform and the loads unconditional (indices clamped to the
-// matrix; quads past a slice's end meet the zero row instead), so the compiler keeps the batches
-// in flight with counted vmcnt waits.
-constexpr int QB = 8, NB = 3;
+// staging round trip and the first weight round trip overlap.  Trip counts are uniform and the
+// loads unconditional (indices clamped to the matrix; quads past a slice's end meet the zero row
+// instead), so the compiler keeps the batches in flight with counted vmcnt waits.  NB = 3 ran
+// the same hop time as NB = 2 (131.6 vs 131.2 us) with 256 VGPRs and spills, so NB = 2.
+constexpr int QB = 8, NB = 2;
 
 template <class T, class Load, class Comp, class Pre>
 __device__ __forceinline__ void pipeline(int nbat, T (&buf)[NB], Load&& load, Comp&& comp, Pre&& pre) {
