@@ -47,6 +47,8 @@ constexpr int RED = NT * 16;     // split-K partial sums (threads x R x CQ)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int ring(int f, int D) { return ((f % D) + D) % D; }
+// log2 of a power of two (every shape the layer helpers divide by is one: host-checked)
+__device__ __forceinline__ int lg2(int v) { return 31 - __builtin_clz(v); }
 
 __device__ __forceinline__ float sigm(float x) {
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-x * 1.4426950408889634f));
@@ -135,17 +137,22 @@ __device__ __forceinline__ void conv(const lds* win, const Geo g, int np, int K4
                                      const float* coef, const float* alpha, lds* out, int of_mul, lds* red,
                                      lds* prm, int mk, Stage&& stage) {
   constexpr int KB = QB / CQ / (PERTAP ? 2 : 1);  // per-quad offsets cost registers
+  constexpr int LR = R == 8 ? 3 : 2, LQ = CQ == 2 ? 1 : 0;
   const int tid = threadIdx.x;
-  const int FG = Fo / R, CG = Co / CQ;
-  const int S = max(1, NT / (np * FG * CG));
-  const int P = FG * CG * S;
-  const int p = __builtin_amdgcn_readfirstlane(tid / P);
-  const int rem = tid - p * P;
-  const int cg = rem % CG, fg = (rem / CG) % FG, ks = rem / (CG * FG);
+  // every count is a power of two: shifts and masks, no integer divisions
+  const int lfo = lg2(Fo), lco = lg2(Co);
+  const int lfg = lfo - LR, lcg = lco - LQ;
+  const int FG = 1 << lfg, CG = 1 << lcg;
+  const int ls = max(0, lg2(NT) - (np == 2 ? 1 : 0) - lfg - lcg);
+  const int S = 1 << ls;
+  const int lp = lfg + lcg + ls;
+  const int p = __builtin_amdgcn_readfirstlane(tid >> lp);
+  const int rem = tid & ((1 << lp) - 1);
+  const int cg = rem & (CG - 1), fg = (rem >> lcg) & (FG - 1), ks = rem >> (lcg + lfg);
   const bool act = p < np;
   const int pc = act ? p : 0;
   const int k4n = pc ? K4b : K4a;
-  int len = (k4n + S - 1) / S;
+  int len = (k4n + S - 1) >> ls;
   len = (len + KB - 1) / KB * KB;
   const int nbat = __builtin_amdgcn_readfirstlane(act ? len / KB : 0);
   const int k0 = ks * len, k1 = min(k4n, k0 + len);
@@ -201,7 +208,7 @@ __device__ __forceinline__ void conv(const lds* win, const Geo g, int np, int K4
         stage();
         for (int q = tid; q < np * Co; q += NT) {
           const float* bp = q >= Co ? b1 : b0;
-          prm[q] = bp ? ldg(bp + q % Co) : 0.f;
+          prm[q] = bp ? ldg(bp + (q & (Co - 1))) : 0.f;
         }
         if (coef) {
           for (int q = tid; q < 2 * Co; q += NT) prm[np * Co + q] = ldg(coef + q);
@@ -235,11 +242,11 @@ __device__ __forceinline__ void conv(const lds* win, const Geo g, int np, int K4
         red[((p * S + ks) * Fo + fg + FG * r) * Co + cg * CQ + q] = acc[r][q].x + acc[r][q].y;
   __syncthreads();
   CMARK(mk < 0 ? -1 : mk + 1);
-  for (int q = tid; q < np * Fo * Co; q += NT) {
-    const int pp = q / (Fo * Co), o = q % (Fo * Co);
+  for (int q = tid; q < (np << (lfo + lco)); q += NT) {
+    const int pp = q >> (lfo + lco), o = q & ((1 << (lfo + lco)) - 1);
     float v = 0.f;
-    for (int s2 = 0; s2 < S; ++s2) v += red[(pp * S + s2) * Fo * Co + o];
-    fin(pp, o / Co, o % Co, v);
+    for (int s2 = 0; s2 < S; ++s2) v += red[(((pp << ls) + s2) << (lfo + lco)) + o];
+    fin(pp, o >> lco, o & (Co - 1), v);
   }
 }
 
@@ -252,9 +259,10 @@ __device__ __forceinline__ void conv_layer(const lds* win, const Geo g, int np, 
                                            lds* red, lds* prm, bool zero, int mk, Stage&& stage) {
   if (zero) {
     stage();
-    for (int q = threadIdx.x; q < np * Fo * Co; q += NT) {
-      const int p = q / (Fo * Co), o = q % (Fo * Co);
-      out[((o / Co) * of_mul + p) * Co + o % Co] = 0.f;
+    const int lfc = lg2(Fo) + lg2(Co);
+    for (int q = threadIdx.x; q < (np << lfc); q += NT) {
+      const int p = q >> lfc, o = q & ((1 << lfc) - 1);
+      out[((o >> lg2(Co)) * of_mul + p) * Co + (o & (Co - 1))] = 0.f;
     }
     return;
   }
@@ -395,18 +403,21 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
   if (a.live) {
     // ---- ConvSTFT row of the newest window -> spectrum ring
     gemv(a.stft_w, nullptr, L(xw), 0, 1, WIN / 4, NBIN, L(spec), 0, L(red), L(zr), stage_x);
-    for (int i = tid; i < WIN; i += NT) gxw[i] = xw[i];  // (every read of gxw is behind gemv's barrier)
     __syncthreads();
     HOP_MARK(1);
-    float* sring = st + a.off_spec;
-    for (int i = tid; i < NBIN; i += NT) sring[ring(t, 7) * NBIN + i] = spec[i];
-    // ---- encoder (DCCRN.py:171-176): window [t-1, t], taps (kf - 2, kt), stride 2 in F
+    // ---- encoder (DCCRN.py:171-176): window [t-1, t], taps (kf - 2, kt), stride 2 in F.
+    //      The ring writes of the previous phase's output are issued in the next phase's staging,
+    //      behind its first weight loads: gfx950's vmcnt counts stores, so a load issued after a
+    //      store would wait for that store's acknowledgement too.
     for (int i = 0; i < 6; ++i) {
       const int Fi = 256 >> i, Fo = Fi / 2, Co = a.enc_cout[i];
       const int Ci = i == 0 ? 4 : a.enc_cin[i];  // encoder 0: (re, im) padded to a quad
       // stage [2][Fi][Ci]: slot 1 = this frame (spectrum / previous layer in LDS), slot 0 = t-1
       auto stage = [&]() {
         if (i == 0) {
+          for (int j = tid; j < WIN; j += NT) gxw[j] = xw[j];  // (every read of gxw is behind gemv's barrier)
+          float* sring = st + a.off_spec;
+          for (int j = tid; j < NBIN; j += NT) sring[ring(t, 7) * NBIN + j] = spec[j];
           const float* sp = st + a.off_spec + ring(t - 1, 7) * NBIN;
           for (int q = tid; q < 4 * Fi; q += NT) {
             const int f = q >> 2, ri = q & 3;
@@ -415,10 +426,13 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
           }
         } else {
           const int D = 7 - (i - 1);
-          const float* rp = st + a.off_enc[i - 1] + (int64_t)ring(t - 1, D) * Fi * Ci;
+          float* ep = st + a.off_enc[i - 1];
+          const float* rp = ep + (int64_t)ring(t - 1, D) * Fi * Ci;
+          float* er = ep + (int64_t)ring(t, D) * Fi * Ci;  // encoder i-1's frame t (its output Fi x Ci)
           for (int q = tid; q < Fi * Ci; q += NT) {
             win[q] = rp[q];
             win[Fi * Ci + q] = cur[q];
+            er[q] = cur[q];
           }
         }
       };
@@ -427,8 +441,6 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
                  a.enc_alpha[i], L(nxt), 1, L(red), L(prm), false, i == 0 ? 32 : i == 4 ? 34 : -1, stage);
       __syncthreads();
       HOP_MARK(2 + i);
-      float* er = st + a.off_enc[i] + (int64_t)ring(t, 7 - i) * Fo * Co;
-      for (int q = tid; q < Fo * Co; q += NT) er[q] = nxt[q];
       float* tmp = cur;
       cur = nxt;
       nxt = tmp;
@@ -442,22 +454,28 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
       float* cs = st + a.off_c + li * 4 * H;
       // gate q = (ws, half, g), W_hh row n = ws*4H + g
       const bool gate = tid < 4 * G4;
-      const int q = gate ? tid : 0, ws = q / (2 * G4), half = (q / G4) % 2, gg = q % G4, n = ws * G4 + gg;
+      const int lh = lg2(H), lg4 = lh + 2;  // G4 = 4H
+      const int q = gate ? tid : 0, ws = q >> (lg4 + 1), half = (q >> lg4) & 1, gg = q & (G4 - 1), n = ws * G4 + gg;
       // gx[half][n] (n < 8H: both weight sets side by side); staged: the input halves (layer 0
       // x[k = f*Ch + c] = enc5[f][half*Ch + c]; layer 1 the combine output), (h, c) and W_hh
       // (rows padded to H + 4 floats: the gate loop's row-per-lane quad reads are conflict-free)
       gemv(a.lstm_w[li], a.lstm_b[li], L(xin), K, 2, K / 4, 8 * H, L(&gx[0][0]), 8 * 64, L(red), L(zr), [&]() {
+        if (li == 0) {  // encoder 5's frame t -> its ring (behind the first weight loads)
+          float* er = st + a.off_enc[5] + (int64_t)ring(t, 2) * D4 * C6;
+          for (int q2 = tid; q2 < D4 * C6; q2 += NT) er[q2] = cur[q2];
+        }
         for (int q2 = tid; q2 < (H / 4) * 2 * G4; q2 += NT) {
-          const int j4 = q2 / (2 * G4), r = q2 % (2 * G4);
+          const int j4 = q2 >> (lg4 + 1), r = q2 & (2 * G4 - 1);
           *reinterpret_cast<f32x4*>(&whh[r * (H + 4) + j4 * 4]) = ldg4(a.lstm_whh[li] + (size_t)q2 * 4);
         }
         for (int q2 = tid; q2 < 2 * K; q2 += NT) {
-          const int half2 = q2 / K, k = q2 % K;
-          xin[q2] = li == 0 ? cur[(k / Ch) * C6 + half2 * Ch + (k % Ch)] : rin[half2][k];
+          const int lk = lg2(K), lch = lg2(Ch);
+          const int half2 = q2 >> lk, k = q2 & (K - 1);
+          xin[q2] = li == 0 ? cur[(k >> lch) * C6 + half2 * Ch + (k & (Ch - 1))] : rin[half2][k];
         }
         for (int q2 = tid; q2 < 4 * H; q2 += NT) {
-          (&hv[0][0][0])[(q2 / H) * 64 + q2 % H] = hs[q2];
-          (&cv[0][0][0])[(q2 / H) * 64 + q2 % H] = cs[q2];
+          (&hv[0][0][0])[(q2 >> lh) * 64 + (q2 & (H - 1))] = hs[q2];
+          (&cv[0][0][0])[(q2 >> lh) * 64 + (q2 & (H - 1))] = cs[q2];
         }
       });
       __syncthreads();
@@ -466,11 +484,11 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
         f32x2 s2 = f32x2{gx[half][n], 0.f};
         for (int j4 = 0; j4 < H / 4; ++j4) fma4(s2, ld4(L(&whh[n * (H + 4) + j4 * 4])), ld4(L(&hv[ws][half][j4 * 4])));
         const float s = s2.x + s2.y;
-        act[ws][half][gg] = (gg / H) == 2 ? fmaf(2.f, sigm(2.f * s), -1.f) : sigm(s);
+        act[ws][half][gg] = (gg >> lh) == 2 ? fmaf(2.f, sigm(2.f * s), -1.f) : sigm(s);
       }
       __syncthreads();
       for (int q2 = tid; q2 < 4 * H; q2 += NT) {
-        const int ws2 = q2 / (2 * H), half2 = (q2 / H) % 2, u = q2 % H;
+        const int ws2 = q2 >> (lh + 1), half2 = (q2 >> lh) & 1, u = q2 & (H - 1);
         const float* ac = act[ws2][half2];
         const float cn = ac[H + u] * cv[ws2][half2][u] + ac[u] * ac[2 * H + u];
         const float hn = ac[3 * H + u] * tanh_f(cn);
@@ -481,7 +499,7 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
       __syncthreads();
       // real = R(r) - I(i), imag = R(i) + I(r)  (tools_for_model.py:168-169)
       for (int q2 = tid; q2 < 2 * H; q2 += NT) {
-        const int half2 = q2 / H, u = q2 % H;
+        const int half2 = q2 >> lh, u = q2 & (H - 1);
         rin[half2][u] = half2 == 0 ? hv[0][0][u] - hv[1][1][u] : hv[0][1][u] + hv[1][0][u];
       }
       __syncthreads();
@@ -495,8 +513,9 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
       __syncthreads();
     }
     for (int q = tid; q < 2 * Ch * D4; q += NT) {
-      const int half = q / (Ch * D4), n = q % (Ch * D4);
-      decin[(n % D4) * C6 + half * Ch + n / D4] = pj[q];
+      const int ld4 = lg2(D4), lcd = lg2(Ch) + ld4;
+      const int half = q >> lcd, n = q & ((1 << lcd) - 1);
+      decin[(n & (D4 - 1)) * C6 + half * Ch + (n >> ld4)] = pj[q];
     }
     __syncthreads();
     HOP_MARK(10);
@@ -516,8 +535,6 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
     }
     __syncthreads();
   }
-  float* dr = st + a.off_decin + ring(t, 2) * D4 * C6;
-  for (int q = tid; q < D4 * C6; q += NT) dr[q] = decin[q];
 
   // ---- decoder (DCCRN.py:201-206): layer d emits frame t-1-d from its input's frames
   //      [t-1-d, t-d] and encoder 5-d's frames [t-1-d, t-d]; both parities in one pass
@@ -538,17 +555,22 @@ __global__ __launch_bounds__(shop::NT) void stream_hop_kernel(const clskd_stream
     conv_layer(L(win), g, 2, 6 * Ci / 4, 4 * Ci / 4, F, Co, a.dec_w[d][0], a.dec_w[d][1], a.dec_b[d][0],
                a.dec_b[d][1], last ? nullptr : a.dec_coef[d], last ? nullptr : a.dec_alpha[d], L(nxt), 2, L(red),
                L(prm), dead, d == 1 ? 36 : -1, [&]() {
+                 // the previous phase's output -> its ring (behind this layer's first weight loads)
+                 if (d == 0) {
+                   float* dr = st + a.off_decin + ring(t, 2) * D4 * C6;
+                   for (int q = tid; q < D4 * C6; q += NT) dr[q] = decin[q];
+                 } else {  // decoder d-1's frame t-d: [2 F_{d-1} = F][Co_{d-1} = Ca]
+                   float* orr = st + a.off_dout[d - 1] + (int64_t)ring(t - d, 2) * F * Ca;
+                   for (int q = tid; q < F * Ca; q += NT) orr[q] = in_cur[q];
+                 }
+                 const int lci = g.lgq + 2;
                  for (int q = tid; q < F * Ci; q += NT) {
-                   const int f = q / Ci, c = q % Ci;
+                   const int f = q >> lci, c = q & (Ci - 1);
                    win[q] = c < Ca ? in_old[f * Ca + c] : sk_old[f * Cb + c - Ca];
                    win[F * Ci + q] = c < Ca ? in_cur[f * Ca + c] : sk_new[f * Cb + c - Ca];
                  }
                });
     __syncthreads();
-    if (!last) {
-      float* orr = st + a.off_dout[d] + (int64_t)ring(out_frame, 2) * 2 * F * Co;
-      for (int q = tid; q < 2 * F * Co; q += NT) orr[q] = nxt[q];
-    }
     in_cur = nxt;
     // ping-pong: the next layer writes the other buffer (cur holds encoder 5 only for d == 0)
     nxt = (nxt == curA) ? curB : curA;
@@ -616,7 +638,7 @@ extern "C" int clskd_stream_hop(const clskd_stream_hop_args* a, void* stream) {
   CLSKD_CHECK_ARG(!a->live || a->x_in, "stream_hop: live hop without input");
   CLSKD_CHECK_SHAPE(a->B >= 1 && a->t >= 0, "stream_hop: B=%d t=%d", a->B, a->t);
   auto pow2 = [](int v) { return v >= 1 && (v & (v - 1)) == 0; };
-  CLSKD_CHECK_SHAPE(a->H >= 4 && a->H % 4 == 0 && 16 * a->H <= shop::NT && a->D4 >= 1 &&
+  CLSKD_CHECK_SHAPE(a->H >= 4 && pow2(a->H) && 16 * a->H <= shop::NT && a->D4 >= 1 &&
                         pow2(a->D4) && a->D4 * a->enc_cout[5] <= 256 && a->enc_cout[5] % 2 == 0,
                     "stream_hop: H=%d D4=%d outside the built LDS budget", a->H, a->D4);
   CLSKD_CHECK_SHAPE(a->enc_cin[0] == 2, "stream_hop: encoder 0 takes (re, im), got %d", a->enc_cin[0]);
