@@ -221,6 +221,115 @@ def run_c1(args, dev):
     print(json.dumps(out))
 
 
+METRIC_C5 = "frames/sec streaming DCCRN student inference (6.25 ms hops, 30 s @16 kHz per stream)"
+
+
+def run_c5(args, dev):
+    """Configuration C5 (BASELINE.json configs[4]): streaming inference of the student (eval BN)
+    over 30 s @ 16 kHz per stream, 100-sample (6.25 ms) hops, one clskd_stream_hop launch per hop
+    for every stream at once (clskd.streaming.FusedStreamingDCCRN; pinned to the oracle's offline
+    eval forward by tests/test_gpu_streaming.py).  A step = one hop of all `--streams` streams over
+    input already resident in HBM; value = frames (hops x streams) per second over the timed
+    hops; the hop kernel's duration is HIP-event-timed on the launching stream.  Also measured:
+    one stream's hop (the latency view) and the per-layer hipGraph hop.  CPU leg: the oracle's
+    OFFLINE eval forward on one 30 s clip (the reference has no streaming path; the same MACs
+    per frame), 1 warm-up + median of 3."""
+    from oracle import ref_cpu as R
+    from clskd.data import synthetic_pairs
+    from clskd.model import DCCRN
+    from clskd.streaming import HOP, FusedStreamingDCCRN, StreamingDCCRN
+    from clskd.weights import STUDENT_SEED, apply_recipe, recipe_state_dict
+    student = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.STUDENT),
+                           STUDENT_SEED).to(dev).eval()
+    S = args.streams
+    L = 480000
+    nh = L // HOP
+    K = min(max(args.steps, 200), nh - args.warmup)  # hops timed (a step = one hop of every stream)
+    noisy, _ = synthetic_pairs(S, L, seed=3)
+    x = torch.from_numpy(noisy).to(dev)
+    legs = {}
+
+    def timed(s, n_streams):
+        for t in range(args.warmup):
+            s.step(x[:n_streams, t * HOP:(t + 1) * HOP])
+        torch.cuda.synchronize()
+        evs = []
+        t0 = time.perf_counter()
+        for t in range(args.warmup, args.warmup + K):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.x_in.copy_(x[:n_streams, t * HOP:(t + 1) * HOP])
+            e0.record()
+            s._hop()
+            e1.record()
+            evs.append((e0, e1))
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        return el / K, kern_ms
+
+    fs = FusedStreamingDCCRN(student, S)
+    per_hop, kern_ms = timed(fs, S)
+    legs["fused_all"] = dict(streams=S, ms_per_hop=round(per_hop * 1e3, 4), kernel_ms=round(kern_ms, 4),
+                             frames_per_s=round(S / per_hop, 1),
+                             real_time_factor=round(per_hop / (HOP / 16000.0), 5))
+    f1 = FusedStreamingDCCRN(student, 1)
+    p1, k1 = timed(f1, 1)
+    legs["fused_1"] = dict(streams=1, ms_per_hop=round(p1 * 1e3, 4), kernel_ms=round(k1, 4),
+                           real_time_factor=round(p1 / (HOP / 16000.0), 5))
+    g1 = StreamingDCCRN(student, 1, graph=True)
+    for t in range(4):
+        g1.step(x[:1, t * HOP:(t + 1) * HOP])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(4, 4 + K):
+        g1.step(x[:1, t * HOP:(t + 1) * HOP])
+    torch.cuda.synchronize()
+    pg = (time.perf_counter() - t0) / K
+    legs["graph_1"] = dict(streams=1, ms_per_hop=round(pg * 1e3, 4),
+                           real_time_factor=round(pg / (HOP / 16000.0), 5))
+    # CPU: the oracle's offline eval forward over one 30 s clip
+    ps = R.to_torch_params(recipe_state_dict(cfg.dccrn_param_shapes(**cfg.STUDENT), STUDENT_SEED))
+    model, total, usable = host_cpu_info()
+    torch.set_num_threads(usable)
+    xc = torch.from_numpy(noisy[:1])
+    with torch.no_grad():
+        R.dccrn_forward(ps, xc, train=False)
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            R.dccrn_forward(ps, xc, train=False)
+            ts.append(time.perf_counter() - t0)
+    cpu_s = float(np.median(ts))
+    frames_clip = cfg.n_frames(L)
+    value = S / per_hop
+    # roofline of the hop kernel: per stream and hop 3.8 MMAC (SURVEY.md §8 d, 7.6 MFLOP) on fp32
+    # v_pk_fma_f32 (fp32 vector peak = the fp32 matrix peak, 157.3 TF/s); the 3.2 MB of weights
+    # per stream and hop come from the XCD L2s (MI355X_MICROARCH.md: 66-73 GB/s per CU gathered)
+    fl = 7.6e6 * S / (kern_ms * 1e-3) / 1e12
+    out = {
+        "metric": METRIC_C5, "value": round(value, 1), "unit": "frames/s", "n_gpus": 1,
+        "steps": K, "warmup": args.warmup, "ms_per_step": round(per_hop * 1e3, 4),
+        "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (seeded 16 kHz enveloped-sinusoid clean + noise); recipe weights",
+        "config": {"workload": f"C5: {S} concurrent streams x 30 s @16 kHz, student eval BN, one "
+                               "clskd_stream_hop launch per 6.25 ms hop (algorithmic latency 9 hops "
+                               "= 56.25 ms)", "legs": legs},
+        "roofline": {"bound": "mfma", "kernel": "stream_hop_kernel", "achieved": round(fl, 3),
+                     "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(fl / PEAK_F32_MFMA_TFLOPS, 5), "traffic": None,
+                     "note": "fp32 VALU (v_pk_fma_f32), one workgroup per stream; per CU the hop "
+                             "is bound by instruction issue and load latency "
+                             "(profiles/r3_stream_c5_sq_counters.json), weights from L2: "
+                             f"{round(3.2e6 * S / (kern_ms * 1e-3) / 1e12, 2)} TB/s aggregate"},
+        "cpu_baseline": {"value": round(frames_clip / cpu_s, 1), "unit": "frames/s",
+                         "cores": usable, "kind": "port", "cpu_model": model, "host_cpus": total,
+                         "sample": "oracle/ref_cpu.dccrn_forward(train=False) offline over one 30 s "
+                                   f"clip ({frames_clip} frames), 1 warm-up + median of 3, "
+                                   f"{usable} threads: {round(cpu_s * 1e3, 1)} ms"},
+    }
+    print(json.dumps(out))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -250,6 +359,10 @@ def main():
                     help="config C4: distill_SPKD.py's step (student + teacher full forwards, MRSTFT "
                          "base, one SPKD Gram over the output waveforms) at B=32 x 4 s per GPU; "
                          "reported under its own metric")
+    ap.add_argument("--c5", action="store_true",
+                    help="config C5: streaming inference, --streams streams x 30 s, one fused "
+                         "clskd_stream_hop launch per hop (see run_c5)")
+    ap.add_argument("--streams", type=int, default=256, help="C5: concurrent streams")
     ap.add_argument("--c1", action="store_true",
                     help="config C1: the student's eval forward at batch 1 (16000 and 8000 "
                          "samples) as a latency, GPU (eager and executor) beside the CPU oracle")
@@ -275,6 +388,8 @@ def main():
     from clskd.data import synthetic_pairs
     if args.c1:
         return run_c1(args, dev)
+    if args.c5:
+        return run_c5(args, dev)
     if args.graph:
         args.launch = "graph"
     if args.spkd and args.train:

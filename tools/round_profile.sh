@@ -20,6 +20,7 @@ timeout -k 10 300 python $R/bench.py > $O/bench.log 2>&1
 timeout -k 10 200 python $R/bench.py --train --no-cpu-baseline > $O/bench_train.log 2>&1
 timeout -k 10 200 python $R/bench.py --spkd --no-cpu-baseline > $O/bench_spkd.log 2>&1
 timeout -k 10 200 python $R/bench.py --c1 > $O/bench_c1.log 2>&1
+timeout -k 10 300 python $R/bench.py --c5 > $O/bench_c5.log 2>&1
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/trace.log 2>&1
 echo done
