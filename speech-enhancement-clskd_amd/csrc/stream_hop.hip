@@ -293,10 +293,12 @@ __device__ __forceinline__ void gemv(const float* W, const float* bias, const ld
                                      lds* y, int ys, lds* red, const lds* zrow, Pre&& pre) {
   const int tid = threadIdx.x;
   const int M = nh * N;
-  // K slices: the fewest quads per thread over rounds of NT units (ties: fewer slices)
+  // K slices: the least work per thread over rounds of NT units, a round costing its quads
+  // plus ~8 quads of fixed work (unit indices, partial store, the pipeline's first round trip);
+  // ties: fewer slices.  (Counting quads alone picked 14 rounds of 8 quads for the STFT row.)
   int S = 1, best = 1 << 30;
   for (int s2 = 1; s2 <= 16 && s2 * M <= RED && s2 <= K4; ++s2) {
-    const int cost = (s2 * M + NT - 1) / NT * ((K4 + s2 - 1) / s2);
+    const int cost = (s2 * M + NT - 1) / NT * ((K4 + s2 - 1) / s2 + 8);
     if (cost < best) {
       best = cost;
       S = s2;
