@@ -94,3 +94,57 @@ def test_gloo_world2_train_step_plumbing():
     for rank, scale, alias, aligned, g in res:
         assert scale == 0.5 and alias and aligned
         assert g == [3.0 * (i + 1) for i in range(len(g))]  # (1 + 2) * (i + 1) summed
+
+
+def _student_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "speech-enhancement-clskd_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from clskd import config as cfg
+    from clskd import dist as cdist
+    from clskd.model import DCCRN
+    from clskd.train import FlatParams, allreduce_grads
+    from clskd.weights import STUDENT_SEED, apply_recipe
+    cdist.init("gloo")
+    student = apply_recipe(DCCRN(masking_mode="E", use_clstm=True, **cfg.STUDENT), STUDENT_SEED)
+    flat = FlatParams(student)
+    g = torch.Generator().manual_seed(100 + rank)  # rank-local gradients of the real layout
+    local = {}
+    for p in flat.params:
+        v = torch.randn(p.shape, generator=g)
+        flat.gviews[p].copy_(v)
+        local[p] = v
+    names = {id(p): n for n, p in student.named_parameters()}
+    scale = allreduce_grads(flat)
+    summed = {names[id(p)]: flat.gviews[p].clone().numpy() for p in flat.params}
+    mine = {names[id(p)]: local[p].numpy() for p in flat.params}
+    q.put((rank, scale, flat.numel, sum(p.numel() for p in flat.params),
+           float(flat.data.double().sum()), summed, mine))
+    torch.distributed.destroy_process_group()
+
+
+def test_gloo_world2_student_gradient_allreduce():
+    """C3 data parallelism on the CLSKD student itself (config.STUDENT, 231,565 trainable
+    parameters in one 256-B-aligned flat buffer): ONE all-reduce of the flat gradient sums every
+    parameter's rank-local gradient, identically on both ranks; the recipe weights are identical
+    on both ranks (the weight state a DDP broadcast would give); scale = 1/world for Adam."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_student_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, s0, n0, k0, w0, sum0, mine0), (_, s1, n1, k1, w1, sum1, mine1) = res
+    assert s0 == s1 == 0.5
+    assert k0 == k1 == 231565 and n0 == n1 == 234048
+    assert w0 == w1  # same parameters on both ranks
+    assert sum0.keys() == mine0.keys() and len(sum0) > 30
+    for name in sum0:
+        np.testing.assert_array_equal(sum0[name], sum1[name])
+        np.testing.assert_allclose(sum0[name], mine0[name] + mine1[name], rtol=1e-6, atol=1e-6)
