@@ -484,6 +484,33 @@ def test_bn_finalize_reads_all_partials(nblk, C):
     np.testing.assert_allclose(_np(bn.running_var), 0.9 * rv.double().cpu().numpy() + 0.1 * unb, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("kind,B,L", [("student", 1, 16037), ("student", 3, 401), ("student", 2, 250),
+                                      ("teacher", 1, 12345), ("student", 5, 8000)])
+@pytest.mark.parametrize("train", [True, False])
+def test_forward_ragged_lengths_against_oracle(kind, B, L, train):
+    """Edge cases of DCCRN.forward (DCCRN.py:149-240) against the oracle: a batch of one, odd
+    batch sizes, lengths that are not a whole number of hops (the ConvSTFT floor, T = (L+200)//100
+    + 1) and clips shorter than one 400-sample window (T = 3 or 5 frames) — train-mode BN (batch
+    statistics over whatever rows exist) and eval-mode BN (running statistics).  Output length,
+    waveform RMS <= 1e-5 and max |diff| <= 1e-4, masks within 2e-4 relative."""
+    from clskd.data import synthetic_pairs
+    from oracle import ref_cpu as R
+    noisy, _ = synthetic_pairs(B, L, seed=B * 1000 + L)
+    m = _models(kind).train(train)
+    p = {k: v.detach().cpu() for k, v in m.state_dict().items() if not k.startswith(("stft.", "istft."))}
+    x = torch.from_numpy(noisy).to(DEV)
+    with torch.no_grad():
+        out = m(x)
+        ref = R.dccrn_forward(p, torch.from_numpy(noisy), train=train)
+    wav = _np(out[4])
+    rw = ref["out_wav"].numpy()
+    assert wav.shape == rw.shape, (wav.shape, rw.shape)
+    assert rms(wav, rw) <= 1e-5
+    assert np.abs(wav - rw).max() <= 1e-4
+    for i, name in ((0, "mask_real"), (1, "mask_imag")):
+        np.testing.assert_allclose(_np(out[i]), ref[name].numpy(), rtol=2e-4, atol=2e-5)
+
+
 def test_forward_eval_golden():
     fx = golden("student_fwd_eval.npz")
     m = _models("student").eval()
@@ -624,6 +651,32 @@ def test_clskd_step_4s_against_oracle():
     np.testing.assert_allclose(_np(out["dec"]), [v.item() for v in ref["dec"]], rtol=5e-5, atol=1e-8)
     assert abs(out["clstm_real"].item() - ref["clstm_real"].item()) <= 5e-5 * ref["clstm_real"].item()
     assert abs(out["clstm_img"].item() - ref["clstm_img"].item()) <= 5e-5 * ref["clstm_img"].item()
+    assert abs(out["loss"].item() - ref["total"].item()) <= 2e-5 * abs(ref["total"].item())
+
+
+@pytest.mark.parametrize("B,L", [(3, 12345), (5, 4321)])
+def test_clskd_step_ragged_against_oracle(B, L):
+    """The CLSKD step (distill.py:72-148) at odd batch sizes and lengths that are not a whole
+    number of hops, against the oracle with fp64 Grams: student waveform RMS <= 1e-4, base loss
+    within 1e-4 relative, the 14 SPKD terms within 5e-5 relative (or 1e-8 absolute), the total
+    within 2e-5.  (Batch 1 is not a reference case: distill.py:100-101 squeezes the batch axis
+    away before the MRSTFT's torch.stft, which then raises on the transpose; the oracle follows.)"""
+    from clskd.data import synthetic_pairs
+    from oracle import ref_cpu as R
+    noisy, clean = synthetic_pairs(B, L, seed=B * 7 + L)
+    kd = _kd()
+    X, y = torch.from_numpy(noisy).to(DEV), torch.from_numpy(clean).to(DEV)
+    out = kd.training_step((X, y), 0, return_parts=True)
+    with torch.no_grad():
+        ref = R.clskd_step(_oracle_params("teacher"), _oracle_params("student"),
+                           _oracle_params("abf"), torch.from_numpy(noisy), torch.from_numpy(clean),
+                           gram_dtype=torch.float64)
+    wav = _np(out["student_wav"])
+    assert wav.shape == tuple(ref["student_wav"].shape)
+    assert rms(wav, ref["student_wav"].numpy()) <= 1e-4
+    assert abs(out["base"].item() - ref["base"].item()) <= 1e-4 * abs(ref["base"].item())
+    np.testing.assert_allclose(_np(out["enc"]), [v.item() for v in ref["enc"]], rtol=5e-5, atol=1e-8)
+    np.testing.assert_allclose(_np(out["dec"]), [v.item() for v in ref["dec"]], rtol=5e-5, atol=1e-8)
     assert abs(out["loss"].item() - ref["total"].item()) <= 2e-5 * abs(ref["total"].item())
 
 
