@@ -627,6 +627,11 @@ int clskd_stream_hop(const clskd_stream_hop_args* a, void* stream);
  * projection, decoders 0-5, mask, iSTFT, end, then per encoder layer (staged, conv done) — n <= 40
  * values (after a synchronize). */
 int clskd_stream_hop_marks(int64_t* out, int32_t n);
+/* Diagnostic (-DCLSKD_EXPERIMENTS builds only; else an error): wall-clock (100 MHz) timeline of
+ * workgroup 0 of the last halo-tiled fp32 conv launched with CLSKD_H32_DEBUG_MODE=5 — waves 0
+ * and 4 (one SIMD) at [0, 64) and [64, 128): after each chunk barrier, after each chunk's MFMAs,
+ * after each tile — n <= 128 values (after a synchronize). */
+int clskd_h32_marks(int64_t* out, int32_t n);
 
 #ifdef __cplusplus
 }

@@ -175,6 +175,7 @@ SIGNATURES = {
     "clskd_exec_marks_read": (_i32, [_p, C.POINTER(C.c_float), _i32]),
     "clskd_stream_hop": (_i32, [C.POINTER(StreamHopArgs), _p]),
     "clskd_stream_hop_marks": (_i32, [C.POINTER(C.c_int64), _i32]),
+    "clskd_h32_marks": (_i32, [C.POINTER(C.c_int64), _i32]),
     "clskd_spkd_bn_bwd": (_i32, [_p, _i32, _i64, _i64, _i32, _i32, _p, _p, _p, _p, _p, _f32, _p, _p,
                                  _i32, _p, _p, _p, _i32, _p]),
 }

@@ -486,6 +486,7 @@ extern "C" int clskd_abf_bn1_partials(const float* s, int32_t B, int32_t F, int3
   const int rows = B * F * T;
   const TapRows g = tap_rows(F, T, sB, sF, sT, cin);
   const hipStream_t st = as_stream(stream);
+  if (skip_kernel(SKIP_ABF)) return CLSKD_OK;
   switch (cin) {
     case 8: launch_moments<8>(s, g, rows, nblk, w1, partial, st); break;
     case 16: launch_moments<16>(s, g, rows, nblk, w1, partial, st); break;
@@ -512,6 +513,7 @@ extern "C" int clskd_abf_conv1_fuse(const float* s, int32_t B, int32_t F, int32_
   const int rows = B * F * T;
   const TapRows g = tap_rows(F, T, sB, sF, sT, cin);
   const hipStream_t st = as_stream(stream);
+  if (skip_kernel(SKIP_ABF)) return CLSKD_OK;
 #define CLSKD_ABF_FUSE(CC)                                                                        \
   if (dtype == CLSKD_BF16)                                                                        \
     launch_fuse<CC, __bf16>(s, g, rows, w1, scale, shift, res, Fr, Tr, w, b, out, \

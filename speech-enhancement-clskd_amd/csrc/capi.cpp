@@ -40,9 +40,11 @@ static const KnobDef kKnobs[KNOB_COUNT] = {
     {"CLSKD_WGRAD_WG", 4096}, {"CLSKD_NO_HALO", 0},      {"CLSKD_BF16_WAVES", 8},
     {"CLSKD_BF16_STAGES", 3}, {"CLSKD_BF16_TILE", 0},    {"CLSKD_NO_POINTWISE", 0},
     {"CLSKD_ABF_MOMENT_DIV", 1}, {"CLSKD_F32_WAVES", 4}, {"CLSKD_EXEC_PRIO", 0}, {"CLSKD_EXEC_GATE", 0},
-    {"CLSKD_EXEC_PACE_NS", 0},
+    {"CLSKD_EXEC_PACE_NS", 0}, {"CLSKD_NO_HALO32", 0},
+    {"CLSKD_HALO32_SPLIT", 0},
     {"CLSKD_LSTM128_TDIV", 0},
-    {"CLSKD_LSTM32_TDIV", 0}, {"CLSKD_BF16_DEBUG_MODE", 0},
+    {"CLSKD_LSTM32_TDIV", 0}, {"CLSKD_BF16_DEBUG_MODE", 0}, {"CLSKD_SKIP", 0},
+    {"CLSKD_H32_DEBUG_MODE", 0},
 };
 static std::atomic<int> g_knob[KNOB_COUNT];
 static std::once_flag g_knob_once;
@@ -64,6 +66,15 @@ static int knob_index(const char* name) {
   for (int i = 0; i < KNOB_COUNT; ++i)
     if (strcmp(name, kKnobs[i].name) == 0) return i;
   return -1;
+}
+
+bool skip_kernel(int bit) {
+#ifdef CLSKD_EXPERIMENTS
+  return (knob(KNOB_SKIP) & bit) != 0;
+#else
+  (void)bit;
+  return false;
+#endif
 }
 
 int experiment_guard(const char* what, int value) {

@@ -21,14 +21,22 @@ enum KnobId {
   KNOB_G8, KNOB_G8_GRID, KNOB_HALO_GRID, KNOB_DIRECT_COOP, KNOB_LSTM_NKS, KNOB_LSTM_NKS32,
   KNOB_WGRAD_WG, KNOB_NO_HALO, KNOB_BF16_WAVES, KNOB_BF16_STAGES, KNOB_BF16_TILE,
   KNOB_NO_POINTWISE, KNOB_ABF_MOMENT_DIV, KNOB_F32_WAVES, KNOB_EXEC_PRIO, KNOB_EXEC_GATE, KNOB_EXEC_PACE_NS,
+  KNOB_NO_HALO32, KNOB_HALO32_SPLIT,
   // timing-only experiment modes (wrong results): -DCLSKD_EXPERIMENTS builds only
-  KNOB_LSTM128_TDIV, KNOB_LSTM32_TDIV, KNOB_BF16_DEBUG_MODE,
+  KNOB_LSTM128_TDIV, KNOB_LSTM32_TDIV, KNOB_BF16_DEBUG_MODE, KNOB_SKIP, KNOB_H32_DEBUG_MODE,
   KNOB_COUNT
 };
 int knob(KnobId k);
 // CLSKD_OK, or CLSKD_E_ARG (with the error message set) when `value` selects a timing-only mode
 // in a product build.
 int experiment_guard(const char* what, int value);
+// Timing-only "what if this kernel family were free" switch (CLSKD_SKIP bit mask, experiments
+// build only; always false in the product library): the entry point returns without launching.
+enum SkipBit {
+  SKIP_BN_FINALIZE = 1, SKIP_BN_APPLY = 2, SKIP_CONV_F32 = 4, SKIP_LSTM = 8, SKIP_ABF = 16,
+  SKIP_GRAM = 32, SKIP_CONV_LOWP = 64, SKIP_CONV_DIRECT = 128
+};
+bool skip_kernel(int bit);
 template <typename T> inline const char* type_name();
 template <> inline const char* type_name<float>() { return "float"; }
 template <> inline const char* type_name<__bf16>() { return "bf16"; }

@@ -120,7 +120,10 @@ __global__ __launch_bounds__(128) void conv_direct_kernel(const DirectArgs args)
 
   // branch-free run load: out-of-bounds taps (and rows past M) read a safe address and are
   // zeroed after the load, so the U loads of an iteration issue back to back
-  const InT* safe = reinterpret_cast<const InT*>(d.seg[0].ptr);
+  // global address space: a generic pointer would make these FLAT loads, which count on lgkmcnt
+  // too — every wait for a scalar weight load would then drain the whole run of input loads
+  using GIn = const __attribute__((address_space(1))) InT;
+  GIn* safe = reinterpret_cast<GIn*>((uintptr_t)d.seg[0].ptr);
   auto load = [&](int j, bool run_ok, XRun<G, InT>& x) {
     const int4 e = kl[j];
     const int dF = (int)(int16_t)(e.y & 0xffff), dT = e.y >> 16;
@@ -129,8 +132,8 @@ __global__ __launch_bounds__(128) void conv_direct_kernel(const DirectArgs args)
     const bool ok = run_ok && valid && fi >= 0 && fi < Fb && ti >= 0 && ti < Tb;
     const int sg = __builtin_amdgcn_readfirstlane(e.z);  // uniform segment of this run
     const int64_t base = rb0 + (sg == 1 ? dl1 : 0) + (sg == 2 ? dl2 : 0) + (sg == 3 ? dl3 : 0);
-    const InT* p = ok ? reinterpret_cast<const InT*>(base) + e.x : safe;
-    x.v = *reinterpret_cast<const decltype(x.v)*>(p);
+    GIn* p = ok ? reinterpret_cast<GIn*>(base) + e.x : safe;
+    x.v = *reinterpret_cast<const __attribute__((address_space(1))) decltype(x.v)*>(p);
     if constexpr (G == 8) {
       typedef uint32_t u4 __attribute__((ext_vector_type(4)));
       u4 w = __builtin_bit_cast(u4, x.v);
@@ -299,7 +302,10 @@ __global__ __launch_bounds__(128) void conv_direct_coop_kernel(const DirectArgs 
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
   const int64_t FoTo = (int64_t)d.Fo * d.To;
-  const InT* safe = reinterpret_cast<const InT*>(d.seg[0].ptr);
+  // global address space: a generic pointer would make these FLAT loads, which count on lgkmcnt
+  // too — every wait for a scalar weight load would then drain the whole run of input loads
+  using GIn = const __attribute__((address_space(1))) InT;
+  GIn* safe = reinterpret_cast<GIn*>((uintptr_t)d.seg[0].ptr);
   OutT* outp = reinterpret_cast<OutT*>(d.out);
   for (int it = 0; it < LPR; ++it) {
     const int64_t m = (int64_t)tile * 128 + it * NG + g;
@@ -330,8 +336,8 @@ __global__ __launch_bounds__(128) void conv_direct_coop_kernel(const DirectArgs 
       const int fi = fi0 + dF, ti = ti0 + dT;
       const bool ok = run_ok && valid && fi >= 0 && fi < Fb && ti >= 0 && ti < Tb;
       const int64_t base = rb0 + (e.z == 1 ? dl1 : 0) + (e.z == 2 ? dl2 : 0) + (e.z == 3 ? dl3 : 0);
-      const InT* p = ok ? reinterpret_cast<const InT*>(base) + e.x : safe;
-      x[r].v = *reinterpret_cast<const decltype(x[r].v)*>(p);
+      GIn* p = ok ? reinterpret_cast<GIn*>(base) + e.x : safe;
+      x[r].v = *reinterpret_cast<const __attribute__((address_space(1))) decltype(x[r].v)*>(p);
       if constexpr (G == 8) {
         typedef uint32_t u4 __attribute__((ext_vector_type(4)));
         u4 wv = __builtin_bit_cast(u4, x[r].v);

@@ -167,7 +167,10 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const HaloArgs a) {
   const int dfmin = sconst(a.dfmin), dtmin = sconst(a.dtmin);
   const int64_t oB = vconst64(d.oB), oF = vconst64(d.oF), oT = vconst64(d.oT);
   const int of_mul = sconst(d.of_mul), of_add = sconst(d.of_add);
-  OutT* const outp = reinterpret_cast<OutT*>(vconst64((int64_t)(uintptr_t)d.out));
+  // global address space: a laundered generic pointer would make the epilogue stores FLAT,
+  // which count on lgkmcnt too — every fragment wait in the loop degrades to lgkmcnt(0)
+  using GOut = __attribute__((address_space(1))) OutT;
+  GOut* const outp = reinterpret_cast<GOut*>(vconst64((int64_t)(uintptr_t)d.out));
   // per-lane DMA slot geometry, packed: hf | ht << 8 | src chunk << 16 | valid << 20
   int dmg[MAXG];
   {
@@ -314,7 +317,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const HaloArgs a) {
     const int fo = cur.fb * FT + wave;
     const int to0 = cur.tb * TT;
     const int64_t rowb = (int64_t)cur.b * oB + (int64_t)(fo * of_mul + of_add) * oF;
-    OutT* sink = reinterpret_cast<OutT*>(g_halo_sink) + lane;
+    GOut* sink = reinterpret_cast<GOut*>((uintptr_t)g_halo_sink) + lane;
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       const bool nok = coff[nb] >= 0;
@@ -331,7 +334,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const HaloArgs a) {
           sm += v;
           sq = fmaf(v, v, sq);
         }
-        OutT* dst = ok ? outp + rowb + (int64_t)to * oT + coff[nb] : sink;
+        GOut* dst = ok ? outp + rowb + (int64_t)to * oT + coff[nb] : sink;
         if constexpr (DBG != 3) *dst = (OutT)v;
       }
       st_s[nb] += (double)sm;

@@ -316,6 +316,7 @@ int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st);
 int launch_conv_direct(const clskd_conv_desc& d, hipStream_t st);
 
 int launch_conv_pointwise(const clskd_conv_desc& d, hipStream_t st, bool* launched);
+int launch_conv_halo_f32(const clskd_conv_desc& d, hipStream_t st, bool* launched);
 
 }  // namespace clskd
 
@@ -366,23 +367,35 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
                                      d.out_dtype == CLSKD_F32),
                   "conv2d: accumulate needs the fp32 engine (wlayout NK, fp32 compute and out)");
   if (d.wlayout == CLSKD_WLAYOUT_DIRECT) {
+    if (skip_kernel(SKIP_CONV_DIRECT)) return CLSKD_OK;
     const int rc = launch_conv_direct(d, st);
     if (rc != CLSKD_OK) return rc;
     CLSKD_LAUNCH_CHECK("conv2d_direct");
     return CLSKD_OK;
   }
   if (lowp) {
+    if (skip_kernel(SKIP_CONV_LOWP)) return CLSKD_OK;
     const int rc = launch_conv_bf16(d, st);
     if (rc != CLSKD_OK) return rc;
     CLSKD_LAUNCH_CHECK("conv2d_bf16");
     return CLSKD_OK;
   }
+  if (skip_kernel(SKIP_CONV_F32)) return CLSKD_OK;
   {  // 1x1 channel lifts with short K: the streaming pointwise kernel (conv_pointwise.hip)
     bool launched = false;
     const int rc = launch_conv_pointwise(d, st, &launched);
     if (rc != CLSKD_OK) return rc;
     if (launched) {
       CLSKD_LAUNCH_CHECK("conv2d_pointwise");
+      return CLSKD_OK;
+    }
+  }
+  if (knob(KNOB_NO_HALO32) != 1) {  // narrow tap-structured layers: halo-tiled fp32 kernel
+    bool launched = false;
+    const int rc = launch_conv_halo_f32(d, st, &launched);
+    if (rc != CLSKD_OK) return rc;
+    if (launched) {
+      CLSKD_LAUNCH_CHECK("conv2d_halo_f32");
       return CLSKD_OK;
     }
   }

@@ -618,6 +618,7 @@ extern "C" int clskd_gram_partial(const clskd_gram_job* jobs, int32_t njobs, int
   const int rc = validate_gram_jobs(jobs, njobs, B, &total);
   if (rc != CLSKD_OK) return rc;
   CLSKD_CHECK_ARG(slabs, "gram_partial: null slab buffer");
+  if (skip_kernel(SKIP_GRAM)) return CLSKD_OK;
   hipStream_t st = as_stream(stream);
   for (int k0 = 0; k0 < njobs; k0 += CLSKD_GRAM_MAX_JOBS) {
     GramJobsArg a;

@@ -446,6 +446,7 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
   CLSKD_CHECK_ARG(gx && whh && out, "lstm: null pointer");
   CLSKD_CHECK_SHAPE(nws >= 1 && nseq >= 1 && T >= 1, "lstm: empty shape");
   CLSKD_CHECK_ARG(((uintptr_t)whh & 15) == 0, "lstm: whh must be 16-byte aligned");
+  if (skip_kernel(SKIP_LSTM)) return CLSKD_OK;
   dim3 grid(nseq, nws);
   hipStream_t st = as_stream(stream);
   // k-slices per unit (measured on MI355X, tools/lstm_micro.py): H = 128 -> 4 (662 ns/step vs

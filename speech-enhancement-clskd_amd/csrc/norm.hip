@@ -515,6 +515,7 @@ extern "C" int clskd_bn_finalize(const double* partial, int32_t nblk, int64_t ro
   CLSKD_CHECK_ARG(partial && scale && shift, "bn_finalize: null pointer");
   CLSKD_CHECK_SHAPE(C > 0 && nblk > 0 && rows > 0, "bn_finalize: shape");
   CLSKD_CHECK_ARG(((uintptr_t)partial & 15) == 0, "bn_finalize: partials must be 16-byte aligned");
+  if (skip_kernel(SKIP_BN_FINALIZE)) return CLSKD_OK;
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(BNF_T), 0, as_stream(stream), partial, nblk,
                      rows, C, gamma, beta, eps, running_mean, running_var, momentum, n_updates,
                      scale, shift, mean_out, var_out);
@@ -540,6 +541,7 @@ static int bn_apply_impl(const void* x, void* y, int64_t rows, int32_t C, const 
   CLSKD_CHECK_SHAPE(C % 8 == 0 && rows > 0, "bn_apply: C=%d must be a multiple of 8", C);
   CLSKD_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0, "bn_apply: alignment");
   CLSKD_CHECK_ARG(dtype == CLSKD_F32 || dtype == CLSKD_BF16 || dtype == CLSKD_F16, "bn_apply: dtype");
+  if (skip_kernel(SKIP_BN_APPLY)) return CLSKD_OK;
   const int64_t items = rows * C / 8;
   const int CG = C / 8;
   // grid a multiple of CG-friendly size: 256 threads/block, stride = 256*grid

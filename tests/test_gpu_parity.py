@@ -279,6 +279,84 @@ def test_conv_halo_kernel_against_torch(case, lp):
     np.testing.assert_allclose(stc[:, :, 1].sum(0).numpy(), (ref ** 2).sum((0, 1, 2)).numpy(), rtol=1e-5)
 
 
+HALO32_CASES = {
+    # name: (segment channels, N, taps, stride_f, Fi, Fo, of_mul, of_add) — the student's layers
+    # (B = 3, T = 101: >= 32 tiles of 8 F-rows x 32 steps, the kernel's eligibility floor)
+    "enc_c16_n32": ((16,), 32, [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)], 2, 38, 19, 1, 0),
+    "enc_c32_n64": ((32,), 64, [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)], 2, 48, 24, 1, 0),
+    # [64][640] weights exceed LDS beside the halo buffers: two 32-column launches
+    "enc_c64_n64_split": ((64,), 64, [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)], 2, 40, 20, 1, 0),
+    "enc_c24_n48": ((8, 16), 48, [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)], 2, 37, 19, 1, 0),
+    "dec_parity0_n64_split": ((64, 64), 64, [(dF, -kt) for dF in (1, 0, -1) for kt in (0, 1)], 1,
+                              20, 20, 2, 0),
+    "dec_parity1_n32": ((32, 32), 32, [(dF, -kt) for dF in (1, 0) for kt in (0, 1)], 1, 20, 20, 2, 1),
+    "abf3x3_n64_split": ((64,), 64, [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], 1, 17, 17,
+                         1, 0),
+}
+
+
+@pytest.mark.parametrize("case", sorted(HALO32_CASES))
+def test_conv_halo_f32_against_torch(case):
+    """Halo-tiled exact-fp32 conv (csrc/conv_halo32.hip: weights resident in LDS in k-quad order,
+    8-channel input halo chunks reused across taps, v_mfma_f32_32x32x2_f32): the student's layer
+    shapes (stride-2 encoder, two-segment polyphase decoder with interleaved output rows, 3x3),
+    N = 32 / 48 / 64, column-split launches (CLSKD_HALO32_SPLIT=1: the dispatcher leaves those to
+    the engine by default), ragged F and T tiles, fused BN statistics; vs torch fp64 and vs the
+    fp32 engine on the same descriptor.  Tolerance 1e-5 relative (fp32 accumulation orders
+    differ); stats 1e-5."""
+    from clskd import _lib, ops
+    segc, N, taps, sf, Fi, Fo, of_mul, of_add = HALO32_CASES[case]
+    g = torch.Generator().manual_seed(len(case) * 11 + N)
+    B, T = 3, 101
+    segs_h = [torch.randn(B, Fi, T, c, generator=g) for c in segc]
+    Cin = sum(segc)
+    K = len(taps) * Cin
+    w = torch.randn(N, len(taps), Cin, generator=g) * 0.05
+    bias = torch.randn(N, generator=g)
+    wp = ops.pack_weight(w.to(DEV), K)
+    assert not ops.direct_ok(N, wp.shape[1])
+    wq = w.double()
+    x = torch.cat([s.double() for s in segs_h], 3)  # [B, Fi, T, Cin]
+    ref = bias.double().view(1, 1, 1, N).expand(B, Fo, T, N).clone()
+    for ti, (dF, dT) in enumerate(taps):
+        fi = torch.arange(Fo) * sf + dF
+        tt = torch.arange(T) + dT
+        vf = (fi >= 0) & (fi < Fi)
+        vt = (tt >= 0) & (tt < T)
+        sub = torch.zeros(B, Fo, T, Cin, dtype=torch.float64)
+        sub[:, vf.nonzero()[:, 0][:, None], vt.nonzero()[:, 0][None, :]] = \
+            x[:, fi[vf][:, None], tt[vt][None, :]]
+        ref += torch.einsum("bftc,nc->bftn", sub, wq[:, ti])
+    Fout = Fo * of_mul
+    res = {}
+    for route in ("halo", "engine"):
+        prev = _lib.set_knob("CLSKD_NO_HALO32", int(route == "engine"))
+        prev_split = _lib.set_knob("CLSKD_HALO32_SPLIT", 1)
+        try:
+            out = torch.zeros(B, Fout, T, N, device=DEV)
+            nblk = ops.conv_mblocks(B, Fo, T)
+            st = torch.full((nblk * N * 2,), float("nan"), device=DEV, dtype=torch.float64)
+            ops.conv([ops.seg_bftc(s.to(DEV)) for s in segs_h], taps, B, Fo, T, N, wp, bias.to(DEV),
+                     out, ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add),
+                     stride_f=sf, stats=st)
+            kname = ops.conv_kernel_of_last_launch()
+        finally:
+            _lib.set_knob("CLSKD_NO_HALO32", prev)
+            _lib.set_knob("CLSKD_HALO32_SPLIT", prev_split)
+        assert kname.startswith("conv_halo_f32_kernel") == (route == "halo"), (route, kname)
+        res[route] = out.double().cpu()
+        o = res[route][:, of_add::of_mul]
+        np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=1e-5, atol=1e-5, err_msg=route)
+        if of_mul > 1:  # the other parity's rows are untouched
+            assert torch.all(res[route][:, (of_add + 1) % of_mul::of_mul] == 0)
+        stc = st.view(nblk, N, 2).cpu()
+        assert torch.isfinite(stc).all(), "every statistics slot must be written"
+        np.testing.assert_allclose(stc[:, :, 0].sum(0).numpy(), ref.sum((0, 1, 2)).numpy(), rtol=1e-5,
+                                   atol=1e-3)
+        np.testing.assert_allclose(stc[:, :, 1].sum(0).numpy(), (ref ** 2).sum((0, 1, 2)).numpy(), rtol=1e-5)
+    np.testing.assert_allclose(res["halo"].numpy(), res["engine"].numpy(), rtol=1e-5, atol=1e-5)
+
+
 def _abf_torch(x, y, shape, abf):
     """framework.py:204-222 in torch fp64 (train-mode BatchNorm): returns (out, x_fused, mean1,
     var1) from NCHW inputs."""
