@@ -105,13 +105,8 @@ struct ConvArgsG8 {
 // 3 = neither, 4 = B operand only (no A gather), 5 = A operand only.  Correct-result variants:
 // 6 = s_setprio 1 around each substep's MFMA cluster, 7 = static priority 1 for waves 4-7, 8 = both;
 // 9 = no DMA wait inside the stream (timing only: DMA latency vs issue cost).
-// IL = 1: each substep's fragment reads go out first, then its MFMAs run one at a time with the
-// K-tile's LDS-DMA pieces (and their address arithmetic) placed BETWEEN them, evenly (GP pieces
-// over FM*FN MFMAs), pinned by scheduling barriers.  IL = 0 issues a substep's MFMAs as one
-// burst and its pieces as a second burst: the two waves of a SIMD, in step after every K-tile
-// barrier, then both leave the MFMA pipe idle while they issue pieces.
 template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8,
-          int EB = 0, typename InT = __bf16, int IL = 0>
+          int EB = 0, typename InT = __bf16>
 __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 args) {
   using namespace g8;
   const clskd_conv_desc& d = args.d;
@@ -382,45 +377,13 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
       // registers), so the next K-tile's head reads return under those MFMAs instead of after
       // the barrier with the MFMA pipe idle
       static_assert(!EB || (NSUB - 1) % NSET >= PF, "EB: the last substep's set must not be a head set");
-      if constexpr (IL) {
-        static_assert(DBG == 0, "interleaved issue: product variant only");
-        constexpr int NMF = FM * FN;
 #pragma unroll
-        for (int s = 0; s < NSUB; ++s) {
-          if (EB && s == NSUB - 1) k_boundary();
-          if (s + PF < NSUB) read_frags(sa, s + PF, fa[(s + PF) % NSET], fb[(s + PF) % NSET]);
-          __builtin_amdgcn_sched_barrier(0);
-          const bf16x8s(&ca)[FM] = fa[s % NSET];
-          const bf16x8s(&cb)[FN] = fb[s % NSET];
-          int done = 0;  // pieces of this substep issued so far (compile-time after unrolling)
-#pragma unroll
-          for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int jj = 0; jj < FN; ++jj) {
-              acc[i][jj] = mfma16<InT>(ca[i], cb[jj], acc[i][jj]);
-              __builtin_amdgcn_sched_barrier(0);
-              // after MFMA q: floor(q * GP / NMF) + 1 pieces (the first right behind MFMA 0)
-              const int want = min(GP, (i * FN + jj) * GP / NMF + 1);
-              if (s < PHI && do_issue) {
-#pragma unroll
-                for (int p = done; p < want; ++p) {
-                  const int g = s * GP + p;
-                  if (g < G) glds16((const void*)piece_src(g, kti, e), dst(g, sn));
-                }
-              }
-              done = want;
-              __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-      } else {
-#pragma unroll
-        for (int s = 0; s < NSUB; ++s) {
-          if (EB && s == NSUB - 1) k_boundary();
-          if (s + PF < NSUB) read_frags(sa, s + PF, fa[(s + PF) % NSET], fb[(s + PF) % NSET]);
-          mfmas(fa[s % NSET], fb[s % NSET]);
-          issue(s);  // behind the MFMAs: the K-entry read / address ALU overlap them
-          __builtin_amdgcn_sched_barrier(0);
-        }
+      for (int s = 0; s < NSUB; ++s) {
+        if (EB && s == NSUB - 1) k_boundary();
+        if (s + PF < NSUB) read_frags(sa, s + PF, fa[(s + PF) % NSET], fb[(s + PF) % NSET]);
+        mfmas(fa[s % NSET], fb[s % NSET]);
+        issue(s);  // behind the MFMAs: the K-entry read / address ALU overlap them
+        __builtin_amdgcn_sched_barrier(0);
       }
       if (!EB) k_boundary();
     }
@@ -547,7 +510,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
 }
 
 template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8,
-          int EB = 0, typename InT = __bf16, int IL = 0>
+          int EB = 0, typename InT = __bf16>
 static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   using namespace g8;
   constexpr int SB = (BM + BN) * 2 * BK;
@@ -557,7 +520,7 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
     set_error("conv2d(bf16 g8): K=%d N=%d needs %zu B of LDS", d.K, d.N, lds);
     return CLSKD_E_SHAPE;
   }
-  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG, PF, NWV, EB, InT, IL>;
+  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG, PF, NWV, EB, InT>;
   static bool attr_set = false;  // per instantiation
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -581,29 +544,12 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NWV * 64), lds, st, a);
   note_kernel_fn((const void*)kern);
   if constexpr (__is_same(InT, _Float16))
-    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d,f16%s>", BM, BN, WM, BK, NS, PHI,
-                type_name<OutT>(), DBG, PF, NWV, EB, IL ? ",il" : "");
+    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d,f16>", BM, BN, WM, BK, NS, PHI,
+                type_name<OutT>(), DBG, PF, NWV, EB);
   else
-    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d%s>", BM, BN, WM, BK, NS, PHI,
-                type_name<OutT>(), DBG, PF, NWV, EB, IL ? ",il" : "");
+    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d>", BM, BN, WM, BK, NS, PHI,
+                type_name<OutT>(), DBG, PF, NWV, EB);
   return CLSKD_OK;
-}
-
-template <int IL>
-static int launch_g8_default(const clskd_conv_desc& d, hipStream_t st, bool f32) {
-  if (d.in_dtype == CLSKD_F16) {  // C4: IEEE-half operands (v_mfma_f32_32x32x16_f16)
-    if (d.N <= 128)
-      return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float, 0, 1, 8, 1, _Float16, IL>(d, st)
-                 : launch_g8<256, 128, 4, 64, 2, 2, _Float16, 0, 1, 8, 1, _Float16, IL>(d, st);
-    return f32 ? launch_g8<256, 256, 2, 64, 2, 2, float, 0, 1, 8, 1, _Float16, IL>(d, st)
-               : launch_g8<256, 256, 2, 64, 2, 2, _Float16, 0, 1, 8, 1, _Float16, IL>(d, st);
-  }
-  if (d.N <= 128) {
-    return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float, 0, 1, 8, 1, __bf16, IL>(d, st)
-               : launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 1, 8, 1, __bf16, IL>(d, st);
-  }
-  return f32 ? launch_g8<256, 256, 2, 64, 2, 2, float, 0, 1, 8, 1, __bf16, IL>(d, st)
-             : launch_g8<256, 256, 2, 64, 2, 2, __bf16, 0, 1, 8, 1, __bf16, IL>(d, st);
 }
 
 // Entry from launch_conv_bf16 for N > 64 bf16 layers.  *launched = false leaves the layer to the
@@ -672,9 +618,19 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
 #endif
   // default: BK 64, two stages, the K-tile boundary before the last substep (EB; 3-5 % on the
   // N = 256 layers against the boundary after it, CLSKD_G8=10)
-  // mode 2: the K-tile's LDS-DMA pieces interleaved between the MFMAs (IL = 1)
-  if (mode == 2) return launch_g8_default<1>(d, st, f32);
-  return launch_g8_default<0>(d, st, f32);
+  if (d.in_dtype == CLSKD_F16) {  // C4: IEEE-half operands (v_mfma_f32_32x32x16_f16)
+    if (d.N <= 128)
+      return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float, 0, 1, 8, 1, _Float16>(d, st)
+                 : launch_g8<256, 128, 4, 64, 2, 2, _Float16, 0, 1, 8, 1, _Float16>(d, st);
+    return f32 ? launch_g8<256, 256, 2, 64, 2, 2, float, 0, 1, 8, 1, _Float16>(d, st)
+               : launch_g8<256, 256, 2, 64, 2, 2, _Float16, 0, 1, 8, 1, _Float16>(d, st);
+  }
+  if (d.N <= 128) {
+    return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float, 0, 1, 8, 1>(d, st)
+               : launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 1, 8, 1>(d, st);
+  }
+  return f32 ? launch_g8<256, 256, 2, 64, 2, 2, float, 0, 1, 8, 1>(d, st)
+             : launch_g8<256, 256, 2, 64, 2, 2, __bf16, 0, 1, 8, 1>(d, st);
 }
 
 }  // namespace clskd

@@ -963,7 +963,7 @@ def test_conv_gemm8_against_torch(case, lp):
     ops.conv([ops.seg_bftc(s.to(DEV)) for s in segs_h], taps, B, Fo, T, N, wp, bias.to(DEV), out,
              ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add), stride_f=sf, stats=st)
     kname = ops.conv_kernel_of_last_launch()
-    assert kname.startswith("conv_gemm8") and ((",f16>" in kname.replace(",il>", ">")) == (lp == "fp16")), kname
+    assert kname.startswith("conv_gemm8") and (kname.endswith(",f16>") == (lp == "fp16")), kname
     o = out.double().cpu()[:, of_add::of_mul]
     tol = _LP_TOL[lp] if out_bf16 else 1e-4
     np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=tol, atol=tol)

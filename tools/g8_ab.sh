@@ -12,5 +12,5 @@ done
 for m in ${MODES:-1 2}; do
   CLSKD_G8=$m timeout -k 10 200 python $R/bench.py --no-cpu-baseline --steps 20 > $O/b$m.log 2>&1
 done
-timeout -k 10 200 python $R/tools/aten_census.py 2 > $O/aten.txt 2>&1
+
 echo ok
