@@ -560,8 +560,10 @@ def main():
         if os.path.exists(tpath) and not args.spkd:  # the PMC passes profile the C2 leg
             kern = json.load(open(tpath))["kernels"]
             tk = kern.get(name)
-            if tk is None:  # rocprof names carry the operand type as one more template argument
-                more = [k for k in kern if k.startswith(name[:-1] + ",") and k.count(",") == name.count(",") + 1]
+            if tk is None:  # rocprof names carry the template arguments the census name omits
+                more = [k for k in kern if k.startswith(name[:-1] + ",")]
+                best = [k for k in more if k.count(",") == name.count(",") + 1]
+                more = best if best else more
                 tk = kern[more[0]] if len(more) == 1 else None
             if tk is not None:
                 traffic = round(tk["hbm_bytes_per_launch"])
