@@ -41,7 +41,7 @@ static const KnobDef kKnobs[KNOB_COUNT] = {
     {"CLSKD_BF16_STAGES", 3}, {"CLSKD_BF16_TILE", 0},    {"CLSKD_NO_POINTWISE", 0},
     {"CLSKD_ABF_MOMENT_DIV", 1}, {"CLSKD_F32_WAVES", 4}, {"CLSKD_EXEC_PRIO", 0}, {"CLSKD_EXEC_GATE", 0},
     {"CLSKD_EXEC_PACE_NS", 0}, {"CLSKD_NO_HALO32", 0},
-    {"CLSKD_HALO32_SPLIT", 0},
+    {"CLSKD_HALO32_SPLIT", 0}, {"CLSKD_HALO32_MIN_N", 32}, {"CLSKD_G8_KORDER", 1},
     {"CLSKD_LSTM128_TDIV", 0},
     {"CLSKD_LSTM32_TDIV", 0}, {"CLSKD_BF16_DEBUG_MODE", 0}, {"CLSKD_SKIP", 0},
     {"CLSKD_H32_DEBUG_MODE", 0},

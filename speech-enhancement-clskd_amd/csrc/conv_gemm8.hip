@@ -97,6 +97,10 @@ struct RowTable {
 struct ConvArgsG8 {
   clskd_conv_desc d;
   int n_mt, ntiles;  // M-tiles per N-block, tiles in the list
+  // K-tile visiting order: kt_taps x kt_cpt K-tiles, visited channel-block-major (all taps of
+  // 64-channel block c, then block c + 1) when every K-tile lies inside one tap (kt_taps = the
+  // tap count, kt_cpt = K-tiles per tap); kt_taps = 1, kt_cpt = K / 64 is the packed order.
+  int kt_taps, kt_cpt;
 };
 
 // BM x BN tile, 8 waves as WM x WN, BK-deep K-tiles (64: 128-B LDS rows; 32: 64-B rows) in NS
@@ -308,9 +312,23 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
 
   // ---- stream of K-tiles over the tile list: K-tile w belongs to tile w / nk ---------------------
   const int total = ntl * nk;
+  // packed K-tile of the next issued stream K-tile: the stream visits each tile's K-tiles
+  // channel-block-major (tap q of block c = packed K-tile q * kt_cpt + c), so consecutive K-tiles
+  // gather rows shifted by one tap — the rows the CU (and its XCD) fetched one K-tile earlier
+  // are still in L2; the packed tap-major order came back to a row only after kt_cpt K-tiles.
+  const int kt_taps = args.kt_taps, kt_cpt = args.kt_cpt;
+  int it_tap = 0, it_cb = 0;
+  auto next_kt = [&]() {
+    const int k = it_tap * kt_cpt + it_cb;
+    if (++it_tap == kt_taps) {
+      it_tap = 0;
+      if (++it_cb == kt_cpt) it_cb = 0;
+    }
+    return k;
+  };
   // issue every piece of stream K-tile w into its stage (geometry moved to its tile first)
   auto issue_all = [&](int w) {
-    const int jt = w / nk, kt = w - jt * nk;
+    const int jt = w / nk, kt = next_kt();
     if (jt != geo_tile) load_geometry(jt);
     const KEnt e = kdecode(ctab[kt * CPR + csrc]);
 #pragma unroll
@@ -345,7 +363,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
       KEnt e{};
       if (do_issue) {
         const int jt = wi / nk;
-        kti = wi - jt * nk;
+        kti = next_kt();
         if (jt != geo_tile) load_geometry(jt);
         e = kdecode(ctab[kti * CPR + csrc]);
       }
@@ -540,7 +558,12 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   const int cap = knob(KNOB_G8_GRID) > 0 ? knob(KNOB_G8_GRID) : ncu;
   const int ncap = cap > 0 && cap < ncu ? cap : ncu;
   const int grid = ntiles <= ncap ? (int)ntiles : (ncap >= 8 ? (ncap & ~7) : ncap);
-  ConvArgsG8 a{d, (int)n_mt, (int)ntiles};
+  ConvArgsG8 a{d, (int)n_mt, (int)ntiles, 1, d.K / BK};
+  // channel-block-major K order when every K-tile lies inside one tap (CLSKD_G8_KORDER=0: packed)
+  if (knob(KNOB_G8_KORDER) != 0 && d.ntaps > 1 && d.ctot % BK == 0 && (int64_t)d.ntaps * d.ctot == d.K) {
+    a.kt_taps = d.ntaps;
+    a.kt_cpt = d.ctot / BK;
+  }
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NWV * 64), lds, st, a);
   note_kernel_fn((const void*)kern);
   if constexpr (__is_same(InT, _Float16))

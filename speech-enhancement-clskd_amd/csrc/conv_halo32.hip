@@ -539,7 +539,10 @@ int launch_conv_halo_f32(const clskd_conv_desc& d, hipStream_t st, bool* launche
   Halo32Args a;
   size_t lds = 0;
   *launched = false;
-  if (d.N < 32) return CLSKD_OK;  // 16-wide layers: a 32-column MFMA block would idle half
+  // 16-wide layers run with the 32-column block half idle (zero weight columns, masked stores);
+  // CLSKD_HALO32_MIN_N selects the narrowest N taken (A/B knob)
+  const int min_n = knob(KNOB_HALO32_MIN_N);
+  if (d.N < (min_n > 0 ? min_n : 32)) return CLSKD_OK;
   const bool split_ok = knob(KNOB_HALO32_SPLIT) == 1;
   if (!split_ok && d.Fo < h32::FT) return CLSKD_OK;
   if (halo32_plan(d, a, lds)) return launch_halo32_planned(a, lds, st, launched);

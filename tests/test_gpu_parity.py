@@ -290,6 +290,10 @@ HALO32_CASES = {
     "dec_parity0_n64_split": ((64, 64), 64, [(dF, -kt) for dF in (1, 0, -1) for kt in (0, 1)], 1,
                               20, 20, 2, 0),
     "dec_parity1_n32": ((32, 32), 32, [(dF, -kt) for dF in (1, 0) for kt in (0, 1)], 1, 20, 20, 2, 1),
+    # 8/16-wide decoder layers (CLSKD_HALO32_MIN_N=8: the 32-column block with zero columns)
+    "dec_parity0_n8": ((16, 16), 8, [(dF, -kt) for dF in (1, 0, -1) for kt in (0, 1)], 1, 20, 20, 2, 0),
+    "dec_parity0_n16": ((32, 32), 16, [(dF, -kt) for dF in (1, 0, -1) for kt in (0, 1)], 1, 20, 20, 2, 0),
+    "dec_parity1_n16": ((32, 32), 16, [(dF, -kt) for dF in (1, 0) for kt in (0, 1)], 1, 20, 20, 2, 1),
     "abf3x3_n64_split": ((64,), 64, [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], 1, 17, 17,
                          1, 0),
 }
@@ -332,6 +336,7 @@ def test_conv_halo_f32_against_torch(case):
     for route in ("halo", "engine"):
         prev = _lib.set_knob("CLSKD_NO_HALO32", int(route == "engine"))
         prev_split = _lib.set_knob("CLSKD_HALO32_SPLIT", 1)
+        prev_min = _lib.set_knob("CLSKD_HALO32_MIN_N", 8)
         try:
             out = torch.zeros(B, Fout, T, N, device=DEV)
             nblk = ops.conv_mblocks(B, Fo, T)
@@ -343,6 +348,7 @@ def test_conv_halo_f32_against_torch(case):
         finally:
             _lib.set_knob("CLSKD_NO_HALO32", prev)
             _lib.set_knob("CLSKD_HALO32_SPLIT", prev_split)
+            _lib.set_knob("CLSKD_HALO32_MIN_N", prev_min)
         assert kname.startswith("conv_halo_f32_kernel") == (route == "halo"), (route, kname)
         res[route] = out.double().cpu()
         o = res[route][:, of_add::of_mul]
