@@ -21,6 +21,9 @@ constexpr int BK = 16;
 
 struct ConvArgs {
   clskd_conv_desc d;
+  // K-tile visiting order (as conv_gemm8): kt_taps x kt_cpt K-tiles visited channel-block-major
+  // when every 16-deep K-tile lies inside one tap; kt_taps = 1, kt_cpt = K / 16: packed order
+  int kt_taps, kt_cpt;
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
@@ -213,10 +216,25 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_f32(const ConvArgs args) {
     for (int r = 0; r < 16; ++r) acc[t][r] = bv;
   }
 
+  // packed K-tile of the next load: all taps of a channel block before the next block, so the
+  // rows a K-tile gathers (one tap further) were fetched by the CU's previous K-tile
+  const int kt_taps = args.kt_taps, kt_cpt = args.kt_cpt;
+  int it_tap = 0, it_cb = 0;
+  auto next_kt = [&]() {
+    const int k = it_tap * kt_cpt + it_cb;
+    if (++it_tap == kt_taps) {
+      it_tap = 0;
+      if (++it_cb == kt_cpt) it_cb = 0;
+    }
+    return k;
+  };
   f32x4 ra[2];
   f32x4 rbv[NBL];
-  load_a(0, ra);
-  load_b(0, rbv);
+  {
+    const int k0 = next_kt();
+    load_a(k0, ra);
+    load_b(k0, rbv);
+  }
   store_tiles(0, ra, rbv);
   __syncthreads();
 
@@ -225,8 +243,9 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_f32(const ConvArgs args) {
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < nk) {
-      load_a(kt + 1, ra);
-      load_b(kt + 1, rbv);
+      const int kn = next_kt();
+      load_a(kn, ra);
+      load_b(kn, rbv);
     }
     const float* as = &As[buf][0];
     const f32x4 a0 = *reinterpret_cast<const f32x4*>(as + arow * BK + swz(arow, 2 * h) * 4);
@@ -399,7 +418,12 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
       return CLSKD_OK;
     }
   }
-  ConvArgs a{d};
+  ConvArgs a{d, 1, d.K / BK};
+  if (knob(KNOB_G8_KORDER) != 0 && d.vec4 && d.ntaps > 1 && d.ctot % BK == 0 &&
+      (int64_t)d.ntaps * d.ctot == d.K) {  // channel-block-major K order (CLSKD_G8_KORDER=0: packed)
+    a.kt_taps = d.ntaps;
+    a.kt_cpt = d.ctot / BK;
+  }
   const size_t ctab_bytes = (size_t)(d.K / 4) * 8;  // VEC4 K-chunk table (dynamic LDS)
   CLSKD_CHECK_SHAPE(!d.vec4 || ctab_bytes <= 32 * 1024, "conv2d(f32): K=%d too long for the chunk table", d.K);
   // 8-wave 256-row tiles (A/B knob CLSKD_F32_WAVES=4|8): half the B staging per FLOP and two
