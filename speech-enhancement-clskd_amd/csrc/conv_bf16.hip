@@ -74,6 +74,8 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 
 struct ConvArgsV2 {
   clskd_conv_desc d;
+  // K-tile visiting order (as conv_gemm8): channel-block-major when every K-tile lies in one tap
+  int kt_taps, kt_cpt;
 };
 
 // Counted wait leaving `ahead` younger K-tiles of this wave's DMAs in flight (NG pieces per
@@ -246,10 +248,22 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
+  // packed K-tile of the next issued K-tile: all taps of a channel block before the next block
+  // (the rows a K-tile gathers are one tap from the previous K-tile's: still in L2)
+  const int kt_taps = args.kt_taps, kt_cpt = args.kt_cpt;
+  int it_tap = 0, it_cb = 0;
+  auto next_kt = [&]() {
+    const int k = it_tap * kt_cpt + it_cb;
+    if (++it_tap == kt_taps) {
+      it_tap = 0;
+      if (++it_cb == kt_cpt) it_cb = 0;
+    }
+    return k;
+  };
   // prologue: NS-1 K-tiles in flight
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t)
-    if (t < nk) issue(t, t);
+    if (t < nk) issue(next_kt(), t);
 
   for (int kt = 0; kt < nk; ++kt) {
     // wait for this wave's DMAs of tile kt; the (up to NS-2) younger tiles stay in flight
@@ -259,7 +273,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (kt + NS - 1 < nk) issue(kt + NS - 1, (kt + NS - 1) % NS);
+    if (kt + NS - 1 < nk) issue(next_kt(), (kt + NS - 1) % NS);
     const unsigned char* sa = stages + (kt % NS) * SB;
     const unsigned char* sb = sa + BM * ROWB;
 #pragma unroll
@@ -403,7 +417,11 @@ static int launch_v2(const clskd_conv_desc& d, hipStream_t st) {
     attr_set = true;
   }
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
-  ConvArgsV2 a{d};
+  ConvArgsV2 a{d, 1, d.K / BK};
+  if (knob(KNOB_G8_KORDER) != 0 && d.ntaps > 1 && d.ctot % BK == 0 && (int64_t)d.ntaps * d.ctot == d.K) {
+    a.kt_taps = d.ntaps;
+    a.kt_cpt = d.ctot / BK;
+  }
   hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(M, BM), (unsigned)cdiv(d.N, BN)), dim3(NW * 64), lds, st, a);
   note_kernel_fn((const void*)kern);
   note_kernel("conv_igemm_bf16_dma<%d,%d,%d,%d,%d,%s,%d>", BM, BK, BN, NW, S, type_name<OutT>(), DBG);
