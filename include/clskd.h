@@ -204,6 +204,11 @@ int clskd_lstm_cell(const float* gx, int64_t gx_ws, int64_t gx_seq, const float*
 /* real = a - b, imag = c + d  (tools_for_model.py:168-169); all [n] contiguous */
 int clskd_complex_combine(const float* rr, const float* ii, const float* ir, const float* ri,
                           float* real_out, float* imag_out, int64_t n, void* stream);
+/* The same with real_out / imag_out stored as out_dtype (CLSKD_F32 | CLSKD_BF16 | CLSKD_F16,
+ * round-to-nearest-even): the frozen teacher's LSTM outputs as the 16-bit operands of its next
+ * GEMMs (precision 'mixed' / 'fp16'). */
+int clskd_complex_combine_dt(const float* rr, const float* ii, const float* ir, const float* ri,
+                             void* real_out, void* imag_out, int64_t n, int32_t out_dtype, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * STFT helpers.

@@ -449,8 +449,13 @@ class DCCRN(nn.Module):
                                2 * B * T * H, T * H, H)
             if tape is not None:
                 tape.setdefault("lstm", []).append(dict(gx=gx, hs=hs, r_in=r_in))
-            ro = torch.empty(B, T, H, **f32)
-            io = torch.empty(B, T, H, **f32)
+            # a 16-bit model (the frozen teacher in precision 'mixed' / 'fp16') stores the layer
+            # output as the 16-bit operand of the next layer's input GEMM and the projection
+            # (one rounding, as every other teacher activation); fp32 models and taped
+            # (backward) forwards keep fp32
+            lo = act if (self.compute != "fp32" and tape is None) else f32
+            ro = torch.empty(B, T, H, **lo)
+            io = torch.empty(B, T, H, **lo)
             ops.complex_combine(hs[0, :B], hs[1, B:], hs[0, B:], hs[1, :B], ro, io)
             r_in = (ro, io)
             lstm_io.append((ro, io))

@@ -436,8 +436,14 @@ def lstm_cell(gx, gx_ws, gx_seq, whh, nws, nseq, H, h, c, s_ws, s_seq, out, o_ws
 
 
 def complex_combine(rr, ii, ir, ri, ro, io):
-    check(lib().clskd_complex_combine(ptr(rr), ptr(ii), ptr(ir), ptr(ri), ptr(ro), ptr(io),
-                                      ro.numel(), _stream()), "complex_combine")
+    """ro = rr - ii, io = ir + ri (fp32 inputs); ro / io may be fp32, bf16 or fp16 storage."""
+    if ro.dtype == torch.float32 and io.dtype == torch.float32:
+        check(lib().clskd_complex_combine(ptr(rr), ptr(ii), ptr(ir), ptr(ri), ptr(ro), ptr(io),
+                                          ro.numel(), _stream()), "complex_combine")
+        return
+    assert ro.dtype == io.dtype
+    check(lib().clskd_complex_combine_dt(ptr(rr), ptr(ii), ptr(ir), ptr(ri), ptr(ro), ptr(io),
+                                         ro.numel(), _dt(ro), _stream()), "complex_combine_dt")
 
 
 def frame_pad(x, pad, Lp, mode, out):

@@ -319,12 +319,13 @@ __global__ void ola_kernel(const float* __restrict__ frames, const float* __rest
 }
 
 // real = rr - ii ; imag = ir + ri   (tools_for_model.py:168-169)
+template <typename OutT>
 __global__ void complex_combine_kernel(const float* rr, const float* ii, const float* ir,
-                                       const float* ri, float* ro, float* io, int64_t n) {
+                                       const float* ri, OutT* ro, OutT* io, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    ro[i] = rr[i] - ii[i];
-    io[i] = ir[i] + ri[i];
+    ro[i] = (OutT)(rr[i] - ii[i]);
+    io[i] = (OutT)(ir[i] + ri[i]);
   }
 }
 
@@ -635,9 +636,29 @@ extern "C" int clskd_complex_combine(const float* rr, const float* ii, const flo
                                      const float* ri, float* real_out, float* imag_out,
                                      int64_t n, void* stream) {
   CLSKD_CHECK_ARG(rr && ii && ir && ri && real_out && imag_out, "complex_combine: null pointer");
-  hipLaunchKernelGGL(complex_combine_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), rr,
-                     ii, ir, ri, real_out, imag_out, n);
+  hipLaunchKernelGGL(complex_combine_kernel<float>, dim3(grid_for(n)), dim3(256), 0, as_stream(stream),
+                     rr, ii, ir, ri, real_out, imag_out, n);
   CLSKD_LAUNCH_CHECK("complex_combine");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_complex_combine_dt(const float* rr, const float* ii, const float* ir,
+                                        const float* ri, void* real_out, void* imag_out, int64_t n,
+                                        int32_t out_dtype, void* stream) {
+  CLSKD_CHECK_ARG(rr && ii && ir && ri && real_out && imag_out, "complex_combine_dt: null pointer");
+  CLSKD_CHECK_ARG(out_dtype == CLSKD_F32 || out_dtype == CLSKD_BF16 || out_dtype == CLSKD_F16,
+                  "complex_combine_dt: dtype");
+  const dim3 g(grid_for(n)), b(256);
+  if (out_dtype == CLSKD_BF16)
+    hipLaunchKernelGGL(complex_combine_kernel<__bf16>, g, b, 0, as_stream(stream), rr, ii, ir, ri,
+                       (__bf16*)real_out, (__bf16*)imag_out, n);
+  else if (out_dtype == CLSKD_F16)
+    hipLaunchKernelGGL(complex_combine_kernel<_Float16>, g, b, 0, as_stream(stream), rr, ii, ir, ri,
+                       (_Float16*)real_out, (_Float16*)imag_out, n);
+  else
+    hipLaunchKernelGGL(complex_combine_kernel<float>, g, b, 0, as_stream(stream), rr, ii, ir, ri,
+                       (float*)real_out, (float*)imag_out, n);
+  CLSKD_LAUNCH_CHECK("complex_combine_dt");
   return CLSKD_OK;
 }
 
