@@ -38,7 +38,8 @@ PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sp
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 B_PER_GPU = 16
 NBATCH = 4
-TRAFFIC_FILE = "r3_pmc_traffic.json"  # written by tools/pmc_traffic.py
+TRAFFIC_FILE = "r3_pmc_traffic.json"
+AUTO_STEPS = 6  # steps per round of the --launch auto trial  # written by tools/pmc_traffic.py
 L = 64000
 
 
@@ -338,8 +339,10 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU-oracle B=16 steps (median)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--abf-reinit", default="step", choices=["step", "once"])
-    ap.add_argument("--launch", default="eager", choices=["exec", "eager", "graph"],
-                    help="eager (default, C2): launch the four-stream schedule from Python every "
+    ap.add_argument("--launch", default="auto", choices=["auto", "exec", "eager", "graph"],
+                    help="auto (default, C2): time a few steps of eager and exec on this host and "
+                         "run the faster (the step turns host-bound under eager when the host is "
+                         "slow); eager: launch the four-stream schedule from Python every "
                          "step (host enqueue ~4.1 ms under a ~5.6 ms device step: device-bound); "
                          "exec: capture the step once and replay it with the library's C++ "
                          "multi-stream executor (clskd.graph.StepExecutor: ~1 ms host enqueue, but "
@@ -394,7 +397,7 @@ def main():
         args.launch = "graph"
     if args.spkd and args.train:
         raise SystemExit("--spkd is its own leg (no --train)")
-    if args.train or args.spkd:
+    if args.train or args.spkd or (args.launch == "auto" and args.ahead):
         args.launch = "eager"  # the C3 / C4 legs launch eagerly (their capture is not wired yet)
     args.graph = args.launch == "graph"
     bsz = B_SPKD if args.spkd else B_PER_GPU
@@ -410,6 +413,37 @@ def main():
         Ys.append(torch.from_numpy(clean).to(dev))
     T = cfg.n_frames(L)
 
+    executor = None
+    launch_auto = None
+    if args.launch == "auto":
+        # eager vs the C++ executor on THIS host (bitwise-equal steps, tests/test_gpu_parity.py):
+        # eager costs ~4 ms of Python enqueue per step against ~5.5 ms of device time and turns
+        # host-bound on a slow or shared host; exec enqueues in ~1 ms but runs the device step
+        # ~15 % longer.  Two alternating rounds of AUTO_STEPS steps each, the faster minimum wins.
+        from clskd.graph import StepExecutor
+        executor = StepExecutor(kd, Xs[0], Ys[0])
+
+        def _eager(i):
+            with torch.no_grad():
+                return kd.training_step((Xs[i % NBATCH], Ys[i % NBATCH]), i)
+
+        def _exec(i):
+            return executor(Xs[i % NBATCH], Ys[i % NBATCH])
+
+        tried = {}
+        for name, fn in (("eager", _eager), ("exec", _exec)) * 2:
+            for i in range(2):
+                fn(i)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(AUTO_STEPS):
+                fn(i)
+            torch.cuda.synchronize()
+            tried.setdefault(name, []).append((time.perf_counter() - t0) / AUTO_STEPS * 1e3)
+        args.launch = min(tried, key=lambda k: min(tried[k]))
+        launch_auto = {k: round(min(v), 3) for k, v in tried.items()}
+        if args.launch != "exec":
+            executor = None
     if args.train:
         from clskd.train import FlatAdam, FlatParams
         flat = FlatParams(kd.student)
@@ -424,7 +458,8 @@ def main():
                 return kd.training_step((Xs[i % NBATCH], Ys[i % NBATCH]), i)
     elif args.launch == "exec":
         from clskd.graph import StepExecutor
-        executor = StepExecutor(kd, Xs[0], Ys[0])
+        if executor is None:
+            executor = StepExecutor(kd, Xs[0], Ys[0])
 
         def step(i):
             return executor(Xs[i % NBATCH], Ys[i % NBATCH])
@@ -634,6 +669,7 @@ def main():
                        "global_batch": world * bsz, "per_gpu_batch": bsz,
                        "clip_samples": L, "frames_per_clip": T, "parallelism": f"dp{world}",
                        "abf_reinit": args.abf_reinit, "loss": round(loss_v, 6),
+                       **({"launch_auto_ms_per_step": launch_auto} if launch_auto else {}),
                        "launch": ("eager, 2 HIP streams (caller: teacher; side: student + "
                                   "MRSTFT)" if args.spkd else
                                   "eager, 4 HIP streams (caller, teacher, student, ReviewKD-"
