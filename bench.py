@@ -397,8 +397,10 @@ def main():
         args.launch = "graph"
     if args.spkd and args.train:
         raise SystemExit("--spkd is its own leg (no --train)")
-    if args.train or args.spkd or (args.launch == "auto" and args.ahead):
-        args.launch = "eager"  # the C3 / C4 legs launch eagerly (their capture is not wired yet)
+    if args.train or args.spkd or (args.launch == "auto" and (args.ahead or world > 1)):
+        # the C3 / C4 legs launch eagerly (their capture is not wired yet); multi-rank C2 runs
+        # launch eagerly too (no graph capture beside the RCCL communicator's watchdog)
+        args.launch = "eager"
     args.graph = args.launch == "graph"
     bsz = B_SPKD if args.spkd else B_PER_GPU
     kd = build_kd(dev, args.abf_reinit, args.precision, spkd=args.spkd)
