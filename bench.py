@@ -38,9 +38,27 @@ PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sp
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 B_PER_GPU = 16
 NBATCH = 4
-TRAFFIC_FILE = "r3_pmc_traffic.json"
-AUTO_STEPS = 6  # steps per round of the --launch auto trial  # written by tools/pmc_traffic.py
+TRAFFIC_FILE = "r3_pmc_traffic.json"  # written by tools/pmc_traffic.py
 L = 64000
+
+
+def _range_push(name):
+    torch.cuda.nvtx.range_push(name)  # roctx on ROCm builds of torch
+
+
+def _range_pop():
+    torch.cuda.nvtx.range_pop()
+
+
+def launches_per_step(kd, X, y):
+    """Kernel launches of one step: the step captured once (clskd.graph.StepExecutor, after the
+    timed region) and its kernel nodes counted — library and torch kernels alike."""
+    from clskd.graph import StepExecutor
+    ex = StepExecutor(kd, X, y)
+    n = dict(kernels=ex.info["kernels"], memsets=ex.info["memsets"], memcpys=ex.info["memcpys"])
+    ex._release()
+    del ex
+    return n
 
 
 def build_kd(dev, abf_reinit, precision="fp32", spkd=False):
@@ -339,10 +357,8 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU-oracle B=16 steps (median)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--abf-reinit", default="step", choices=["step", "once"])
-    ap.add_argument("--launch", default="eager", choices=["auto", "exec", "eager", "graph"],
-                    help="auto: time a few steps of eager and exec on this host and run the "
-                         "faster (measured biased: with the executor captured, eager runs ~6.5 "
-                         "ms in the trial against 5.5-5.6 ms on its own); eager (default): launch the four-stream schedule from Python every "
+    ap.add_argument("--launch", default="eager", choices=["exec", "eager", "graph"],
+                    help="eager (default): launch the four-stream schedule from Python every "
                          "step (host enqueue ~4.1 ms under a ~5.6 ms device step: device-bound); "
                          "exec: capture the step once and replay it with the library's C++ "
                          "multi-stream executor (clskd.graph.StepExecutor: ~1 ms host enqueue, but "
@@ -397,7 +413,7 @@ def main():
         args.launch = "graph"
     if args.spkd and args.train:
         raise SystemExit("--spkd is its own leg (no --train)")
-    if args.train or args.spkd or (args.launch == "auto" and (args.ahead or world > 1)):
+    if args.train or args.spkd or world > 1:
         # the C3 / C4 legs launch eagerly (their capture is not wired yet); multi-rank C2 runs
         # launch eagerly too (no graph capture beside the RCCL communicator's watchdog)
         args.launch = "eager"
@@ -430,37 +446,6 @@ def main():
             gc.disable()
 
     executor = None
-    launch_auto = None
-    if args.launch == "auto":
-        # eager vs the C++ executor on THIS host (bitwise-equal steps, tests/test_gpu_parity.py):
-        # eager costs ~4 ms of Python enqueue per step against ~5.5 ms of device time and turns
-        # host-bound on a slow or shared host; exec enqueues in ~1 ms but runs the device step
-        # ~15 % longer.  Two alternating rounds of AUTO_STEPS steps each, the faster minimum wins.
-        from clskd.graph import StepExecutor
-        executor = StepExecutor(kd, Xs[0], Ys[0])
-
-        def _eager(i):
-            with torch.no_grad():
-                return kd.training_step((Xs[i % NBATCH], Ys[i % NBATCH]), i)
-
-        def _exec(i):
-            return executor(Xs[i % NBATCH], Ys[i % NBATCH])
-
-        _gc_setting()
-        tried = {}
-        for name, fn in (("eager", _eager), ("exec", _exec)) * 2:
-            for i in range(2):
-                fn(i)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for i in range(AUTO_STEPS):
-                fn(i)
-            torch.cuda.synchronize()
-            tried.setdefault(name, []).append((time.perf_counter() - t0) / AUTO_STEPS * 1e3)
-        args.launch = min(tried, key=lambda k: min(tried[k]))
-        launch_auto = {k: round(min(v), 3) for k, v in tried.items()}
-        if args.launch != "exec":
-            executor = None
     if args.train:
         from clskd.train import FlatAdam, FlatParams
         flat = FlatParams(kd.student)
@@ -499,13 +484,21 @@ def main():
     # dominant kernel (largest total isolated time) is the same instance in every run.
     from clskd.distill import serialized_streams
     census = None
+    serial_ms = None
     for i in range(args.warmup):
         last = i == args.warmup - 1 and not args.graph
         if last:
+            torch.cuda.synchronize()
+            _range_push("clskd_census")
+            c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ops.KernelTimer.start()
+            c0.record()
             with serialized_streams():
                 (eager_step if args.launch == "exec" else step)(i)
+            c1.record()
             census = ops.KernelTimer.stop()
+            serial_ms = c0.elapsed_time(c1)
+            _range_pop()
         else:
             step(i)
     torch.cuda.synchronize()
@@ -519,6 +512,9 @@ def main():
     _gc_setting()
     # ---- timed region: exactly K steps, barrier + sync on both sides --------------------
     cdist.barrier(dev)
+    # roctx range (rocprofv3 --marker-trace): tools/region_stats.py splits the kernel trace at it,
+    # so the profile's per-kernel averages are those of exactly the timed steps
+    _range_push("clskd_timed")
     if args.launch == "eager":
         ops.KernelTimer.start(only=dominant)
     t0 = time.perf_counter()
@@ -527,6 +523,7 @@ def main():
     host_el = time.perf_counter() - t0  # host enqueue of K steps (no sync inside the loop)
     cdist.barrier(dev)
     el = time.perf_counter() - t0
+    _range_pop()
     if args.launch == "exec":
         import ctypes
         tot, cnt = ctypes.c_double(0), ctypes.c_int32(0)
@@ -583,6 +580,11 @@ def main():
                        loss=round(loss_v, 6), loss_fp32_step=round(float(o32["loss"].item()), 6),
                        note="timed batch (last step) vs the all-fp32 step on the same batch; the "
                             "oracle-pinned full-size check is tests/test_gpu_c2_mixed.py")
+
+    step_counts = None
+    if world == 1 and not args.train and not args.spkd and not args.graph:
+        # after the timed region: one capture of the step, its kernel nodes counted
+        step_counts = launches_per_step(kd, Xs[0], Ys[0])
 
     if rank == 0:
         frames = world * bsz * T * args.steps
@@ -677,6 +679,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3),
             "host_enqueue_ms_per_step": round(host_el / args.steps * 1e3, 3),
+            "launches_per_step": step_counts["kernels"] if step_counts else None,
+            "launch_count_detail": (dict(step_counts, how="kernel nodes of one captured step "
+                                         "(library + torch kernels)") if step_counts else None),
+            "serialized_kernel_ms_per_step": round(serial_ms, 3) if serial_ms else None,
+            "serialized_note": ("census step: the same step with all four streams folded onto one "
+                                "(distill.serialized_streams), HIP-event timed end to end — the sum "
+                                "of the step's isolated kernel times plus launch gaps")
+                               if serial_ms else None,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -687,7 +697,6 @@ def main():
                        "global_batch": world * bsz, "per_gpu_batch": bsz,
                        "clip_samples": L, "frames_per_clip": T, "parallelism": f"dp{world}",
                        "abf_reinit": args.abf_reinit, "loss": round(loss_v, 6),
-                       **({"launch_auto_ms_per_step": launch_auto} if launch_auto else {}),
                        "launch": ("eager, 2 HIP streams (caller: teacher; side: student + "
                                   "MRSTFT)" if args.spkd else
                                   "eager, 4 HIP streams (caller, teacher, student, ReviewKD-"

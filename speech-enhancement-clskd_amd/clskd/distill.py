@@ -44,21 +44,6 @@ def _mark(label, stream):
         _MARKS.append((label, ev))
 
 
-_PRIO = os.environ.get("CLSKD_STREAM_PRIO", "none")
-# ReviewKD-decoder placement (A/B knob): "pipelined" (default) runs it level by level on the
-# caller's stream behind the student decoder; "after" runs it on the student stream after the
-# student.  Measured on MI355X with the persistent conv engines (round 2, four passes each,
-# one box): 5.71-5.81 vs 5.89-5.95 ms per C2 step (round 1's engines: "after" was faster).
-_RKD_DEC = os.environ.get("CLSKD_RKD_DEC", "pipelined")
-# host enqueue order of the step's two chains (A/B knob): "1" enqueues the teacher chain — the
-# critical path — before the student-side chains
-_TEACHER_FIRST = os.environ.get("CLSKD_TEACHER_FIRST", "1") == "1"
-# A/B knob: CLSKD_RKD_FORK=1 (default) forks every ReviewKD-encoder conv2 (+ BN, Grams) onto the
-# caller's stream, off the level-to-level residual chain (round 1's engines: 6.18 vs 6.08 ms,
-# off; round 2, persistent conv engines + pipelined ReviewKD decoder: 5.52 vs 5.64 ms, on)
-_RKD_FORK = os.environ.get("CLSKD_RKD_FORK", "1") == "1"
-
-
 _SERIAL = os.environ.get("CLSKD_SERIAL_STREAMS") == "1"  # diagnostic: the whole step on one stream
 
 
@@ -82,17 +67,15 @@ def _side_stream(dev, which=0):
     """Extra HIP streams per device.  which = 0, 1: the student chain and the ReviewKD-encoder /
     MRSTFT chain run beside the teacher, overlapping the latency-bound LSTM recurrences and small
     kernels with the GEMMs.  which = 2: the teacher's stream (the step's critical path when the
-    three share the CUs).  CLSKD_STREAM_PRIO=teacher creates it at high priority; measured on
-    MI355X that is 0.5-1 % slower than equal priorities (the default), since the side chains'
-    small kernels then queue behind the teacher's large GEMMs.  (CU-masked side streams,
-    hipExtStreamCreateWithCUMask leaving 32-128 CUs to the teacher, measured 8.6-9.9 ms against
-    5.6 ms.)"""
+    three share the CUs).  All at equal priority: a high-priority teacher stream measured 0.5-1 %
+    slower on MI355X (the side chains' small kernels then queue behind the teacher's large
+    GEMMs), CU-masked side streams (hipExtStreamCreateWithCUMask leaving 32-128 CUs to the
+    teacher) 8.6-9.9 ms against 5.6 ms; both experiments were removed in round 4."""
     if _SERIAL:
         return torch.cuda.current_stream(dev)
     key = (torch.device(dev).index, which)
     if key not in _SIDE:
-        prio = -1 if ((which == 2 and _PRIO == "teacher") or (which == 0 and _PRIO == "student")) else 0
-        _SIDE[key] = torch.cuda.Stream(device=dev, priority=prio)
+        _SIDE[key] = torch.cuda.Stream(device=dev)
     return _SIDE[key]
 
 
@@ -292,6 +275,7 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     under graph capture, tapes or serialised streams."""
     if not (isinstance(teacher, DCCRN) and isinstance(student, DCCRN)):
         raise TypeError("clskd_step expects clskd.DCCRN teacher and student")
+    X0, y0 = X, y
     X = X.float()
     if X.dim() == 3:
         X = X.squeeze(1)
@@ -303,7 +287,17 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     capturing = torch.cuda.is_current_stream_capturing()
     ring = _AHEAD.setdefault(dev.index, dict(joins=collections.deque(maxlen=2),
                                              held=collections.deque(maxlen=2)))
-    ahead = teacher_ahead and not _SERIAL and not tape and not capturing and len(ring["joins"]) == 2
+    # ahead only when BOTH previous steps ran ahead-mode (their tensors are held in the ring): a
+    # step run with teacher_ahead off freed its teacher-stream blocks at return, and an ahead
+    # teacher that waited only for the join before it could reuse them while that step's Grams
+    # still read them
+    ahead = (teacher_ahead and not _SERIAL and not tape and not capturing
+             and len(ring["joins"]) == 2 and all(h is not None for h in ring["held"]))
+    if ahead and (X.data_ptr() != X0.data_ptr() or y.data_ptr() != y0.data_ptr()):
+        # the conversions above were queued on the caller's stream, which the ahead teacher chain
+        # does not wait for: the resident-input contract of teacher_ahead is fp32 contiguous X, y
+        raise ValueError("clskd_step(teacher_ahead=True) needs fp32 contiguous [B, L] inputs "
+                         "already resident on the device")
     spec_ev = None
     if ahead:
         # the teacher chain (spectrum included) waits for the join of step i-1, not step i
@@ -336,7 +330,7 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     # the ReviewKD conv2s (+ BN, SPKD Grams) run on the caller's stream, which is otherwise idle
     # between the teacher's encoder Grams and the join: they are off the level-to-level residual
     # chain of the fusions (framework.py:254-261), which stays on side / side2
-    c2 = main if _RKD_FORK else None
+    c2 = main
     if reinit is not None:  # fresh ABF modules (distill.py:92-96): only ReviewKD reads them
         with torch.cuda.stream(side2):
             reinit("encoder")
@@ -356,9 +350,9 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
                                                 conv2_stream=c2)
             _mark("side2: review encoder done", side2)
             held["s_enc"] = s_enc
-        with torch.cuda.stream(c2 or side2):
+        with torch.cuda.stream(c2):
             held["g_enc"] = ops.GramSlabs([_gram_bftc(a) for a in s_enc], B)
-            _mark("enc grams done", c2 or side2)
+            _mark("enc grams done", c2)
 
     # ReviewKD-decoder pipelined behind the student decoder on the caller's stream: level j
     # (framework.py:254-261, forward order) starts as soon as its student tap exists
@@ -388,22 +382,14 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
 
     def run_student():
         with torch.cuda.stream(side):
-            pipelined = _RKD_DEC == "pipelined"
             sf = student.run(X, train=student.training, bn_updates=2 if student.training else 0,
                              spec=s_spec, want_masks=False, on_encoder=fork_review_encoder,
                              tape=tapes["s"] if tapes else None,
-                             on_decoder_tap=review_decoder_level if pipelined else None)
+                             on_decoder_tap=review_decoder_level)
             student_done = torch.cuda.Event()
             student_done.record(side)
             _mark("side: student done", side)
-            if not pipelined:
-                if reinit is not None:
-                    reinit("decoder")
-                rd["outs"] = review_decoder.forward_bftc([sf["dec_in"]] + sf["dec"][:5],
-                                                         conv2_stream=c2,
-                                                         defer_bn=True,
-                                                         tape=tapes["rd"] if tapes else None)
-        rstream = main if pipelined else (c2 or side)
+        rstream = main
         with torch.cuda.stream(rstream):
             s_dec = rd["outs"]
             assert len(s_dec) == len(review_decoder.abfs)
@@ -451,12 +437,10 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
         out_t.update(tf=tf, g_td=g_td)
 
     out_s, out_t = {}, {}
-    if _TEACHER_FIRST:
-        run_teacher()
-        run_student()
-    else:
-        run_student()
-        run_teacher()
+    # host enqueue order: the teacher chain (the critical path) first — wait_stream dependencies
+    # are taken at enqueue time (measured: student chain first = 7.29 ms vs 5.60 per C2 step)
+    run_teacher()
+    run_student()
     sf, s_dec, g_dec = out_s["sf"], out_s["s_dec"], out_s["g_dec"]
     tf, g_td = out_t["tf"], out_t["g_td"]
     s_enc, g_enc = held["s_enc"], held["g_enc"]

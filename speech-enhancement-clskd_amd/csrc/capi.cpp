@@ -32,26 +32,35 @@ void note_kernel_fn(const void* fn) { g_kernel_fn = fn; }
 struct KnobDef {
   const char* name;
   int dflt;
+  // product knobs are parity-tested dispatch routes (tests/test_gpu_parity.py); every other knob
+  // is an A/B or timing experiment: a product build holds it at its default (the environment is
+  // not read for it and clskd_set_knob refuses another value)
+  bool product;
 };
 // order = KnobId
 static const KnobDef kKnobs[KNOB_COUNT] = {
-    {"CLSKD_G8", 1},          {"CLSKD_G8_GRID", 0},      {"CLSKD_HALO_GRID", 0},
-    {"CLSKD_DIRECT_COOP", 0}, {"CLSKD_LSTM_NKS", 4},     {"CLSKD_LSTM_NKS32", 1},
-    {"CLSKD_WGRAD_WG", 4096}, {"CLSKD_NO_HALO", 0},      {"CLSKD_BF16_WAVES", 8},
-    {"CLSKD_BF16_STAGES", 3}, {"CLSKD_BF16_TILE", 0},    {"CLSKD_NO_POINTWISE", 0},
-    {"CLSKD_ABF_MOMENT_DIV", 1}, {"CLSKD_F32_WAVES", 4}, {"CLSKD_EXEC_PRIO", 0}, {"CLSKD_EXEC_GATE", 0},
-    {"CLSKD_EXEC_PACE_NS", 0}, {"CLSKD_NO_HALO32", 0},
-    {"CLSKD_HALO32_SPLIT", 0}, {"CLSKD_HALO32_MIN_N", 32}, {"CLSKD_G8_KORDER", 1},
-    {"CLSKD_LSTM128_TDIV", 0},
-    {"CLSKD_LSTM32_TDIV", 0}, {"CLSKD_BF16_DEBUG_MODE", 0}, {"CLSKD_SKIP", 0},
-    {"CLSKD_H32_DEBUG_MODE", 0},
+    {"CLSKD_G8", 1, false},          {"CLSKD_G8_GRID", 0, false},     {"CLSKD_HALO_GRID", 0, false},
+    {"CLSKD_LSTM_NKS", 4, false},    {"CLSKD_LSTM_NKS32", 1, true},   {"CLSKD_WGRAD_WG", 4096, false},
+    {"CLSKD_NO_HALO", 0, false},     {"CLSKD_BF16_WAVES", 8, false},  {"CLSKD_BF16_STAGES", 3, false},
+    {"CLSKD_BF16_TILE", 0, false},   {"CLSKD_NO_POINTWISE", 0, false},
+    {"CLSKD_ABF_MOMENT_DIV", 1, false}, {"CLSKD_F32_WAVES", 4, false}, {"CLSKD_EXEC_GATE", 0, false},
+    {"CLSKD_NO_HALO32", 0, true},
+    {"CLSKD_HALO32_SPLIT", 0, true}, {"CLSKD_HALO32_MIN_N", 32, true}, {"CLSKD_G8_KORDER", 1, false},
+    {"CLSKD_LSTM128_TDIV", 0, false},
+    {"CLSKD_LSTM32_TDIV", 0, false}, {"CLSKD_BF16_DEBUG_MODE", 0, false}, {"CLSKD_SKIP", 0, false},
+    {"CLSKD_H32_DEBUG_MODE", 0, false},
 };
+#ifdef CLSKD_EXPERIMENTS
+static constexpr bool kAllKnobs = true;
+#else
+static constexpr bool kAllKnobs = false;
+#endif
 static std::atomic<int> g_knob[KNOB_COUNT];
 static std::once_flag g_knob_once;
 
 static void init_knobs() {
   for (int i = 0; i < KNOB_COUNT; ++i) {
-    const char* e = getenv(kKnobs[i].name);
+    const char* e = (kAllKnobs || kKnobs[i].product) ? getenv(kKnobs[i].name) : nullptr;
     g_knob[i].store(e && *e ? atoi(e) : kKnobs[i].dflt, std::memory_order_relaxed);
   }
 }
@@ -100,6 +109,10 @@ extern "C" int clskd_version(void) { return 1; }
 extern "C" int clskd_set_knob(const char* name, int32_t value) {
   const int i = clskd::knob_index(name);
   CLSKD_CHECK_ARG(i >= 0, "set_knob: unknown knob '%s'", name ? name : "(null)");
+  CLSKD_CHECK_ARG(clskd::kAllKnobs || clskd::kKnobs[i].product || value == clskd::kKnobs[i].dflt,
+                  "set_knob: %s is an experiment knob; values other than its default %d exist only "
+                  "in a -DCLSKD_EXPERIMENTS build of libclskd_hip.so (CLSKD_EXPERIMENTS)",
+                  name, clskd::kKnobs[i].dflt);
   std::call_once(clskd::g_knob_once, clskd::init_knobs);
   clskd::g_knob[i].store(value, std::memory_order_relaxed);
   return CLSKD_OK;

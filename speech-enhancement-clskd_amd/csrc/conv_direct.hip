@@ -261,189 +261,6 @@ __global__ __launch_bounds__(128) void conv_direct_kernel(const DirectArgs args)
   }
 }
 
-// Row-cooperative variant for the 2-channel output layers (no fused statistics): LPR lanes share
-// one output row, lane s taking K runs s, s+LPR, s+2*LPR, ...  With LPR = channel runs per tap
-// (K ordered tap, segment, channel), the LPR lanes of a row read one tap's channels as contiguous
-// pieces and the 64/LPR rows of a wave are consecutive time steps, so one wave load touches a
-// few contiguous 64-128 B pieces per segment instead of 64 lines at the row pitch (the
-// one-row-per-thread kernel above is bound by that gather in the texture path).  A lane's run
-// weights live in VGPRs; the partial sums meet in a butterfly over the LPR lanes.  The block
-// still owns rows tile*128 .. +127 (each row group walks LPR of them, consecutive groups taking
-// consecutive rows).  R = runs per lane, padded: runs past the K table load nothing useful and
-// are zeroed.
-template <int NP, int G, typename InT, typename OutT, int LPR, int R>
-__global__ __launch_bounds__(128) void conv_direct_coop_kernel(const DirectArgs args) {
-  constexpr int NG = 128 / LPR;                // row groups per block
-  constexpr int WPR = (G == 8 ? 4 : G) * NP;   // weight words (u32 pairs / fp32) per run
-  const clskd_conv_desc& d = args.d;
-  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-  const int nrun = d.K / G;
-  int4* kl = reinterpret_cast<int4*>(dsm);  // [nrun] {off, dF|dT<<16, seg, F|T<<16}
-  const int tid = threadIdx.x;
-  for (int j = tid; j < nrun; j += 128) {
-    const clskd_ktab_entry e = d.ktab[j * G];
-    const int sg = d.kseg[j * G];
-    const int FT = (int)(uint16_t)sel4d(sg, d.seg[0].F, d.seg[1].F, d.seg[2].F, d.seg[3].F) |
-                   (sel4d(sg, d.seg[0].T, d.seg[1].T, d.seg[2].T, d.seg[3].T) << 16);
-    kl[j] = make_int4(e.off, (int)(uint16_t)e.dF | ((int)e.dT << 16), sg, FT);
-  }
-  const int s = tid % LPR, g = tid / LPR;
-  // this lane's weights: runs j = s + r*LPR (zero past the table)
-  uint32_t w[R][WPR];
-  const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(d.weight);
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int j = s + r * LPR;
-#pragma unroll
-    for (int q = 0; q < WPR; ++q) w[r][q] = j < nrun ? wsrc[(int64_t)j * WPR + q] : 0u;
-  }
-  __syncthreads();
-
-  const int64_t M = (int64_t)d.B * d.Fo * d.To;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
-  const int64_t FoTo = (int64_t)d.Fo * d.To;
-  // global address space: a generic pointer would make these FLAT loads, which count on lgkmcnt
-  // too — every wait for a scalar weight load would then drain the whole run of input loads
-  using GIn = const __attribute__((address_space(1))) InT;
-  GIn* safe = reinterpret_cast<GIn*>((uintptr_t)d.seg[0].ptr);
-  OutT* outp = reinterpret_cast<OutT*>(d.out);
-  for (int it = 0; it < LPR; ++it) {
-    const int64_t m = (int64_t)tile * 128 + it * NG + g;
-    const bool valid = m < M;
-    const int64_t mm = valid ? m : 0;
-    const int b = (int)(mm / FoTo);
-    const int64_t rr = mm - (int64_t)b * FoTo;
-    const int fo = (int)(rr / d.To);
-    const int to = (int)(rr - (int64_t)fo * d.To);
-    const int fi0 = fo * d.stride_f, ti0 = to * d.stride_t;
-    auto row_base = [&](int sgi) {
-      return (int64_t)(uintptr_t)d.seg[sgi].ptr +
-             ((int64_t)b * d.seg[sgi].sB + (int64_t)fi0 * d.seg[sgi].sF +
-              (int64_t)ti0 * d.seg[sgi].sT) * (int64_t)sizeof(InT);
-    };
-    const int64_t rb0 = row_base(0);
-    const int64_t dl1 = d.nseg > 1 ? row_base(1) - rb0 : 0;
-    const int64_t dl2 = d.nseg > 2 ? row_base(2) - rb0 : 0;
-    const int64_t dl3 = d.nseg > 3 ? row_base(3) - rb0 : 0;
-    XRun<G, InT> x[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {  // all R loads in flight before the first use
-      const int j = s + r * LPR;
-      const bool run_ok = j < nrun;
-      const int4 e = kl[run_ok ? j : 0];
-      const int dF = (int)(int16_t)(e.y & 0xffff), dT = e.y >> 16;
-      const int Fb = e.w & 0xffff, Tb = (int)((unsigned)e.w >> 16);
-      const int fi = fi0 + dF, ti = ti0 + dT;
-      const bool ok = run_ok && valid && fi >= 0 && fi < Fb && ti >= 0 && ti < Tb;
-      const int64_t base = rb0 + (e.z == 1 ? dl1 : 0) + (e.z == 2 ? dl2 : 0) + (e.z == 3 ? dl3 : 0);
-      GIn* p = ok ? reinterpret_cast<GIn*>(base) + e.x : safe;
-      x[r].v = *reinterpret_cast<const __attribute__((address_space(1))) decltype(x[r].v)*>(p);
-      if constexpr (G == 8) {
-        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-        u4 wv = __builtin_bit_cast(u4, x[r].v);
-        wv = ok ? wv : u4{0u, 0u, 0u, 0u};
-        x[r].v = __builtin_bit_cast(decltype(x[r].v), wv);
-      } else if constexpr (G == 1) {
-        x[r].v = ok ? x[r].v : 0.f;
-      } else {
-#pragma unroll
-        for (int q = 0; q < G; ++q) x[r].v[q] = ok ? x[r].v[q] : 0.f;
-      }
-    }
-    float acc[NP];
-#pragma unroll
-    for (int n = 0; n < NP; ++n) acc[n] = 0.f;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-#pragma unroll
-      for (int n = 0; n < NP; ++n) {
-        if constexpr (G == 8) {
-          float a = acc[n];
-          a = dot2_pair<0>(x[r].v, w[r][0 * NP + n], a);
-          a = dot2_pair<1>(x[r].v, w[r][1 * NP + n], a);
-          a = dot2_pair<2>(x[r].v, w[r][2 * NP + n], a);
-          a = dot2_pair<3>(x[r].v, w[r][3 * NP + n], a);
-          acc[n] = a;
-        } else if constexpr (G == 1) {
-          acc[n] = fmaf(x[r].v, __uint_as_float(w[r][n]), acc[n]);
-        } else {
-#pragma unroll
-          for (int q = 0; q < G; ++q)
-            acc[n] = fmaf(x[r].v[q], __uint_as_float(w[r][q * NP + n]), acc[n]);
-        }
-      }
-    }
-    // butterfly over the LPR lanes of the row (aligned lane groups: xor stays inside)
-#pragma unroll
-    for (int o = LPR / 2; o > 0; o >>= 1) {
-#pragma unroll
-      for (int n = 0; n < NP; ++n) acc[n] += __shfl_xor(acc[n], o, 64);
-    }
-    // lane s < min(N, NP) writes channel n = s
-    if (valid && s < NP && s < d.N) {
-      float v = acc[0];
-#pragma unroll
-      for (int n = 1; n < NP; ++n) v = s == n ? acc[n] : v;
-      if (d.bias) v += d.bias[s];
-      const int64_t ro = (int64_t)b * d.oB + (int64_t)(fo * d.of_mul + d.of_add) * d.oF +
-                         (int64_t)to * d.oT;
-      outp[ro + (int64_t)(s / d.nlo) * d.oNhi + (int64_t)(s % d.nlo) * d.oNlo] = (OutT)v;
-    }
-  }
-}
-
-// Row-cooperative dispatch, opt-in while it is being validated (knob CLSKD_DIRECT_COOP=1;
-// tests switch it with clskd_set_knob): N <= 2, no fused statistics, a (tap, segment, channel) K
-// table whose channel runs per tap LPR = ctot / kvec is 2, 4, 8 or 16, at most 8 runs per lane.
-static bool coop_lpr(const clskd_conv_desc& d, int g, int* lpr, int* runs) {
-  const bool on = knob(KNOB_DIRECT_COOP) == 1;
-  if (!on || d.stats || d.N > 2 || d.ntaps <= 0 || d.ctot % g) return false;
-  const int L = d.ctot / g;
-  if (L != 2 && L != 4 && L != 8 && L != 16) return false;
-  const int R = cdiv(d.K / g, L);
-  if (R > 8) return false;
-  *lpr = L;
-  *runs = R <= 4 ? 4 : (R <= 6 ? 6 : 8);
-  return true;
-}
-
-template <int G, typename InT, int LPR, int R>
-static void launch_coop_r(const clskd_conv_desc& d, hipStream_t st) {
-  const int64_t M = (int64_t)d.B * d.Fo * d.To;
-  const size_t lds = (size_t)(d.K / G) * 16;
-  DirectArgs a{d};
-  if (d.out_dtype == CLSKD_F16) {
-    hipLaunchKernelGGL((conv_direct_coop_kernel<2, G, InT, _Float16, LPR, R>),
-                       dim3((unsigned)cdiv(M, 128)), dim3(128), lds, st, a);
-    note_kernel_fn((const void*)conv_direct_coop_kernel<2, G, InT, _Float16, LPR, R>);
-  } else if (d.out_dtype == CLSKD_BF16) {
-    hipLaunchKernelGGL((conv_direct_coop_kernel<2, G, InT, __bf16, LPR, R>),
-                       dim3((unsigned)cdiv(M, 128)), dim3(128), lds, st, a);
-    note_kernel_fn((const void*)conv_direct_coop_kernel<2, G, InT, __bf16, LPR, R>);
-  } else {
-    hipLaunchKernelGGL((conv_direct_coop_kernel<2, G, InT, float, LPR, R>),
-                       dim3((unsigned)cdiv(M, 128)), dim3(128), lds, st, a);
-    note_kernel_fn((const void*)conv_direct_coop_kernel<2, G, InT, float, LPR, R>);
-  }
-  note_kernel("conv_direct_coop_kernel<2,%d,%s,%s,%d,%d>", G, type_name<InT>(),
-              d.out_dtype == CLSKD_BF16 ? "bf16" : d.out_dtype == CLSKD_F16 ? "f16" : "float", LPR, R);
-}
-
-template <int G, typename InT, int LPR>
-static void launch_coop_l(const clskd_conv_desc& d, int R, hipStream_t st) {
-  if (R == 4) launch_coop_r<G, InT, LPR, 4>(d, st);
-  else if (R == 6) launch_coop_r<G, InT, LPR, 6>(d, st);
-  else launch_coop_r<G, InT, LPR, 8>(d, st);
-}
-
-template <int G, typename InT>
-static void launch_coop(const clskd_conv_desc& d, int L, int R, hipStream_t st) {
-  if (L == 2) launch_coop_l<G, InT, 2>(d, R, st);
-  else if (L == 4) launch_coop_l<G, InT, 4>(d, R, st);
-  else if (L == 8) launch_coop_l<G, InT, 8>(d, R, st);
-  else launch_coop_l<G, InT, 16>(d, R, st);
-}
-
 static int np_of(int N) {
   return N <= 2 ? 2 : N <= 4 ? 4 : N <= 8 ? 8 : N <= 16 ? 16 : N <= 32 ? 32 : 64;
 }
@@ -501,16 +318,12 @@ int launch_conv_direct(const clskd_conv_desc& d, hipStream_t st) {
   int g = d.kvec;
   if (g == 0) g = is_lowp(d.in_dtype) ? 8 : (d.vec4 ? 4 : 1);
   CLSKD_CHECK_SHAPE(d.K % g == 0, "conv2d(direct): K=%d not a multiple of kvec %d", d.K, g);
-  int lpr = 0, runs = 0;
-  const bool coop = coop_lpr(d, g, &lpr, &runs);
   if (d.in_dtype == CLSKD_BF16) {
     CLSKD_CHECK_SHAPE(g == 8, "conv2d(direct): bf16 segments need kvec 8");
-    if (coop) launch_coop<8, __bf16>(d, lpr, runs, st);
-    else launch_g<8, __bf16>(d, st);
+    launch_g<8, __bf16>(d, st);
   } else if (d.in_dtype == CLSKD_F16) {
     CLSKD_CHECK_SHAPE(g == 8, "conv2d(direct): f16 segments need kvec 8");
-    if (coop) launch_coop<8, _Float16>(d, lpr, runs, st);
-    else launch_g<8, _Float16>(d, st);
+    launch_g<8, _Float16>(d, st);
   } else {
     for (int s = 0; s < d.nseg; ++s) {
       const clskd_seg& sg = d.seg[s];
@@ -518,9 +331,9 @@ int launch_conv_direct(const clskd_conv_desc& d, hipStream_t st) {
                           sg.sT % g == 0,
                       "conv2d(direct): segment %d not aligned for kvec %d", s, g);
     }
-    if (g == 4) coop ? launch_coop<4, float>(d, lpr, runs, st) : launch_g<4, float>(d, st);
-    else if (g == 2) coop ? launch_coop<2, float>(d, lpr, runs, st) : launch_g<2, float>(d, st);
-    else if (g == 1) coop ? launch_coop<1, float>(d, lpr, runs, st) : launch_g<1, float>(d, st);
+    if (g == 4) launch_g<4, float>(d, st);
+    else if (g == 2) launch_g<2, float>(d, st);
+    else if (g == 1) launch_g<1, float>(d, st);
     else CLSKD_CHECK_SHAPE(false, "conv2d(direct): fp32 kvec %d unsupported", g);
   }
   return CLSKD_OK;

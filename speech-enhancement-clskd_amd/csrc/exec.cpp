@@ -354,13 +354,7 @@ extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, void* const*
       ex->own[s - 1] = as_stream(side_streams[s - 1]);
       continue;
     }
-    // knob CLSKD_EXEC_PRIO: bit s = create stream s at the highest priority (A/B)
-    int lo = 0, hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-    if ((knob(KNOB_EXEC_PRIO) >> s) & 1)
-      e = hipStreamCreateWithPriority(&ex->own[s - 1], hipStreamNonBlocking, hi);
-    else
-      e = hipStreamCreateWithFlags(&ex->own[s - 1], hipStreamNonBlocking);
+    e = hipStreamCreateWithFlags(&ex->own[s - 1], hipStreamNonBlocking);
     if (e != hipSuccess) {
       clskd_exec_destroy(ex);
       return hip_fail("hipStreamCreateWithFlags", e);
@@ -396,18 +390,8 @@ extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, void* const*
   return CLSKD_OK;
 }
 
-static inline void pace(int ns) {  // diagnostic host pacing (knob CLSKD_EXEC_PACE_NS)
-  if (ns <= 0) return;
-  struct timespec t0, t1;
-  clock_gettime(CLOCK_MONOTONIC, &t0);
-  do {
-    clock_gettime(CLOCK_MONOTONIC, &t1);
-  } while ((t1.tv_sec - t0.tv_sec) * 1000000000LL + (t1.tv_nsec - t0.tv_nsec) < ns);
-}
-
 extern "C" int clskd_exec_launch(clskd_exec* ex, void* stream) {
   CLSKD_CHECK_ARG(ex, "exec_launch: null executor");
-  const int pace_ns = knob(KNOB_EXEC_PACE_NS);
   hipStream_t st[8];
   st[0] = as_stream(stream);
   for (int s = 1; s < ex->nstreams; ++s) st[s] = ex->own[s - 1];
@@ -424,7 +408,6 @@ extern "C" int clskd_exec_launch(clskd_exec* ex, void* stream) {
         if (tm) (void)hipEventRecord(ex->tev[2 * ex->t_used], s);
         e = hipLaunchKernel(k.func, k.grid, k.block, k.args, k.shmem, s);
         if (tm) (void)hipEventRecord(ex->tev[2 * ex->t_used++ + 1], s);
-        pace(pace_ns);
         break;
       }
       case OP_MEMSET: {
