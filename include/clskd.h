@@ -362,6 +362,15 @@ typedef struct {
    * followed by a plain gram).  Ctot <= 1024 when given. */
   const float* scale;
   const float* shift;
+  /* optional, with scale/shift: PReLU slope alpha[0] applied after the affine (NULL = none) —
+   * z = t >= 0 ? t : alpha[0]*t, t = x*scale + shift, then the storage rounding, exactly as
+   * clskd_bn_apply computes it */
+  const float* alpha;
+  /* optional output (NULL = none): every element the job loads is ALSO written, transformed, to
+   * out at the same element offset (out may equal ptr: an in-place BatchNorm+PReLU apply fused
+   * with the tap's SPKD Gram partials — the tap is read once instead of twice).  The job must
+   * then cover the channels it writes; 16-byte aligned, the job's storage type. */
+  void* out;
 } clskd_gram_job;
 
 int clskd_gram_partial(const clskd_gram_job* jobs, int32_t njobs, int32_t B, float* slabs,

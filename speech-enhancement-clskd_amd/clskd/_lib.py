@@ -45,7 +45,8 @@ class GramJob(C.Structure):
     _fields_ = [("ptr", C.c_void_p), ("sB", C.c_int64), ("P", C.c_int64), ("Ctot", C.c_int32),
                 ("c0", C.c_int32), ("Cs", C.c_int32), ("chunk", C.c_int32),
                 ("first_slab", C.c_int32), ("nslab", C.c_int32), ("dtype", C.c_int32),
-                ("reserved", C.c_int32), ("scale", C.c_void_p), ("shift", C.c_void_p)]
+                ("reserved", C.c_int32), ("scale", C.c_void_p), ("shift", C.c_void_p),
+                ("alpha", C.c_void_p), ("out", C.c_void_p)]
 
 
 class DrawJob(C.Structure):
@@ -81,7 +82,7 @@ class StreamHopArgs(C.Structure):
 
 assert C.sizeof(KtabEntry) == 8
 assert C.sizeof(DrawJob) == 48
-assert C.sizeof(GramJob) == 72
+assert C.sizeof(GramJob) == 88
 
 _p, _i32, _i64, _f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float
 

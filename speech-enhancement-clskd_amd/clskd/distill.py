@@ -408,33 +408,42 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
         tstream = _side_stream(dev, 2)
         if not ahead:
             tstream.wait_stream(main)
-        # the teacher's encoder-tap Grams run on the caller's stream (idle until the join) as soon
-        # as the teacher encoder is done, keeping them off the teacher chain — the step's critical
-        # path.  (Four streams in all: GPU_MAX_HW_QUEUES is 4; a fifth would share a hardware queue.)
-        tgram = main
+        # train-mode teacher: every BatchNorm'd tap's apply pass is fused with its SPKD Gram
+        # partials (DCCRN.run(gram_taps=...), ops.bn_apply_gram) — the teacher taps are never
+        # read again for their Grams; dec_in (the LSTM projection, no BatchNorm) and its two
+        # clstm halves get one Gram launch as soon as it exists
+        fused = teacher.training
+        tg, dg = [], {}
 
-        def fork_teacher_grams(enc):
-            ev = torch.cuda.Event()
-            ev.record(tstream)
-            with torch.cuda.stream(tgram):
-                tgram.wait_event(ev)
-                held["g_te"] = ops.GramSlabs([_gram_bftc(a) for a in enc], B)
-                _mark("tgram: teacher enc grams done", tgram)
+        def dec_in_grams(tap):
+            if "g" not in dg:  # the first decoder-side tap is dec_in
+                Cht = tap.shape[-1] // 2
+                dg["g"] = ops.GramSlabs([_gram_bftc(tap), _gram_bftc(tap, 0, Cht),
+                                         _gram_bftc(tap, Cht, Cht)], B)
 
         with torch.cuda.stream(tstream):
             # the teacher's last decoder layer, mask and iSTFT are dead for the loss: stop at its taps
             tf = teacher.run(X, train=teacher.training, bn_updates=1, spec=spec, want_masks=False,
-                             on_encoder=fork_teacher_grams, taps_only=True,
+                             taps_only=True, gram_taps=tg if fused else None,
+                             on_decoder_tap=dec_in_grams if fused else None,
                              mark=(lambda lab: _mark("teacher: " + lab, tstream))
                              if _MARKS is not None else None)
             _mark("teacher: done", tstream)
-            t_dec = [tf["dec_in"]] + tf["dec"][:5]
-            Cht = tf["dec_in"].shape[-1] // 2
-            g_td = ops.GramSlabs([_gram_bftc(a) for a in t_dec] +
-                                 [_gram_bftc(tf["dec_in"], 0, Cht), _gram_bftc(tf["dec_in"], Cht, Cht)],
-                                 B)
+            if fused:
+                assert len(tg) == 11 and "g" in dg, len(tg)
+                d = dg["g"]
+                g_te = _SlabRefs([g.refs[0] for g in tg[:6]], tg[:6])
+                g_td = _SlabRefs([d.refs[0]] + [g.refs[0] for g in tg[6:]] + d.refs[1:],
+                                 (d, tg[6:]))
+            else:  # eval-mode teacher: BatchNorm applied in place, Gram passes of their own
+                g_te = ops.GramSlabs([_gram_bftc(a) for a in tf["enc"]], B)
+                t_dec = [tf["dec_in"]] + tf["dec"][:5]
+                Cht = tf["dec_in"].shape[-1] // 2
+                g_td = ops.GramSlabs([_gram_bftc(a) for a in t_dec] +
+                                     [_gram_bftc(tf["dec_in"], 0, Cht),
+                                      _gram_bftc(tf["dec_in"], Cht, Cht)], B)
             _mark("teacher: grams done", tstream)
-        out_t.update(tf=tf, g_td=g_td)
+        out_t.update(tf=tf, g_td=g_td, g_te=g_te)
 
     out_s, out_t = {}, {}
     # host enqueue order: the teacher chain (the critical path) first — wait_stream dependencies
@@ -442,10 +451,10 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     run_teacher()
     run_student()
     sf, s_dec, g_dec = out_s["sf"], out_s["s_dec"], out_s["g_dec"]
-    tf, g_td = out_t["tf"], out_t["g_td"]
+    tf, g_td, g_te = out_t["tf"], out_t["g_td"], out_t["g_te"]
     s_enc, g_enc = held["s_enc"], held["g_enc"]
     tstream = _side_stream(dev, 2)
-    g_t = _SlabRefs(held["g_te"].refs + g_td.refs, (held["g_te"], g_td))
+    g_t = _SlabRefs(g_te.refs + g_td.refs, (g_te, g_td))
     main.wait_stream(tstream)
     main.wait_stream(side)
     main.wait_stream(side2)

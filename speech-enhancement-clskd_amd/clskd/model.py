@@ -351,7 +351,7 @@ class DCCRN(nn.Module):
         return spec
 
     def run(self, x, train=True, bn_updates=1, spec=None, want_masks=True, on_encoder=None,
-            tape=None, taps_only=False, mark=None, on_decoder_tap=None):
+            tape=None, taps_only=False, mark=None, on_decoder_tap=None, gram_taps=None):
         """Full forward on the HIP device.  Returns a dict of BFTC buffers and NCHW views.
         on_encoder(enc): called (on the launching stream) right after the encoder, so a caller can
         fork work that only needs the encoder taps before the LSTM and decoder are enqueued.
@@ -363,7 +363,12 @@ class DCCRN(nn.Module):
         behind the decoder on another stream.
         taps_only: stop after the taps a distillation step reads (encoder outputs, dec_in,
         decoder outputs 0..nl-2): the last decoder layer, mask 'E' and ConviSTFT are dead for
-        the CLSKD loss (SURVEY.md §8 d) and are skipped — out_wav is None."""
+        the CLSKD loss (SURVEY.md §8 d) and are skipped — out_wav is None.
+        gram_taps: a list (train mode, no tape) that receives, for every BatchNorm'd SPKD tap —
+        encoder outputs 0..nl-1, then decoder outputs 0..nl-2 — the GramSlabs of that tap: its
+        BatchNorm + PReLU apply pass is fused with its SPKD Gram partials (ops.bn_apply_gram),
+        so the step never reads the tap again for its Gram."""
+        fuse_gram = gram_taps is not None and train and tape is None
         if not x.is_cuda:
             raise RuntimeError("clskd.DCCRN.forward needs inputs on the HIP device")
         x = x.float()
@@ -412,6 +417,12 @@ class DCCRN(nn.Module):
                                               stats_out=(mv[0], mv[1]), return_coef=True)
                 tape.setdefault("enc_bn", []).append((raw, coef, mv))
                 enc.append(post)
+            elif fuse_gram:
+                coef = ops.batch_norm_bftc(raw, None, bn.weight, bn.bias, bn.running_mean,
+                                           bn.running_var, train, bn.momentum, bn.eps, bn_updates,
+                                           partial=(part, nmb))
+                gram_taps.append(ops.bn_apply_gram(raw, coef, pr.weight, B))
+                enc.append(raw)
             else:
                 ops.batch_norm_bftc(raw, raw, bn.weight, bn.bias, bn.running_mean,
                                     bn.running_var, train, bn.momentum, bn.eps, bn_updates,
@@ -511,6 +522,11 @@ class DCCRN(nn.Module):
                         stats_out=(mv[0], mv[1]), return_coef=True)
                     tape.setdefault("dec_bn", []).append((raw, coef, mv))
                     raw = post
+                elif fuse_gram and d < nl - 1:
+                    coef = ops.batch_norm_bftc(raw, None, bn.weight, bn.bias, bn.running_mean,
+                                               bn.running_var, train, bn.momentum, bn.eps,
+                                               bn_updates, partial=(part, 2 * nmb))
+                    gram_taps.append(ops.bn_apply_gram(raw, coef, pr.weight, B))
                 else:
                     ops.batch_norm_bftc(raw, raw, bn.weight, bn.bias, bn.running_mean,
                                         bn.running_var, train, bn.momentum, bn.eps, bn_updates,

@@ -581,6 +581,9 @@ class GramView:
     c0: int
     Cs: int
     affine: torch.Tensor = None  # optional [scale | shift] (2 x Ctot fp32) applied on load
+    alpha: torch.Tensor = None   # optional PReLU slope (with affine), applied after it
+    out: torch.Tensor = None     # optional: the transformed elements are also written here
+                                 # (same layout as the view's tensor; may be the tensor itself)
 
 
 class DeferredBN:
@@ -671,13 +674,20 @@ class GramSlabs:
             chunk = max(1, ce // v.Cs)
             ns = -(-v.P // chunk)
             assert v.Cs % (8 if dt == _lib.BF16 else 4) == 0
-            sc = sh = None
+            sc = sh = al = out = None
             if v.affine is not None:
                 assert v.affine.dtype == torch.float32 and v.affine.numel() == 2 * v.Ctot
                 sc = v.affine.data_ptr()
                 sh = sc + 4 * v.Ctot
+            if v.alpha is not None:
+                assert v.affine is not None and v.alpha.dtype == torch.float32
+                al = v.alpha.data_ptr()
+            if v.out is not None:
+                assert v.affine is not None and v.out.dtype == v.tensor.dtype
+                assert v.out.numel() == v.tensor.numel() and v.out.is_contiguous()
+                out = v.out.data_ptr() + v.out.element_size() * v.offset
             jobs[j] = _lib.GramJob(v.tensor.data_ptr() + v.tensor.element_size() * v.offset, v.sB,
-                                   v.P, v.Ctot, v.c0, v.Cs, chunk, first, ns, dt, 0, sc, sh)
+                                   v.P, v.Ctot, v.c0, v.Cs, chunk, first, ns, dt, 0, sc, sh, al, out)
             spans.append((first, ns))
             first += ns
         self.slabs = torch.empty(first * 1024, dtype=torch.float32, device=dev)
@@ -685,6 +695,27 @@ class GramSlabs:
         self.refs = [(base + 4096 * f, n) for f, n in spans]
         # job table is a host array passed as kernel arguments (no upload, capturable)
         check(lib().clskd_gram_partial(jobs, len(views), B, base, _stream()), "gram_partial")
+
+
+# fused BatchNorm-apply + Gram (bn_apply_gram): slabs per tap.  The launch sits on the producing
+# chain (it replaces the bn_apply pass), so it gets enough workgroups to stream the tap at the
+# HBM rate; the SPKD finalize sums every slab, so not many more.
+_APPLY_GRAM_SLABS = 512
+
+
+def bn_apply_gram(x, coef, alpha, B, out=None):
+    """In-place BatchNorm (+ PReLU alpha) apply of the BFTC tensor x with the [scale | shift]
+    coefficients `coef`, fused with the SPKD Gram partials of the applied tensor (one pass over
+    the tap instead of an apply pass and a Gram pass; bitwise the same tensor as clskd_bn_apply
+    and the same partials as a Gram over it).  Returns the GramSlabs (keep it until the finalize
+    ran)."""
+    Bn, F, T, C = x.shape
+    assert x.is_contiguous() and Bn == B
+    per_row = F * T * C
+    ce = -(-per_row // _APPLY_GRAM_SLABS)
+    ce = max(C, min(16384, -(-ce // C) * C))
+    view = GramView(x, 0, per_row, F * T, C, 0, C, coef, alpha, x if out is None else out)
+    return GramSlabs([view], B, chunk_elems=ce)
 
 
 def spkd_finalize(s_refs, t_refs, B, batchmean=True, out=None, return_grams=False, device=None):

@@ -63,42 +63,61 @@ __device__ __forceinline__ void split_e(uint32_t e, const ESplit& s, uint32_t& p
   }
 }
 
-template <bool AFF>
-__device__ __forceinline__ f32x4 load_row4_f32(const clskd_gram_job& j, const ESplit& sp,
-                                               int64_t rowbase, uint32_t e,
-                                               const float (*aff)[GRAM_AFF_MAX]) {
-  // 4 fp32 elements at slab-relative element e (Cs % 4 == 0, e % 4 == 0; e < nel)
-  uint32_t pr, c;
+// Element transform of a job (MODE): 0 = as stored; 1 = folded BatchNorm affine; 2 = affine +
+// PReLU(alpha) — both with the fmaf + compare + storage rounding of clskd_bn_apply, so a Gram
+// over the transformed elements is bitwise a Gram over the applied tensor.  OUT: the transformed
+// elements are also written back to job.out at the same offset (the fused apply pass).
+struct GramXf {
+  const float (*aff)[GRAM_AFF_MAX];
+  float alpha;
+};
+
+template <int MODE>
+__device__ __forceinline__ float gram_xf(float x, float sc, float sh, float a) {
+  if constexpr (MODE == 0) {
+    return x;
+  } else {
+    const float t = fmaf(x, sc, sh);
+    if constexpr (MODE == 2) return t >= 0.f ? t : a * t;
+    return t;
+  }
+}
+
+// Slab-relative element e -> element offset of the job's row (rowbase) and the channel c of
+// its first element.
+__device__ __forceinline__ int64_t elem_off(const ESplit& sp, int64_t rowbase, uint32_t e,
+                                            uint32_t& c) {
+  uint32_t pr;
   split_e(e, sp, pr, c);
-  f32x4 v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(j.ptr) + rowbase +
-                                            (int64_t)((uint64_t)pr * sp.ctot + c));
-  if constexpr (AFF) {
-    const f32x4 sc = *reinterpret_cast<const f32x4*>(&aff[0][sp.c0 + c]);
-    const f32x4 sh = *reinterpret_cast<const f32x4*>(&aff[1][sp.c0 + c]);
+  return rowbase + (int64_t)((uint64_t)pr * sp.ctot + c);
+}
+
+// Loads of a batch are all issued before any transform or store: a store issued between two
+// loads would be waited for with the later load (vmcnt counts both), and the output may alias
+// the input (in-place apply).
+template <int MODE>
+__device__ __forceinline__ f32x4 xf4_f32(f32x4 v, uint32_t c, const ESplit& sp, const GramXf& xf) {
+  if constexpr (MODE != 0) {
+    const f32x4 sc = *reinterpret_cast<const f32x4*>(&xf.aff[0][sp.c0 + c]);
+    const f32x4 sh = *reinterpret_cast<const f32x4*>(&xf.aff[1][sp.c0 + c]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = fmaf(v[i], sc[i], sh[i]);
+    for (int i = 0; i < 4; ++i) v[i] = gram_xf<MODE>(v[i], sc[i], sh[i], xf.alpha);
   }
   return v;
 }
 
-template <bool AFF>
-__device__ __forceinline__ bf16x8g load_row8_bf16(const clskd_gram_job& j, const ESplit& sp,
-                                                  int64_t rowbase, uint32_t e,
-                                                  const float (*aff)[GRAM_AFF_MAX]) {
-  // 8 bf16 elements (one 16-B load) at slab-relative element e (Cs % 8 == 0, e % 8 == 0)
-  uint32_t pr, c;
-  split_e(e, sp, pr, c);
-  bf16x8g v = *reinterpret_cast<const bf16x8g*>(reinterpret_cast<const __bf16*>(j.ptr) + rowbase +
-                                                (int64_t)((uint64_t)pr * sp.ctot + c));
-  if constexpr (AFF) {  // the same fmaf + RNE rounding as clskd_bn_apply
-    const f32x4 s0 = *reinterpret_cast<const f32x4*>(&aff[0][sp.c0 + c]);
-    const f32x4 s1 = *reinterpret_cast<const f32x4*>(&aff[0][sp.c0 + c + 4]);
-    const f32x4 h0 = *reinterpret_cast<const f32x4*>(&aff[1][sp.c0 + c]);
-    const f32x4 h1 = *reinterpret_cast<const f32x4*>(&aff[1][sp.c0 + c + 4]);
+template <int MODE>
+__device__ __forceinline__ bf16x8g xf8_bf16(bf16x8g v, uint32_t c, const ESplit& sp,
+                                            const GramXf& xf) {
+  if constexpr (MODE != 0) {  // the same fmaf (+ PReLU) + RNE rounding as clskd_bn_apply
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(&xf.aff[0][sp.c0 + c]);
+    const f32x4 s1 = *reinterpret_cast<const f32x4*>(&xf.aff[0][sp.c0 + c + 4]);
+    const f32x4 h0 = *reinterpret_cast<const f32x4*>(&xf.aff[1][sp.c0 + c]);
+    const f32x4 h1 = *reinterpret_cast<const f32x4*>(&xf.aff[1][sp.c0 + c + 4]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      v[i] = (__bf16)fmaf((float)v[i], s0[i], h0[i]);
-      v[i + 4] = (__bf16)fmaf((float)v[i + 4], s1[i], h1[i]);
+      v[i] = (__bf16)gram_xf<MODE>((float)v[i], s0[i], h0[i], xf.alpha);
+      v[i + 4] = (__bf16)gram_xf<MODE>((float)v[i + 4], s1[i], h1[i], xf.alpha);
     }
   }
   return v;
@@ -130,11 +149,10 @@ __device__ __forceinline__ void gram_store_slab(float (*red)[3][256], const f32x
   }
 }
 
-template <int NB, bool AFF>
+template <int NB, int MODE, bool OUT>
 __device__ __forceinline__ void gram_accumulate(const clskd_gram_job& j, int B, int64_t nel,
-                                                int64_t p0, int64_t p1,
-                                                const float (*aff)[GRAM_AFF_MAX], f32x4& acc00,
-                                                f32x4& acc01, f32x4& acc11) {
+                                                int64_t p0, int64_t p1, const GramXf& xf,
+                                                f32x4& acc00, f32x4& acc01, f32x4& acc11) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int r = lane & 15;
@@ -149,14 +167,39 @@ __device__ __forceinline__ void gram_accumulate(const clskd_gram_job& j, int B, 
     // 16x16x32 bf16 MFMA: lane (r, g) holds row r, 8 consecutive k; A and B are the same
     // register (G = Z Z^T), so one 16-B load feeds both operands.  64 B per row per load.
     constexpr int U = 8;
+    const __bf16* src = reinterpret_cast<const __bf16*>(j.ptr);
+    __bf16* dst = reinterpret_cast<__bf16*>(j.out);
     for (uint32_t base = (uint32_t)wave * 32; base < n32; base += 128 * U) {
       bf16x8g v0[U], v1[U];
+      int64_t o0[U], o1[U];
+      uint32_t c0[U], c1[U];
+      bool k0[U], k1[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t e = base + (uint32_t)u * 128 + 8 * g;
         const bool ok = e < n32;
-        v0[u] = ok && in0 ? load_row8_bf16<AFF>(j, sp, rb0, e, aff) : bf16x8g{};
-        if constexpr (NB == 2) v1[u] = ok && in1 ? load_row8_bf16<AFF>(j, sp, rb1, e, aff) : bf16x8g{};
+        k0[u] = ok && in0;
+        o0[u] = elem_off(sp, rb0, e, c0[u]);
+        v0[u] = k0[u] ? *reinterpret_cast<const bf16x8g*>(src + o0[u]) : bf16x8g{};
+        if constexpr (NB == 2) {
+          k1[u] = ok && in1;
+          o1[u] = elem_off(sp, rb1, e, c1[u]);
+          v1[u] = k1[u] ? *reinterpret_cast<const bf16x8g*>(src + o1[u]) : bf16x8g{};
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if constexpr (MODE != 0) {
+          // rows / elements that were not loaded stay zero (the MFMA must see zeros for them)
+          v0[u] = k0[u] ? xf8_bf16<MODE>(v0[u], c0[u], sp, xf) : bf16x8g{};
+          if constexpr (OUT)
+            if (k0[u]) *reinterpret_cast<bf16x8g*>(dst + o0[u]) = v0[u];
+          if constexpr (NB == 2) {
+            v1[u] = k1[u] ? xf8_bf16<MODE>(v1[u], c1[u], sp, xf) : bf16x8g{};
+            if constexpr (OUT)
+              if (k1[u]) *reinterpret_cast<bf16x8g*>(dst + o1[u]) = v1[u];
+          }
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -170,14 +213,38 @@ __device__ __forceinline__ void gram_accumulate(const clskd_gram_job& j, int B, 
   } else {
     // fp32: 16x16x4 f32 MFMA, lane (r, g) holds row r, 4 consecutive elements per load
     constexpr int U = 4;
+    const float* src = reinterpret_cast<const float*>(j.ptr);
+    float* dst = reinterpret_cast<float*>(j.out);
     for (uint32_t base = (uint32_t)wave * 16; base < n32; base += 64 * U) {
       f32x4 v0[U], v1[U];
+      int64_t o0[U], o1[U];
+      uint32_t c0[U], c1[U];
+      bool k0[U], k1[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t e = base + (uint32_t)u * 64 + 4 * g;
         const bool ok = e < n32;
-        v0[u] = ok && in0 ? load_row4_f32<AFF>(j, sp, rb0, e, aff) : f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (NB == 2) v1[u] = ok && in1 ? load_row4_f32<AFF>(j, sp, rb1, e, aff) : f32x4{0.f, 0.f, 0.f, 0.f};
+        k0[u] = ok && in0;
+        o0[u] = elem_off(sp, rb0, e, c0[u]);
+        v0[u] = k0[u] ? *reinterpret_cast<const f32x4*>(src + o0[u]) : f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (NB == 2) {
+          k1[u] = ok && in1;
+          o1[u] = elem_off(sp, rb1, e, c1[u]);
+          v1[u] = k1[u] ? *reinterpret_cast<const f32x4*>(src + o1[u]) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if constexpr (MODE != 0) {
+          v0[u] = k0[u] ? xf4_f32<MODE>(v0[u], c0[u], sp, xf) : f32x4{0.f, 0.f, 0.f, 0.f};
+          if constexpr (OUT)
+            if (k0[u]) *reinterpret_cast<f32x4*>(dst + o0[u]) = v0[u];
+          if constexpr (NB == 2) {
+            v1[u] = k1[u] ? xf4_f32<MODE>(v1[u], c1[u], sp, xf) : f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (OUT)
+              if (k1[u]) *reinterpret_cast<f32x4*>(dst + o1[u]) = v1[u];
+          }
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -209,15 +276,21 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const GramJobsArg job
   const int64_t nel = (p1 - p0) * j.Cs;  // elements per row in this slab
   f32x4 acc00 = {0, 0, 0, 0}, acc01 = {0, 0, 0, 0}, acc11 = {0, 0, 0, 0};
   __shared__ __attribute__((aligned(16))) float aff[2][GRAM_AFF_MAX];
+  GramXf xf{aff, j.alpha ? j.alpha[0] : 0.f};
   if (j.scale) {  // uniform per workgroup
     for (int c = threadIdx.x; c < j.Ctot; c += 256) {
       aff[0][c] = j.scale[c];
       aff[1][c] = j.shift[c];
     }
     __syncthreads();
-    gram_accumulate<NB, true>(j, B, nel, p0, p1, aff, acc00, acc01, acc11);
+    if (j.out) {
+      if (j.alpha) gram_accumulate<NB, 2, true>(j, B, nel, p0, p1, xf, acc00, acc01, acc11);
+      else gram_accumulate<NB, 1, true>(j, B, nel, p0, p1, xf, acc00, acc01, acc11);
+    } else {
+      gram_accumulate<NB, 1, false>(j, B, nel, p0, p1, xf, acc00, acc01, acc11);
+    }
   } else {
-    gram_accumulate<NB, false>(j, B, nel, p0, p1, aff, acc00, acc01, acc11);
+    gram_accumulate<NB, 0, false>(j, B, nel, p0, p1, xf, acc00, acc01, acc11);
   }
   __shared__ float red[4][3][256];
   gram_store_slab(red, acc00, acc01, acc11, slabs + (int64_t)slab * 1024);
@@ -603,6 +676,9 @@ static int validate_gram_jobs(const clskd_gram_job* jobs, int32_t njobs, int32_t
                     "gram: job %d scale and shift go together", k);
     CLSKD_CHECK_SHAPE(!j.scale || j.Ctot <= GRAM_AFF_MAX, "gram: job %d folded affine needs Ctot <= %d",
                       k, GRAM_AFF_MAX);
+    CLSKD_CHECK_ARG(!j.alpha || j.scale, "gram: job %d PReLU alpha needs the folded affine", k);
+    CLSKD_CHECK_ARG(!j.out || (j.scale && ((uintptr_t)j.out & 15) == 0),
+                    "gram: job %d output needs the folded affine and 16-byte alignment", k);
     CLSKD_CHECK_SHAPE(j.first_slab == next && j.nslab == (int32_t)((j.P + j.chunk - 1) / j.chunk),
                       "gram: job %d slab range [%d, +%d) is not contiguous", k, j.first_slab,
                       j.nslab);

@@ -459,6 +459,42 @@ def test_gram_batch32_and_determinism():
     assert abs(l1.item() - R.spkd_loss(a, b).item()) <= 1e-4 * R.spkd_loss(a, b).item()
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("B", [16, 29])
+def test_bn_apply_gram_fused_matches_separate_passes(dtype, B):
+    """ops.bn_apply_gram (the teacher taps' BatchNorm + PReLU apply fused with their SPKD Gram
+    partials, in place) against the two passes it replaces: the applied tensor is bitwise
+    clskd_bn_apply's, the Gram slabs are bitwise those of a Gram over that tensor (same slab
+    split), and the normalised Gram matches fp64 torch."""
+    from clskd import _lib, ops
+    from oracle import ref_cpu as R
+    g = torch.Generator().manual_seed(B)
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    F, T, C = 6, 37, 64
+    x = (torch.randn(B, F, T, C, generator=g) * 2 + 0.5).to(tdt).to(DEV)
+    coef = torch.cat([torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g)]).to(DEV)
+    alpha = torch.tensor([0.25], device=DEV)
+    # separate passes: clskd_bn_apply, then a Gram with the slab split bn_apply_gram picks
+    y = torch.empty_like(x)
+    sc = coef.data_ptr()
+    ops.check(ops.lib().clskd_bn_apply(x.data_ptr(), y.data_ptr(), B * F * T, C, sc, sc + 4 * C,
+                                       alpha.data_ptr(), ops._dt(x), ops._stream()), "bn_apply")
+    per_row = F * T * C
+    ce = max(C, min(16384, -(-(-(-per_row // ops._APPLY_GRAM_SLABS)) // C) * C))
+    ref = ops.GramSlabs([ops.gram_view(y)], B, chunk_elems=ce)
+    xf = x.clone()
+    fused = ops.bn_apply_gram(xf, coef, alpha, B)
+    torch.cuda.synchronize()
+    assert torch.equal(xf, y), "fused apply differs from clskd_bn_apply"
+    assert fused.slabs.numel() == ref.slabs.numel()
+    assert torch.equal(fused.slabs, ref.slabs), "fused Gram partials differ"
+    loss, gs, gt = ops.spkd_finalize(fused.refs, ref.refs, B, return_grams=True)
+    torch.cuda.synchronize()
+    assert loss.item() == 0.0
+    np.testing.assert_allclose(_np(gs[0]), R.spkd_gram(y.permute(0, 3, 1, 2).double().cpu()).numpy(),
+                               rtol=1e-4, atol=1e-6)
+
+
 # ------------------------------------------------------------------------------------------
 # model forwards
 # ------------------------------------------------------------------------------------------
