@@ -132,7 +132,49 @@ typedef struct {
      compute only) — lets several data-gradient contributions of one tensor sum in place. */
   int32_t accumulate;
   int32_t reserved_;
+  /* Optional folded BatchNorm finalize (HOST pointer, read at launch; NULL = none): the launch
+     accumulates its output channels' batch statistics (fixed-point, order-independent) into
+     bn_fold->acc and, when bn_fold->finalize, its last workgroup writes the coefficients — no
+     clskd_bn_finalize launch.  Only for launches clskd_conv_fold_capable() accepts; `stats`
+     must then be NULL. */
+  const struct clskd_bn_fold_s* bn_fold;
 } clskd_conv_desc;
+
+/* ------------------------------------------------------------------------------------------
+ * Folded BatchNorm finalize (round 4; replaces the clskd_bn_finalize launch after a conv with
+ * fused statistics — the finalize of nn.BatchNorm2d.forward in train mode, tools_for_model.py
+ * encoder/decoder blocks, framework.py:188-199 ABF BatchNorms).  A BatchNorm's launches all
+ * point at the same acc/ticket state (device, zero at rest, returned to zero by the finalizing
+ * workgroup); the LAST launch of the layer carries finalize = 1.  Coefficients: scale = gamma *
+ * invstd, shift = beta - mean * scale; batch mean / var (biased) optionally; running statistics
+ * updated n_updates times with the unbiased variance (as clskd_bn_finalize).
+ * clskd_bn_fold_state_size(C): int64 elements of acc for C channels (CLSKD_BN_FOLD_REPL replicas).
+ * clskd_conv_fold_capable(d): 1 if the kernel d dispatches to folds the finalize (the persistent
+ *                     engines: conv_gemm8, conv_halo, conv_halo_f32), else 0 (use `stats` +
+ *                     clskd_bn_finalize).
+ * -------------------------------------------------------------------------------------- */
+#define CLSKD_BN_FOLD_REPL 8
+typedef struct clskd_bn_fold_s {
+  int64_t* acc;            /* device [REPL][C][2][3] int64, zero at rest */
+  uint32_t* ticket;        /* device, zero at rest */
+  int32_t finalize;        /* 1 on the layer's last launch */
+  int32_t C;               /* BatchNorm channels */
+  int32_t c_off;           /* the launch's first channel (column-split / output-offset launches) */
+  int32_t n_updates;       /* running-statistics updates (0: none) */
+  int64_t count;           /* rows of the whole layer (all launches) */
+  const float* gamma;      /* [C] or NULL (1) */
+  const float* beta;       /* [C] or NULL (0) */
+  float eps, momentum;
+  float* running_mean;     /* [C] or NULL */
+  float* running_var;
+  float* scale;            /* out [C] */
+  float* shift;            /* out [C] */
+  float* mean_out;         /* out [C] or NULL */
+  float* var_out;          /* out [C] or NULL */
+} clskd_bn_fold;
+
+int64_t clskd_bn_fold_state_size(int32_t C);
+int32_t clskd_conv_fold_capable(const clskd_conv_desc* d);
 
 #define CLSKD_WLAYOUT_NK 0
 #define CLSKD_WLAYOUT_DIRECT 1

@@ -38,7 +38,21 @@ class ConvDesc(C.Structure):
                 ("in_dtype", C.c_int32), ("out_dtype", C.c_int32), ("stats", C.c_void_p),
                 ("kvec", C.c_int32), ("wlayout", C.c_int32), ("ntaps", C.c_int32),
                 ("ctot", C.c_int32), ("seg_c", C.c_int32 * MAX_SEGS), ("tap_df", C.c_int16 * 16),
-                ("tap_dt", C.c_int16 * 16), ("accumulate", C.c_int32), ("reserved_", C.c_int32)]
+                ("tap_dt", C.c_int16 * 16), ("accumulate", C.c_int32), ("reserved_", C.c_int32),
+                ("bn_fold", C.c_void_p)]
+
+
+BN_FOLD_REPL = 8
+
+
+class BnFold(C.Structure):
+    """clskd_bn_fold (include/clskd.h): the folded BatchNorm finalize of a conv launch."""
+    _fields_ = [("acc", C.c_void_p), ("ticket", C.c_void_p), ("finalize", C.c_int32),
+                ("C", C.c_int32), ("c_off", C.c_int32), ("n_updates", C.c_int32),
+                ("count", C.c_int64), ("gamma", C.c_void_p), ("beta", C.c_void_p),
+                ("eps", C.c_float), ("momentum", C.c_float), ("running_mean", C.c_void_p),
+                ("running_var", C.c_void_p), ("scale", C.c_void_p), ("shift", C.c_void_p),
+                ("mean_out", C.c_void_p), ("var_out", C.c_void_p)]
 
 
 class GramJob(C.Structure):
@@ -95,6 +109,8 @@ SIGNATURES = {
     "clskd_get_knob": (_i32, [C.c_char_p, C.POINTER(C.c_int32)]),
     "clskd_experiments_build": (_i32, []),
     "clskd_conv2d_fwd": (_i32, [C.POINTER(ConvDesc), _p]),
+    "clskd_conv_fold_capable": (_i32, [C.POINTER(ConvDesc)]),
+    "clskd_bn_fold_state_size": (_i64, [_i32]),
     "clskd_conv_direct_np": (_i32, [_i32]),
     "clskd_conv_direct_ok": (_i32, [_i32, _i32]),
     "clskd_bn_partial_blocks": (_i32, [_i64, _i32]),

@@ -369,26 +369,27 @@ class ABF(nn.Module):
         f64 = dict(device=dev, dtype=torch.float64)
         Cout = w2p.shape[0]
         out = torch.empty(B, Fn, Tn, Cout, **act)
-        part2 = torch.empty(nmb * Cout * 2, **f64) if train else None
-        ops.conv([seg_bftc(x1)], [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], B, Fn,
-                 Tn, Cout, w2p, None, out, OutMap(Fn * Tn * Cout, Tn * Cout, Cout), stats=part2)
         bn = self.conv2[1]
-        if tape is not None:
-            mv2 = torch.empty(2, Cout, device=dev, dtype=torch.float32)
+        mv2 = torch.empty(2, Cout, device=dev, dtype=torch.float32) if tape is not None else None
+        # train: conv2's BatchNorm statistics folded into the conv launch (ops.BnStats)
+        st = (ops.BnStats(bn, Cout, B * Fn * Tn, 1, dev,
+                          stats_out=(mv2[0], mv2[1]) if mv2 is not None else None)
+              if train else None)
+        ops.conv([seg_bftc(x1)], [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], B, Fn,
+                 Tn, Cout, w2p, None, out, OutMap(Fn * Tn * Cout, Tn * Cout, Cout),
+                 bn_stats=(st, True) if st is not None else None)
+        if train:
+            coef = st.coefficients()
+        else:
             coef = ops.batch_norm_bftc(out, None, bn.weight, bn.bias, bn.running_mean,
-                                       bn.running_var, train, bn.momentum, bn.eps, 1,
-                                       partial=(part2, nmb), stats_out=(mv2[0], mv2[1]))
+                                       bn.running_var, False, bn.momentum, bn.eps, 1)
+        if tape is not None:
             tape.update(xf=x1, out_raw=out, coef2=coef, mv2=mv2)
             d = ops.DeferredBN(out, coef)
             return (d if defer_bn else d.materialize()), x1
         if defer_bn:
-            coef = ops.batch_norm_bftc(out, None, bn.weight, bn.bias, bn.running_mean,
-                                       bn.running_var, train, bn.momentum, bn.eps, 1,
-                                       partial=(part2, nmb) if train else None)
             return ops.DeferredBN(out, coef), x1
-        ops.batch_norm_bftc(out, out, bn.weight, bn.bias, bn.running_mean, bn.running_var, train,
-                            bn.momentum, bn.eps, 1, partial=(part2, nmb) if train else None)
-        return out, x1
+        return ops.bn_apply(out, out, coef), x1
 
     def forward(self, x, y=None, shape=None, out_shape=None, feature_type=None):
         out, xf = self.forward_bftc(to_bftc(x), to_bftc(y) if y is not None else None, shape,

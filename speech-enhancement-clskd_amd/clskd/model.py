@@ -350,6 +350,33 @@ class DCCRN(nn.Module):
                  OutMap(T * 514, 0, 514))
         return spec
 
+    @staticmethod
+    def _norm(raw, bn, pr, st, train, bn_updates, tape, key, mv, gram_taps, B):
+        """BatchNorm + PReLU of a conv output (train: batch statistics from the conv launches'
+        BnStats — folded into them or one finalize launch; eval: running statistics).  In place
+        unless a tape keeps the raw output; gram_taps: the apply pass also computes the tap's
+        SPKD Gram partials (ops.bn_apply_gram).  Returns the normalised tensor."""
+        if not train:
+            if tape is not None:
+                post = torch.empty_like(raw)
+                _, coef = ops.batch_norm_bftc(raw, post, bn.weight, bn.bias, bn.running_mean,
+                                              bn.running_var, False, bn.momentum, bn.eps,
+                                              bn_updates, alpha=pr.weight, return_coef=True)
+                tape.setdefault(key, []).append((raw, coef, mv))
+                return post
+            return ops.batch_norm_bftc(raw, raw, bn.weight, bn.bias, bn.running_mean,
+                                       bn.running_var, False, bn.momentum, bn.eps, bn_updates,
+                                       alpha=pr.weight)
+        coef = st.coefficients()
+        if tape is not None:
+            post = ops.bn_apply(raw, torch.empty_like(raw), coef, pr.weight)
+            tape.setdefault(key, []).append((raw, coef, mv))
+            return post
+        if gram_taps is not None:
+            gram_taps.append(ops.bn_apply_gram(raw, coef, pr.weight, B))
+            return raw
+        return ops.bn_apply(raw, raw, coef, pr.weight)
+
     def run(self, x, train=True, bn_updates=1, spec=None, want_masks=True, on_encoder=None,
             tape=None, taps_only=False, mark=None, on_decoder_tap=None, gram_taps=None):
         """Full forward on the HIP device.  Returns a dict of BFTC buffers and NCHW views.
@@ -402,32 +429,15 @@ class DCCRN(nn.Module):
             wp, bias = self._enc_w(i, self._cmp(segs, 10 * kn[i]))
             taps = [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)]
             raw = torch.empty(B, Fo, T, Co, **act)
-            nmb = ops.conv_mblocks(B, Fo, T)
-            part = torch.empty(nmb * Co * 2, device=dev, dtype=torch.float64) if train else None
-            ops.conv(segs, taps, B, Fo, T, Co, wp, bias, raw, OutMap(Fo * T * Co, T * Co, Co),
-                     stride_f=2, stats=part)
             bn, pr = self.encoder[i][1], self.encoder[i][2]
-            if tape is not None:
-                post = torch.empty_like(raw)
-                mv = torch.empty(2, Co, **f32)
-                _, coef = ops.batch_norm_bftc(raw, post, bn.weight, bn.bias, bn.running_mean,
-                                              bn.running_var, train, bn.momentum, bn.eps,
-                                              bn_updates, alpha=pr.weight,
-                                              partial=(part, nmb) if train else None,
-                                              stats_out=(mv[0], mv[1]), return_coef=True)
-                tape.setdefault("enc_bn", []).append((raw, coef, mv))
-                enc.append(post)
-            elif fuse_gram:
-                coef = ops.batch_norm_bftc(raw, None, bn.weight, bn.bias, bn.running_mean,
-                                           bn.running_var, train, bn.momentum, bn.eps, bn_updates,
-                                           partial=(part, nmb))
-                gram_taps.append(ops.bn_apply_gram(raw, coef, pr.weight, B))
-                enc.append(raw)
-            else:
-                ops.batch_norm_bftc(raw, raw, bn.weight, bn.bias, bn.running_mean,
-                                    bn.running_var, train, bn.momentum, bn.eps, bn_updates,
-                                    alpha=pr.weight, partial=(part, nmb) if train else None)
-                enc.append(raw)
+            mv = torch.empty(2, Co, **f32) if tape is not None else None
+            st = (ops.BnStats(bn, Co, B * Fo * T, bn_updates, dev,
+                              stats_out=(mv[0], mv[1]) if mv is not None else None)
+                  if train else None)
+            ops.conv(segs, taps, B, Fo, T, Co, wp, bias, raw, OutMap(Fo * T * Co, T * Co, Co),
+                     stride_f=2, bn_stats=(st, True) if st is not None else None)
+            enc.append(self._norm(raw, bn, pr, st, train, bn_updates, tape, "enc_bn", mv,
+                                  gram_taps if fuse_gram else None, B))
             F = Fo
         if mark is not None:
             mark("encoder done")
@@ -501,37 +511,22 @@ class DCCRN(nn.Module):
             raw = torch.empty(B, 2 * F, T + 1, Co, **(f32 if last else act))
             Ci = sum(sg.geom.C for sg in segs)
             has_bn = len(self.decoder[d]) > 1
-            nmb = ops.conv_mblocks(B, F, T + 1)
-            part = (torch.empty(2 * nmb * Co * 2, device=dev, dtype=torch.float64)
-                    if (train and has_bn) else None)
+            bn = pr = mv = st = None
+            if has_bn:
+                bn, pr = self.decoder[d][1], self.decoder[d][2]
+                mv = torch.empty(2, Co, **f32) if tape is not None else None
+                if train:  # one BatchNorm over both polyphase parities (2 x B*F*(T+1) rows)
+                    st = ops.BnStats(bn, Co, 2 * B * F * (T + 1), bn_updates, dev,
+                                     stats_out=(mv[0], mv[1]) if mv is not None else None)
             for parity in (0, 1):
                 taps = [(dF, -kt) for _, dF in self._DEC_TAPS[parity] for kt in (0, 1)]
                 wp, bias = self._dec_w(d, parity, self._cmp(segs, len(taps) * Ci))
                 ops.conv(segs, taps, B, F, T + 1, Co, wp, bias, raw,
                          OutMap(2 * F * (T + 1) * Co, (T + 1) * Co, Co, of_mul=2, of_add=parity),
-                         stats=part, stats_offset=parity * nmb * Co * 2)
+                         bn_stats=(st, parity == 1) if st is not None else None)
             if has_bn:
-                bn, pr = self.decoder[d][1], self.decoder[d][2]
-                if tape is not None:
-                    post = torch.empty_like(raw)
-                    mv = torch.empty(2, Co, **f32)
-                    _, coef = ops.batch_norm_bftc(
-                        raw, post, bn.weight, bn.bias, bn.running_mean, bn.running_var, train,
-                        bn.momentum, bn.eps, bn_updates, alpha=pr.weight,
-                        partial=(part, 2 * nmb) if part is not None else None,
-                        stats_out=(mv[0], mv[1]), return_coef=True)
-                    tape.setdefault("dec_bn", []).append((raw, coef, mv))
-                    raw = post
-                elif fuse_gram and d < nl - 1:
-                    coef = ops.batch_norm_bftc(raw, None, bn.weight, bn.bias, bn.running_mean,
-                                               bn.running_var, train, bn.momentum, bn.eps,
-                                               bn_updates, partial=(part, 2 * nmb))
-                    gram_taps.append(ops.bn_apply_gram(raw, coef, pr.weight, B))
-                else:
-                    ops.batch_norm_bftc(raw, raw, bn.weight, bn.bias, bn.running_mean,
-                                        bn.running_var, train, bn.momentum, bn.eps, bn_updates,
-                                        alpha=pr.weight,
-                                        partial=(part, 2 * nmb) if part is not None else None)
+                raw = self._norm(raw, bn, pr, st, train, bn_updates, tape, "dec_bn", mv,
+                                 gram_taps if (fuse_gram and d < nl - 1) else None, B)
             elif tape is not None:
                 tape.setdefault("dec_bn", []).append(None)
             dec.append(raw)

@@ -18,6 +18,9 @@ from ._lib import check, ptr
 BK = 16
 ZERO_DF = -32768
 _NO_DIRECT = os.environ.get("CLSKD_NO_DIRECT", "") == "1"  # host switch: MFMA engines only
+# A/B switch (measurement only): CLSKD_BN_FOLD=0 keeps every BatchNorm on fused partials + one
+# clskd_bn_finalize launch even where the dispatched kernel could fold the finalize
+_BN_FOLD = os.environ.get("CLSKD_BN_FOLD", "1") == "1"
 
 
 def lib():
@@ -229,7 +232,7 @@ def conv_mblocks(B, Fo, To):
 class _ConvPlan:
     """Launch descriptor of one conv signature, built once; per call only the pointers change."""
     __slots__ = ("desc", "segs", "nseg", "direct", "name", "fn", "flops", "bytes", "shape", "nstats",
-                 "osize")
+                 "osize", "fold")
 
 
 _CONV_PLANS = {}
@@ -301,24 +304,31 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
     pl.shape = (B * Fo * To, N, K, {_lib.BF16: "bf16", _lib.F16: "f16"}.get(in_dt, "f32"))
     pl.nstats = conv_mblocks(B, Fo, To) * N * 2
     pl.osize = out.element_size()
+    pl.fold = None  # the dispatched kernel folds a BatchNorm finalize (asked at the first launch)
     _CONV_PLANS[key] = pl
     return pl
 
 
 def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, stride_f=1,
-         stride_t=1, stats=None, stats_offset=0, accumulate=False, mfma_only=False):
+         stride_t=1, stats=None, stats_offset=0, accumulate=False, mfma_only=False, bn_stats=None):
     """out[b, fo*of_mul+of_add, to, n] = bias[n] + sum_k A[(b,fo,to),k] W[n,k].
     bf16 segments run the LDS-DMA bf16-MFMA engine (weights packed bf16, K % 64); fp32 segments
     the fp32-MFMA engine (weights fp32, K % 16).  `out` may be fp32 or bf16 storage.
     The descriptor of each launch signature (geometry, taps, output map, dtypes, pointer
     alignment class) is built once (_conv_plan); a call patches only the pointers.
     accumulate=True adds into `out` (fp32 engine; data-gradient sums); mfma_only skips the
-    direct-convolution kernel."""
+    direct-convolution kernel.
+    bn_stats=(BnStats, is_last): the launch produces (part of) a train-mode BatchNorm's batch
+    statistics — folded into the launch when the dispatched kernel can (clskd_bn_fold), else as
+    fused partials for BnStats.coefficients()."""
     addrs = [s.tensor.data_ptr() + s.tensor.element_size() * s.offset for s in segs]
     taps = tuple(taps)
     geoms = tuple(s.geom for s in segs)
+    if bn_stats is not None and stats is not None:
+        raise ValueError("conv: stats and bn_stats are exclusive")
     key = (geoms, taps, B, Fo, To, N, wpacked.shape, wpacked.dtype, omap, stride_f, stride_t,
-           out.dtype, out.device.index, stats is None, bias is None,
+           out.dtype, out.device.index, "bn" if bn_stats is not None else stats is None,
+           bias is None,
            tuple(a % 16 for a in addrs), tuple(s.tensor.dtype for s in segs), accumulate, mfma_only)
     pl = _CONV_PLANS.get(key)
     if pl is None:
@@ -335,6 +345,21 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
     d.weight = direct_weight(wpacked).data_ptr() if pl.direct else wpacked.data_ptr()
     d.bias = bias.data_ptr() if bias is not None else None
     d.out = out.data_ptr() + pl.osize * out_offset
+    L = lib()
+    fold = None
+    d.bn_fold = None
+    if bn_stats is not None:
+        st, last = bn_stats
+        if out_offset or N != st.C:
+            raise ValueError("conv: bn_stats needs the launch to produce all the BatchNorm's channels")
+        fold = st.fold_struct(bool(last), 0)
+        d.bn_fold = C.addressof(fold)
+        if pl.fold is None:  # which kernel the library dispatches this signature to
+            pl.fold = bool(L.clskd_conv_fold_capable(C.byref(d))) and _BN_FOLD
+        if not pl.fold:
+            d.bn_fold = None
+            stats, stats_offset = st.partials(conv_mblocks(B, Fo, To))
+        st.launched(pl.fold)
     if stats is not None:
         if stats.dtype != torch.float64 or stats.numel() < stats_offset + pl.nstats:
             raise RuntimeError("conv: fused statistics buffer must be float64 with room for "
@@ -342,7 +367,6 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
         d.stats = stats.data_ptr() + 8 * stats_offset
     else:
         d.stats = None
-    L = lib()
     if KernelTimer.active and not torch.cuda.is_current_stream_capturing() \
             and KernelTimer.wants(pl.name):
         e0 = torch.cuda.Event(enable_timing=True)
@@ -418,6 +442,102 @@ def batch_norm_bftc(x, y, gamma, beta, running_mean, running_var, train, momentu
     check(L.clskd_bn_apply(ptr(x), ptr(y), rows, Cn, scale, shift, ptr(alpha), _dt(x), st),
           "bn_apply")
     return (y, coef) if return_coef else y
+
+
+def bn_fold_state(bn, Cn, device):
+    """Device state of a BatchNorm's folded finalize (clskd_bn_fold): int64 limb accumulators
+    and the last-arriver ticket, zero at rest (the finalizing workgroup returns them to zero), so
+    one allocation per module and device serves every step, graph replay included."""
+    states = bn.__dict__.setdefault("_clskd_fold", {})
+    key = (torch.device(device).index, Cn)
+    st = states.get(key)
+    if st is None:
+        n = int(lib().clskd_bn_fold_state_size(Cn))
+        st = (torch.zeros(n, dtype=torch.int64, device=device),
+              torch.zeros(2, dtype=torch.int32, device=device))
+        states[key] = st
+    return st
+
+
+class BnStats:
+    """Train-mode batch statistics of one BatchNorm over the conv launches that produce its input
+    (the decoder's two polyphase parities are two launches of one layer).  Each launch passes
+    bn_stats=(this, is_last) to conv(); the library either folds the finalize into the launch
+    (the persistent engines: no clskd_bn_finalize launch, coefficients written by the last
+    workgroup) or writes fused per-128-row partials that coefficients() finalizes with one
+    clskd_bn_finalize launch.  coefficients() returns the [scale | shift] fp32 tensor; the
+    running statistics are updated n_updates times (nn.BatchNorm2d train forward) and the batch
+    mean / biased var written to stats_out if given."""
+
+    def __init__(self, bn, Cn, rows, n_updates, device, stats_out=None, gamma=None, beta=None):
+        self.bn, self.C, self.rows, self.dev = bn, Cn, int(rows), device
+        self.gamma = bn.weight if gamma is None else gamma
+        self.beta = bn.bias if beta is None else beta
+        upd = bn.running_mean is not None and bn.running_var is not None and n_updates > 0
+        self.rm = bn.running_mean if upd else None
+        self.rv = bn.running_var if upd else None
+        self.n_updates = n_updates if upd else 0
+        self.coef = torch.empty(2 * Cn, device=device, dtype=torch.float32)
+        self.stats_out = stats_out
+        self.mode = None  # "fold" | "part", set by the first launch
+        self.part, self.used, self.nblk = None, 0, 0
+        self._keep = []
+
+    def fold_struct(self, last, c_off):
+        acc, ticket = bn_fold_state(self.bn, self.C, self.dev)
+        sc = self.coef.data_ptr()
+        mo, vo = self.stats_out if self.stats_out is not None else (None, None)
+        f = _lib.BnFold(acc.data_ptr(), ticket.data_ptr(), int(last), self.C, int(c_off),
+                        self.n_updates, self.rows, ptr(self.gamma), ptr(self.beta), self.bn.eps,
+                        self.bn.momentum, ptr(self.rm), ptr(self.rv), sc, sc + 4 * self.C,
+                        ptr(mo), ptr(vo))
+        self._keep.append(f)
+        return f
+
+    def partials(self, nblk):
+        """(buffer, element offset) for the next non-folding launch's partials."""
+        if self.part is None:  # sized for the largest layer this object can describe
+            self.nblk = -(-self.rows // 128) + 64
+            self.part = torch.empty(self.nblk * self.C * 2, device=self.dev, dtype=torch.float64)
+        off = self.used * self.C * 2
+        self.used += nblk
+        assert self.used <= self.nblk, "BnStats: more partial blocks than rows / 128"
+        return self.part, off
+
+    def launched(self, fold):
+        mode = "fold" if fold else "part"
+        if self.mode is None:
+            self.mode = mode
+        elif self.mode != mode:
+            raise RuntimeError("BnStats: the launches of one BatchNorm dispatch to folding and "
+                               "non-folding kernels")
+
+    def coefficients(self):
+        if self.mode == "part":
+            L = lib()
+            sc = self.coef.data_ptr()
+            mo, vo = self.stats_out if self.stats_out is not None else (None, None)
+            check(L.clskd_bn_finalize(ptr(self.part), self.used, self.rows, self.C,
+                                      ptr(self.gamma), ptr(self.beta), self.bn.eps, ptr(self.rm),
+                                      ptr(self.rv), self.bn.momentum, self.n_updates, sc,
+                                      sc + 4 * self.C, ptr(mo), ptr(vo), _stream()),
+                  "bn_finalize")
+            self.mode = "done"
+        elif self.mode not in ("fold", "done"):
+            raise RuntimeError("BnStats: no launch produced these statistics")
+        self._keep = []
+        return self.coef
+
+
+def bn_apply(x, y, coef, alpha=None):
+    """y = x * scale + shift per channel (BFTC, channels last) [then PReLU(alpha)] with the
+    [scale | shift] coefficients coef; y may be x."""
+    Cn = x.shape[-1]
+    sc = coef.data_ptr()
+    assert x.dtype == y.dtype and coef.numel() == 2 * Cn
+    check(lib().clskd_bn_apply(ptr(x), ptr(y), x.numel() // Cn, Cn, sc, sc + 4 * Cn, ptr(alpha),
+                               _dt(x), _stream()), "bn_apply")
+    return y
 
 
 # ------------------------------------------------------------------------------------------

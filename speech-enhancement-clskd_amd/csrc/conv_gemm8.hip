@@ -29,6 +29,7 @@
 //    its L2.
 #include <stdlib.h>
 
+#include "bnfold.h"
 #include "common.h"
 
 namespace clskd {
@@ -101,6 +102,7 @@ struct ConvArgsG8 {
   // 64-channel block c, then block c + 1) when every K-tile lies inside one tap (kt_taps = the
   // tap count, kt_cpt = K-tiles per tap); kt_taps = 1, kt_cpt = K / 64 is the packed order.
   int kt_taps, kt_cpt;
+  BnFoldArgs f;  // folded BatchNorm finalize (f.acc != nullptr; needs one N-tile: N <= BN)
 };
 
 // BM x BN tile, 8 waves as WM x WN, BK-deep K-tiles (64: 128-B LDS rows; 32: 64-B rows) in NS
@@ -161,7 +163,13 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
     t_step = grid;
     ntl = b < args.ntiles ? (args.ntiles - b + grid - 1) / grid : 0;
   }
-  if (ntl == 0) return;  // whole workgroup: no barrier is left waiting
+  const bool fold = args.f.acc != nullptr;
+  if (ntl == 0) {  // whole workgroup: no barrier is left waiting
+    if (fold)  // it still takes its ticket (a zero contribution); flag in the (unused) stages
+      bnfold_commit(args.f, 0, [](int, double& S, double& Q) { S = Q = 0.0; },
+                    reinterpret_cast<int*>(smem), b, grid);
+    return;
+  }
   auto tile_mt = [&](int j) { return (t_first + j * t_step) % args.n_mt; };
   auto tile_nt = [&](int j) { return (t_first + j * t_step) / args.n_mt; };
 
@@ -353,6 +361,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
   if constexpr (DBG == 7 || DBG == 8)
     if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   int gk = 0;  // stream index of the K-tile being computed
+  double fS = 0.0, fQ = 0.0;  // fold: thread tid < HALVES*BN owns (half tid / BN, column tid % BN)
   for (int j = 0; j < ntl; ++j) {
     for (int kt = 0; kt < nk; ++kt, ++gk) {
       const unsigned char* sa = stages + (gk % NS) * SB;
@@ -411,7 +420,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
     const RowTable<BM>& tb = tabs[j & 1];
     const int64_t m0 = (int64_t)tile_mt(j) * BM;
     const int n0 = tile_nt(j) * BN;
-    if (d.stats) {  // fused BatchNorm statistics: one fp64 partial per 128 output rows
+    if (d.stats || fold) {  // fused BatchNorm statistics: one fp64 partial per 128 output rows
       constexpr int HALVES = BM / 128;
       constexpr int WPH = WM / HALVES;  // waves along M per 128-row half
       double* red = reinterpret_cast<double*>(scratch);  // [WM][BN][2]
@@ -451,8 +460,18 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
         }
       }
       raw_barrier();
+      if (fold) {  // the workgroup's running sums (tiles in list order)
+        if (tid < HALVES * BN) {
+          const int hv = tid / BN, c = tid % BN;
+#pragma unroll
+          for (int w = 0; w < WPH; ++w) {
+            fS += red[((hv * WPH + w) * BN + c) * 2];
+            fQ += red[((hv * WPH + w) * BN + c) * 2 + 1];
+          }
+        }
+      }
       const int64_t nblk128 = (M + 127) / 128;
-      for (int idx = tid; idx < HALVES * BN; idx += NT) {
+      for (int idx = tid; idx < (fold ? 0 : HALVES * BN); idx += NT) {
         const int hv = idx / BN, c = idx % BN;
         const int n = n0 + c;
         const int64_t blk = m0 / 128 + hv;
@@ -525,6 +544,28 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
       read_head(stages + (gk % NS) * SB);
     }
   }
+  if (fold) {  // the two 128-row halves in a fixed order, then the folded finalize
+    static_assert(BM / 128 * BN <= NT, "one (half, column) pair per thread");
+    constexpr int HALVES = BM / 128;
+    double* fin = reinterpret_cast<double*>(stages);  // [HALVES][BN][2]; every stage is free
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid < HALVES * BN) {
+      fin[tid * 2] = fS;
+      fin[tid * 2 + 1] = fQ;
+    }
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(fin + HALVES * BN * 2);
+    bnfold_commit(args.f, d.N, [&](int n, double& S, double& Q) {
+      S = 0.0;
+      Q = 0.0;
+#pragma unroll
+      for (int hv = 0; hv < HALVES; ++hv) {
+        S += fin[(hv * BN + n) * 2];
+        Q += fin[(hv * BN + n) * 2 + 1];
+      }
+    }, flag, b, grid);
+  }
 }
 
 template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8,
@@ -558,7 +599,7 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   const int cap = knob(KNOB_G8_GRID) > 0 ? knob(KNOB_G8_GRID) : ncu;
   const int ncap = cap > 0 && cap < ncu ? cap : ncu;
   const int grid = ntiles <= ncap ? (int)ntiles : (ncap >= 8 ? (ncap & ~7) : ncap);
-  ConvArgsG8 a{d, (int)n_mt, (int)ntiles, 1, d.K / BK};
+  ConvArgsG8 a{d, (int)n_mt, (int)ntiles, 1, d.K / BK, make_bnfold(d)};
   // channel-block-major K order when every K-tile lies inside one tap (CLSKD_G8_KORDER=0: packed)
   if (knob(KNOB_G8_KORDER) != 0 && d.ntaps > 1 && d.ctot % BK == 0 && (int64_t)d.ntaps * d.ctot == d.K) {
     a.kt_taps = d.ntaps;
@@ -578,6 +619,13 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
 // Entry from launch_conv_bf16 for N > 64 bf16 layers.  *launched = false leaves the layer to the
 // older engine (CLSKD_G8=0 selects that everywhere; an A/B switch).  CLSKD_G8 = 10*cfg + dbg
 // selects timing-experiment variants (bf16 outputs only); read per launch (tests switch it).
+// Whether launch_conv_gemm8 would take the layer (default mode).
+bool conv_gemm8_takes(const clskd_conv_desc& d) {
+  return knob(KNOB_G8) != 0 && d.N > 64 && d.K % 64 == 0 && d.nseg <= 2 &&
+         (int64_t)d.B * d.Fo * d.To < ((int64_t)1 << 31) && (int64_t)d.Fo * d.stride_f < 32768 &&
+         (int64_t)d.To * d.stride_t < 32768;
+}
+
 int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) {
   *launched = false;
   const int mode = knob(KNOB_G8);

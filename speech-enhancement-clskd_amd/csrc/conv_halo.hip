@@ -21,6 +21,7 @@
 // Same descriptor, output map and bias/stats semantics as the engines.
 #include <stdlib.h>
 
+#include "bnfold.h"
 #include "common.h"
 
 #ifndef HALO_TRACE
@@ -78,6 +79,7 @@ struct HaloArgs {
   int32_t nblk128;                 // statistics slots (ceil(M/128))
   int32_t tap_pix[16];             // halo pixel offset of tap t for output (0, 0)
   int32_t tap_k[16];               // k offset of tap t (t * ctot)
+  BnFoldArgs f;                    // folded BatchNorm finalize (f.acc != nullptr)
   int32_t stats_ld;                // channels per statistics slot row (N, or the full N of a
                                    // column-split launch whose stats pointer is pre-offset)
 };
@@ -346,7 +348,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const HaloArgs a) {
   }
   HALO_TRACE(40);
 
-  if (d.stats) {  // workgroup partial: lanes (h halves) and waves in a fixed order
+  if (d.stats || a.f.acc) {  // workgroup partial: lanes (h halves) and waves in a fixed order
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     double* red = reinterpret_cast<double*>(smem);  // reuse the halo buffers: [NW][BN][2]
@@ -360,7 +362,16 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const HaloArgs a) {
       }
     }
     __syncthreads();
-    if (blockIdx.x < a.nblk128) {
+    if (a.f.acc) {  // folded finalize: waves in the same fixed order
+      bnfold_commit(a.f, d.N, [&](int n, double& S, double& Q) {
+        S = 0.0;
+        Q = 0.0;
+        for (int w = 0; w < NW; ++w) {
+          S += red[(w * BN + n) * 2];
+          Q += red[(w * BN + n) * 2 + 1];
+        }
+      }, reinterpret_cast<int*>(red + NW * BN * 2), blockIdx.x, gridDim.x);
+    } else if (blockIdx.x < a.nblk128) {
       for (int n = tid; n < d.N; n += 512) {
         double S = 0.0, Q = 0.0;
         for (int w = 0; w < NW; ++w) {
@@ -423,7 +434,7 @@ static bool halo_plan(const clskd_conv_desc& d, HaloArgs& a, size_t& lds) {
   for (int s = 0; s < d.nseg; ++s)
     if (d.seg[s].sB > INT32_MAX || d.seg[s].sF > INT32_MAX || d.seg[s].sT > INT32_MAX) return false;
   if (lds > 160 * 1024) return false;
-  if (d.stats && (size_t)NW * BN * 16 > 2 * (size_t)a.halo_bytes) return false;
+  if ((d.stats || d.bn_fold) && (size_t)NW * BN * 16 + 16 > 2 * (size_t)a.halo_bytes) return false;
   a.nfb = (int)cdiv(d.Fo, FT);
   a.ntb = (int)cdiv(d.To, TT);
   const int64_t nt = (int64_t)d.B * a.nfb * a.ntb;
@@ -431,6 +442,7 @@ static bool halo_plan(const clskd_conv_desc& d, HaloArgs& a, size_t& lds) {
   a.ntiles = (int)nt;
   a.nblk128 = (int)cdiv((int64_t)d.B * d.Fo * d.To, 128);
   a.stats_ld = d.N;
+  a.f = make_bnfold(d);
   return true;
 }
 
@@ -441,6 +453,20 @@ static int launch_halo_planned(const HaloArgs& a, size_t lds, hipStream_t st, bo
 // re-reads the input halo (~N/K of the staged-bytes saving is kept) but stays on the halo path
 // instead of the im2col engine.  Output columns, bias and the statistics slots of the second
 // launch are offset by 32 (statistics rows keep the full N as leading dimension).
+// Whether launch_conv_halo would take the layer (the same plans, nothing launched).
+bool conv_halo_takes(const clskd_conv_desc& d) {
+  HaloArgs a;
+  size_t lds = 0;
+  if (halo_plan(d, a, lds)) return true;
+  if (d.N <= 32 || d.N > 64 || d.nlo < d.N || !is_lowp(d.in_dtype)) return false;
+  clskd_conv_desc d1 = d, d2 = d;
+  d1.N = 32;
+  d2.N = d.N - 32;
+  HaloArgs a2;
+  size_t lds2 = 0;
+  return halo_plan(d1, a, lds) && halo_plan(d2, a2, lds2);
+}
+
 int launch_conv_halo(const clskd_conv_desc& d, hipStream_t st, bool* launched) {
   HaloArgs a;
   size_t lds = 0;
@@ -459,6 +485,11 @@ int launch_conv_halo(const clskd_conv_desc& d, hipStream_t st, bool* launched) {
   if (d.stats) d2.stats = d.stats + 64;
   if (!halo_plan(d1, a, lds) || !halo_plan(d2, a2, lds2)) return CLSKD_OK;
   a.stats_ld = a2.stats_ld = d.N;
+  if (a.f.acc) {  // column halves: the second one (channels +32) finalizes the layer
+    a2.f = a.f;
+    a.f.finalize = 0;
+    a2.f.c_off += 32;
+  }
   bool l1 = false, l2 = false;
   int rc = launch_halo_planned(a, lds, st, &l1);
   if (rc != CLSKD_OK || !l1) return rc;

@@ -24,6 +24,7 @@
 // launches (the input halo is staged twice; cheap at fp32 MFMA rates).
 #include <stdlib.h>
 
+#include "bnfold.h"
 #include "common.h"
 
 namespace clskd {
@@ -91,6 +92,7 @@ struct Halo32Args {
   int32_t nblk128;                 // statistics slots (ceil(M/128))
   int32_t tap_pix[16];             // halo pixel offset of tap t for output (0, 0)
   int32_t tap_kq[16];              // k-quad offset of tap t (t * ctot / 4)
+  BnFoldArgs f;                    // folded BatchNorm finalize (f.acc != nullptr)
   int32_t stats_ld;                // channels per statistics slot row
 };
 
@@ -383,7 +385,7 @@ __global__ __launch_bounds__(512) void conv_halo_f32_kernel(const Halo32Args a) 
   if (have_out) flush();
   mark();
 
-  if (d.stats) {  // workgroup partial: lanes (h halves) and waves in a fixed order
+  if (d.stats || a.f.acc) {  // workgroup partial: lanes (h halves) and waves in a fixed order
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     double* red = reinterpret_cast<double*>(smem);  // reuse the halo buffers: [NW][NBW][2]
@@ -397,7 +399,16 @@ __global__ __launch_bounds__(512) void conv_halo_f32_kernel(const Halo32Args a) 
       }
     }
     __syncthreads();
-    if (blockIdx.x < a.nblk128) {
+    if (a.f.acc) {  // folded finalize: waves in the same fixed order
+      bnfold_commit(a.f, d.N, [&](int n, double& S, double& Q) {
+        S = 0.0;
+        Q = 0.0;
+        for (int w = 0; w < NW; ++w) {
+          S += red[(w * NBW + n) * 2];
+          Q += red[(w * NBW + n) * 2 + 1];
+        }
+      }, reinterpret_cast<int*>(red + NW * NBW * 2), blockIdx.x, gridDim.x);
+    } else if (blockIdx.x < a.nblk128) {
       for (int n = tid; n < d.N; n += 512) {
         double S = 0.0, Q = 0.0;
         for (int w = 0; w < NW; ++w) {
@@ -462,7 +473,7 @@ static bool halo32_plan(const clskd_conv_desc& d, Halo32Args& a, size_t& lds) {
   const int NBW = d.N <= 32 ? 32 : 64;
   lds = 2 * (size_t)a.halo_bytes + (size_t)a.k4 * NBW * 16 + 2 * MAXCH * 16 + 16 * 4;
   if (lds > 160 * 1024) return false;
-  if (d.stats && (size_t)NW * NBW * 16 > 2 * (size_t)a.halo_bytes) return false;
+  if ((d.stats || d.bn_fold) && (size_t)NW * NBW * 16 + 16 > 2 * (size_t)a.halo_bytes) return false;
   a.nfb = (int)cdiv(d.Fo, FT);
   a.ntb = (int)cdiv(d.To, TT);
   const int64_t nt = (int64_t)d.B * a.nfb * a.ntb;
@@ -470,6 +481,7 @@ static bool halo32_plan(const clskd_conv_desc& d, Halo32Args& a, size_t& lds) {
   a.ntiles = (int)nt;
   a.nblk128 = (int)cdiv((int64_t)d.B * d.Fo * d.To, 128);
   a.stats_ld = d.N;
+  a.f = make_bnfold(d);
   return true;
 }
 
@@ -535,6 +547,24 @@ static int launch_halo32_planned(const Halo32Args& a, size_t lds, hipStream_t st
 // vs 138 / 88.  Layers that need the two-launch column split (64 x K >= 512 weights) or have
 // Fo < 8 (half the waves idle) measured slower than the engine (e.g. the 4-row encoder layer 119
 // vs 64 us); CLSKD_HALO32_SPLIT=1 still takes them (the split path stays parity-tested).
+// Whether launch_conv_halo_f32 would take the layer (the same plans, nothing launched).
+bool conv_halo_f32_takes(const clskd_conv_desc& d) {
+  Halo32Args a;
+  size_t lds = 0;
+  const int min_n = knob(KNOB_HALO32_MIN_N);
+  if (d.N < (min_n > 0 ? min_n : 32)) return false;
+  const bool split_ok = knob(KNOB_HALO32_SPLIT) == 1;
+  if (!split_ok && d.Fo < h32::FT) return false;
+  if (halo32_plan(d, a, lds)) return true;
+  if (!split_ok || d.N <= 32 || d.N > 64 || d.nlo < d.N) return false;
+  clskd_conv_desc d1 = d, d2 = d;
+  d1.N = 32;
+  d2.N = d.N - 32;
+  Halo32Args a2;
+  size_t lds2 = 0;
+  return halo32_plan(d1, a, lds) && halo32_plan(d2, a2, lds2);
+}
+
 int launch_conv_halo_f32(const clskd_conv_desc& d, hipStream_t st, bool* launched) {
   Halo32Args a;
   size_t lds = 0;
@@ -558,6 +588,11 @@ int launch_conv_halo_f32(const clskd_conv_desc& d, hipStream_t st, bool* launche
   if (d.stats) d2.stats = d.stats + 64;
   if (!halo32_plan(d1, a, lds) || !halo32_plan(d2, a2, lds2)) return CLSKD_OK;
   a.stats_ld = a2.stats_ld = d.N;
+  if (a.f.acc) {  // column halves: the second one (channels +32) finalizes the layer
+    a2.f = a.f;
+    a.f.finalize = 0;
+    a2.f.c_off += 32;
+  }
   bool l1 = false, l2 = false;
   int rc = launch_halo32_planned(a, lds, st, &l1);
   if (rc != CLSKD_OK || !l1) return rc;

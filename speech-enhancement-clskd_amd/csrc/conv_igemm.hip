@@ -341,12 +341,48 @@ int launch_conv_halo_f32(const clskd_conv_desc& d, hipStream_t st, bool* launche
 
 using namespace clskd;
 
+namespace clskd {
+bool conv_halo_takes(const clskd_conv_desc& d);
+bool conv_halo_f32_takes(const clskd_conv_desc& d);
+bool conv_gemm8_takes(const clskd_conv_desc& d);
+bool conv_pointwise_takes(const clskd_conv_desc& d);
+}  // namespace clskd
+
+// The kernel a descriptor dispatches to folds the BatchNorm finalize (clskd_bn_fold): the
+// persistent engines.  Mirrors the dispatch order of clskd_conv2d_fwd.
+static bool fold_capable(const clskd_conv_desc& d) {
+  if (d.wlayout == CLSKD_WLAYOUT_DIRECT || d.accumulate) return false;
+  if (is_lowp(d.compute)) {
+    if (conv_halo_takes(d)) return true;
+    return conv_gemm8_takes(d) && d.N <= 256;  // one N-tile (256x256 / 256x128 instances)
+  }
+  if (conv_pointwise_takes(d)) return false;
+  return knob(KNOB_NO_HALO32) != 1 && conv_halo_f32_takes(d);
+}
+
+extern "C" int32_t clskd_conv_fold_capable(const clskd_conv_desc* dp) {
+  if (!dp) return 0;
+  return fold_capable(*dp) ? 1 : 0;
+}
+
+extern "C" int64_t clskd_bn_fold_state_size(int32_t C) {
+  return C > 0 ? (int64_t)CLSKD_BN_FOLD_REPL * C * 6 : 0;
+}
+
 extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
   CLSKD_CHECK_ARG(dp != nullptr, "conv2d: null descriptor");
   const clskd_conv_desc& d = *dp;
   CLSKD_CHECK_ARG(d.compute == CLSKD_F32 || d.compute == CLSKD_BF16 || d.compute == CLSKD_F16,
                   "conv2d: unknown compute %d", d.compute);
   CLSKD_CHECK_SHAPE(d.B > 0 && d.Fo > 0 && d.To > 0 && d.N > 0 && d.K > 0, "conv2d: empty shape");
+  if (const clskd_bn_fold* f = d.bn_fold) {
+    CLSKD_CHECK_ARG(!d.stats, "conv2d: bn_fold and stats are exclusive");
+    CLSKD_CHECK_ARG(f->acc && f->ticket && f->scale && f->shift, "conv2d: bn_fold null pointer");
+    CLSKD_CHECK_SHAPE(f->C > 0 && f->c_off >= 0 && f->c_off + d.N <= f->C && f->count > 0,
+                      "conv2d: bn_fold channels [%d, +%d) outside C=%d", f->c_off, d.N, f->C);
+    CLSKD_CHECK_ARG(fold_capable(d), "conv2d: N=%d K=%d dispatches to a kernel without the folded "
+                    "BatchNorm finalize (clskd_conv_fold_capable)", d.N, d.K);
+  }
   const bool lowp = is_lowp(d.compute);
   const int kmul = lowp ? 64 : BK;
   CLSKD_CHECK_SHAPE(d.K % kmul == 0, "conv2d: K=%d must be padded to a multiple of %d", d.K, kmul);

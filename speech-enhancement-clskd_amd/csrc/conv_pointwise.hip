@@ -199,6 +199,8 @@ static void launch_pw_c(const clskd_conv_desc& d, hipStream_t st) {
   }
 }
 
+bool conv_pointwise_takes(const clskd_conv_desc& d) { return pointwise_ok(d); }
+
 int launch_conv_pointwise(const clskd_conv_desc& d, hipStream_t st, bool* launched) {
   *launched = false;
   if (!pointwise_ok(d)) return CLSKD_OK;

@@ -35,13 +35,15 @@ def test_struct_layouts_match_header(tmp_path):
 #include <stddef.h>
 #include "clskd.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(clskd_seg),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(clskd_seg),
          sizeof(clskd_ktab_entry), sizeof(clskd_gram_job), offsetof(clskd_gram_job, shift),
          sizeof(clskd_draw_job), offsetof(clskd_draw_job, stream_id), sizeof(clskd_conv_desc),
          offsetof(clskd_conv_desc, tap_dt), offsetof(clskd_conv_desc, accumulate),
          sizeof(clskd_gram_bwd_job), offsetof(clskd_gram_bwd_job, accumulate),
          sizeof(clskd_stream_hop_args), offsetof(clskd_stream_hop_args, dec_co),
-         offsetof(clskd_stream_hop_args, off_frames));
+         offsetof(clskd_stream_hop_args, off_frames), offsetof(clskd_conv_desc, bn_fold),
+         sizeof(clskd_bn_fold), offsetof(clskd_bn_fold, count), offsetof(clskd_bn_fold, eps),
+         offsetof(clskd_bn_fold, var_out), offsetof(clskd_gram_job, out));
   return 0;
 }
 """)
@@ -54,7 +56,9 @@ int main(void) {
             ctypes.sizeof(_lib.ConvDesc), _lib.ConvDesc.tap_dt.offset,
             _lib.ConvDesc.accumulate.offset, ctypes.sizeof(_lib.GramBwdJob),
             _lib.GramBwdJob.accumulate.offset, ctypes.sizeof(_lib.StreamHopArgs),
-            _lib.StreamHopArgs.dec_co.offset, _lib.StreamHopArgs.off_frames.offset]
+            _lib.StreamHopArgs.dec_co.offset, _lib.StreamHopArgs.off_frames.offset,
+            _lib.ConvDesc.bn_fold.offset, ctypes.sizeof(_lib.BnFold), _lib.BnFold.count.offset,
+            _lib.BnFold.eps.offset, _lib.BnFold.var_out.offset, _lib.GramJob.out.offset]
     assert got == want
 
 

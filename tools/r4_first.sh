@@ -28,6 +28,10 @@ for P in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
   if [ $rc -eq 124 ] || [ $rc -eq 137 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit 1; fi
 done
 cd $R
+# A/B: the folded BatchNorm finalize off (fused partials + clskd_bn_finalize launches)
+CLSKD_BN_FOLD=0 timeout -k 10 300 python $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_nofold.log 2>&1 || echo "nofold bench rc=$?"
+timeout -k 10 300 python $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_fold.log 2>&1 || echo "fold bench rc=$?"
+timeout -k 10 200 python $R/tools/conv_census.py > $O/census.txt 2>&1 || echo "census rc=$?"
 bash $R/tools/skip_sweep.sh "0 1 2 32 4 64 8 16 128 0" > $O/skip.log 2>&1 || true
 cp -r $R/gpurun_out/skip $O/skip || true
 echo r4a-done
