@@ -174,6 +174,11 @@ typedef struct clskd_bn_fold_s {
 } clskd_bn_fold;
 
 int64_t clskd_bn_fold_state_size(int32_t C);
+/* clskd_abf_bn1_partials with the finalize folded (fold->C = 64 conv1 channels, finalize = 1,
+ * count = B*F*T): the ABF conv1 BatchNorm's coefficients straight from the tap's moments. */
+int clskd_abf_bn1_fold(const float* s, int32_t B, int32_t F, int32_t T, int64_t sB, int64_t sF,
+                       int64_t sT, int32_t cin, const float* w1, const clskd_bn_fold* fold,
+                       int32_t nblk, void* stream);
 int32_t clskd_conv_fold_capable(const clskd_conv_desc* d);
 
 #define CLSKD_WLAYOUT_NK 0

@@ -111,6 +111,7 @@ SIGNATURES = {
     "clskd_conv2d_fwd": (_i32, [C.POINTER(ConvDesc), _p]),
     "clskd_conv_fold_capable": (_i32, [C.POINTER(ConvDesc)]),
     "clskd_bn_fold_state_size": (_i64, [_i32]),
+    "clskd_abf_bn1_fold": (_i32, [_p, _i32, _i32, _i32, _i64, _i64, _i64, _i32, _p, _p, _i32, _p]),
     "clskd_conv_direct_np": (_i32, [_i32]),
     "clskd_conv_direct_ok": (_i32, [_i32, _i32]),
     "clskd_bn_partial_blocks": (_i32, [_i64, _i32]),
@@ -233,6 +234,9 @@ def load(require_gpu=True):
     return _LIB
 
 
+KNOB_EPOCH = 0
+
+
 def set_knob(name, value):
     """Switch a dispatch knob of the loaded library (include/clskd.h: read from the environment
     once, then only through this call).  Returns the previous value."""
@@ -240,6 +244,8 @@ def set_knob(name, value):
     prev = C.c_int32(0)
     check(lib.clskd_get_knob(name.encode(), C.byref(prev)), f"get_knob {name}")
     check(lib.clskd_set_knob(name.encode(), int(value)), f"set_knob {name}")
+    global KNOB_EPOCH
+    KNOB_EPOCH += 1  # dispatch decisions cached per launch signature are re-asked
     return prev.value
 
 

@@ -111,6 +111,10 @@ def direct_weight(wpacked):
 _stream = _lib.stream_ptr
 
 
+def _addr(struct):
+    return C.addressof(struct)
+
+
 # ------------------------------------------------------------------------------------------
 # implicit-GEMM convolution
 # ------------------------------------------------------------------------------------------
@@ -354,12 +358,13 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
             raise ValueError("conv: bn_stats needs the launch to produce all the BatchNorm's channels")
         fold = st.fold_struct(bool(last), 0)
         d.bn_fold = C.addressof(fold)
-        if pl.fold is None:  # which kernel the library dispatches this signature to
-            pl.fold = bool(L.clskd_conv_fold_capable(C.byref(d))) and _BN_FOLD
-        if not pl.fold:
+        if pl.fold is None or pl.fold[0] != _lib.KNOB_EPOCH:
+            # which kernel the library dispatches this signature to (re-asked after a knob change)
+            pl.fold = (_lib.KNOB_EPOCH, bool(L.clskd_conv_fold_capable(C.byref(d))) and _BN_FOLD)
+        if not pl.fold[1]:
             d.bn_fold = None
             stats, stats_offset = st.partials(conv_mblocks(B, Fo, To))
-        st.launched(pl.fold)
+        st.launched(pl.fold[1])
     if stats is not None:
         if stats.dtype != torch.float64 or stats.numel() < stats_offset + pl.nstats:
             raise RuntimeError("conv: fused statistics buffer must be float64 with room for "
@@ -643,8 +648,15 @@ def abf_bn1_coef(x, w1, bn, train, stats_out=None):
                                      ptr(bn.bias), bn.eps, mid, scale, shift, st), "bn_eval")
         return coef
     nblk = int(L.clskd_abf_moment_blocks(rows, C))
-    part = torch.empty(nblk * mid * 2, device=dev, dtype=torch.float64)
     sB, sF, sT, _ = x.stride()
+    if _BN_FOLD:  # the moments kernel's last block writes the coefficients (clskd_bn_fold)
+        bst = BnStats(bn, mid, rows, 1, dev, stats_out=stats_out)
+        f = bst.fold_struct(True, 0)
+        check(L.clskd_abf_bn1_fold(ptr(x), B, F, T, sB, sF, sT, C, ptr(w1.reshape(mid, C)),
+                                   _addr(f), nblk, st), "abf_bn1_fold")
+        bst.launched(True)
+        return bst.coefficients()
+    part = torch.empty(nblk * mid * 2, device=dev, dtype=torch.float64)
     check(L.clskd_abf_bn1_partials(ptr(x), B, F, T, sB, sF, sT, C, ptr(w1.reshape(mid, C)),
                                    ptr(part), nblk, st), "abf_bn1_partials")
     return bn_coef_from_partials(part, nblk, rows, mid, bn, coef, stats_out)

@@ -21,6 +21,7 @@
 
 #include <algorithm>
 
+#include "bnfold.h"
 #include "common.h"
 
 namespace clskd {
@@ -65,7 +66,8 @@ template <int C>
 __global__ __launch_bounds__(256) void abf_moments_kernel(const float* __restrict__ s,
                                                           TapRows g, int rows, int rpb,
                                                           const float* __restrict__ w1,
-                                                          double* __restrict__ partial) {
+                                                          double* __restrict__ partial,
+                                                          const BnFoldArgs fold) {
   constexpr int NT = C >= 16 ? C / 16 : 1;        // 16-channel tiles
   constexpr int NP = NT * (NT + 1) / 2;           // tiles with ti <= tj
   constexpr int RPG = C == 8 ? 8 : 4;             // rows per MFMA k-group
@@ -212,6 +214,20 @@ __global__ __launch_bounds__(256) void abf_moments_kernel(const float* __restric
   q += __shfl_xor(q, 2, 4);
   sm += __shfl_xor(sm, 1, 4);
   sm += __shfl_xor(sm, 2, 4);
+  if (fold.acc) {  // folded finalize (clskd_abf_bn1_fold): the block's 64 sums, then the ticket
+    __shared__ double fin[64 * 2];
+    __shared__ int flag;
+    if (part == 0) {
+      fin[n * 2] = sm;
+      fin[n * 2 + 1] = q;
+    }
+    __syncthreads();
+    bnfold_commit(fold, 64, [&](int c, double& S1, double& Q1) {
+      S1 = fin[c * 2];
+      Q1 = fin[c * 2 + 1];
+    }, &flag, blockIdx.x, gridDim.x);
+    return;
+  }
   if (part == 0) {
     partial[((int64_t)blockIdx.x * 64 + n) * 2] = sm;
     partial[((int64_t)blockIdx.x * 64 + n) * 2 + 1] = q;
@@ -425,10 +441,10 @@ static TapRows tap_rows(int F, int T, int64_t sB, int64_t sF, int64_t sT, int C)
 
 template <int C>
 static void launch_moments(const float* s, const TapRows& g, int rows, int nblk, const float* w1,
-                           double* partial, hipStream_t st) {
+                           double* partial, hipStream_t st, const BnFoldArgs& fold = BnFoldArgs{}) {
   const int rpb = (int)cdiv(rows, nblk);
   hipLaunchKernelGGL(abf_moments_kernel<C>, dim3(nblk), dim3(256), 0, st, s, g, rows, rpb, w1,
-                     partial);
+                     partial, fold);
 }
 
 template <int C, typename DT>
@@ -494,6 +510,35 @@ extern "C" int clskd_abf_bn1_partials(const float* s, int32_t B, int32_t F, int3
     default: launch_moments<64>(s, g, rows, nblk, w1, partial, st); break;
   }
   CLSKD_LAUNCH_CHECK("abf_bn1_partials");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_abf_bn1_fold(const float* s, int32_t B, int32_t F, int32_t T, int64_t sB,
+                                  int64_t sF, int64_t sT, int32_t cin, const float* w1,
+                                  const clskd_bn_fold* fold, int32_t nblk, void* stream) {
+  CLSKD_CHECK_ARG(s && w1 && fold && fold->acc && fold->ticket && fold->scale && fold->shift,
+                  "abf_bn1_fold: null pointer");
+  CLSKD_CHECK_SHAPE(B > 0 && F > 0 && T > 0 && nblk > 0 && nblk <= 1024 && cin_ok(cin),
+                    "abf_bn1_fold: shape (cin=%d must be 8/16/32/64, nblk <= 1024)", cin);
+  CLSKD_CHECK_SHAPE(fold->C == 64 && fold->c_off == 0 && fold->finalize == 1 &&
+                        fold->count == (int64_t)B * F * T,
+                    "abf_bn1_fold: the fold describes the 64 conv1 channels of these rows");
+  CLSKD_CHECK_ARG(tap_ok(s, B, F, T, sB, sF, sT, cin),
+                  "abf_bn1_fold: tap rows must be 16-B aligned channel runs with 32-bit offsets");
+  const int rows = B * F * T;
+  const TapRows g = tap_rows(F, T, sB, sF, sT, cin);
+  const hipStream_t st = as_stream(stream);
+  if (skip_kernel(SKIP_ABF)) return CLSKD_OK;
+  clskd_conv_desc d{};
+  d.bn_fold = fold;
+  const BnFoldArgs f = make_bnfold(d);
+  switch (cin) {
+    case 8: launch_moments<8>(s, g, rows, nblk, w1, nullptr, st, f); break;
+    case 16: launch_moments<16>(s, g, rows, nblk, w1, nullptr, st, f); break;
+    case 32: launch_moments<32>(s, g, rows, nblk, w1, nullptr, st, f); break;
+    default: launch_moments<64>(s, g, rows, nblk, w1, nullptr, st, f); break;
+  }
+  CLSKD_LAUNCH_CHECK("abf_bn1_fold");
   return CLSKD_OK;
 }
 

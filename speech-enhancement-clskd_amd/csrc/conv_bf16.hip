@@ -25,10 +25,6 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 
 __device__ __attribute__((aligned(64))) unsigned char g_zero_page[64];
 
-// The round-1 engine below is no default-path kernel any more (no launch in the C2-C5 censuses:
-// every bf16 / f16 layer runs on conv_halo (N <= 64) or conv_gemm8 (N > 64)); it stays as the
-// A/B reference of the experiments build (-DCLSKD_EXPERIMENTS, CLSKD_G8=0 / CLSKD_NO_HALO=1).
-#ifdef CLSKD_EXPERIMENTS
 namespace v2 {
 // Tile geometry: BM output rows x BK reduction columns per stage; LDS rows of BK bf16
 // (ROWB = 2*BK bytes = CPR 16-B chunks); one DMA wave instruction fills RPD = 64/CPR rows.
@@ -459,26 +455,10 @@ static int launch_big(const clskd_conv_desc& d, hipStream_t st) { return launch_
 // engine is bound by DMA issue/latency, not MFMA (tools/conv_micro.py: 13-25 % faster for
 // BN >= 64).  BN = 32 keeps 4 waves (four 32x32 MFMA tiles).  CLSKD_BF16_WAVES=4 selects the
 // 4-wave tiles everywhere (A/B measurements).
-#endif  // CLSKD_EXPERIMENTS
-
 int launch_conv_halo(const clskd_conv_desc& d, hipStream_t st, bool* launched);
 int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched);
 
 int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
-#ifndef CLSKD_EXPERIMENTS
-  // product dispatch: narrow layers on the halo kernel, N > 64 on the persistent engine; a layer
-  // that fits neither is an error (never a silent slower path)
-  {
-    bool launched = false;
-    int rc = launch_conv_halo(d, st, &launched);
-    if (rc != CLSKD_OK || launched) return rc;
-    rc = launch_conv_gemm8(d, st, &launched);
-    if (rc != CLSKD_OK || launched) return rc;
-  }
-  set_error("conv2d(%s): N=%d K=%d nseg=%d Fo=%d To=%d fits neither conv_halo nor conv_gemm8",
-            d.in_dtype == CLSKD_F16 ? "f16" : "bf16", d.N, d.K, d.nseg, d.Fo, d.To);
-  return CLSKD_E_SHAPE;
-#else
   const bool no_halo = knob(KNOB_NO_HALO) == 1;  // A/B switch: 1 keeps narrow layers on the engine
   if (!no_halo) {
     bool launched = false;
@@ -486,23 +466,48 @@ int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
     if (rc != CLSKD_OK || launched) return rc;
   }
   const int dbg = knob(KNOB_BF16_DEBUG_MODE);
+  {
+    const int rc = experiment_guard("CLSKD_BF16_DEBUG_MODE", dbg);
+    if (rc != CLSKD_OK) return rc;
+  }
   if (dbg == 0) {
     bool launched = false;
     const int rc = launch_conv_gemm8(d, st, &launched);
     if (rc != CLSKD_OK || launched) return rc;
   }
+  // the generic fallback: every bf16 layer neither the halo kernel nor the persistent engine
+  // takes (short or ragged clips, halo tiles that do not fit LDS; no launch in the C2-C5
+  // censuses).  bf16 only: an f16 layer that reaches it is an error, never a silent bf16
+  // computation
   CLSKD_CHECK_ARG(d.in_dtype == CLSKD_BF16,
                   "conv2d(f16): N=%d K=%d nseg=%d fits neither the halo kernel nor conv_gemm8", d.N,
                   d.K, d.nseg);
   const int nw = knob(KNOB_BF16_WAVES) == 4 ? 4 : 8;
   const int stages = knob(KNOB_BF16_STAGES) == 4 ? 4 : 3;  // experiment knob: 3 | 4
   const int tilecfg = knob(KNOB_BF16_TILE);  // A/B knob: 128 | 256 forces one row-tile height
+#ifdef CLSKD_EXPERIMENTS
   // timing experiments only: 1 = no DMA, 2 = no MFMA, ... (wrong results)
   if (dbg == 1 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<128, 64, 256, 8, 3, __bf16, 1>(d, st);
   if (dbg == 2 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<128, 64, 256, 8, 3, __bf16, 2>(d, st);
   if (dbg == 1 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 3, __bf16, 1>(d, st);
   if (dbg == 2 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 3, __bf16, 2>(d, st);
+  if (dbg == 3 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 3, __bf16, 3>(d, st);
+  if (dbg == 4 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 32, 256, 16, 4, __bf16, 4>(d, st);
+  if (dbg == 5 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 32, 256, 16, 4, __bf16, 5>(d, st);
+  if (dbg == 4 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 4, __bf16, 4>(d, st);
+  if (dbg == 5 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 4, __bf16, 5>(d, st);
+  if (dbg == 7 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 32, 256, 16, 4, __bf16, 7>(d, st);
+  if (dbg == 8 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 32, 256, 16, 4, __bf16, 8>(d, st);
+  if (dbg == 7 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 4, __bf16, 7>(d, st);
+  if (dbg == 8 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 4, __bf16, 8>(d, st);
+  if (dbg == 6 && d.out_dtype == CLSKD_BF16 && d.N > 128) return launch_v2<256, 32, 256, 16, 4, __bf16, 0>(d, st);
+  if (dbg == 6 && d.out_dtype == CLSKD_BF16 && d.N > 64) return launch_v2<256, 32, 128, 16, 4, __bf16, 0>(d, st);
+#endif
   if (d.N > 32 && d.K % 32 == 0 && tilecfg != 128) {
+    // 256-row tiles stage a third fewer bytes per FLOP (measured 1.1-1.25x faster per tile
+    // worth of work) but halve the workgroup count: pick them unless the tail rounds eat the
+    // gain — a 256-row tile costs ~1.6 rounds-equivalents of a 128-row tile, one workgroup per
+    // CU either way.
     static const int ncu = [] {
       int v = 256;
       (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, 0);
@@ -515,7 +520,6 @@ int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
   }
   if (stages == 4) return nw == 8 ? launch_nw<8, 4>(d, st) : launch_nw<4, 4>(d, st);
   return nw == 8 ? launch_nw<8, 3>(d, st) : launch_nw<4, 3>(d, st);
-#endif
 }
 
 }  // namespace clskd

@@ -19,13 +19,17 @@ DEV = "cuda"
 def _conv_case(kind, N, dt, g):
     """(segments, taps, geometry, packed weight, bias, torch fp64 reference [B, N, Fo, To])."""
     from clskd import ops
-    B, T = 3, 61
-    if kind == "enc":  # 5x2 stride-(2,1), the encoder blocks
-        F, Cin = 34, 64 if dt == "bf16" else 32
+    # sizes the persistent kernels take (conv_halo needs >= 32 tiles of 8 x 32 outputs)
+    B, T = 4, 128
+    if kind == "enc":  # 5x2 stride-(2,1), the encoder blocks (fp32: the student's enc2 / enc3)
+        if dt == "bf16":
+            F, Cin = (128, 32) if N == 64 else (34, 64)  # teacher enc1 (halo) / gemm8 shapes
+        else:
+            F, Cin = (64, 16) if N == 32 else (32, 32)
         taps = [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)]
         Fo, sf = (F + 4 - 5) // 2 + 1, 2
     else:  # 3x3, the ABF conv2
-        F, Cin = 20, 64
+        F, Cin = 40, 64
         taps = [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)]
         Fo, sf = F, 1
     tdt = torch.bfloat16 if dt == "bf16" else torch.float32

@@ -136,12 +136,10 @@ def test_conv_direct_against_torch_and_engine(dt, C1, C2, N):
 @pytest.mark.parametrize("N", [45, 64, 96, 100, 136, 256, 300])
 @pytest.mark.parametrize("out_bf16", [False, True])
 def test_conv_bf16_engine_against_torch(N, out_bf16):
-    """The bf16 dispatch (conv_halo for N <= 64, the persistent conv_gemm8 above; every tile
-    configuration it picks for these N): 2-segment 5x2 stride-(2,1) conv with fused BN
-    statistics, M not a tile multiple, vs torch in fp64 on the same bf16 operands.  A shape
-    neither kernel takes (N = 45 here) is refused by the product library, never run on a slower
-    fallback.  Tolerance: outputs 1e-4 relative (fp32 accumulation; bf16 output storage adds
-    its own rounding: 8e-3), statistics 1e-5 relative."""
+    """bf16 LDS-DMA MFMA engine (every tile configuration the dispatcher picks for these N):
+    2-segment 5x2 stride-(2,1) conv with fused BN statistics, M not a tile multiple, vs torch in
+    fp64 on the same bf16 operands.  Tolerance: outputs 1e-4 relative (fp32 accumulation;
+    bf16 output storage adds its own rounding: 8e-3), statistics 1e-5 relative."""
     from clskd import ops
     g = torch.Generator().manual_seed(N)
     B, F, T, C1, C2 = 3, 34, 61, 64, 32
@@ -161,13 +159,8 @@ def test_conv_bf16_engine_against_torch(N, out_bf16):
     out = torch.empty(B, Fo, To, N, device=DEV, dtype=torch.bfloat16 if out_bf16 else torch.float32)
     nblk = ops.conv_mblocks(B, Fo, To)
     st = torch.full((nblk * N * 2,), float("nan"), device=DEV, dtype=torch.float64)
-    args = ([ops.seg_bftc(x.to(DEV)) for x in segs_h], taps, B, Fo, To, N, wp, bias.to(DEV), out,
-            ops.OutMap(Fo * To * N, To * N, N))
-    if N == 45:
-        with pytest.raises(RuntimeError, match="fits neither"):
-            ops.conv(*args, stride_f=2, stats=st)
-        return
-    ops.conv(*args, stride_f=2, stats=st)
+    ops.conv([ops.seg_bftc(x.to(DEV)) for x in segs_h], taps, B, Fo, To, N, wp, bias.to(DEV), out,
+             ops.OutMap(Fo * To * N, To * N, N), stride_f=2, stats=st)
     o = out.permute(0, 3, 1, 2).double().cpu()
     tol = 8e-3 if out_bf16 else 1e-4
     np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=tol, atol=tol)
@@ -488,7 +481,7 @@ def test_bn_apply_gram_fused_matches_separate_passes(dtype, B):
     assert torch.equal(xf, y), "fused apply differs from clskd_bn_apply"
     assert fused.slabs.numel() == ref.slabs.numel()
     assert torch.equal(fused.slabs, ref.slabs), "fused Gram partials differ"
-    loss, gs, gt = ops.spkd_finalize(fused.refs, ref.refs, B, return_grams=True)
+    loss, gs, gt = ops.spkd_finalize(fused.refs, ref.refs, B, return_grams=True, device=x.device)
     torch.cuda.synchronize()
     assert loss.item() == 0.0
     np.testing.assert_allclose(_np(gs[0]), R.spkd_gram(y.permute(0, 3, 1, 2).double().cpu()).numpy(),
