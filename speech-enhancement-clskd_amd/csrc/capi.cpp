@@ -46,6 +46,8 @@ static const KnobDef kKnobs[KNOB_COUNT] = {
     {"CLSKD_ABF_MOMENT_DIV", 1, false}, {"CLSKD_F32_WAVES", 4, false}, {"CLSKD_EXEC_GATE", 0, false},
     {"CLSKD_NO_HALO32", 0, true},
     {"CLSKD_HALO32_SPLIT", 0, true}, {"CLSKD_HALO32_MIN_N", 32, true}, {"CLSKD_G8_KORDER", 1, false},
+    {"CLSKD_G8_PP", 0, true},
+    {"CLSKD_F32_SPLIT", 0, true},
     {"CLSKD_LSTM128_TDIV", 0, false},
     {"CLSKD_LSTM32_TDIV", 0, false}, {"CLSKD_BF16_DEBUG_MODE", 0, false}, {"CLSKD_SKIP", 0, false},
     {"CLSKD_H32_DEBUG_MODE", 0, false},

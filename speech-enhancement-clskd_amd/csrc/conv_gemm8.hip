@@ -112,7 +112,7 @@ struct ConvArgsG8 {
 // 6 = s_setprio 1 around each substep's MFMA cluster, 7 = static priority 1 for waves 4-7, 8 = both;
 // 9 = no DMA wait inside the stream (timing only: DMA latency vs issue cost).
 template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8,
-          int EB = 0, typename InT = __bf16>
+          int EB = 0, typename InT = __bf16, int PP = 0>
 __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 args) {
   using namespace g8;
   const clskd_conv_desc& d = args.d;
@@ -357,12 +357,56 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
 #pragma unroll
     for (int s = 0; s < PF; ++s) read_frags(sa, s, fa[s], fb[s]);
   };
-  read_head(stages);
+  if constexpr (!PP) read_head(stages);
   if constexpr (DBG == 7 || DBG == 8)
     if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   int gk = 0;  // stream index of the K-tile being computed
   double fS = 0.0, fQ = 0.0;  // fold: thread tid < HALVES*BN owns (half tid / BN, column tid % BN)
   for (int j = 0; j < ntl; ++j) {
+    if constexpr (PP) {
+      // Ping-pong K loop (cdna_hip_programming.md §5 8-phase template, T3-T5): every 16-deep
+      // substep is a phase {LOAD: this substep's fragments + this wave's share of the next
+      // K-tile's LDS-DMA pieces; barrier; MFMA cluster at priority 1; barrier}.  Waves w and
+      // w + 4 share a SIMD; group 1 (waves 4-7) runs one barrier behind group 0, so on every
+      // SIMD one wave's MFMA cluster covers the other wave's LDS reads, DMA issue and address
+      // VALU.  The groups re-align (group 0's extra barrier) for the tile epilogue.
+      static_assert(NS == 2 && NWV == 8 && PF == 1, "ping-pong: two stages, 8 waves");
+      const bool lag = wave >= 4;
+      if (lag) raw_barrier();
+      for (int kt = 0; kt < nk; ++kt, ++gk) {
+        const unsigned char* sa = stages + (gk % NS) * SB;
+        const int wi = gk + 1;  // the K-tile whose pieces this K-tile issues
+        const bool do_issue = wi < total;
+        int kti = 0;
+        KEnt e{};
+        if (do_issue) {
+          const int jt = wi / nk;
+          kti = next_kt();
+          if (jt != geo_tile) load_geometry(jt);
+          e = kdecode(ctab[kti * CPR + csrc]);
+        }
+        const int sn = wi % NS;
+        constexpr int GH = (G + 1) / 2;  // pieces per issuing phase (phases 0 and 1)
+#pragma unroll
+        for (int s = 0; s < NSUB; ++s) {
+          read_frags(sa, s, fa[0], fb[0]);
+          if (s < 2 && do_issue) {
+#pragma unroll
+            for (int g = s * GH; g < (s + 1) * GH && g < G; ++g)
+              glds16((const void*)piece_src(g, kti, e), dst(g, sn));
+          }
+          // the next K-tile's pieces (issued in phases 0-1) landed before the barrier that
+          // every wave passes ahead of the next K-tile's first fragment read
+          if (s == NSUB - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          raw_barrier();
+          __builtin_amdgcn_s_setprio(1);
+          mfmas(fa[0], fb[0]);
+          __builtin_amdgcn_s_setprio(0);
+          raw_barrier();
+        }
+      }
+      if (!lag) raw_barrier();  // re-align the groups: the epilogue runs in lockstep
+    } else
     for (int kt = 0; kt < nk; ++kt, ++gk) {
       const unsigned char* sa = stages + (gk % NS) * SB;
       // the K-tile issued during this one: stream gk + NS - 1
@@ -541,7 +585,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
       if (j + 2 < ntl) build_table(j + 2, j & 1);
       raw_barrier();
       init_acc(j + 1);
-      read_head(stages + (gk % NS) * SB);
+      if constexpr (!PP) read_head(stages + (gk % NS) * SB);
     }
   }
   if (fold) {  // the two 128-row halves in a fixed order, then the folded finalize
@@ -569,7 +613,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
 }
 
 template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8,
-          int EB = 0, typename InT = __bf16>
+          int EB = 0, typename InT = __bf16, int PP = 0>
 static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   using namespace g8;
   constexpr int SB = (BM + BN) * 2 * BK;
@@ -579,7 +623,7 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
     set_error("conv2d(bf16 g8): K=%d N=%d needs %zu B of LDS", d.K, d.N, lds);
     return CLSKD_E_SHAPE;
   }
-  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG, PF, NWV, EB, InT>;
+  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG, PF, NWV, EB, InT, PP>;
   static bool attr_set = false;  // per instantiation
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -608,11 +652,11 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NWV * 64), lds, st, a);
   note_kernel_fn((const void*)kern);
   if constexpr (__is_same(InT, _Float16))
-    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d,f16>", BM, BN, WM, BK, NS, PHI,
-                type_name<OutT>(), DBG, PF, NWV, EB);
+    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d,f16%s>", BM, BN, WM, BK, NS, PHI,
+                type_name<OutT>(), DBG, PF, NWV, EB, PP ? ",pp" : "");
   else
-    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d>", BM, BN, WM, BK, NS, PHI,
-                type_name<OutT>(), DBG, PF, NWV, EB);
+    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d%s>", BM, BN, WM, BK, NS, PHI,
+                type_name<OutT>(), DBG, PF, NWV, EB, PP ? ",bf16,pp" : "");
   return CLSKD_OK;
 }
 
@@ -695,6 +739,13 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
                  : launch_g8<256, 128, 4, 64, 2, 2, _Float16, 0, 1, 8, 1, _Float16>(d, st);
     return f32 ? launch_g8<256, 256, 2, 64, 2, 2, float, 0, 1, 8, 1, _Float16>(d, st)
                : launch_g8<256, 256, 2, 64, 2, 2, _Float16, 0, 1, 8, 1, _Float16>(d, st);
+  }
+  if (knob(KNOB_G8_PP) == 1) {  // ping-pong K loop (A/B; tests/test_gpu_parity.py)
+    if (d.N <= 128)
+      return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float, 0, 1, 8, 1, __bf16, 1>(d, st)
+                 : launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 1, 8, 1, __bf16, 1>(d, st);
+    return f32 ? launch_g8<256, 256, 2, 64, 2, 2, float, 0, 1, 8, 1, __bf16, 1>(d, st)
+               : launch_g8<256, 256, 2, 64, 2, 2, __bf16, 0, 1, 8, 1, __bf16, 1>(d, st);
   }
   if (d.N <= 128) {
     return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float, 0, 1, 8, 1>(d, st)

@@ -336,6 +336,7 @@ int launch_conv_direct(const clskd_conv_desc& d, hipStream_t st);
 
 int launch_conv_pointwise(const clskd_conv_desc& d, hipStream_t st, bool* launched);
 int launch_conv_halo_f32(const clskd_conv_desc& d, hipStream_t st, bool* launched);
+int launch_conv_split3(const clskd_conv_desc& d, hipStream_t st, bool* launched);
 
 }  // namespace clskd
 
@@ -346,6 +347,7 @@ bool conv_halo_takes(const clskd_conv_desc& d);
 bool conv_halo_f32_takes(const clskd_conv_desc& d);
 bool conv_gemm8_takes(const clskd_conv_desc& d);
 bool conv_pointwise_takes(const clskd_conv_desc& d);
+bool conv_split3_takes(const clskd_conv_desc& d);
 }  // namespace clskd
 
 // The kernel a descriptor dispatches to folds the BatchNorm finalize (clskd_bn_fold): the
@@ -357,6 +359,7 @@ static bool fold_capable(const clskd_conv_desc& d) {
     return conv_gemm8_takes(d) && d.N <= 256;  // one N-tile (256x256 / 256x128 instances)
   }
   if (conv_pointwise_takes(d)) return false;
+  if (conv_split3_takes(d)) return true;
   return knob(KNOB_NO_HALO32) != 1 && conv_halo_f32_takes(d);
 }
 
@@ -442,6 +445,15 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
     if (rc != CLSKD_OK) return rc;
     if (launched) {
       CLSKD_LAUNCH_CHECK("conv2d_pointwise");
+      return CLSKD_OK;
+    }
+  }
+  {  // fp32-accurate 3 x bf16 split products on the bf16 MFMA pipe (CLSKD_F32_SPLIT=1)
+    bool launched = false;
+    const int rc = launch_conv_split3(d, st, &launched);
+    if (rc != CLSKD_OK) return rc;
+    if (launched) {
+      CLSKD_LAUNCH_CHECK("conv2d_split3");
       return CLSKD_OK;
     }
   }

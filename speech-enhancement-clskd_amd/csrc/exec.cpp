@@ -57,6 +57,7 @@ struct clskd_exec {
   std::vector<hipMemsetParams> memsets;
   std::vector<hipMemcpy3DParms> memcpys;
   std::vector<Op> program;
+  size_t join_at = 0;  // program[join_at..]: every used side stream's join into stream 0
   int32_t n_nodes = 0, n_waits = 0, n_records = 0, n_empty = 0;
   int32_t per_stream[8] = {0};
   // optional live timing of one kernel (bench: the dominant instance): an event pair around
@@ -175,6 +176,15 @@ extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, void* const*
       if (!p.func || (p.extra && !p.kernelParams)) {
         delete ex;
         set_error("exec_create: kernel node %zu has no host function or uses 'extra' arguments", i);
+        return CLSKD_E_ARG;
+      }
+      // replayed with hipLaunchKernel: p.func must be a registered host stub, not a
+      // hipFunction_t captured from a module launch (rejected here instead of failing mid-step)
+      hipFuncAttributes fa{};
+      if (hipFuncGetAttributes(&fa, p.func) != hipSuccess) {
+        (void)hipGetLastError();
+        delete ex;
+        set_error("exec_create: kernel node %zu is not a host-stub launch (module kernel?)", i);
         return CLSKD_E_ARG;
       }
       slot[i] = (int)ex->kernels.size();
@@ -381,6 +391,7 @@ extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, void* const*
       ++ex->n_records;
     }
   }
+  ex->join_at = ex->program.size();
   for (int s = 1; s < S; ++s)
     if (used[s]) {
       ex->program.push_back(Op{OP_RECORD, (uint8_t)s, ev_join0 + s - 1});
@@ -398,7 +409,8 @@ extern "C" int clskd_exec_launch(clskd_exec* ex, void* stream) {
   const int S1 = ex->nstreams + 1;
   hipEvent_t* mk = ex->mk.empty() ? nullptr : &ex->mk[(size_t)(ex->mk_n % clskd_exec::MK) * S1];
   if (mk) (void)hipEventRecord(mk[0], st[0]);
-  for (const Op& op : ex->program) {
+  for (size_t i = 0; i < ex->program.size(); ++i) {
+    const Op& op = ex->program[i];
     hipError_t e = hipSuccess;
     const hipStream_t s = st[op.stream];
     switch (op.kind) {
@@ -432,7 +444,16 @@ extern "C" int clskd_exec_launch(clskd_exec* ex, void* stream) {
         e = hipEventRecord(ex->events[op.idx], s);
         break;
     }
-    if (e != hipSuccess) return hip_fail("launch", e);
+    if (e != hipSuccess) {
+      // still join every side stream back into the caller's, so later work on stream 0 stays
+      // ordered after whatever part of the step was enqueued
+      for (size_t j = ex->join_at; j < ex->program.size(); ++j) {
+        const Op& jo = ex->program[j];
+        if (jo.kind == OP_RECORD) (void)hipEventRecord(ex->events[jo.idx], st[jo.stream]);
+        else (void)hipStreamWaitEvent(st[jo.stream], ex->events[jo.idx], 0);
+      }
+      return hip_fail("launch", e);
+    }
   }
   if (mk) {
     for (int s = ex->nstreams - 1; s >= 0; --s) (void)hipEventRecord(mk[1 + s], st[s]);

@@ -962,15 +962,19 @@ G8_CASES = {
 }
 
 
+@pytest.mark.parametrize("loop", ["phased", "pingpong"])
 @pytest.mark.parametrize("lp", ["bf16", "fp16"])
 @pytest.mark.parametrize("case", sorted(G8_CASES))
-def test_conv_gemm8_against_torch(case, lp):
+def test_conv_gemm8_against_torch(case, lp, loop):
     """Phase-interleaved 8-wave bf16 GEMM engine (conv_gemm8.hip; N > 64): im2col 5x2 stride-2,
     two-segment polyphase decoder layers with an interleaved output map, ABF 3x3, and pointwise
     layers with 1-3 K-tiles (pipeline prologue/drain edge cases), fused BN statistics, M not a
     tile multiple; vs torch fp64 on the same bf16 operands.  Tolerance 1e-4 relative (fp32 out)
-    / 8e-3 (bf16 out); statistics 1e-5."""
-    from clskd import ops
+    / 8e-3 (bf16 out); statistics 1e-5.  loop: the phase-interleaved K loop or the ping-pong one
+    (CLSKD_G8_PP=1, bf16 operands)."""
+    from clskd import _lib, ops
+    if loop == "pingpong" and lp == "fp16":
+        pytest.skip("the ping-pong K loop is built for bf16 operands")
     segc, N, taps, sf, Fi, Fo, of_mul, of_add, out_bf16 = G8_CASES[case]
     g = torch.Generator().manual_seed(len(case) * 13 + N)
     B, T = 3, 97
@@ -996,10 +1000,16 @@ def test_conv_gemm8_against_torch(case, lp):
     out = torch.zeros(B, Fout, T, N, device=DEV, dtype=_LP[lp] if out_bf16 else torch.float32)
     nblk = ops.conv_mblocks(B, Fo, T)
     st = torch.full((nblk * N * 2,), float("nan"), device=DEV, dtype=torch.float64)
-    ops.conv([ops.seg_bftc(s.to(DEV)) for s in segs_h], taps, B, Fo, T, N, wp, bias.to(DEV), out,
-             ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add), stride_f=sf, stats=st)
-    kname = ops.conv_kernel_of_last_launch()
+    prev = _lib.set_knob("CLSKD_G8_PP", int(loop == "pingpong"))
+    try:
+        ops.conv([ops.seg_bftc(s.to(DEV)) for s in segs_h], taps, B, Fo, T, N, wp, bias.to(DEV),
+                 out, ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add),
+                 stride_f=sf, stats=st)
+        kname = ops.conv_kernel_of_last_launch()
+    finally:
+        _lib.set_knob("CLSKD_G8_PP", prev)
     assert kname.startswith("conv_gemm8") and (kname.endswith(",f16>") == (lp == "fp16")), kname
+    assert kname.endswith(",pp>") == (loop == "pingpong"), kname
     o = out.double().cpu()[:, of_add::of_mul]
     tol = _LP_TOL[lp] if out_bf16 else 1e-4
     np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=tol, atol=tol)
