@@ -322,9 +322,16 @@ def run_c5(args, dev):
     frames_clip = cfg.n_frames(L)
     value = S / per_hop
     # roofline of the hop kernel: per stream and hop 3.8 MMAC (SURVEY.md §8 d, 7.6 MFLOP) on fp32
-    # v_pk_fma_f32 (fp32 vector peak = the fp32 matrix peak, 157.3 TF/s); the 3.2 MB of weights
-    # per stream and hop come from the XCD L2s (MI355X_MICROARCH.md: 66-73 GB/s per CU gathered)
+    # v_pk_fma_f32, one 512-thread workgroup per stream.  The hop is bound by VALU instruction
+    # issue, not by FLOPs: profiles/r3_stream_c5_sq_counters.json counts 137.3 k VALU wave-
+    # instructions per hop (8 waves), i.e. 34.3 k per SIMD; a wave64 VALU instruction holds its
+    # SIMD 4 cycles (16 lanes), so one hop cannot take less than 137 k cycles = 57 us at 2.4 GHz
+    # whatever its FLOP count.  Priced as achieved VALU issue rate per SIMD (instructions per
+    # cycle) against that 0.25 ceiling; the FLOP rate against the fp32 vector peak is the note.
     fl = 7.6e6 * S / (kern_ms * 1e-3) / 1e12
+    valu_per_hop, clk = 137344.0, 2.4e9
+    cus = min(S, 256)
+    issue = valu_per_hop * S / (kern_ms * 1e-3 * clk * 4 * cus)
     out = {
         "metric": METRIC_C5, "value": round(value, 1), "unit": "frames/s", "n_gpus": 1,
         "steps": K, "warmup": args.warmup, "ms_per_step": round(per_hop * 1e3, 4),
@@ -333,13 +340,15 @@ def run_c5(args, dev):
         "config": {"workload": f"C5: {S} concurrent streams x 30 s @16 kHz, student eval BN, one "
                                "clskd_stream_hop launch per 6.25 ms hop (algorithmic latency 9 hops "
                                "= 56.25 ms)", "legs": legs},
-        "roofline": {"bound": "mfma", "kernel": "stream_hop_kernel", "achieved": round(fl, 3),
-                     "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(fl / PEAK_F32_MFMA_TFLOPS, 5), "traffic": None,
-                     "note": "fp32 VALU (v_pk_fma_f32), one workgroup per stream; per CU the hop "
-                             "is bound by instruction issue and load latency "
-                             "(profiles/r3_stream_c5_sq_counters.json), weights from L2: "
-                             f"{round(3.2e6 * S / (kern_ms * 1e-3) / 1e12, 2)} TB/s aggregate"},
+        "roofline": {"bound": "valu_issue", "kernel": "stream_hop_kernel", "achieved": round(issue, 4),
+                     "peak": 0.25, "unit": "VALU wave-instructions / cycle / SIMD",
+                     "frac": round(issue / 0.25, 4), "traffic": None,
+                     "note": "137.3 k VALU wave-instructions per hop and stream "
+                             "(profiles/r3_stream_c5_sq_counters.json) on the stream's CU at 2.4 GHz; "
+                             "a wave64 VALU op holds a SIMD 4 cycles (ceiling 0.25/cycle); the rest "
+                             "of the hop is load latency (SQ_WAIT_ANY 53 % of wave cycles). FLOP view: "
+                             f"{round(fl, 3)} TF/s = {round(fl / PEAK_F32_MFMA_TFLOPS, 4)} of the fp32 "
+                             f"vector peak; weights from L2 {round(3.2e6 * S / (kern_ms * 1e-3) / 1e12, 2)} TB/s"},
         "cpu_baseline": {"value": round(frames_clip / cpu_s, 1), "unit": "frames/s",
                          "cores": usable, "kind": "port", "cpu_model": model, "host_cpus": total,
                          "sample": "oracle/ref_cpu.dccrn_forward(train=False) offline over one 30 s "

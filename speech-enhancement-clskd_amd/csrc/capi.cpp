@@ -48,6 +48,7 @@ static const KnobDef kKnobs[KNOB_COUNT] = {
     {"CLSKD_HALO32_SPLIT", 0, true}, {"CLSKD_HALO32_MIN_N", 32, true}, {"CLSKD_G8_KORDER", 1, false},
     {"CLSKD_G8_PP", 0, true},
     {"CLSKD_F32_SPLIT", 0, true},
+    {"CLSKD_LSTM_PRIO", 0, true},
     {"CLSKD_LSTM128_TDIV", 0, false},
     {"CLSKD_LSTM32_TDIV", 0, false}, {"CLSKD_BF16_DEBUG_MODE", 0, false}, {"CLSKD_SKIP", 0, false},
     {"CLSKD_H32_DEBUG_MODE", 0, false},

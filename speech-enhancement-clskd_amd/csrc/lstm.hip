@@ -52,7 +52,10 @@ template <int H, int NKS, int DBG = 0>
 __global__ __launch_bounds__(NKS * H) void lstm_recurrent_kernel(
     const float* __restrict__ gx, int64_t gx_ws, int64_t gx_seq, int64_t gx_t,
     const float* __restrict__ whh, int T, float* __restrict__ out, int64_t o_ws, int64_t o_seq,
-    int64_t o_t) {
+    int64_t o_t, int prio) {
+  // the serial chain shares its CU with the concurrent streams' GEMMs: issue priority keeps its
+  // per-step latency close to the isolated one (CLSKD_LSTM_PRIO)
+  if (prio) __builtin_amdgcn_s_setprio(3);
   constexpr int G = 4 * H;     // gate rows
   constexpr int KW = H / NKS;  // k-slice width
   constexpr int NT = NKS * H;  // threads
@@ -184,7 +187,8 @@ template <int H>
 __global__ __launch_bounds__(64) void lstm_wave_kernel(
     const float* __restrict__ gx, int64_t gx_ws, int64_t gx_seq, int64_t gx_t,
     const float* __restrict__ whh, int T, float* __restrict__ out, int64_t o_ws, int64_t o_seq,
-    int64_t o_t) {
+    int64_t o_t, int prio) {
+  if (prio) __builtin_amdgcn_s_setprio(3);
   constexpr int S = 64 / H;   // k-slices per unit
   constexpr int KW = H / S;   // k-slice width
   constexpr int G = 4 * H;
@@ -460,6 +464,7 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
   // H = 32: CLSKD_LSTM_NKS32 = 2 | 4 | 8 selects the k-sliced multi-wave kernel, 1 (default)
   // the single-wave kernel (lstm_wave_kernel: 245 ns/step against 281 for the 8-slice kernel)
   const int nks32 = knob(KNOB_LSTM_NKS32);
+  const int prio = knob(KNOB_LSTM_PRIO) == 1 ? 1 : 0;
   {
     const int rc = experiment_guard("CLSKD_LSTM32_TDIV", H == 32 ? knob(KNOB_LSTM32_TDIV) : 0);
     if (rc != CLSKD_OK) return rc;
@@ -468,7 +473,7 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
   }
 #define LSTM_LAUNCH(H_, NKS_) \
   hipLaunchKernelGGL((lstm_recurrent_kernel<H_, NKS_>), grid, dim3(NKS_ * H_), 0, st, gx, gx_ws, \
-                     gx_seq, gx_t, whh, T, out, o_ws, o_seq, o_t)
+                     gx_seq, gx_t, whh, T, out, o_ws, o_seq, o_t, prio)
   switch (H) {
     case 16:
       LSTM_LAUNCH(16, 4);
@@ -481,7 +486,7 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
       else if (nks32 == 2) LSTM_LAUNCH(32, 2);
       else if (nks32 == 8) LSTM_LAUNCH(32, 8);
       else hipLaunchKernelGGL(lstm_wave_kernel<32>, grid, dim3(64), 0, st, gx, gx_ws, gx_seq, gx_t,
-                              whh, T, out, o_ws, o_seq, o_t);
+                              whh, T, out, o_ws, o_seq, o_t, prio);
       break;
     case 64:
       LSTM_LAUNCH(64, 4);

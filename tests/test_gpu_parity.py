@@ -1022,27 +1022,30 @@ def test_conv_gemm8_against_torch(case, lp, loop):
 
 
 
-@pytest.mark.parametrize("variant", ["1", "8"])
-def test_lstm_recurrence_against_torch(variant):
+@pytest.mark.parametrize("prio", [0, 1])
+@pytest.mark.parametrize("variant", ["1", "8", "h128"])
+def test_lstm_recurrence_against_torch(variant, prio):
     """Complex-LSTM recurrence (tools_for_model.py:159-174, nn.LSTM gates i, f, g, o, zero
-    state) at the student's H = 32: the single-wave kernel (CLSKD_LSTM_NKS32=1, default) and the
-    8-slice multi-wave kernel, vs a torch fp64 recurrence on the same gate inputs.  Tolerance
+    state) at the student's H = 32 — the single-wave kernel (CLSKD_LSTM_NKS32=1, default) and the
+    8-slice multi-wave kernel — and the teacher's H = 128, each with and without the issue
+    priority (CLSKD_LSTM_PRIO), vs a torch fp64 recurrence on the same gate inputs.  Tolerance
     2e-5 (v_exp / v_rcp gate activations, fp32 state)."""
-    from clskd import ops
     from clskd import _lib
-    prev = _lib.set_knob("CLSKD_LSTM_NKS32", int(variant))
+    prev = _lib.set_knob("CLSKD_LSTM_NKS32", 1 if variant == "h128" else int(variant))
+    prev_p = _lib.set_knob("CLSKD_LSTM_PRIO", prio)
     try:
-        _lstm_recurrence_check()
+        _lstm_recurrence_check(128 if variant == "h128" else 32)
     finally:
         _lib.set_knob("CLSKD_LSTM_NKS32", prev)
+        _lib.set_knob("CLSKD_LSTM_PRIO", prev_p)
 
 
-def _lstm_recurrence_check():
+def _lstm_recurrence_check(H=32):
     from clskd import ops
     g = torch.Generator().manual_seed(3)
-    nws, nseq, T, H = 2, 5, 37, 32
+    nws, nseq, T = 2, 5, 37
     gx = torch.randn(nseq, T, nws * 4 * H, generator=g)
-    whh = torch.randn(nws, 4 * H, H, generator=g) * 0.2
+    whh = torch.randn(nws, 4 * H, H, generator=g) * (0.2 * (32 / H) ** 0.5)
     out = torch.empty(nws, nseq, T, H, device=DEV)
     ops.lstm_recurrent(gx.to(DEV), 4 * H, T * nws * 4 * H, nws * 4 * H, whh.to(DEV), nws, nseq, T, H,
                        out, nseq * T * H, T * H, H)
