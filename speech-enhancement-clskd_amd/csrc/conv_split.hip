@@ -35,8 +35,10 @@ namespace sp3 {
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
-// 16-B half h of a 32-B row (16 bf16 k's) holding k = 8h..8h+7
-__device__ __forceinline__ int swz(int row) { return (row >> 3) & 1; }
+// 16-B chunk swizzle of a plane row (BK bf16 k's = BK / 8 chunks): conflict-free 16-lane
+// fragment reads (BK 16: rows of 32 B, 8 rows cover the 64 banks; BK 32: rows of 64 B, 4 rows)
+template <int BK>
+__device__ __forceinline__ int swz(int row) { return BK == 16 ? (row >> 3) & 1 : (row >> 2) & 3; }
 
 // hi / lo bf16 split of 4 fp32 values (RNE both)
 __device__ __forceinline__ void split4(const f32x4 v, s16x4& hi, s16x4& lo) {
@@ -66,15 +68,18 @@ struct SplitArgs {
   BnFoldArgs f;
 };
 
-template <int NT, int NW>
+template <int NT, int NW, int BK>
 __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs args) {
   using namespace sp3;
   const clskd_conv_desc& d = args.d;
   constexpr int BM = 32 * NW, BN = 32 * NT, NTH = NW * 64;
-  constexpr int RSTEP = NTH / 4;                  // rows per pass of the A gather (4 k-quads a row)
+  constexpr int QR = BK / 4;                      // k-quads per row of a K-tile
+  constexpr int ROWB = BK * 2;                    // bytes of a plane row (BK bf16)
+  constexpr int RSTEP = NTH / QR;                 // rows per pass of the A gather
   constexpr int NRA = BM / RSTEP;                 // A float4 loads per thread per K-tile
-  constexpr int NBL = (BN * 4 + NTH - 1) / NTH;   // B float4 loads per thread per K-tile
-  constexpr int PA = BM * 32, PB = BN * 32;       // bytes of one bf16 plane (16 k's per row)
+  constexpr int NBL = (BN * QR + NTH - 1) / NTH;  // B float4 loads per thread per K-tile
+  constexpr int PA = BM * ROWB, PB = BN * ROWB;   // bytes of one bf16 plane
+  static_assert(BK == 16 || BK == 32, "K-tile depth");
   static_assert(NRA * RSTEP == BM, "A gather covers the tile");
   __shared__ __attribute__((aligned(16))) unsigned char sA[2][2][PA];  // [stage][hi, lo]
   __shared__ __attribute__((aligned(16))) unsigned char sB[2][2][PB];
@@ -89,7 +94,7 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
   const int l32 = lane & 31, h = lane >> 5;
   const int64_t M = (int64_t)d.B * d.Fo * d.To;
   const int64_t FoTo = (int64_t)d.Fo * d.To;
-  const int nk = d.K / 16;
+  const int nk = d.K / BK;
   const bool fold = args.f.acc != nullptr;
 
   // ---- this workgroup's tile list (XCD-aware contiguous runs, as conv_gemm8) ----------------
@@ -148,13 +153,13 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
   __syncthreads();
 
   // ---- per-thread gather geometry of the stream's current tile -------------------------------
-  const int kq = tid & 3;
+  const int kq = tid % QR;
   int rfi[NRA], rti[NRA], rvl[NRA], arb[NRA][4];
   int geo = -1, geo_n0 = 0;
   auto load_geometry = [&](int j) {
 #pragma unroll
     for (int i = 0; i < NRA; ++i) {
-      const int row = (tid >> 2) + RSTEP * i;
+      const int row = tid / QR + RSTEP * i;
       const int4 ri = rinfo[j & 1][row];
       rfi[i] = ri.x;
       rti[i] = ri.y;
@@ -172,7 +177,7 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
   const float* wgt = reinterpret_cast<const float*>(d.weight);
   f32x4 ra[NRA], rb[NBL];
   auto load_kt = [&](int kt) {
-    const int2 ce = ctab[kt * 4 + kq];
+    const int2 ce = ctab[kt * QR + kq];
     const int sg = (int)((unsigned)ce.y >> 24);
     const int dF = (int)(short)(ce.y & 0xFFFF);
     const int dT = (int)(signed char)((ce.y >> 16) & 0xFF);
@@ -191,19 +196,19 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
 #pragma unroll
     for (int i = 0; i < NBL; ++i) {
       const int idx = tid + NTH * i;
-      const int n = geo_n0 + (idx >> 2);
+      const int n = geo_n0 + idx / QR;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if ((idx >> 2) < BN && n < d.N)
-        v = *reinterpret_cast<const f32x4*>(wgt + (int64_t)n * d.K + kt * 16 + (idx & 3) * 4);
+      if (idx / QR < BN && n < d.N)
+        v = *reinterpret_cast<const f32x4*>(wgt + (int64_t)n * d.K + kt * BK + (idx % QR) * 4);
       rb[i] = v;
     }
   };
-  // split + write the registers into stage s: k-quad kq of a row = 8 B inside half kq >> 1
+  // split + write the registers into stage s: k-quad q of a row = 8 B inside chunk q >> 1
   auto store_kt = [&](int s) {
 #pragma unroll
     for (int i = 0; i < NRA; ++i) {
-      const int row = (tid >> 2) + RSTEP * i;
-      const int off = row * 32 + (((kq >> 1) ^ swz(row)) << 4) + (kq & 1) * 8;
+      const int row = tid / QR + RSTEP * i;
+      const int off = row * ROWB + (((kq >> 1) ^ swz<BK>(row)) << 4) + (kq & 1) * 8;
       s16x4 hi, lo;
       split4(ra[i], hi, lo);
       *reinterpret_cast<s16x4*>(&sA[s][0][off]) = hi;
@@ -212,9 +217,9 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
 #pragma unroll
     for (int i = 0; i < NBL; ++i) {
       const int idx = tid + NTH * i;
-      const int row = idx >> 2, q = idx & 3;
+      const int row = idx / QR, q = idx % QR;
       if (row < BN) {
-        const int off = row * 32 + (((q >> 1) ^ swz(row)) << 4) + (q & 1) * 8;
+        const int off = row * ROWB + (((q >> 1) ^ swz<BK>(row)) << 4) + (q & 1) * 8;
         s16x4 hi, lo;
         split4(rb[i], hi, lo);
         *reinterpret_cast<s16x4*>(&sB[s][0][off]) = hi;
@@ -256,7 +261,6 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
   __syncthreads();
 
   const int arow = wave * 32 + l32;
-  const int aoff = arow * 32 + ((h ^ swz(arow)) << 4);
   double st_s[NT], st_q[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) st_s[t] = st_q[t] = 0.0;
@@ -272,17 +276,21 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
         if (jn != geo) load_geometry(jn);
         load_kt(next_kt());
       }
-      const s16x8 ahi = *reinterpret_cast<const s16x8*>(&sA[s][0][aoff]);
-      const s16x8 alo = *reinterpret_cast<const s16x8*>(&sA[s][1][aoff]);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int brow = t * 32 + l32;
-        const int boff = brow * 32 + ((h ^ swz(brow)) << 4);
-        const s16x8 bhi = *reinterpret_cast<const s16x8*>(&sB[s][0][boff]);
-        const s16x8 blo = *reinterpret_cast<const s16x8*>(&sB[s][1][boff]);
-        acc[t] = mfma16<__bf16>(ahi, bhi, acc[t]);
-        accx[t] = mfma16<__bf16>(ahi, blo, accx[t]);
-        accx[t] = mfma16<__bf16>(alo, bhi, accx[t]);
+      for (int ks = 0; ks < BK / 16; ++ks) {  // 16-deep MFMA steps: chunk 2 ks + h of a row
+        const int aoff = arow * ROWB + (((2 * ks + h) ^ swz<BK>(arow)) << 4);
+        const s16x8 ahi = *reinterpret_cast<const s16x8*>(&sA[s][0][aoff]);
+        const s16x8 alo = *reinterpret_cast<const s16x8*>(&sA[s][1][aoff]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int brow = t * 32 + l32;
+          const int boff = brow * ROWB + (((2 * ks + h) ^ swz<BK>(brow)) << 4);
+          const s16x8 bhi = *reinterpret_cast<const s16x8*>(&sB[s][0][boff]);
+          const s16x8 blo = *reinterpret_cast<const s16x8*>(&sB[s][1][boff]);
+          acc[t] = mfma16<__bf16>(ahi, bhi, acc[t]);
+          accx[t] = mfma16<__bf16>(ahi, blo, accx[t]);
+          accx[t] = mfma16<__bf16>(alo, bhi, accx[t]);
+        }
       }
       if (pf) store_kt(s ^ 1);
       __syncthreads();
@@ -353,10 +361,10 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
 }
 
 // Plan: which instance, grid and K order; false = not this kernel (the caller's engines run).
-static bool split_plan(const clskd_conv_desc& d, SplitArgs& a, int& nt, int& grid) {
+static bool split_plan(const clskd_conv_desc& d, SplitArgs& a, int& nt, int& bk, int& grid) {
   if (d.compute != CLSKD_F32 || d.in_dtype != CLSKD_F32 || d.out_dtype != CLSKD_F32) return false;
   if (d.accumulate || d.wlayout != CLSKD_WLAYOUT_NK || !d.vec4) return false;
-  if (d.K % 16 || (int64_t)(d.K / 4) * 8 > 32 * 1024) return false;
+  if (d.K % 16 || (int64_t)(d.K / 4) * 8 > 32 * 1024) return false;  // K padded to 16 (host)
   if (d.nseg < 1 || d.nseg > 4 || d.stride_t < 1) return false;
   nt = d.N <= 32 ? 1 : d.N <= 64 ? 2 : 4;
   const int BN = 32 * nt, BM = 128;
@@ -368,11 +376,13 @@ static bool split_plan(const clskd_conv_desc& d, SplitArgs& a, int& nt, int& gri
   a.n_mt = (int)n_mt;
   a.ntiles = (int)(n_mt * n_nt);
   a.nblk128 = (int)cdiv(M, 128);
+  // 32-deep K-tiles (128-B row segments per gather, half the barriers per MFMA) when K allows
+  bk = d.K % 32 == 0 ? 32 : 16;
   a.kt_taps = 1;
-  a.kt_cpt = d.K / 16;
-  if (d.ntaps > 1 && d.ctot % 16 == 0 && (int64_t)d.ntaps * d.ctot == d.K) {
+  a.kt_cpt = d.K / bk;
+  if (d.ntaps > 1 && d.ctot % bk == 0 && (int64_t)d.ntaps * d.ctot == d.K) {
     a.kt_taps = d.ntaps;
-    a.kt_cpt = d.ctot / 16;
+    a.kt_cpt = d.ctot / bk;
   }
   a.f = make_bnfold(d);
   static int ncu = [] {
@@ -390,27 +400,33 @@ static bool split_plan(const clskd_conv_desc& d, SplitArgs& a, int& nt, int& gri
 bool conv_split3_takes(const clskd_conv_desc& d) {
   if (knob(KNOB_F32_SPLIT) != 1) return false;
   SplitArgs a;
-  int nt = 0, grid = 0;
-  return split_plan(d, a, nt, grid);
+  int nt = 0, bk = 0, grid = 0;
+  return split_plan(d, a, nt, bk, grid);
 }
 
 int launch_conv_split3(const clskd_conv_desc& d, hipStream_t st, bool* launched) {
   *launched = false;
   if (knob(KNOB_F32_SPLIT) != 1) return CLSKD_OK;
   SplitArgs a;
-  int nt = 0, grid = 0;
-  if (!split_plan(d, a, nt, grid)) return CLSKD_OK;
+  int nt = 0, bk = 0, grid = 0;
+  if (!split_plan(d, a, nt, bk, grid)) return CLSKD_OK;
   const size_t ctab_bytes = (size_t)(d.K / 4) * 8;
-#define SP3(NT_)                                                                       \
+#define SP3(NT_, BK_)                                                                  \
   do {                                                                                 \
-    auto k = conv_split3_kernel<NT_, 4>;                                               \
+    auto k = conv_split3_kernel<NT_, 4, BK_>;                                          \
     hipLaunchKernelGGL(k, dim3(grid), dim3(256), ctab_bytes, st, a);                   \
     note_kernel_fn((const void*)k);                                                    \
-    note_kernel("conv_split3_kernel<%d,4>", NT_);                                      \
+    note_kernel("conv_split3_kernel<%d,4,%d>", NT_, BK_);                              \
   } while (0)
-  if (nt == 1) SP3(1);
-  else if (nt == 2) SP3(2);
-  else SP3(4);
+  if (bk == 32) {
+    if (nt == 1) SP3(1, 32);
+    else if (nt == 2) SP3(2, 32);
+    else SP3(4, 32);
+  } else {
+    if (nt == 1) SP3(1, 16);
+    else if (nt == 2) SP3(2, 16);
+    else SP3(4, 16);
+  }
 #undef SP3
   *launched = true;
   return CLSKD_OK;

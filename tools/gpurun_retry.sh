@@ -4,7 +4,7 @@
 # charged).  Any run that actually executed — pass or fail — is returned as is, never retried.
 #   tools/gpurun_retry.sh <timeout_s> '<command>'
 T=$1; shift
-for attempt in 1 2 3 4 5 6 7 8 9 10; do
+for attempt in $(seq 1 ${RETRIES:-10}); do
   out=$(/usr/local/graft/bin/gpurun --timeout "$T" -- "$@" 2>&1)
   rc=$?
   echo "$out" | grep -v "every call sends" | tail -12
