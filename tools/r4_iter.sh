@@ -23,6 +23,7 @@ rc=0; CLSKD_F32_SPLIT=1 timeout -k 10 200 python $R/tools/conv_census.py > $O/ce
 rc=0; CLSKD_F32_SPLIT=1 timeout -k 10 300 python $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_split.log 2>&1 || rc=$?; ok $rc
 rc=0; CLSKD_LSTM_PRIO=1 timeout -k 10 300 python $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_lprio.log 2>&1 || rc=$?; ok $rc
 rc=0; CLSKD_LSTM_PRIO=1 CLSKD_F32_SPLIT=1 CLSKD_G8_PP=1 timeout -k 10 300 python $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_all.log 2>&1 || rc=$?; ok $rc
+rc=0; timeout -k 10 200 python $R/tools/host_profile.py > $O/host_profile.txt 2>&1 || rc=$?; ok $rc
 cd /tmp && export TMPDIR=/tmp
 rc=0; timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/trace.log 2>&1 || rc=$?; ok $rc
 python3 $R/tools/region_stats.py $O/trace/run 20 $O/region_stats.json > $O/region_stats.txt 2>&1 || true
