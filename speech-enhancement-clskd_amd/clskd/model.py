@@ -518,12 +518,17 @@ class DCCRN(nn.Module):
                 if train:  # one BatchNorm over both polyphase parities (2 x B*F*(T+1) rows)
                     st = ops.BnStats(bn, Co, 2 * B * F * (T + 1), bn_updates, dev,
                                      stats_out=(mv[0], mv[1]) if mv is not None else None)
+            launches = []
             for parity in (0, 1):
                 taps = [(dF, -kt) for _, dF in self._DEC_TAPS[parity] for kt in (0, 1)]
                 wp, bias = self._dec_w(d, parity, self._cmp(segs, len(taps) * Ci))
-                ops.conv(segs, taps, B, F, T + 1, Co, wp, bias, raw,
-                         OutMap(2 * F * (T + 1) * Co, (T + 1) * Co, Co, of_mul=2, of_add=parity),
-                         bn_stats=(st, parity == 1) if st is not None else None)
+                launches.append((segs, taps, B, F, T + 1, Co, wp, bias, raw,
+                                 OutMap(2 * F * (T + 1) * Co, (T + 1) * Co, Co, of_mul=2,
+                                        of_add=parity)))
+            if st is not None and not all(ops.conv_folds(*a) for a in launches):
+                st.partials_only()  # the parities dispatch to different kernels: no fold
+            for parity, a in enumerate(launches):
+                ops.conv(*a, bn_stats=(st, parity == 1) if st is not None else None)
             if has_bn:
                 raw = self._norm(raw, bn, pr, st, train, bn_updates, tape, "dec_bn", mv,
                                  gram_taps if (fuse_gram and d < nl - 1) else None, B)

@@ -313,8 +313,17 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
     return pl
 
 
+def conv_folds(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, stride_f=1, stride_t=1):
+    """Whether a conv(..., bn_stats=...) launch with these arguments dispatches to a kernel that
+    folds the BatchNorm finalize (nothing launched).  A layer produced by several launches (the
+    decoder's polyphase parities) folds only if all of them can: BnStats.partials_only()."""
+    return conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, stride_f=stride_f,
+                stride_t=stride_t, bn_stats=(None, False), _query=True)
+
+
 def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, stride_f=1,
-         stride_t=1, stats=None, stats_offset=0, accumulate=False, mfma_only=False, bn_stats=None):
+         stride_t=1, stats=None, stats_offset=0, accumulate=False, mfma_only=False, bn_stats=None,
+         _query=False):
     """out[b, fo*of_mul+of_add, to, n] = bias[n] + sum_k A[(b,fo,to),k] W[n,k].
     bf16 segments run the LDS-DMA bf16-MFMA engine (weights packed bf16, K % 64); fp32 segments
     the fp32-MFMA engine (weights fp32, K % 16).  `out` may be fp32 or bf16 storage.
@@ -354,17 +363,20 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
     d.bn_fold = None
     if bn_stats is not None:
         st, last = bn_stats
-        if out_offset or N != st.C:
-            raise ValueError("conv: bn_stats needs the launch to produce all the BatchNorm's channels")
-        fold = st.fold_struct(bool(last), 0)
-        d.bn_fold = C.addressof(fold)
         if pl.fold is None or pl.fold[0] != _lib.KNOB_EPOCH:
             # which kernel the library dispatches this signature to (re-asked after a knob change)
-            pl.fold = (_lib.KNOB_EPOCH, bool(L.clskd_conv_fold_capable(C.byref(d))) and _BN_FOLD)
-        if not pl.fold[1]:
             d.bn_fold = None
+            pl.fold = (_lib.KNOB_EPOCH, bool(L.clskd_conv_fold_capable(C.byref(d))) and _BN_FOLD)
+        if _query:
+            return pl.fold[1]
+        if out_offset or N != st.C:
+            raise ValueError("conv: bn_stats needs the launch to produce all the BatchNorm's channels")
+        if pl.fold[1] and not st.no_fold:
+            fold = st.fold_struct(bool(last), 0)
+            d.bn_fold = C.addressof(fold)
+        else:
             stats, stats_offset = st.partials(conv_mblocks(B, Fo, To))
-        st.launched(pl.fold[1])
+        st.launched(d.bn_fold is not None)
     if stats is not None:
         if stats.dtype != torch.float64 or stats.numel() < stats_offset + pl.nstats:
             raise RuntimeError("conv: fused statistics buffer must be float64 with room for "
@@ -485,8 +497,14 @@ class BnStats:
         self.coef = torch.empty(2 * Cn, device=device, dtype=torch.float32)
         self.stats_out = stats_out
         self.mode = None  # "fold" | "part", set by the first launch
+        self.no_fold = False  # partials_only(): some launch of the layer cannot fold
         self.part, self.used, self.nblk = None, 0, 0
         self._keep = []
+
+    def partials_only(self):
+        """Every launch of this BatchNorm writes partials (one of them cannot fold)."""
+        self.no_fold = True
+        return self
 
     def fold_struct(self, last, c_off):
         acc, ticket = bn_fold_state(self.bn, self.C, self.dev)

@@ -46,7 +46,7 @@ static const KnobDef kKnobs[KNOB_COUNT] = {
     {"CLSKD_ABF_MOMENT_DIV", 1, false}, {"CLSKD_F32_WAVES", 4, false}, {"CLSKD_EXEC_GATE", 0, false},
     {"CLSKD_NO_HALO32", 0, true},
     {"CLSKD_HALO32_SPLIT", 0, true}, {"CLSKD_HALO32_MIN_N", 32, true}, {"CLSKD_G8_KORDER", 1, false},
-    {"CLSKD_G8_PP", 0, true},
+    {"CLSKD_G8_PP", 0, false},
     {"CLSKD_F32_SPLIT", 0, true},
     {"CLSKD_LSTM_PRIO", 0, true},
     {"CLSKD_LSTM128_TDIV", 0, false},
