@@ -17,6 +17,8 @@ rc=0; CLSKD_LSTM_PRIO=1 timeout -k 10 200 $B > $O/bench_lprio.log 2>&1 || rc=$?;
 rc=0; CLSKD_F32_SPLIT=1 timeout -k 10 200 $B > $O/bench_split.log 2>&1 || rc=$?; ok $rc
 rc=0; CLSKD_LSTM_PRIO=1 CLSKD_F32_SPLIT=1 timeout -k 10 200 $B > $O/bench_both.log 2>&1 || rc=$?; ok $rc
 rc=0; timeout -k 10 200 $B > $O/bench_a1.log 2>&1 || rc=$?; ok $rc
+rc=0; timeout -k 10 200 $B --launch exec > $O/bench_exec.log 2>&1 || rc=$?; ok $rc
+rc=0; CLSKD_LSTM_PRIO=1 CLSKD_F32_SPLIT=1 timeout -k 10 200 $B --launch exec > $O/bench_exec_both.log 2>&1 || rc=$?; ok $rc
 rc=0; CLSKD_F32_SPLIT=1 timeout -k 10 200 python $R/tools/conv_census.py > $O/census_split.txt 2>&1 || rc=$?; ok $rc
 rc=0; timeout -k 10 200 python $R/tools/host_profile.py > $O/host_profile.txt 2>&1 || rc=$?; ok $rc
 for f in $O/bench_*.log; do echo "$f $(grep '^{' $f | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d.get("host_enqueue_ms_per_step"), d.get("serialized_kernel_ms_per_step"))')"; done
