@@ -313,6 +313,9 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
     return pl
 
 
+_PROBE_FOLD = _lib.BnFold()  # zero fold record: clskd_conv_fold_capable inspects only presence
+
+
 def conv_folds(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, stride_f=1, stride_t=1):
     """Whether a conv(..., bn_stats=...) launch with these arguments dispatches to a kernel that
     folds the BatchNorm finalize (nothing launched).  A layer produced by several launches (the
@@ -365,8 +368,10 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
         st, last = bn_stats
         if pl.fold is None or pl.fold[0] != _lib.KNOB_EPOCH:
             # which kernel the library dispatches this signature to (re-asked after a knob change)
-            d.bn_fold = None
+            # — asked with a fold attached: eligibility can depend on it (epilogue scratch)
+            d.bn_fold = C.addressof(_PROBE_FOLD)
             pl.fold = (_lib.KNOB_EPOCH, bool(L.clskd_conv_fold_capable(C.byref(d))) and _BN_FOLD)
+            d.bn_fold = None
         if _query:
             return pl.fold[1]
         if out_offset or N != st.C:
