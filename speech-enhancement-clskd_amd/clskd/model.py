@@ -197,6 +197,8 @@ class DCCRN(nn.Module):
                 mods += [nn.BatchNorm2d(kn[idx - 1]), nn.PReLU()]
             self.decoder.append(nn.Sequential(*mods))
         self._wcache = {}
+        self._pgroups = {}
+        self._refs = None
         self._tap_sinks = []
         # MFMA operand type of the large GEMMs: "fp32" (exact-f32 MFMA), "bf16" / "fp16" (16-bit operands,
         # fp32 accumulation).  STFT/iSTFT framing GEMMs always run fp32.
@@ -234,6 +236,15 @@ class DCCRN(nn.Module):
         return {"bf16": torch.bfloat16, "fp16": torch.float16}.get(self.compute, torch.float32)
 
     def _packed(self, key, params, build):
+        """Packed operands of a parameter group, rebuilt when a parameter's storage or in-place
+        version changes.  params: the group's tensors, or a callable returning them (resolved
+        once per key: the module tree is fixed after construction, and nn.Module attribute
+        lookups are a measurable part of the step's host time)."""
+        if callable(params):
+            pg = self._pgroups.get(key)
+            if pg is None:
+                pg = self._pgroups[key] = tuple(params())
+            params = pg
         ent = self._wcache.get(key)
         ver = _pv(*params)
         if ent is None or ent[0] != ver:
@@ -242,8 +253,18 @@ class DCCRN(nn.Module):
             self._wcache[key] = ent
         return ent[1]
 
+    def _layer_refs(self):
+        """Per-layer module references, resolved once: encoder (conv, bn, prelu), decoder
+        (conv, bn | None, prelu | None), the LSTM stack."""
+        if self._refs is None:
+            enc = [(s[0], s[1], s[2]) for s in self.encoder]
+            dec = [(s[0], s[1] if len(s) > 1 else None, s[2] if len(s) > 1 else None)
+                   for s in self.decoder]
+            self._refs = dict(enc=enc, dec=dec, lstm=list(self.enhance))
+        return self._refs
+
     def _enc_w(self, i, compute="fp32"):
-        cc = self.encoder[i][0]
+        cc = self._layer_refs()["enc"][i][0]
 
         def build():
             wr, wi = cc.real_conv.weight, cc.imag_conv.weight  # [Co/2, Ci/2, 5, 2]
@@ -255,13 +276,13 @@ class DCCRN(nn.Module):
             bias = torch.cat([cc.real_conv.bias - cc.imag_conv.bias,
                               cc.imag_conv.bias + cc.real_conv.bias]).float().contiguous()
             return ops.pack_weight(w, 10 * Ci, compute), bias
-        return self._packed(("enc", i, compute), (cc.real_conv.weight, cc.imag_conv.weight,
-                                                  cc.real_conv.bias, cc.imag_conv.bias), build)
+        return self._packed(("enc", i, compute), lambda: (cc.real_conv.weight, cc.imag_conv.weight,
+                                                          cc.real_conv.bias, cc.imag_conv.bias), build)
 
     _DEC_TAPS = {0: ((0, 1), (2, 0), (4, -1)), 1: ((1, 1), (3, 0))}  # parity -> (kf, dF)
 
     def _dec_w(self, d, parity, compute="fp32"):
-        cc = self.decoder[d][0]
+        cc = self._layer_refs()["dec"][d][0]
 
         def build():
             wr, wi = cc.real_conv.weight, cc.imag_conv.weight  # [Ci/2, Co/2, 5, 2]
@@ -282,11 +303,12 @@ class DCCRN(nn.Module):
             bias = torch.cat([cc.real_conv.bias - cc.imag_conv.bias,
                               cc.imag_conv.bias + cc.real_conv.bias]).float().contiguous()
             return ops.pack_weight(w, len(taps) * Ci, compute), bias
-        return self._packed(("dec", d, parity, compute), (cc.real_conv.weight, cc.imag_conv.weight,
-                                                          cc.real_conv.bias, cc.imag_conv.bias), build)
+        return self._packed(("dec", d, parity, compute),
+                            lambda: (cc.real_conv.weight, cc.imag_conv.weight, cc.real_conv.bias,
+                                     cc.imag_conv.bias), build)
 
     def _lstm_w(self, li, compute="fp32"):
-        m = self.enhance[li]
+        m = self._layer_refs()["lstm"][li]
         R, I = m.real_lstm, m.imag_lstm
 
         def build():
@@ -307,10 +329,12 @@ class DCCRN(nn.Module):
                     out += [ops.pack_weight(lin.weight.unsqueeze(1), lin.weight.shape[1], compute),
                             lin.bias.float().contiguous()]
             return out
-        ps = [R.weight_ih_l0, I.weight_ih_l0, R.weight_hh_l0, I.weight_hh_l0, R.bias_ih_l0,
-              R.bias_hh_l0, I.bias_ih_l0, I.bias_hh_l0]
-        if m.projection_dim is not None:
-            ps += [m.r_trans.weight, m.r_trans.bias, m.i_trans.weight, m.i_trans.bias]
+        def ps():
+            p = [R.weight_ih_l0, I.weight_ih_l0, R.weight_hh_l0, I.weight_hh_l0, R.bias_ih_l0,
+                 R.bias_hh_l0, I.bias_ih_l0, I.bias_hh_l0]
+            if m.projection_dim is not None:
+                p += [m.r_trans.weight, m.r_trans.bias, m.i_trans.weight, m.i_trans.bias]
+            return p
         return self._packed(("lstm", li, compute), ps, build)
 
     def _stft_w(self):
@@ -429,7 +453,7 @@ class DCCRN(nn.Module):
             wp, bias = self._enc_w(i, self._cmp(segs, 10 * kn[i]))
             taps = [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)]
             raw = torch.empty(B, Fo, T, Co, **act)
-            bn, pr = self.encoder[i][1], self.encoder[i][2]
+            _, bn, pr = self._layer_refs()["enc"][i]
             mv = torch.empty(2, Co, **f32) if tape is not None else None
             st = (ops.BnStats(bn, Co, B * Fo * T, bn_updates, dev,
                               stats_out=(mv[0], mv[1]) if mv is not None else None)
@@ -482,7 +506,7 @@ class DCCRN(nn.Module):
             lstm_io.append((ro, io))
         # projection into the decoder input [B][D4][T][C6] (DCCRN.py:188-199)
         dec_in = torch.empty(B, D4, T, C6, **act)
-        m = self.enhance[self.hidden_layers - 1]
+        m = self._layer_refs()["lstm"][self.hidden_layers - 1]
         P = m.projection_dim
         for half in range(2):
             segs = [Seg(r_in[half], 0, SegGeom(H, T * H, 0, H, 1, T))]
@@ -506,14 +530,15 @@ class DCCRN(nn.Module):
             # the packed weights take K per tap as [out_t (re|im), skip (re|im)] (_dec_w)
             assert Cof == Csk, "DCCRN decoder: input and skip channel counts match"
             segs = [seg_bftc(out_t, 0, Cof, out_t0, out_T), seg_bftc(skip, 0, Csk)]
-            Co = self.decoder[d][0].out_channels * 2
+            dcv, dbn, dpr = self._layer_refs()["dec"][d]
+            Co = dcv.out_channels * 2
             last = d == nl - 1
             raw = torch.empty(B, 2 * F, T + 1, Co, **(f32 if last else act))
             Ci = sum(sg.geom.C for sg in segs)
-            has_bn = len(self.decoder[d]) > 1
+            has_bn = dbn is not None
             bn = pr = mv = st = None
             if has_bn:
-                bn, pr = self.decoder[d][1], self.decoder[d][2]
+                bn, pr = dbn, dpr
                 mv = torch.empty(2, Co, **f32) if tape is not None else None
                 if train:  # one BatchNorm over both polyphase parities (2 x B*F*(T+1) rows)
                     st = ops.BnStats(bn, Co, 2 * B * F * (T + 1), bn_updates, dev,
