@@ -622,6 +622,10 @@ int clskd_exec_tag(void* stream, int32_t tag);
 void clskd_exec_tag_reset(void);
 int clskd_exec_launch(clskd_exec* ex, void* stream);
 int clskd_exec_info(const clskd_exec* ex, int32_t* info, int32_t n);
+/* Text listing of the replay program (one op per line: index, kind, stream, slot, and for kernel
+ * ops the grid size, block size and kernel name) into buf (NUL-terminated, truncated at cap);
+ * returns the full length, or -1 for a null executor.  Diagnostic. */
+int64_t clskd_exec_dump(const clskd_exec* ex, char* buf, int64_t cap);
 void clskd_exec_destroy(clskd_exec* ex);
 /* Live timing of one kernel under the executor: every launch of host function `fn` (e.g.
  * clskd_conv_last_kernel_fn() after a conv call) gets a HIP event pair around it on its stream,

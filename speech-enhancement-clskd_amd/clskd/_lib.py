@@ -187,6 +187,7 @@ SIGNATURES = {
     "clskd_exec_tag_reset": (None, []),
     "clskd_exec_launch": (_i32, [_p, _p]),
     "clskd_exec_info": (_i32, [_p, C.POINTER(C.c_int32), _i32]),
+    "clskd_exec_dump": (_i64, [_p, C.c_char_p, _i64]),
     "clskd_exec_destroy": (None, [_p]),
     "clskd_exec_profile": (_i32, [_p, _p, _i32]),
     "clskd_exec_profile_read": (_i32, [_p, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),

@@ -38,7 +38,9 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 // 16-B chunk swizzle of a plane row (BK bf16 k's = BK / 8 chunks): conflict-free 16-lane
 // fragment reads (BK 16: rows of 32 B, 8 rows cover the 64 banks; BK 32: rows of 64 B, 4 rows)
 template <int BK>
-__device__ __forceinline__ int swz(int row) { return BK == 16 ? (row >> 3) & 1 : (row >> 2) & 3; }
+__device__ __forceinline__ int swz(int row) {
+  return BK == 16 ? (row >> 3) & 1 : BK == 32 ? (row >> 2) & 3 : (row >> 1) & 7;
+}
 
 // hi / lo bf16 split of 4 fp32 values (RNE both)
 __device__ __forceinline__ void split4(const f32x4 v, s16x4& hi, s16x4& lo) {
@@ -68,7 +70,10 @@ struct SplitArgs {
   BnFoldArgs f;
 };
 
-template <int NT, int NW, int BK>
+// NS LDS stages: 2 = the next K-tile is written to the other stage (one barrier per K-tile);
+// 1 = it is written in place after a second barrier (half the LDS: more workgroups per CU to
+// hide the register-staged gather's latency, which bounds this engine: ~1 µs per K-tile round)
+template <int NT, int NW, int BK, int NS>
 __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs args) {
   using namespace sp3;
   const clskd_conv_desc& d = args.d;
@@ -79,10 +84,13 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
   constexpr int NRA = BM / RSTEP;                 // A float4 loads per thread per K-tile
   constexpr int NBL = (BN * QR + NTH - 1) / NTH;  // B float4 loads per thread per K-tile
   constexpr int PA = BM * ROWB, PB = BN * ROWB;   // bytes of one bf16 plane
-  static_assert(BK == 16 || BK == 32, "K-tile depth");
+  static_assert(BK == 16 || BK == 32 || BK == 64, "K-tile depth");
+  static_assert(NS == 1 || NS == 2, "LDS stages");
   static_assert(NRA * RSTEP == BM, "A gather covers the tile");
-  __shared__ __attribute__((aligned(16))) unsigned char sA[2][2][PA];  // [stage][hi, lo]
-  __shared__ __attribute__((aligned(16))) unsigned char sB[2][2][PB];
+  // cross-term chain: NT >= 2 interleaves independent column accumulators already
+  constexpr bool XACC = NT == 1;
+  __shared__ __attribute__((aligned(16))) unsigned char sA[NS][2][PA];  // [stage][hi, lo]
+  __shared__ __attribute__((aligned(16))) unsigned char sB[NS][2][PB];
   __shared__ int4 rinfo[2][BM];  // fi0, ti0, valid
   __shared__ int rbase[2][4][BM];
   __shared__ int64_t orow[2][BM];
@@ -239,7 +247,7 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
     return k;
   };
 
-  f32x16 acc[NT], accx[NT];
+  f32x16 acc[NT], accx[XACC ? NT : 1];
   auto init_acc = [&](int j) {
     const int n0 = tile_nt(j) * BN;
 #pragma unroll
@@ -249,7 +257,7 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         acc[t][r] = bv;
-        accx[t][r] = 0.f;
+        if constexpr (XACC) accx[t][r] = 0.f;
       }
     }
   };
@@ -269,7 +277,7 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
   for (int j = 0; j < ntl; ++j) {
     init_acc(j);
     for (int kt = 0; kt < nk; ++kt, ++gk) {
-      const int s = gk & 1;
+      const int s = NS == 2 ? (gk & 1) : 0;
       const bool pf = gk + 1 < total;
       if (pf) {
         const int jn = (gk + 1) / nk;
@@ -288,12 +296,36 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
           const s16x8 bhi = *reinterpret_cast<const s16x8*>(&sB[s][0][boff]);
           const s16x8 blo = *reinterpret_cast<const s16x8*>(&sB[s][1][boff]);
           acc[t] = mfma16<__bf16>(ahi, bhi, acc[t]);
-          accx[t] = mfma16<__bf16>(ahi, blo, accx[t]);
-          accx[t] = mfma16<__bf16>(alo, bhi, accx[t]);
+          if constexpr (XACC) {
+            accx[t] = mfma16<__bf16>(ahi, blo, accx[t]);
+            accx[t] = mfma16<__bf16>(alo, bhi, accx[t]);
+          }
+        }
+        if constexpr (!XACC) {  // cross terms after every column's main term: no back-to-back
+#pragma unroll                   // dependent MFMA on one accumulator
+          for (int t = 0; t < NT; ++t) {
+            const int brow = t * 32 + l32;
+            const int boff = brow * ROWB + (((2 * ks + h) ^ swz<BK>(brow)) << 4);
+            const s16x8 bhi = *reinterpret_cast<const s16x8*>(&sB[s][0][boff]);
+            acc[t] = mfma16<__bf16>(alo, bhi, acc[t]);
+          }
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            const int brow = t * 32 + l32;
+            const int boff = brow * ROWB + (((2 * ks + h) ^ swz<BK>(brow)) << 4);
+            const s16x8 blo = *reinterpret_cast<const s16x8*>(&sB[s][1][boff]);
+            acc[t] = mfma16<__bf16>(ahi, blo, acc[t]);
+          }
         }
       }
-      if (pf) store_kt(s ^ 1);
-      __syncthreads();
+      if constexpr (NS == 2) {
+        if (pf) store_kt(s ^ 1);
+        __syncthreads();
+      } else {
+        __syncthreads();  // every wave is done reading the stage
+        if (pf) store_kt(0);
+        __syncthreads();
+      }
     }
 
     // ---- tile epilogue: statistics (valid rows / columns) and predicated stores ---------------
@@ -308,7 +340,8 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
       for (int r = 0; r < 16; ++r) {
         const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int64_t ro = orow[j & 1][row];
-        const float v = acc[t][r] + accx[t][r];
+        float v = acc[t][r];
+        if constexpr (XACC) v += accx[t][r];
         if (nok && ro >= 0) {
           sm += v;
           sq = fmaf(v, v, sq);
@@ -376,8 +409,11 @@ static bool split_plan(const clskd_conv_desc& d, SplitArgs& a, int& nt, int& bk,
   a.n_mt = (int)n_mt;
   a.ntiles = (int)(n_mt * n_nt);
   a.nblk128 = (int)cdiv(M, 128);
-  // 32-deep K-tiles (128-B row segments per gather, half the barriers per MFMA) when K allows
-  bk = d.K % 32 == 0 ? 32 : 16;
+  // the deepest K-tile K allows: each K-tile round costs about one gather latency, so deeper
+  // tiles carry more MFMA work per round (64: single LDS stage, two or three workgroups per CU)
+  bk = d.K % 64 == 0 ? 64 : d.K % 32 == 0 ? 32 : 16;
+  const int cap_bk = knob(KNOB_SPLIT_BK);  // A/B: the deepest K-tile allowed (0: 64)
+  if (cap_bk == 16 || cap_bk == 32) bk = bk < cap_bk ? bk : cap_bk;
   a.kt_taps = 1;
   a.kt_cpt = d.K / bk;
   if (d.ntaps > 1 && d.ctot % bk == 0 && (int64_t)d.ntaps * d.ctot == d.K) {
@@ -390,8 +426,12 @@ static bool split_plan(const clskd_conv_desc& d, SplitArgs& a, int& nt, int& bk,
     (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, 0);
     return v > 0 ? v : 256;
   }();
-  // two 4-wave workgroups per CU (two waves per SIMD hide the gather latency)
-  const int cap = 2 * ncu;
+  // 4-wave workgroups, as many per CU as LDS holds (up to three): more waves per SIMD hide more
+  // of the gather latency
+  const size_t tab = (size_t)2 * 128 * (16 + 16 + 8);
+  const size_t lds = (bk == 64 ? 1 : 2) * 2 * (size_t)(128 + 32 * nt) * bk * 2 + tab + (size_t)(d.K / 4) * 8;
+  const int per_cu = lds * 3 <= 160 * 1024 ? 3 : lds * 2 <= 160 * 1024 ? 2 : 1;
+  const int cap = per_cu * ncu;
   grid = a.ntiles < cap ? a.ntiles : cap;
   if (d.stats && grid > a.nblk128) return false;  // (never: BM = 128 rows a tile)
   return true;
@@ -413,12 +453,17 @@ int launch_conv_split3(const clskd_conv_desc& d, hipStream_t st, bool* launched)
   const size_t ctab_bytes = (size_t)(d.K / 4) * 8;
 #define SP3(NT_, BK_)                                                                  \
   do {                                                                                 \
-    auto k = conv_split3_kernel<NT_, 4, BK_>;                                          \
+    constexpr int NS_ = BK_ == 64 ? 1 : 2;                                             \
+    auto k = conv_split3_kernel<NT_, 4, BK_, NS_>;                                     \
     hipLaunchKernelGGL(k, dim3(grid), dim3(256), ctab_bytes, st, a);                   \
     note_kernel_fn((const void*)k);                                                    \
-    note_kernel("conv_split3_kernel<%d,4,%d>", NT_, BK_);                              \
+    note_kernel("conv_split3_kernel<%d,4,%d,%d>", NT_, BK_, NS_);                      \
   } while (0)
-  if (bk == 32) {
+  if (bk == 64) {
+    if (nt == 1) SP3(1, 64);
+    else if (nt == 2) SP3(2, 64);
+    else SP3(4, 64);
+  } else if (bk == 32) {
     if (nt == 1) SP3(1, 32);
     else if (nt == 2) SP3(2, 32);
     else SP3(4, 32);

@@ -24,6 +24,7 @@
 #include <mutex>
 #include <queue>
 #include <unordered_map>
+#include <string>
 #include <vector>
 
 #include "common.h"
@@ -505,6 +506,33 @@ extern "C" int clskd_exec_info(const clskd_exec* ex, int32_t* info, int32_t n) {
   info[7] = (int32_t)ex->program.size();
   for (int s = 0; s < 8 && 8 + s < n; ++s) info[8 + s] = ex->per_stream[s];
   return CLSKD_OK;
+}
+
+extern "C" int64_t clskd_exec_dump(const clskd_exec* ex, char* buf, int64_t cap) {
+  if (!ex) return -1;
+  std::string out;
+  char line[512];
+  static const char* kinds[] = {"kernel", "memset", "memcpy", "wait", "record"};
+  for (size_t i = 0; i < ex->program.size(); ++i) {
+    const Op& op = ex->program[i];
+    const char* name = "";
+    if (op.kind == OP_KERNEL) {
+      const KNode& k = ex->kernels[op.idx];
+      name = hipKernelNameRefByPtr(k.func, nullptr);
+      if (!name) name = "?";
+      snprintf(line, sizeof line, "%zu %s s%d #%d grid %u block %u %s\n", i, kinds[op.kind],
+               (int)op.stream, op.idx, k.grid.x * k.grid.y * k.grid.z, k.block.x, name);
+    } else {
+      snprintf(line, sizeof line, "%zu %s s%d #%d\n", i, kinds[op.kind], (int)op.stream, op.idx);
+    }
+    out += line;
+  }
+  if (buf && cap > 0) {
+    const size_t n = out.size() < (size_t)cap - 1 ? out.size() : (size_t)cap - 1;
+    memcpy(buf, out.data(), n);
+    buf[n] = 0;
+  }
+  return (int64_t)out.size();
 }
 
 static void drop_timing(clskd_exec* ex) {

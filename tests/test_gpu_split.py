@@ -53,8 +53,19 @@ SPLIT_CASES = {
 }
 
 
+@pytest.mark.parametrize("bk", [0, 32, 16])
 @pytest.mark.parametrize("case", sorted(SPLIT_CASES))
-def test_split_conv_against_torch(case, split_on):
+def test_split_conv_against_torch(case, bk, split_on):
+    """Every K-tile depth the dispatch can pick (CLSKD_SPLIT_BK caps it: 0 = deepest K allows)."""
+    from clskd import _lib, ops
+    prev_bk = _lib.set_knob("CLSKD_SPLIT_BK", bk)
+    try:
+        _split_case(case)
+    finally:
+        _lib.set_knob("CLSKD_SPLIT_BK", prev_bk)
+
+
+def _split_case(case):
     from clskd import ops
     segc, N, taps, sf, Fi, Fo, of_mul, of_add = SPLIT_CASES[case]
     g = torch.Generator().manual_seed(len(case) * 7 + N)

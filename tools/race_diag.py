@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--replays", type=int, default=8)
     ap.add_argument("--kind", default="exec")
     ap.add_argument("--streams", type=int, default=4)
+    ap.add_argument("--dump", action="store_true")
     args = ap.parse_args()
     from clskd.data import synthetic_pairs
     from clskd.graph import StepExecutor, StepGraph
@@ -59,6 +60,14 @@ def main():
     kd_e, kd_g = P._kd().set_precision("mixed"), P._kd().set_precision("mixed")
     g = StepExecutor(kd_g, *batches[0], nstreams=args.streams) if args.kind == "exec" else \
         StepGraph(kd_g, *batches[0])
+    if args.kind == "exec" and args.dump:
+        import ctypes as C
+        from clskd import _lib
+        L = _lib.load()
+        n = L.clskd_exec_dump(g._ex, None, 0)
+        b = C.create_string_buffer(int(n) + 1)
+        L.clskd_exec_dump(g._ex, b, n + 1)
+        print(b.value.decode(), flush=True)
     nbad = 0
     for r in range(args.replays):
         X, y = batches[r % 2]
