@@ -577,18 +577,25 @@ def main():
         last = (args.steps - 1) % NBATCH
         src = executor.out if args.launch == "exec" else (graph.out if args.graph else kd.last)
         wav_m = src["student_wav"].clone()
+        from clskd import _lib
         with torch.no_grad():
+            # the reference leg is the EXACT fp32 path: fp32 MFMA engines even where the benched
+            # step runs its fp32 layers as 3 x bf16 split products (CLSKD_F32_SPLIT)
+            split = _lib.set_knob("CLSKD_F32_SPLIT", 0)
             kd.set_precision("fp32")
             o32 = kd.training_step((Xs[last], Ys[last]), 0, return_parts=True)
             kd.set_precision(args.precision)
+            _lib.set_knob("CLSKD_F32_SPLIT", split)
             s_m = si_snr(wav_m, Ys[last]).item()
             s_32 = si_snr(o32["student_wav"], Ys[last]).item()
             wav_rms = float((wav_m - o32["student_wav"]).pow(2).mean().sqrt())
         quality = dict(si_snr_db=round(s_m, 6), si_snr_fp32_step_db=round(s_32, 6),
                        si_snr_delta_db=abs(s_m - s_32), student_wav_rms_vs_fp32_step=wav_rms,
                        loss=round(loss_v, 6), loss_fp32_step=round(float(o32["loss"].item()), 6),
-                       note="timed batch (last step) vs the all-fp32 step on the same batch; the "
-                            "oracle-pinned full-size check is tests/test_gpu_c2_mixed.py")
+                       f32_split=bool(split),
+                       note="timed batch (last step) vs the exact all-fp32 step on the same batch "
+                            "(fp32 MFMA engines, no split products); the oracle-pinned full-size "
+                            "check is tests/test_gpu_c2_mixed.py")
 
     step_counts = None
     if world == 1 and not args.train and not args.spkd and not args.graph:
