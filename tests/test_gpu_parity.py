@@ -85,14 +85,24 @@ _DIRECT_SHAPES = [(2, 0, 8), (2, 0, 16), (8, 8, 2), (16, 16, 2), (6, 0, 4), (6, 
 
 # 16-bit segments need channel runs of 8 (the kernel's 16-B loads): only those shapes run in
 # bf16 / fp16, every shape in fp32
-@pytest.mark.parametrize("dt,C1,C2,N", [("f32",) + s for s in _DIRECT_SHAPES] +
-                         [(d,) + s for d in ("bf16", "fp16") for s in _DIRECT_SHAPES
+@pytest.mark.parametrize("dt,C1,C2,N,cl", [("f32",) + s + (0,) for s in _DIRECT_SHAPES] +
+                         [("f32",) + s + (1,) for s in _DIRECT_SHAPES if 4 < s[2] <= 32] +
+                         [(d,) + s + (0,) for d in ("bf16", "fp16") for s in _DIRECT_SHAPES
                           if s[0] % 8 == 0 and s[1] % 8 == 0])
-def test_conv_direct_against_torch_and_engine(dt, C1, C2, N):
+def test_conv_direct_against_torch_and_engine(dt, C1, C2, N, cl):
     """Direct-convolution kernel (narrow N / short K): 2-segment 5x2 stride-(2,1) conv with fused
     BN statistics against torch (fp64 on the same bf16-rounded operands for bf16) and against the
     MFMA engines on the same descriptor (CLSKD_WLAYOUT_NK).  Tolerance: 1e-5 relative (fp32
-    accumulation orders differ)."""
+    accumulation orders differ).  cl=1: the channel-lane fp32 kernel (CLSKD_DIRECT_CL=1)."""
+    from clskd import _lib
+    prev = _lib.set_knob("CLSKD_DIRECT_CL", cl)
+    try:
+        _direct_case(dt, C1, C2, N, cl)
+    finally:
+        _lib.set_knob("CLSKD_DIRECT_CL", prev)
+
+
+def _direct_case(dt, C1, C2, N, cl):
     from clskd import ops
     g = torch.Generator().manual_seed(C1 * 100 + C2 * 10 + N)
     B, F, T = 3, 33, 29
@@ -123,6 +133,9 @@ def test_conv_direct_against_torch_and_engine(dt, C1, C2, N):
             st = torch.empty(nblk * N * 2, device=DEV, dtype=torch.float64)
             ops.conv(segs, taps, B, Fo, To, N, wp, bias.to(DEV), out, ops.OutMap(Fo * To * N, To * N, N),
                      stride_f=2, stats=st)
+            if route == "direct":
+                kn = ops.conv_kernel_of_last_launch()
+                assert kn.startswith("conv_direct_cl_kernel" if cl else "conv_direct_kernel"), kn
             res[route] = (out.permute(0, 3, 1, 2).double().cpu(), st.view(nblk, N, 2).sum(0).cpu())
         finally:
             ops._NO_DIRECT = False
