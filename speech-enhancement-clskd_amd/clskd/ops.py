@@ -88,8 +88,7 @@ def direct_weight(wpacked):
     fp32 [Kp][NP]; bf16 [Kp/2][NP][2].  Cached per packed tensor (pointer + version; the cache
     holds the source alive so a pointer is never reused while its entry exists)."""
     key = (wpacked.data_ptr(), wpacked._version, tuple(wpacked.shape), wpacked.dtype)
-    capturing = torch.cuda.is_current_stream_capturing()
-    ent = None if capturing else _DIRECT_W.get(key)
+    ent = _DIRECT_W.get(key)
     if ent is not None:
         _DIRECT_W.move_to_end(key)
         return ent[1]
@@ -101,10 +100,14 @@ def direct_weight(wpacked):
     else:
         wd = wpacked.new_zeros(Kp, NP)
         wd[:, :N] = wpacked.t()
-    if not capturing:
-        _DIRECT_W[key] = (wpacked, wd)
-        while len(_DIRECT_W) > 512:
-            _DIRECT_W.popitem(last=False)
+    # cached under graph capture too: the caller passes wd's address to a kernel and drops the
+    # tensor, and a block freed inside a capture is handed to the next allocation of the same
+    # capture — the BN partials of the very launch that reads these weights (a race in every
+    # replay; the eager path always hit this cache).  A capture-built entry keeps its graph-pool
+    # block alive; the captured repack rewrites the same values on every replay.
+    _DIRECT_W[key] = (wpacked, wd)
+    while len(_DIRECT_W) > 512:
+        _DIRECT_W.popitem(last=False)
     return wd
 
 

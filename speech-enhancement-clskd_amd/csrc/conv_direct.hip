@@ -341,9 +341,8 @@ __global__ __launch_bounds__(256) void conv_direct_cl_kernel(const DirectArgs ar
     for (int i = 0; i < RPT; ++i) {
       const int fi = fi0[i] + dF, ti = ti0[i] + dT;
       const bool ok = rv[i] && (unsigned)fi < (unsigned)Fb && (unsigned)ti < (unsigned)Tb;
-      const int64_t off = (sg == 0 ? rb0[i] : seg_row(sg, i)) +
-                          (int64_t)dF * sel4d(sg, d.seg[0].sF, d.seg[1].sF, d.seg[2].sF, d.seg[3].sF) +
-                          (int64_t)dT * sel4d(sg, d.seg[0].sT, d.seg[1].sT, d.seg[2].sT, d.seg[3].sT) + e.x;
+      // the K-table offset already holds the tap displacement (dF sF + dT sT) and the channel
+      const int64_t off = (sg == 0 ? rb0[i] : seg_row(sg, i)) + e.x;
       const float* p = ok ? sp + off : d.seg[0].ptr;
       if constexpr (G == 1) {
         x[i][0] = ok ? *p : 0.f;
