@@ -11,7 +11,7 @@ rc=0; timeout -k 10 170 python -u -m pytest "$R/tests/test_gpu_parity.py::test_c
 tail -3 $O/gpu_tests.log; ok $rc
 rc=0; timeout -k 10 170 python -u $R/tools/race_diag.py --kind exec --replays 6 > $O/race_exec.txt 2>&1 || rc=$?; ok $rc
 tail -1 $O/race_exec.txt
-for leg in a0:: cl:CLSKD_DIRECT_CL=1 split:CLSKD_F32_SPLIT=1 both:CLSKD_F32_SPLIT=1,CLSKD_DIRECT_CL=1 a1::; do
+for leg in a0: cl:CLSKD_DIRECT_CL=1 split:CLSKD_F32_SPLIT=1 both:CLSKD_F32_SPLIT=1,CLSKD_DIRECT_CL=1 a1:; do
   name=${leg%%:*}; envs=${leg#*:}
   rc=0; env ${envs//,/ } timeout -k 10 150 $B > $O/bench_$name.log 2>&1 || rc=$?; ok $rc
   echo "$name $(grep '^{' $O/bench_$name.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d.get("host_enqueue_ms_per_step"), d.get("serialized_kernel_ms_per_step"))')"
