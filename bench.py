@@ -396,7 +396,7 @@ def main():
                          "samples) as a latency, GPU (eager and executor) beside the CPU oracle")
     ap.add_argument("--precision", default=None, choices=["mixed", "fp16", "fp32"],
                     help="mixed (C2/C3 default): teacher + ReviewKD GEMMs on bf16 MFMA operands (fp32 "
-                         "accumulate), student fp32; fp16 (C4 default, --spkd only): the teacher on "
+                         "accumulate), student fp32 (C2: its fp32 convs as 3 x bf16 split products); fp16 (C4 default, --spkd only): the teacher on "
                          "IEEE-half operands and fp16 storage; fp32: every GEMM on exact-f32 MFMA")
     args = ap.parse_args()
     if args.precision is None:
@@ -734,6 +734,12 @@ def main():
                                      "LSTM recurrence, BN, losses fp32")
                        if args.precision == "fp16" else
                                     ("teacher+ReviewKD GEMMs bf16 MFMA operands / fp32 accumulate; "
+                                     "student fp32 storage/accumulation with its fp32 convs as "
+                                     "3 x bf16 split-product MFMA (CLSKD_F32X3, <= ~3*2^-18 per "
+                                     "product; the reference trains with TF32 matmuls); "
+                                     "STFT, LSTM recurrence, BN, losses fp32"
+                                     if kd.student.compute == "f32x3" else
+                                     "teacher+ReviewKD GEMMs bf16 MFMA operands / fp32 accumulate; "
                                      "student, STFT/iSTFT, LSTM recurrence, BN, losses fp32")
                        if args.precision == "mixed" else "fp32 MFMA everywhere"},
             "roofline": roof,

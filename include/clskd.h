@@ -35,8 +35,11 @@ typedef enum {
 
 /* storage / MFMA operand types.  CLSKD_F16 (IEEE half) is the operand type of configuration C4
  * (distill_SPKD.py at fp16): the conv engines, BN and STFT-side kernels of a DCCRN forward
- * take it wherever they take bf16. */
-typedef enum { CLSKD_F32 = 0, CLSKD_BF16 = 1, CLSKD_F16 = 2 } clskd_compute;
+ * take it wherever they take bf16.  CLSKD_F32X3 (conv descriptors only, fp32 storage): fp32
+ * products formed from three bf16 MFMA products of split operands (hi = bf16(x), lo =
+ * bf16(x - hi): hi*hi + hi*lo + lo*hi, fp32 accumulation; <= ~3 * 2^-18 relative per product)
+ * where the split engine takes the layer, the exact fp32 engines elsewhere. */
+typedef enum { CLSKD_F32 = 0, CLSKD_BF16 = 1, CLSKD_F16 = 2, CLSKD_F32X3 = 3 } clskd_compute;
 
 const char* clskd_last_error(void);
 int clskd_version(void);

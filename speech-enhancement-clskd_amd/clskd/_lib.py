@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libclskd_hip_exp.so" if os.environ.get("CLSKD_LI
 
 MAX_SEGS = 4
 F32, BF16, F16 = 0, 1, 2
+F32X3 = 3  # conv compute: fp32 storage, 3 x bf16 split-product MFMA (include/clskd.h)
 WLAYOUT_NK, WLAYOUT_DIRECT = 0, 1
 
 

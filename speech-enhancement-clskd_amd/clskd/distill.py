@@ -44,6 +44,8 @@ def _mark(label, stream):
         _MARKS.append((label, ev))
 
 
+# A/B switch: CLSKD_STUDENT_SPLIT=0 keeps the student of precision 'mixed' on the exact fp32 engines
+_STUDENT_SPLIT = os.environ.get("CLSKD_STUDENT_SPLIT", "1") == "1"
 _SERIAL = os.environ.get("CLSKD_SERIAL_STREAMS") == "1"  # diagnostic: the whole step on one stream
 
 
@@ -159,7 +161,9 @@ class KnowledgeDistillation(nn.Module):
         """"fp32": every GEMM on exact-f32 MFMA.  "mixed": the frozen teacher and the ReviewKD
         fusions (95 % of the step's FLOPs; they only feed the SPKD similarity Grams) run bf16
         MFMA operands with fp32 accumulation; the student — whose waveform is the product and
-        the SI-SNR / RMS parity target — stays fp32."""
+        the SI-SNR / RMS parity target — keeps fp32 storage and accumulation, its fp32 convs on
+        3 x bf16 split products (compute 'f32x3': <= ~3 * 2^-18 relative per product, against the
+        reference training script's TF32 at 2^-11; exact fp32 under a tape / in training)."""
         if precision not in ("fp32", "mixed"):
             raise ValueError(precision)
         self.precision = precision
@@ -167,7 +171,7 @@ class KnowledgeDistillation(nn.Module):
         self.teacher.compute = c
         self.review_encoder.set_compute(c)
         self.review_decoder.set_compute(c)
-        self.student.compute = "fp32"
+        self.student.compute = "f32x3" if (precision == "mixed" and _STUDENT_SPLIT) else "fp32"
         return self
 
     def forward(self, x):

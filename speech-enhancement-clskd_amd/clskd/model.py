@@ -200,8 +200,9 @@ class DCCRN(nn.Module):
         self._pgroups = {}
         self._refs = None
         self._tap_sinks = []
-        # MFMA operand type of the large GEMMs: "fp32" (exact-f32 MFMA), "bf16" / "fp16" (16-bit operands,
-        # fp32 accumulation).  STFT/iSTFT framing GEMMs always run fp32.
+        # MFMA operand type of the large GEMMs: "fp32" (exact-f32 MFMA), "f32x3" (fp32 storage, 3 x
+        # bf16 split-product MFMA for the fp32 convs), "bf16" / "fp16" (16-bit operands, fp32
+        # accumulation).  STFT/iSTFT framing GEMMs run fp32 ("f32x3": split products).
         self.compute = "fp32"
 
     # ---------------------------------------------------------------- reference helpers
@@ -403,6 +404,15 @@ class DCCRN(nn.Module):
 
     def run(self, x, train=True, bn_updates=1, spec=None, want_masks=True, on_encoder=None,
             tape=None, taps_only=False, mark=None, on_decoder_tap=None, gram_taps=None):
+        """See _run.  compute 'f32x3' (the student in precision 'mixed'): the fp32 convs of a
+        forward without a tape run as 3 x bf16 split products (CLSKD_F32X3); a taped (training)
+        forward stays on the exact fp32 engines its backward mirrors."""
+        with ops.split_products(self.compute == "f32x3" and tape is None):
+            return self._run(x, train, bn_updates, spec, want_masks, on_encoder, tape, taps_only,
+                             mark, on_decoder_tap, gram_taps)
+
+    def _run(self, x, train=True, bn_updates=1, spec=None, want_masks=True, on_encoder=None,
+             tape=None, taps_only=False, mark=None, on_decoder_tap=None, gram_taps=None):
         """Full forward on the HIP device.  Returns a dict of BFTC buffers and NCHW views.
         on_encoder(enc): called (on the launching stream) right after the encoder, so a caller can
         fork work that only needs the encoder taps before the LSTM and decoder are enqueued.

@@ -5,6 +5,7 @@ the library.  Tensors are BFTC ([batch][freq][time][channel]) unless noted.
 """
 import ctypes as C
 import os
+import threading
 from collections import OrderedDict
 from dataclasses import dataclass
 from functools import lru_cache
@@ -246,7 +247,7 @@ _CONV_PLANS = {}
 
 
 def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, stride_f, stride_t,
-               stats, accumulate=False, mfma_only=False):
+               stats, accumulate=False, mfma_only=False, split=False):
     in_dt = {_dt(s.tensor) for s in segs}
     assert len(in_dt) == 1, "all segments of one conv share a storage type"
     in_dt = in_dt.pop()
@@ -283,7 +284,9 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
     d.oB, d.oF, d.oT, d.oNhi, d.oNlo = omap.oB, omap.oF, omap.oT, omap.oNhi, omap.oNlo
     d.nlo = min(omap.nlo, 1 << 30)
     d.of_mul, d.of_add = omap.of_mul, omap.of_add
-    d.compute = in_dt
+    # split products: fp32 layers of a split_products(True) forward (not the accumulating
+    # data-gradient sums of the backward)
+    d.compute = _lib.F32X3 if (split and in_dt == _lib.F32 and not accumulate) else in_dt
     d.in_dtype = in_dt
     d.out_dtype = _dt(out)
     d.kvec = kvec
@@ -318,6 +321,27 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
 
 _PROBE_FOLD = _lib.BnFold()  # zero fold record: clskd_conv_fold_capable inspects only presence
 
+# fp32 convs launched inside split_products(True) ask for 3 x bf16 split products (CLSKD_F32X3:
+# the student's layers in precision 'mixed'); a thread-local flag, so a model can switch its
+# whole forward (DCCRN.run) without threading an argument through every call site
+_SPLIT = threading.local()
+
+
+class split_products:
+    """Context manager: fp32 conv launches of this thread ask for split-product MFMA."""
+
+    def __init__(self, on):
+        self.on = bool(on)
+
+    def __enter__(self):
+        self.prev = getattr(_SPLIT, "on", False)
+        _SPLIT.on = self.on
+        return self
+
+    def __exit__(self, *exc):
+        _SPLIT.on = self.prev
+        return False
+
 
 def conv_folds(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, stride_f=1, stride_t=1):
     """Whether a conv(..., bn_stats=...) launch with these arguments dispatches to a kernel that
@@ -345,14 +369,16 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
     geoms = tuple(s.geom for s in segs)
     if bn_stats is not None and stats is not None:
         raise ValueError("conv: stats and bn_stats are exclusive")
+    split = getattr(_SPLIT, "on", False)
     key = (geoms, taps, B, Fo, To, N, wpacked.shape, wpacked.dtype, omap, stride_f, stride_t,
            out.dtype, out.device.index, "bn" if bn_stats is not None else stats is None,
            bias is None,
-           tuple(a % 16 for a in addrs), tuple(s.tensor.dtype for s in segs), accumulate, mfma_only)
+           tuple(a % 16 for a in addrs), tuple(s.tensor.dtype for s in segs), accumulate, mfma_only,
+           split)
     pl = _CONV_PLANS.get(key)
     if pl is None:
         pl = _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, stride_f,
-                        stride_t, stats, accumulate, mfma_only)
+                        stride_t, stats, accumulate, mfma_only, split)
     if not wpacked.is_contiguous():
         raise RuntimeError("conv: packed weight must be contiguous")
     d = pl.desc

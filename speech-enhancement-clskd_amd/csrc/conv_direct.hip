@@ -261,154 +261,6 @@ __global__ __launch_bounds__(128) void conv_direct_kernel(const DirectArgs args)
   }
 }
 
-// Channel-lane variant (round 4) for fp32 inputs and 8 / 16 / 32 output channels: lane = (row
-// slot, output channel), so a lane's weights are one column (read from LDS, conflict-free) and
-// the FMAs pair two rows per v_pk_fma_f32; the one-row-per-thread kernel above keeps every
-// weight of the row in SGPRs and, at N = 32, spills them to VGPR lanes (232 v_readlane per
-// iteration) and runs 4x its FMA time.  A 4-wave block covers 128 output rows (the statistics
-// slot); in a wave, LPR = 64 / NP row slots x NP channels, each lane RPT = NP / 2 rows; at every
-// row step the wave's lanes cover LPR consecutive rows x NP channels (coalesced loads and stores
-// when the output rows are contiguous).
-template <int NP, int G, typename OutT>
-__global__ __launch_bounds__(256) void conv_direct_cl_kernel(const DirectArgs args) {
-  const clskd_conv_desc& d = args.d;
-  constexpr int LPR = 64 / NP, RPT = NP / 2;
-  static_assert(LPR * RPT == 32 && RPT % 2 == 0, "32 rows per wave, row pairs per lane");
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  typedef typename VecOf<float, G == 1 ? 2 : G>::T XV;  // G = 1 loads one float (see below)
-  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-  const int K = d.K;
-  const int nrun = K / G;
-  int4* kl = reinterpret_cast<int4*>(dsm);                                // [nrun]
-  float* wl = reinterpret_cast<float*>(dsm + (size_t)nrun * 16);          // [K][NP]
-  double* red = reinterpret_cast<double*>(wl + (size_t)K * NP);           // [4][NP][2]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int j = tid; j < nrun; j += 256) {
-    const clskd_ktab_entry e = d.ktab[j * G];
-    const int sg = d.kseg[j * G];
-    const int FT = (int)(uint16_t)sel4d(sg, d.seg[0].F, d.seg[1].F, d.seg[2].F, d.seg[3].F) |
-                   (sel4d(sg, d.seg[0].T, d.seg[1].T, d.seg[2].T, d.seg[3].T) << 16);
-    kl[j] = make_int4(e.off, (int)(uint16_t)e.dF | ((int)e.dT << 16), sg, FT);
-  }
-  const float* wg = reinterpret_cast<const float*>(d.weight);  // direct layout [K][NP]
-  for (int i = tid; i < K * NP; i += 256) wl[i] = wg[i];
-  __syncthreads();
-
-  const int c = lane % NP, rs = lane / NP;
-  const int64_t M = (int64_t)d.B * d.Fo * d.To;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
-  const int64_t FoTo = (int64_t)d.Fo * d.To;
-  // rows of this lane: m0 + i * LPR + rs, i = 0 .. RPT-1
-  const int64_t m0 = (int64_t)tile * 128 + wave * 32;
-  int fi0[RPT], ti0[RPT];
-  int64_t rb0[RPT];
-  bool rv[RPT];
-#pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    const int64_t m = m0 + i * LPR + rs;
-    rv[i] = m < M;
-    const int64_t mm = rv[i] ? m : 0;
-    const int b = (int)(mm / FoTo);
-    const int64_t r = mm - (int64_t)b * FoTo;
-    const int fo = (int)(r / d.To);
-    const int to = (int)(r - (int64_t)fo * d.To);
-    fi0[i] = fo * d.stride_f;
-    ti0[i] = to * d.stride_t;
-    rb0[i] = (int64_t)b * d.seg[0].sB + (int64_t)fi0[i] * d.seg[0].sF + (int64_t)ti0[i] * d.seg[0].sT;
-  }
-  // per-segment base deltas: (b, fi0, ti0) offsets in segment s minus segment 0's
-  auto seg_row = [&](int sg, int i) -> int64_t {
-    if (sg == 0) return rb0[i];
-    const int64_t m = m0 + i * LPR + rs;
-    const int64_t mm = m < M ? m : 0;
-    const int b = (int)(mm / FoTo);
-    return (int64_t)b * d.seg[sg].sB + (int64_t)fi0[i] * d.seg[sg].sF + (int64_t)ti0[i] * d.seg[sg].sT;
-  };
-  f2 acc[RPT / 2];
-  {
-    const float bv = (d.bias && c < d.N) ? d.bias[c] : 0.f;
-#pragma unroll
-    for (int i = 0; i < RPT / 2; ++i) acc[i] = f2{bv, bv};
-  }
-  for (int j = 0; j < nrun; ++j) {
-    const int4 e = kl[j];
-    const int dF = (int)(int16_t)(e.y & 0xffff), dT = e.y >> 16;
-    const int Fb = e.w & 0xffff, Tb = (int)((unsigned)e.w >> 16);
-    const int sg = __builtin_amdgcn_readfirstlane(e.z);
-    const float* sp = sel4d(sg, d.seg[0].ptr, d.seg[1].ptr, d.seg[2].ptr, d.seg[3].ptr);
-    float x[RPT][G];
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-      const int fi = fi0[i] + dF, ti = ti0[i] + dT;
-      const bool ok = rv[i] && (unsigned)fi < (unsigned)Fb && (unsigned)ti < (unsigned)Tb;
-      // the K-table offset already holds the tap displacement (dF sF + dT sT) and the channel
-      const int64_t off = (sg == 0 ? rb0[i] : seg_row(sg, i)) + e.x;
-      const float* p = ok ? sp + off : d.seg[0].ptr;
-      if constexpr (G == 1) {
-        x[i][0] = ok ? *p : 0.f;
-      } else {
-        const XV v = *reinterpret_cast<const XV*>(p);
-#pragma unroll
-        for (int g = 0; g < G; ++g) x[i][g] = ok ? v[g] : 0.f;
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const float w = wl[(j * G + g) * NP + c];
-      const f2 w2 = {w, w};
-#pragma unroll
-      for (int i = 0; i < RPT / 2; ++i)
-        acc[i] = __builtin_elementwise_fma(f2{x[2 * i][g], x[2 * i + 1][g]}, w2, acc[i]);
-    }
-  }
-  // statistics: this lane's channel over its valid rows, then the wave's row slots, then waves
-  if (d.stats) {
-    double S = 0.0, Q = 0.0;
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-      const float v = acc[i / 2][i & 1];
-      if (rv[i]) {
-        S += (double)v;
-        Q = fma((double)v, (double)v, Q);
-      }
-    }
-#pragma unroll
-    for (int o = NP; o < 64; o <<= 1) {
-      S += __shfl_xor(S, o, 64);
-      Q += __shfl_xor(Q, o, 64);
-    }
-    if (rs == 0) {
-      red[(wave * NP + c) * 2] = S;
-      red[(wave * NP + c) * 2 + 1] = Q;
-    }
-    __syncthreads();
-    if (tid < d.N) {
-      double S4 = 0.0, Q4 = 0.0;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        S4 += red[(w * NP + tid) * 2];
-        Q4 += red[(w * NP + tid) * 2 + 1];
-      }
-      d.stats[((int64_t)tile * d.N + tid) * 2] = S4;
-      d.stats[((int64_t)tile * d.N + tid) * 2 + 1] = Q4;
-    }
-  }
-  if (c >= d.N) return;
-  OutT* outp = reinterpret_cast<OutT*>(d.out);
-  const int64_t coff = (int64_t)(c / d.nlo) * d.oNhi + (int64_t)(c % d.nlo) * d.oNlo;
-#pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    if (!rv[i]) continue;
-    const int64_t m = m0 + i * LPR + rs;
-    const int b = (int)(m / FoTo);
-    const int64_t r = m - (int64_t)b * FoTo;
-    const int fo = (int)(r / d.To);
-    const int to = (int)(r - (int64_t)fo * d.To);
-    const int64_t ro = (int64_t)b * d.oB + (int64_t)(fo * d.of_mul + d.of_add) * d.oF + (int64_t)to * d.oT;
-    outp[ro + coff] = (OutT)acc[i / 2][i & 1];
-  }
-}
-
 static int np_of(int N) {
   return N <= 2 ? 2 : N <= 4 ? 4 : N <= 8 ? 8 : N <= 16 ? 16 : N <= 32 ? 32 : 64;
 }
@@ -459,35 +311,6 @@ static void launch_g(const clskd_conv_desc& d, hipStream_t st) {
   else launch_np<64, G, InT>(d, st);
 }
 
-template <int NP, int G>
-static void launch_cl_np(const clskd_conv_desc& d, hipStream_t st) {
-  const int64_t M = (int64_t)d.B * d.Fo * d.To;
-  const size_t lds = (size_t)(d.K / G) * 16 + (size_t)d.K * NP * 4 + 4 * NP * 16;
-  DirectArgs a{d};
-  if (d.out_dtype == CLSKD_BF16) {
-    hipLaunchKernelGGL((conv_direct_cl_kernel<NP, G, __bf16>), dim3((unsigned)cdiv(M, 128)),
-                       dim3(256), lds, st, a);
-    note_kernel_fn((const void*)conv_direct_cl_kernel<NP, G, __bf16>);
-  } else if (d.out_dtype == CLSKD_F16) {
-    hipLaunchKernelGGL((conv_direct_cl_kernel<NP, G, _Float16>), dim3((unsigned)cdiv(M, 128)),
-                       dim3(256), lds, st, a);
-    note_kernel_fn((const void*)conv_direct_cl_kernel<NP, G, _Float16>);
-  } else {
-    hipLaunchKernelGGL((conv_direct_cl_kernel<NP, G, float>), dim3((unsigned)cdiv(M, 128)),
-                       dim3(256), lds, st, a);
-    note_kernel_fn((const void*)conv_direct_cl_kernel<NP, G, float>);
-  }
-  note_kernel("conv_direct_cl_kernel<%d,%d,%s>", NP, G,
-              d.out_dtype == CLSKD_BF16 ? "bf16" : d.out_dtype == CLSKD_F16 ? "f16" : "float");
-}
-
-template <int G>
-static void launch_cl_g(const clskd_conv_desc& d, int np, hipStream_t st) {
-  if (np == 8) launch_cl_np<8, G>(d, st);
-  else if (np == 16) launch_cl_np<16, G>(d, st);
-  else launch_cl_np<32, G>(d, st);
-}
-
 int launch_conv_direct(const clskd_conv_desc& d, hipStream_t st) {
   CLSKD_CHECK_SHAPE(conv_direct_ok(d.N, d.K), "conv2d(direct): N=%d K=%d outside the direct path",
                     d.N, d.K);
@@ -507,14 +330,6 @@ int launch_conv_direct(const clskd_conv_desc& d, hipStream_t st) {
       CLSKD_CHECK_ARG(((uintptr_t)sg.ptr % (4 * g)) == 0 && sg.sB % g == 0 && sg.sF % g == 0 &&
                           sg.sT % g == 0,
                       "conv2d(direct): segment %d not aligned for kvec %d", s, g);
-    }
-    const int np = np_of(d.N);
-    if (knob(KNOB_DIRECT_CL) == 1 && np >= 8 && np <= 32) {
-      if (g == 4) launch_cl_g<4>(d, np, st);
-      else if (g == 2) launch_cl_g<2>(d, np, st);
-      else if (g == 1) launch_cl_g<1>(d, np, st);
-      else CLSKD_CHECK_SHAPE(false, "conv2d(direct): fp32 kvec %d unsupported", g);
-      return CLSKD_OK;
     }
     if (g == 4) launch_g<4, float>(d, st);
     else if (g == 2) launch_g<2, float>(d, st);

@@ -336,7 +336,7 @@ int launch_conv_direct(const clskd_conv_desc& d, hipStream_t st);
 
 int launch_conv_pointwise(const clskd_conv_desc& d, hipStream_t st, bool* launched);
 int launch_conv_halo_f32(const clskd_conv_desc& d, hipStream_t st, bool* launched);
-int launch_conv_split3(const clskd_conv_desc& d, hipStream_t st, bool* launched);
+int launch_conv_split3(const clskd_conv_desc& d, hipStream_t st, bool* launched, bool force);
 
 }  // namespace clskd
 
@@ -347,19 +347,22 @@ bool conv_halo_takes(const clskd_conv_desc& d);
 bool conv_halo_f32_takes(const clskd_conv_desc& d);
 bool conv_gemm8_takes(const clskd_conv_desc& d);
 bool conv_pointwise_takes(const clskd_conv_desc& d);
-bool conv_split3_takes(const clskd_conv_desc& d);
+bool conv_split3_takes(const clskd_conv_desc& d, bool force);
 }  // namespace clskd
 
 // The kernel a descriptor dispatches to folds the BatchNorm finalize (clskd_bn_fold): the
 // persistent engines.  Mirrors the dispatch order of clskd_conv2d_fwd.
-static bool fold_capable(const clskd_conv_desc& d) {
-  if (d.wlayout == CLSKD_WLAYOUT_DIRECT || d.accumulate) return false;
-  if (is_lowp(d.compute)) {
-    if (conv_halo_takes(d)) return true;
-    return conv_gemm8_takes(d) && d.N <= 256;  // one N-tile (256x256 / 256x128 instances)
+static bool fold_capable(const clskd_conv_desc& dd) {
+  if (dd.wlayout == CLSKD_WLAYOUT_DIRECT || dd.accumulate) return false;
+  if (is_lowp(dd.compute)) {
+    if (conv_halo_takes(dd)) return true;
+    return conv_gemm8_takes(dd) && dd.N <= 256;  // one N-tile (256x256 / 256x128 instances)
   }
+  const bool split = dd.compute == CLSKD_F32X3;
+  clskd_conv_desc d = dd;  // the fp32 engines see CLSKD_F32 (F32X3 only asks for the split)
+  d.compute = CLSKD_F32;
   if (conv_pointwise_takes(d)) return false;
-  if (conv_split3_takes(d)) return true;
+  if (conv_split3_takes(d, split)) return true;
   return knob(KNOB_NO_HALO32) != 1 && conv_halo_f32_takes(d);
 }
 
@@ -374,16 +377,23 @@ extern "C" int64_t clskd_bn_fold_state_size(int32_t C) {
 
 extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
   CLSKD_CHECK_ARG(dp != nullptr, "conv2d: null descriptor");
-  const clskd_conv_desc& d = *dp;
-  CLSKD_CHECK_ARG(d.compute == CLSKD_F32 || d.compute == CLSKD_BF16 || d.compute == CLSKD_F16,
-                  "conv2d: unknown compute %d", d.compute);
+  CLSKD_CHECK_ARG(dp->compute == CLSKD_F32 || dp->compute == CLSKD_BF16 || dp->compute == CLSKD_F16 ||
+                      dp->compute == CLSKD_F32X3,
+                  "conv2d: unknown compute %d", dp->compute);
+  CLSKD_CHECK_ARG(dp->compute != CLSKD_F32X3 || dp->in_dtype == CLSKD_F32,
+                  "conv2d: split products (CLSKD_F32X3) take fp32 segments");
+  // CLSKD_F32X3 asks for the split engine; every fp32 engine sees the descriptor as CLSKD_F32
+  const bool want_split = dp->compute == CLSKD_F32X3;
+  clskd_conv_desc dcopy = *dp;
+  if (want_split) dcopy.compute = CLSKD_F32;
+  const clskd_conv_desc& d = dcopy;
   CLSKD_CHECK_SHAPE(d.B > 0 && d.Fo > 0 && d.To > 0 && d.N > 0 && d.K > 0, "conv2d: empty shape");
   if (const clskd_bn_fold* f = d.bn_fold) {
     CLSKD_CHECK_ARG(!d.stats, "conv2d: bn_fold and stats are exclusive");
     CLSKD_CHECK_ARG(f->acc && f->ticket && f->scale && f->shift, "conv2d: bn_fold null pointer");
     CLSKD_CHECK_SHAPE(f->C > 0 && f->c_off >= 0 && f->c_off + d.N <= f->C && f->count > 0,
                       "conv2d: bn_fold channels [%d, +%d) outside C=%d", f->c_off, d.N, f->C);
-    CLSKD_CHECK_ARG(fold_capable(d), "conv2d: N=%d K=%d dispatches to a kernel without the folded "
+    CLSKD_CHECK_ARG(fold_capable(*dp), "conv2d: N=%d K=%d dispatches to a kernel without the folded "
                     "BatchNorm finalize (clskd_conv_fold_capable)", d.N, d.K);
   }
   const bool lowp = is_lowp(d.compute);
@@ -448,9 +458,10 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
       return CLSKD_OK;
     }
   }
-  {  // fp32-accurate 3 x bf16 split products on the bf16 MFMA pipe (CLSKD_F32_SPLIT=1)
+  {  // fp32-accurate 3 x bf16 split products on the bf16 MFMA pipe (CLSKD_F32X3 descriptors;
+     // every fp32 descriptor with the A/B knob CLSKD_F32_SPLIT=1)
     bool launched = false;
-    const int rc = launch_conv_split3(d, st, &launched);
+    const int rc = launch_conv_split3(d, st, &launched, want_split);
     if (rc != CLSKD_OK) return rc;
     if (launched) {
       CLSKD_LAUNCH_CHECK("conv2d_split3");

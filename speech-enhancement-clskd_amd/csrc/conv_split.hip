@@ -437,16 +437,18 @@ static bool split_plan(const clskd_conv_desc& d, SplitArgs& a, int& nt, int& bk,
   return true;
 }
 
-bool conv_split3_takes(const clskd_conv_desc& d) {
-  if (knob(KNOB_F32_SPLIT) != 1) return false;
+// force: the descriptor asked for split products (CLSKD_F32X3, passed here as CLSKD_F32);
+// otherwise the global A/B knob CLSKD_F32_SPLIT routes every fp32 descriptor
+bool conv_split3_takes(const clskd_conv_desc& d, bool force) {
+  if (!force && knob(KNOB_F32_SPLIT) != 1) return false;
   SplitArgs a;
   int nt = 0, bk = 0, grid = 0;
   return split_plan(d, a, nt, bk, grid);
 }
 
-int launch_conv_split3(const clskd_conv_desc& d, hipStream_t st, bool* launched) {
+int launch_conv_split3(const clskd_conv_desc& d, hipStream_t st, bool* launched, bool force) {
   *launched = false;
-  if (knob(KNOB_F32_SPLIT) != 1) return CLSKD_OK;
+  if (!force && knob(KNOB_F32_SPLIT) != 1) return CLSKD_OK;
   SplitArgs a;
   int nt = 0, bk = 0, grid = 0;
   if (!split_plan(d, a, nt, bk, grid)) return CLSKD_OK;

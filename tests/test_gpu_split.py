@@ -56,13 +56,23 @@ SPLIT_CASES = {
 @pytest.mark.parametrize("bk", [0, 32, 16])
 @pytest.mark.parametrize("case", sorted(SPLIT_CASES))
 def test_split_conv_against_torch(case, bk, split_on):
-    """Every K-tile depth the dispatch can pick (CLSKD_SPLIT_BK caps it: 0 = deepest K allows)."""
-    from clskd import _lib, ops
+    """Every K-tile depth the dispatch can pick (CLSKD_SPLIT_BK caps it: 0 = deepest K allows),
+    routed by the global A/B knob CLSKD_F32_SPLIT=1."""
+    from clskd import _lib
     prev_bk = _lib.set_knob("CLSKD_SPLIT_BK", bk)
     try:
         _split_case(case)
     finally:
         _lib.set_knob("CLSKD_SPLIT_BK", prev_bk)
+
+
+@pytest.mark.parametrize("case", sorted(SPLIT_CASES))
+def test_split_descriptor_against_torch(case):
+    """The same layers asked for per descriptor (compute CLSKD_F32X3, ops.split_products: how the
+    student of precision 'mixed' runs), the global knob off."""
+    from clskd import ops
+    with ops.split_products(True):
+        _split_case(case)
 
 
 def _split_case(case):
