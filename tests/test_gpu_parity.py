@@ -900,7 +900,9 @@ def test_step_graph_matches_eager(launch):
         for kd in (kd_e, kd_g):
             kd.student.encoder[0][0].real_conv.weight.mul_(1.01)
     X, y = batches[2]
-    l3 = kd_e.training_step((X, y), 0).item()
+    # return_parts: the no-tape step the graph captured (without it, grad mode routes through
+    # autograd's taped step, whose student runs the exact engines, not the split products)
+    l3 = kd_e.training_step((X, y), 0, return_parts=True)["loss"].item()
     assert g(X, y).item() == l3 and g.captures == 2
 
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 end evidence on one MI355X (via gpurun from the repo root): two PMC passes of the bench
+# Round-4 end evidence on one MI355X (via gpurun from the repo root): the GPU suite; two PMC passes of the bench
 # (FETCH_SIZE, WRITE_SIZE separately) joined by tools/pmc_traffic.py; a rocprofv3 kernel + marker
 # trace of the driver's bench command split at its roctx ranges (tools/region_stats.py: census
 # step and timed steps separately); the default bench line; the C3 / C4 / C1 / C5 lines.  Every
@@ -8,6 +8,8 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${ITER:-r4final}
 mkdir -p $O
 ok() { local rc=$1; if [ $rc -ne 0 ]; then echo "stop: rc=$rc"; exit $rc; fi; }
+rc=0; timeout -k 10 400 python -u -m pytest $R/tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_suite.log 2>&1 || rc=$?; ok $rc
+tail -2 $O/gpu_suite.log
 (
   cd /tmp && export TMPDIR=/tmp
   rc=0; timeout -k 10 170 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/fetch.log 2>&1 || rc=$?; ok $rc
