@@ -38,7 +38,7 @@ PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sp
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 B_PER_GPU = 16
 NBATCH = 4
-TRAFFIC_FILE = "r3_pmc_traffic.json"  # written by tools/pmc_traffic.py
+TRAFFIC_FILE = "r4_pmc_traffic.json"  # written by tools/pmc_traffic.py
 L = 64000
 
 
@@ -582,6 +582,7 @@ def main():
             # the reference leg is the EXACT fp32 path: fp32 MFMA engines even where the benched
             # step runs its fp32 layers as 3 x bf16 split products (CLSKD_F32_SPLIT)
             split = _lib.set_knob("CLSKD_F32_SPLIT", 0)
+            s_compute = getattr(kd.student, "compute", None)
             kd.set_precision("fp32")
             o32 = kd.training_step((Xs[last], Ys[last]), 0, return_parts=True)
             kd.set_precision(args.precision)
@@ -592,7 +593,7 @@ def main():
         quality = dict(si_snr_db=round(s_m, 6), si_snr_fp32_step_db=round(s_32, 6),
                        si_snr_delta_db=abs(s_m - s_32), student_wav_rms_vs_fp32_step=wav_rms,
                        loss=round(loss_v, 6), loss_fp32_step=round(float(o32["loss"].item()), 6),
-                       f32_split=bool(split),
+                       f32_split_knob=bool(split), student_compute=s_compute,
                        note="timed batch (last step) vs the exact all-fp32 step on the same batch "
                             "(fp32 MFMA engines, no split products); the oracle-pinned full-size "
                             "check is tests/test_gpu_c2_mixed.py")
