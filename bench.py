@@ -366,8 +366,9 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU-oracle B=16 steps (median)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--abf-reinit", default="step", choices=["step", "once"])
-    ap.add_argument("--launch", default="eager", choices=["exec", "eager", "graph"],
-                    help="eager (default): launch the four-stream schedule from Python every "
+    ap.add_argument("--launch", default=None, choices=["exec", "eager", "graph"],
+                    help="default: eager for C2 / C4, exec for C3 (--train) on one GPU.  "
+                         "eager: launch the four-stream schedule from Python every "
                          "step (host enqueue ~4.1 ms under a ~5.6 ms device step: device-bound); "
                          "exec: capture the step once and replay it with the library's C++ "
                          "multi-stream executor (clskd.graph.StepExecutor: ~1 ms host enqueue, but "
@@ -422,9 +423,13 @@ def main():
         args.launch = "graph"
     if args.spkd and args.train:
         raise SystemExit("--spkd is its own leg (no --train)")
-    if args.train or args.spkd or world > 1:
-        # the C3 / C4 legs launch eagerly (their capture is not wired yet); multi-rank C2 runs
-        # launch eagerly too (no graph capture beside the RCCL communicator's watchdog)
+    if args.launch is None:
+        # C3 on one GPU: the captured training step replayed by the C++ executor (its eager host
+        # path issues ~1,000 launches per step); C2 / C4: eager
+        args.launch = "exec" if (args.train and world == 1) else "eager"
+    if args.spkd or world > 1 or (args.train and args.launch == "graph"):
+        # the C4 leg launches eagerly (its capture is not wired yet); multi-rank runs launch
+        # eagerly too (no graph capture beside the RCCL communicator's watchdog)
         args.launch = "eager"
     args.graph = args.launch == "graph"
     bsz = B_SPKD if args.spkd else B_PER_GPU
@@ -458,10 +463,18 @@ def main():
     if args.train:
         from clskd.train import FlatAdam, FlatParams
         flat = FlatParams(kd.student)
-        opt = FlatAdam(flat, lr=cfg.learning_rate)
+        opt = FlatAdam(flat, lr=cfg.learning_rate, device_step=args.launch == "exec")
 
-        def step(i):
+        def eager_step(i):
             return kd.train_step((Xs[i % NBATCH], Ys[i % NBATCH]), flat, opt)
+        if args.launch == "exec":
+            from clskd.graph import TrainStepExecutor
+            executor = TrainStepExecutor(kd, flat, opt, Xs[0], Ys[0])
+
+            def step(i):
+                return executor(Xs[i % NBATCH], Ys[i % NBATCH])
+        else:
+            step = eager_step
     elif args.launch == "eager":
         def step(i):
             # fwd+loss only: no autograd tape (the C3 leg above records and consumes one)

@@ -485,6 +485,11 @@ int clskd_index_gather(const float* src, const int32_t* idx, const float* sgn, i
 int clskd_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr,
                     float beta1, float beta2, float eps, float weight_decay, int32_t step,
                     float grad_scale, void* stream);
+/* The same step with the step count in device memory (for a captured, replayed training step):
+ * applies step *step + 1, then stores *step + 1 (stream-ordered, two launches). */
+int clskd_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr,
+                        float beta1, float beta2, float eps, float weight_decay, int32_t* step,
+                        float grad_scale, void* stream);
 int clskd_fill_f32(float* p, int64_t n, float value, void* stream);
 int clskd_axpy_f32(const float* x, float* y, int64_t n, float alpha, int32_t accumulate,
                    void* stream);

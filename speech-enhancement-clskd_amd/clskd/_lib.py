@@ -160,6 +160,7 @@ SIGNATURES = {
     "clskd_conv2d_wgrad": (_i32, [C.POINTER(ConvDesc), _p, _p, _p, _p, _i64, _i32, _p]),
     "clskd_index_gather": (_i32, [_p, _p, _p, _i32, _i64, _p, _i32, _p]),
     "clskd_adam_step": (_i32, [_p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _f32, _p]),
+    "clskd_adam_step_dev": (_i32, [_p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _p, _f32, _p]),
     "clskd_fill_f32": (_i32, [_p, _i64, _f32, _p]),
     "clskd_axpy_f32": (_i32, [_p, _p, _i64, _f32, _i32, _p]),
     "clskd_bn_bwd_blocks": (_i32, [_i64, _i32]),

@@ -200,6 +200,80 @@ class StepExecutor(StepGraph):
             pass
 
 
+class TrainStepExecutor(StepExecutor):
+    """Configuration C3 as one captured step: ``kd.train_step`` — fwd+loss with the autograd
+    tape, the HIP backward into the flat gradient buffer, Adam over the flat parameters
+    (distill.py:72-148, 202-204) — recorded once and replayed by the C++ step executor on the
+    step's four streams.  Every replay packs the student's weights from the parameters the
+    previous replay's Adam wrote (DCCRN.repack_in_capture) and advances the optimizer's device
+    step count (FlatAdam(device_step=True)), so N replays are N training steps, bitwise equal to
+    N eager ``train_step`` calls with the same optimizer (tests/test_gpu_train_graph.py).  The
+    eager path spends ~16 ms of host time per step issuing ~1,000 launches; the executor issues
+    the captured step in a few.  Single process only (a collective inside the capture is not
+    wired: multi-rank training steps launch eagerly).
+
+        flat = FlatParams(kd.student); opt = FlatAdam(flat, lr=..., device_step=True)
+        step = TrainStepExecutor(kd, flat, opt, X, y)
+        loss = step(X_next, y_next)        # one training step on the new batch
+    """
+
+    def __init__(self, kd, flat, opt, X, y, warmup=1, nstreams=None):
+        import torch.distributed as dist
+        if not getattr(opt, "device_step", False):
+            raise ValueError("TrainStepExecutor needs FlatAdam(device_step=True): the step count "
+                             "must live on the device to be replayed")
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            raise NotImplementedError("TrainStepExecutor: multi-rank steps launch eagerly "
+                                      "(no all-reduce inside the capture)")
+        self.flat, self.opt = flat, opt
+        super().__init__(kd, X, y, warmup, nstreams)
+
+    def _baked(self):
+        # the trainable student parameters are the step's state, not baked constants
+        trainable = {id(p) for p in self.flat.params}
+        return [p for p in super()._baked() if id(p) not in trainable]
+
+    def _run(self):
+        return self.kd.train_step((self.X, self.y), self.flat, self.opt)
+
+    def _capture(self):
+        self._release()
+        dev = self.X.device
+        from .distill import _side_stream
+        for w in (0, 1, 2):
+            _side_stream(dev, w)
+        cur = torch.cuda.current_stream(dev)
+        # warm-up (tables, index maps, caches) restores every piece of state a step changes:
+        # BatchNorm running statistics, the parameters, Adam's moments and step count
+        state = _bn_buffers(self.kd) + self.opt.state()
+        saved = [t.clone() for t in state]
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            for _ in range(self.warmup):
+                self._run()
+        cur.wait_stream(s)
+        torch.cuda.synchronize(dev)
+        with torch.no_grad():
+            for t, v in zip(state, saved):
+                t.copy_(v)
+        self.graph = None
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        student = self.kd.student
+        student.repack_in_capture = True
+        self._tagging(True)
+        try:
+            with torch.cuda.graph(g):
+                self.out = dict(loss=self._run())
+        finally:
+            self._tagging(False)
+            student.repack_in_capture = False
+        self.graph = g
+        self.sig = self._sig()
+        self.captures += 1
+        self._after_capture()
+
+
 class CapturedCall:
     """Any stream-ordered device computation ``fn(*inputs)`` captured once and replayed by the
     step executor (clskd_exec_launch) — e.g. the B=1 eval forward of configuration C1, whose

@@ -204,6 +204,9 @@ class DCCRN(nn.Module):
         # bf16 split-product MFMA for the fp32 convs), "bf16" / "fp16" (16-bit operands, fp32
         # accumulation).  STFT/iSTFT framing GEMMs run fp32 ("f32x3": split products).
         self.compute = "fp32"
+        # a captured training step (clskd.graph.TrainStepExecutor) records the packing of every
+        # trainable parameter group, so each replay packs the weights its own optimizer step wrote
+        self.repack_in_capture = False
 
     # ---------------------------------------------------------------- reference helpers
     def flatten_parameters(self):
@@ -248,7 +251,9 @@ class DCCRN(nn.Module):
             params = pg
         ent = self._wcache.get(key)
         ver = _pv(*params)
-        if ent is None or ent[0] != ver:
+        if ent is None or ent[0] != ver or (
+                self.repack_in_capture and torch.cuda.is_current_stream_capturing()
+                and any(p.requires_grad for p in params)):
             with torch.no_grad():
                 ent = (ver, build())
             self._wcache[key] = ent

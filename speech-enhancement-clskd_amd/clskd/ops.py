@@ -1185,6 +1185,14 @@ def adam_step(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale=
                                 weight_decay, step, grad_scale, _stream()), "adam")
 
 
+def adam_step_dev(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
+    """adam_step with the step count in `step` (int32 device tensor, advanced by the call)."""
+    if step.dtype != torch.int32 or step.device != p.device:
+        raise ValueError("adam_step_dev: step must be an int32 tensor on the parameters' device")
+    check(lib().clskd_adam_step_dev(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, beta1, beta2,
+                                    eps, weight_decay, ptr(step), grad_scale, _stream()), "adam_dev")
+
+
 def fill(t, value=0.0):
     check(lib().clskd_fill_f32(ptr(t), t.numel(), value, _stream()), "fill")
     return t

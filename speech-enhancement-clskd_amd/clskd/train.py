@@ -54,20 +54,40 @@ class FlatParams:
 
 
 class FlatAdam:
-    """torch.optim.Adam semantics over a FlatParams buffer, one clskd_adam_step launch."""
+    """torch.optim.Adam semantics over a FlatParams buffer, one clskd_adam_step launch.
 
-    def __init__(self, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+    device_step=True keeps the step count in device memory (`self.t`, int32) and advances it
+    in-stream (clskd_adam_step_dev), so a captured training step (clskd.graph.TrainStepExecutor)
+    replays with the right bias corrections; `step_count` then reads it back."""
+
+    def __init__(self, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 device_step=False):
         self.flat = flat
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
         self.m = torch.zeros_like(flat.data)
         self.v = torch.zeros_like(flat.data)
-        self.step_count = 0
+        self.device_step = device_step
+        self.t = torch.zeros(1, dtype=torch.int32, device=flat.data.device) if device_step else None
+        self._host_steps = 0
+
+    @property
+    def step_count(self):
+        return int(self.t.item()) if self.device_step else self._host_steps
 
     def step(self, grad_scale=1.0):
-        self.step_count += 1
-        ops.adam_step(self.flat.data, self.flat.grad, self.m, self.v, self.lr, self.betas[0],
-                      self.betas[1], self.eps, self.weight_decay, self.step_count, grad_scale)
+        if self.device_step:
+            ops.adam_step_dev(self.flat.data, self.flat.grad, self.m, self.v, self.lr,
+                              self.betas[0], self.betas[1], self.eps, self.weight_decay, self.t,
+                              grad_scale)
+        else:
+            self._host_steps += 1
+            ops.adam_step(self.flat.data, self.flat.grad, self.m, self.v, self.lr, self.betas[0],
+                          self.betas[1], self.eps, self.weight_decay, self._host_steps, grad_scale)
         self.flat.bump_versions()
+
+    def state(self):
+        """The optimizer's and the parameters' device state (snapshot / restore)."""
+        return [self.flat.data, self.m, self.v] + ([self.t] if self.device_step else [])
 
     def zero_grad(self):
         ops.fill(self.flat.grad, 0.0)

@@ -224,6 +224,34 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   }
 }
 
+// The same update with the step count on the device (a captured training step replays it): every
+// thread derives the bias corrections of step *step + 1; step_advance_kernel then stores it.
+__global__ __launch_bounds__(256) void adam_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                       float* __restrict__ m, float* __restrict__ v,
+                                                       int64_t n, float lr, float beta1, float beta2,
+                                                       float eps, float wd, const int32_t* __restrict__ step,
+                                                       float gscale) {
+  const float t = (float)(*step + 1);
+  const float bc1 = 1.f - powf(beta1, t);
+  const float bc2s = sqrtf(1.f - powf(beta2, t));
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float gi = g[i] * gscale;
+    const float pi = p[i];
+    if (wd != 0.f) gi = fmaf(wd, pi, gi);
+    const float mi = beta1 * m[i] + (1.f - beta1) * gi;
+    const float vi = beta2 * v[i] + (1.f - beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    p[i] = pi - (lr / bc1) * (mi / denom);
+  }
+}
+
+__global__ void step_advance_kernel(int32_t* step) {
+  if (threadIdx.x == 0) *step += 1;
+}
+
 __global__ void fill_f32_kernel(float* p, int64_t n, float v) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -326,6 +354,19 @@ extern "C" int clskd_adam_step(float* p, const float* g, float* m, float* v, int
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, g, m, v,
                      n, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, grad_scale);
   CLSKD_LAUNCH_CHECK("adam");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr,
+                                   float beta1, float beta2, float eps, float weight_decay,
+                                   int32_t* step, float grad_scale, void* stream) {
+  CLSKD_CHECK_ARG(p && g && m && v && step, "adam_dev: bad argument");
+  hipStream_t st = as_stream(stream);
+  if (n > 0)
+    hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, g, m, v, n, lr, beta1,
+                       beta2, eps, weight_decay, step, grad_scale);
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, st, step);
+  CLSKD_LAUNCH_CHECK("adam_dev");
   return CLSKD_OK;
 }
 

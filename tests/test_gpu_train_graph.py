@@ -1,0 +1,74 @@
+"""Configuration C3 as a captured step (clskd.graph.TrainStepExecutor): the training step —
+fwd+loss with the tape, HIP backward, Adam — recorded once and replayed by the C++ executor must
+be the same computation as eager ``train_step`` calls: loss, every parameter, Adam's moments and
+step count bitwise equal after each of three steps on different batches (same kernels, same
+arguments, deterministic reductions).  Plus the device-step Adam kernel against the host-step
+one and torch.optim.Adam (distill.py:202-204)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+torch.set_num_threads(min(16, os.cpu_count() or 1))
+
+
+def test_adam_device_step_matches_host_step_and_torch():
+    from clskd import ops
+    g = torch.Generator().manual_seed(5)
+    p0 = torch.randn(5000, generator=g)
+    ref = p0.clone().requires_grad_()
+    opt = torch.optim.Adam([ref], lr=6e-4, weight_decay=0.01)
+    p_h, p_d = p0.clone().to(DEV), p0.clone().to(DEV)
+    m_h, v_h = torch.zeros_like(p_h), torch.zeros_like(p_h)
+    m_d, v_d = torch.zeros_like(p_d), torch.zeros_like(p_d)
+    t = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for step in range(1, 5):
+        grad = torch.randn(5000, generator=g)
+        ref.grad = grad.clone()
+        opt.step()
+        ops.adam_step(p_h, grad.to(DEV), m_h, v_h, 6e-4, 0.9, 0.999, 1e-8, 0.01, step)
+        ops.adam_step_dev(p_d, grad.to(DEV), m_d, v_d, 6e-4, 0.9, 0.999, 1e-8, 0.01, t)
+    assert int(t.item()) == 4
+    # bias corrections: powf on the device vs on the host (a few ulp at most)
+    np.testing.assert_allclose(p_d.cpu().numpy(), p_h.cpu().numpy(), rtol=2e-7, atol=1e-9)
+    np.testing.assert_allclose(p_d.cpu().numpy(), ref.detach().numpy(), rtol=1e-6, atol=1e-7)
+    assert torch.equal(m_d, m_h) and torch.equal(v_d, v_h)
+
+
+@pytest.mark.parametrize("precision", ["mixed", "fp32"])
+def test_train_executor_matches_eager_train_steps(precision):
+    from clskd.data import synthetic_pairs
+    from clskd.graph import TrainStepExecutor
+    from clskd.train import FlatAdam, FlatParams
+    from test_gpu_parity import _kd
+    batches = []
+    for seed in (31, 32, 33):
+        n, c = synthetic_pairs(4, 16000, seed=seed)
+        batches.append((torch.from_numpy(n).to(DEV), torch.from_numpy(c).to(DEV)))
+    kd_e, kd_g = _kd().set_precision(precision), _kd().set_precision(precision)
+    runs = []
+    for kd in (kd_e, kd_g):
+        flat = FlatParams(kd.student)
+        runs.append((flat, FlatAdam(flat, lr=6e-4, device_step=True)))
+    (fe, oe), (fg, og) = runs
+    assert torch.equal(fe.data, fg.data)
+    ex = TrainStepExecutor(kd_g, fg, og, *batches[0])
+    assert og.step_count == 0 and torch.equal(fe.data, fg.data)  # warm-up state restored
+    print("executor:", ex.info)
+    for i, (X, y) in enumerate(batches):
+        le = kd_e.train_step((X, y), fe, oe)
+        lg = ex(X, y)
+        torch.cuda.synchronize()
+        assert lg.item() == le.item(), (i, lg.item(), le.item())
+        assert torch.equal(fg.grad, fe.grad), i
+        assert torch.equal(fg.data, fe.data), i
+    assert oe.step_count == og.step_count == 3
+    assert torch.equal(oe.m, og.m) and torch.equal(oe.v, og.v)
+    assert ex.captures == 1
+    # BatchNorm running statistics of the student (updated inside the replayed forward)
+    for (k, a), b in zip(kd_e.student.state_dict().items(), kd_g.student.state_dict().values()):
+        assert torch.equal(a, b), k

@@ -80,3 +80,18 @@ def test_spkd_perturbation_bound_holds():
             L1 = spkd_term(_gram(zs + es), _gram(zt + et))
             bnd = spkd_bound(_gram(zs), _gram(zt), rho_s, rho_t)
             assert abs(L1 - L0) <= bnd, (trial, aligned, abs(L1 - L0), bnd)
+
+
+def test_train_executor_requires_device_step_optimizer():
+    """TrainStepExecutor replays the optimizer: a host-side step count would be frozen into the
+    capture, so it refuses FlatAdam(device_step=False) before touching the model."""
+    import pytest
+    import torch
+    from clskd.graph import TrainStepExecutor
+    from clskd.train import FlatAdam, FlatParams
+    m = torch.nn.Linear(4, 3)
+    flat = FlatParams(m)
+    with pytest.raises(ValueError, match="device_step"):
+        TrainStepExecutor(None, flat, FlatAdam(flat), torch.zeros(1, 8), torch.zeros(1, 8))
+    opt = FlatAdam(flat, device_step=True)
+    assert opt.step_count == 0 and len(opt.state()) == 4

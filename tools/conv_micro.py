@@ -24,13 +24,20 @@ CFGS.update({
     "abf3": ("abf", 64, 256, 16),     # 3x3, 64 -> 256
     "abf4": ("abf", 64, 128, 32),     # 3x3, 64 -> 128 (the 256x128-tile engine config)
     "abf5": ("abf", 64, 64, 64),
+    # plain GEMMs through the same engine (1x1 "conv", contiguous rows: no tap gather)
+    "pw_enc4": ("pw", 2560, 256, 8),          # enc4's M x N x K without the im2col gather
+    "pw4k": ("pw", 4096, 4096, 1, 1, 4096),   # 4096^3 (cdna_hip_programming.md's GEMM size)
+    "pw64k": ("pw", 4096, 256, 1, 16, 4096),  # M 65536 x N 256 x K 4096: 256 tiles, 64 K-tiles each
 })
 
 
-def make(kind, ci, co, fi, dev):
+def make(kind, ci, co, fi, B=B, T=T, dev=None):
     g = torch.Generator(device="cpu").manual_seed(0)
     x = (torch.randn(B, fi, T, ci, generator=g) * 0.5).to(torch.bfloat16).to(dev)
-    if kind == "enc":
+    if kind == "pw":
+        taps = [(0, 0)]
+        Fo, To, sf, omap_f = fi, T, 1, 1
+    elif kind == "enc":
         taps = [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)]
         Fo, To, sf, omap_f = fi // 2, T, 2, 1
     elif kind == "dec":
@@ -62,7 +69,7 @@ def main():
     dev = torch.device("cuda", 0)
     names = [n for n in CFGS if not a.only or n in a.only.split(",")]
     for name in names:
-        run, fl, (M, N, K) = make(*CFGS[name], dev)
+        run, fl, (M, N, K) = make(*CFGS[name], dev=dev)
         for _ in range(3):
             run()
         torch.cuda.synchronize()
