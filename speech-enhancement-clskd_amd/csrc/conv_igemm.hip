@@ -346,6 +346,7 @@ namespace clskd {
 bool conv_halo_takes(const clskd_conv_desc& d);
 bool conv_halo_f32_takes(const clskd_conv_desc& d);
 bool conv_gemm8_takes(const clskd_conv_desc& d);
+bool conv_halow_takes(const clskd_conv_desc& d);
 bool conv_pointwise_takes(const clskd_conv_desc& d);
 bool conv_split3_takes(const clskd_conv_desc& d, bool force);
 }  // namespace clskd
@@ -356,6 +357,7 @@ static bool fold_capable(const clskd_conv_desc& dd) {
   if (dd.wlayout == CLSKD_WLAYOUT_DIRECT || dd.accumulate) return false;
   if (is_lowp(dd.compute)) {
     if (conv_halo_takes(dd)) return true;
+    if (conv_halow_takes(dd)) return true;
     return conv_gemm8_takes(dd) && dd.N <= 256;  // one N-tile (256x256 / 256x128 instances)
   }
   const bool split = dd.compute == CLSKD_F32X3;

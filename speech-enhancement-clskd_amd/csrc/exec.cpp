@@ -18,6 +18,7 @@
 // point to in the capture's memory pool, so the caller keeps both alive while the executor is
 // used (clskd.graph.StepExecutor owns the torch CUDAGraph for this).
 #include <stdint.h>
+#include <stdio.h>
 #include <time.h>
 
 #include <algorithm>
@@ -57,6 +58,15 @@ struct clskd_exec {
   std::vector<KNode> kernels;
   std::vector<hipMemsetParams> memsets;
   std::vector<hipMemcpy3DParms> memcpys;
+  // a memcpy node that is one contiguous range between linear allocations (torch's clone /
+  // copy_ under capture) replays as a flat hipMemcpyAsync: {dst, src, bytes}, bytes = 0 -> 3D
+  struct Flat {
+    void* dst;
+    const void* src;
+    size_t bytes;
+    hipMemcpyKind kind;
+  };
+  std::vector<Flat> flat;
   std::vector<Op> program;
   size_t join_at = 0;  // program[join_at..]: every used side stream's join into stream 0
   int32_t n_nodes = 0, n_waits = 0, n_records = 0, n_empty = 0;
@@ -215,6 +225,15 @@ extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, void* const*
       }
       slot[i] = (int)ex->memcpys.size();
       ex->memcpys.push_back(p);
+      clskd_exec::Flat f{nullptr, nullptr, 0, p.kind};
+      if (!p.srcArray && !p.dstArray && p.extent.height <= 1 && p.extent.depth <= 1 &&
+          p.srcPos.y == 0 && p.srcPos.z == 0 && p.dstPos.y == 0 && p.dstPos.z == 0 &&
+          p.srcPtr.ptr && p.dstPtr.ptr) {
+        f.dst = static_cast<char*>(p.dstPtr.ptr) + p.dstPos.x;
+        f.src = static_cast<const char*>(p.srcPtr.ptr) + p.srcPos.x;
+        f.bytes = p.extent.width;
+      }
+      ex->flat.push_back(f);
     } else if (t == hipGraphNodeTypeEmpty) {
       ++ex->n_empty;
     } else {
@@ -435,9 +454,12 @@ extern "C" int clskd_exec_launch(clskd_exec* ex, void* stream) {
           e = hipMemsetD8Async((hipDeviceptr_t)p.dst, (unsigned char)p.value, p.width, s);
         break;
       }
-      case OP_MEMCPY:
-        e = hipMemcpy3DAsync(&ex->memcpys[op.idx], s);
+      case OP_MEMCPY: {
+        const clskd_exec::Flat& f = ex->flat[op.idx];
+        e = f.bytes ? hipMemcpyAsync(f.dst, f.src, f.bytes, f.kind, s)
+                    : hipMemcpy3DAsync(&ex->memcpys[op.idx], s);
         break;
+      }
       case OP_WAIT:
         e = hipStreamWaitEvent(s, ex->events[op.idx], 0);
         break;
@@ -453,7 +475,11 @@ extern "C" int clskd_exec_launch(clskd_exec* ex, void* stream) {
         if (jo.kind == OP_RECORD) (void)hipEventRecord(ex->events[jo.idx], st[jo.stream]);
         else (void)hipStreamWaitEvent(st[jo.stream], ex->events[jo.idx], 0);
       }
-      return hip_fail("launch", e);
+      static const char* kinds[] = {"kernel", "memset", "memcpy", "wait", "record"};
+      char what[96];
+      snprintf(what, sizeof what, "launch (program op %zu: %s #%d, stream %d)", i,
+               op.kind >= 0 && op.kind < 5 ? kinds[op.kind] : "?", op.idx, op.stream);
+      return hip_fail(what, e);
     }
   }
   if (mk) {

@@ -982,22 +982,31 @@ G8_CASES = {
     "pw_k64_nk1_n256": ((64,), 200, [(0, 0)], 1, 9, 9, 1, 0, False),
     "pw_k128_nk2_n128": ((128,), 128, [(0, 0)], 1, 9, 9, 1, 0, True),
     "pw_k192_nk3_n256": ((192,), 256, [(0, 0)], 1, 9, 9, 1, 0, True),
+    "enc5x2_fo4_n256": ((128,), 256, [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)], 2, 8, 4, 1, 0, True),
+    "abf3x3_n200": ((64,), 200, [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], 1, 16, 16, 1, 0, False),
 }
 
 
+@pytest.mark.parametrize("engine", ["gemm8", "halow"])
 @pytest.mark.parametrize("lp", ["bf16", "fp16"])
 @pytest.mark.parametrize("case", sorted(G8_CASES))
-def test_conv_gemm8_against_torch(case, lp, loop="phased"):
-    """Phase-interleaved 8-wave bf16 GEMM engine (conv_gemm8.hip; N > 64): im2col 5x2 stride-2,
-    two-segment polyphase decoder layers with an interleaved output map, ABF 3x3, and pointwise
-    layers with 1-3 K-tiles (pipeline prologue/drain edge cases), fused BN statistics, M not a
-    tile multiple; vs torch fp64 on the same bf16 operands.  Tolerance 1e-4 relative (fp32 out)
-    / 8e-3 (bf16 out); statistics 1e-5.  loop="pingpong" (CLSKD_G8_PP=1, bf16 operands): the
-    ping-pong K loop of the experiments build (CLSKD_LIB=exp; not in the product library)."""
+def test_conv_gemm8_against_torch(case, lp, engine, loop="phased"):
+    """The wide-layer bf16 engines (N > 64), each forced in turn (CLSKD_HALOW):
+    engine="gemm8": the phase-interleaved 8-wave implicit GEMM (conv_gemm8.hip) — im2col 5x2
+    stride-2, two-segment polyphase decoder layers with an interleaved output map, ABF 3x3, and
+    pointwise layers with 1-3 K-tiles (pipeline prologue/drain edge cases);
+    engine="halow": the halo-tiled kernel with streamed weight slabs (conv_halow.hip) on every
+    tap-structured case (8x32 tiles, 4x64 tiles at Fo = 4, N not a multiple of 32);
+    fused BN statistics, M not a tile multiple; vs torch fp64 on the same bf16 operands.
+    Tolerance 1e-4 relative (fp32 out) / 8e-3 (bf16 out); statistics 1e-5.  loop="pingpong"
+    (CLSKD_G8_PP=1, bf16 operands): the ping-pong K loop of the experiments build (CLSKD_LIB=exp;
+    not in the product library)."""
     from clskd import _lib, ops
     if loop == "pingpong" and lp == "fp16":
         pytest.skip("the ping-pong K loop is built for bf16 operands")
     segc, N, taps, sf, Fi, Fo, of_mul, of_add, out_bf16 = G8_CASES[case]
+    if engine == "halow" and (len(taps) < 3 or loop == "pingpong"):
+        pytest.skip("conv_halow takes tap-structured layers (>= 3 taps)")
     g = torch.Generator().manual_seed(len(case) * 13 + N)
     B, T = 3, 97
     segs_h = [torch.randn(B, Fi, T, c, generator=g).to(_LP[lp]) for c in segc]
@@ -1023,6 +1032,7 @@ def test_conv_gemm8_against_torch(case, lp, loop="phased"):
     nblk = ops.conv_mblocks(B, Fo, T)
     st = torch.full((nblk * N * 2,), float("nan"), device=DEV, dtype=torch.float64)
     prev = _lib.set_knob("CLSKD_G8_PP", int(loop == "pingpong"))
+    prev_hw = _lib.set_knob("CLSKD_HALOW", int(engine == "halow"))
     try:
         ops.conv([ops.seg_bftc(s.to(DEV)) for s in segs_h], taps, B, Fo, T, N, wp, bias.to(DEV),
                  out, ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add),
@@ -1030,7 +1040,9 @@ def test_conv_gemm8_against_torch(case, lp, loop="phased"):
         kname = ops.conv_kernel_of_last_launch()
     finally:
         _lib.set_knob("CLSKD_G8_PP", prev)
-    assert kname.startswith("conv_gemm8") and (kname.endswith(",f16>") == (lp == "fp16")), kname
+        _lib.set_knob("CLSKD_HALOW", prev_hw)
+    prefix = "conv_gemm8" if engine == "gemm8" else "conv_halow"
+    assert kname.startswith(prefix) and (kname.endswith(",f16>") == (lp == "fp16")), kname
     assert kname.endswith(",pp>") == (loop == "pingpong"), kname
     o = out.double().cpu()[:, of_add::of_mul]
     tol = _LP_TOL[lp] if out_bf16 else 1e-4

@@ -26,7 +26,6 @@ CFGS.update({
     "abf5": ("abf", 64, 64, 64),
     # plain GEMMs through the same engine (1x1 "conv", contiguous rows: no tap gather)
     "pw_enc4": ("pw", 2560, 256, 8),          # enc4's M x N x K without the im2col gather
-    "pw4k": ("pw", 4096, 4096, 1, 1, 4096),   # 4096^3 (cdna_hip_programming.md's GEMM size)
     "pw64k": ("pw", 4096, 256, 1, 16, 4096),  # M 65536 x N 256 x K 4096: 256 tiles, 64 K-tiles each
 })
 
