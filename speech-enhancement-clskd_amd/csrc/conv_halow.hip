@@ -41,6 +41,7 @@ constexpr int CW = 32;     // channels per chunk: 64-B pixel / weight rows
 constexpr int MAXG = 6;    // halo DMA instructions per wave per chunk
 constexpr int MAXCH = 32;  // chunks
 constexpr int BST = 3;     // weight-slab ring stages (two steps in flight)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_base) {
   unsigned keep;
@@ -396,9 +397,9 @@ __global__ __launch_bounds__(512) void conv_halow_kernel(const HwArgs a) {
             const int rr = q / CPRW, cc = q % CPRW;
             const int n = nb + cc * CH;
             if (fo < Fo && tb0 + rr < To && n < Nn)
-              *reinterpret_cast<__attribute__((address_space(1))) uint4*>(
+              *reinterpret_cast<__attribute__((address_space(1))) hw::u32x4*>(
                   outp + rowb + (int64_t)(tb0 + rr) * oT + n) =
-                  *reinterpret_cast<const uint4*>(wt + rr * 32 + cc * CH);
+                  *reinterpret_cast<const hw::u32x4*>(wt + rr * 32 + cc * CH);
           }
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: tile read back
           __builtin_amdgcn_sched_barrier(0);
