@@ -38,7 +38,7 @@ __device__ __attribute__((aligned(64))) unsigned char g_hw_zero[64];
 namespace hw {
 constexpr int NW = 8;      // waves
 constexpr int CW = 32;     // channels per chunk: 64-B pixel / weight rows
-constexpr int MAXG = 6;    // halo DMA instructions per wave per chunk
+constexpr int MAXG = 7;    // halo DMA instructions per wave per chunk
 constexpr int MAXCH = 32;  // chunks
 constexpr int BST = 3;     // weight-slab ring stages (two steps in flight)
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -100,7 +100,7 @@ struct HwArgs {
   int32_t dfmin, dtmin;           // halo origin relative to (fo*stride_f, to)
   int32_t HF, HT, NPIX;           // halo extent (pixels) and count
   int32_t NGH;                    // halo DMA wave-instructions per wave per chunk
-  int32_t halo_bytes;             // bytes per halo buffer (NW * NGH KiB)
+  int32_t halo_bytes;             // bytes per halo buffer (ceil(NPIX / 16) KiB)
   int32_t nfb, ntb, ntiles;       // tile grid: F-blocks, T-blocks, total
   int32_t nblk128;                // statistics slots (ceil(M/128))
   int32_t tap_pix[16];            // halo pixel offset of tap t for output (0, 0)
@@ -231,6 +231,9 @@ __global__ __launch_bounds__(512) void conv_halow_kernel(const HwArgs a) {
   auto issue_halo = [&](const Cur& c, int ch, int hb) -> int {
     const int NGH = __builtin_amdgcn_readfirstlane(kc->NGH);
     const int NPIX = kc->NPIX;
+    // pieces past the halo (the last waves' tail) are not issued: the buffer holds
+    // ceil(NPIX / 16) KiB, not NW * NGH
+    const int nown = max(0, min(NGH, ((NPIX + 15) >> 4) - wave * NGH));
     const int4 ea = ctA[ch];
     const int4 eb = ctB[ch];
     const InT* base = reinterpret_cast<const InT*>(((uint64_t)(unsigned)ea.y << 32) | (unsigned)ea.x) +
@@ -238,7 +241,7 @@ __global__ __launch_bounds__(512) void conv_halow_kernel(const HwArgs a) {
     const int fi_lo = c.fb * FT * kc->sfr + kc->dfmin, ti_lo = c.tb * TT + kc->dtmin;
     const float inv_ht = 1.0f / (float)HT;
     const unsigned dst = hlds0 + hb * halo_bytes;
-    for (int i = 0; i < NGH; ++i) {
+    for (int i = 0; i < nown; ++i) {
       const int slot = (wave * NGH + i) * 64 + lane;
       const int p = slot >> 2;
       const int hf = (int)(((float)p + 0.5f) * inv_ht);
@@ -250,7 +253,7 @@ __global__ __launch_bounds__(512) void conv_halow_kernel(const HwArgs a) {
                               : zero_addr;
       glds16((const void*)src, dst + (wave * NGH + i) * 1024);
     }
-    return NGH;
+    return nown;
   };
   // weight slab of (chunk ch, tap t) into ring stage st: piece q = wave * GB + i covers slab
   // rows 16q .. 16q + 15; lane -> row 16q + lane / 4, 16-B chunk lane % 4
@@ -499,7 +502,7 @@ static bool halow_plan(const clskd_conv_desc& d, HwArgs& a, size_t& lds, int& tt
   }
   a.NGH = (int)cdiv((int64_t)a.NPIX * 4, 64 * NW);  // 4 x 16-B slots per pixel
   if (a.NGH > MAXG) return false;
-  a.halo_bytes = NW * a.NGH * 1024;
+  a.halo_bytes = (int)cdiv(a.NPIX, 16) * 1024;  // whole 1-KiB pieces of 16 pixels
   lds = 2 * (size_t)a.halo_bytes + (size_t)BST * bn * 64 + 2 * MAXCH * 16 + 16 * 4 +
         sizeof(HwConsts) + (size_t)bn * (4 + 8);
   for (int s = 0; s < d.nseg; ++s)
