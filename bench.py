@@ -427,7 +427,7 @@ def main():
         # C3 on one GPU: the captured training step replayed by the C++ executor (its eager host
         # path issues ~1,000 launches per step); C2 / C4: eager
         args.launch = "exec" if (args.train and world == 1) else "eager"
-    if args.spkd or world > 1 or (args.train and args.launch == "graph"):
+    if args.spkd or world > 1:
         # the C4 leg launches eagerly (its capture is not wired yet); multi-rank runs launch
         # eagerly too (no graph capture beside the RCCL communicator's watchdog)
         args.launch = "eager"
@@ -463,16 +463,21 @@ def main():
     if args.train:
         from clskd.train import FlatAdam, FlatParams
         flat = FlatParams(kd.student)
-        opt = FlatAdam(flat, lr=cfg.learning_rate, device_step=args.launch == "exec")
+        opt = FlatAdam(flat, lr=cfg.learning_rate, device_step=args.launch in ("exec", "graph"))
 
         def eager_step(i):
             return kd.train_step((Xs[i % NBATCH], Ys[i % NBATCH]), flat, opt)
-        if args.launch == "exec":
-            from clskd.graph import TrainStepExecutor
-            executor = TrainStepExecutor(kd, flat, opt, Xs[0], Ys[0])
+        if args.launch in ("exec", "graph"):
+            # the captured training step: replayed by the C++ executor (exec) or hipGraphLaunch
+            from clskd.graph import TrainStepExecutor, TrainStepGraph
+            if args.launch == "exec":
+                executor = TrainStepExecutor(kd, flat, opt, Xs[0], Ys[0])
+                captured = executor
+            else:
+                graph = captured = TrainStepGraph(kd, flat, opt, Xs[0], Ys[0])
 
             def step(i):
-                return executor(Xs[i % NBATCH], Ys[i % NBATCH])
+                return captured(Xs[i % NBATCH], Ys[i % NBATCH])
         else:
             step = eager_step
     elif args.launch == "eager":
@@ -739,7 +744,7 @@ def main():
                                   f"({executor.info['kernels']} kernels, "
                                   f"{executor.info['waits']} cross-stream waits per step)"
                                   if args.launch == "exec"
-                                  else "hipGraph replay (clskd.graph.StepGraph)"),
+                                  else f"hipGraph replay (clskd.graph.{type(graph).__name__})"),
                        "precision": ("teacher GEMMs bf16 MFMA operands / fp32 accumulate; "
                                      "student, STFT/iSTFT, LSTM recurrence, BN, losses fp32")
                        if (args.spkd and args.precision == "mixed") else

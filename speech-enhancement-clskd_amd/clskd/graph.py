@@ -200,7 +200,7 @@ class StepExecutor(StepGraph):
             pass
 
 
-class TrainStepExecutor(StepExecutor):
+class TrainStepGraph(StepGraph):
     """Configuration C3 as one captured step: ``kd.train_step`` — fwd+loss with the autograd
     tape, the HIP backward into the flat gradient buffer, Adam over the flat parameters
     (distill.py:72-148, 202-204) — recorded once and replayed by the C++ step executor on the
@@ -213,11 +213,13 @@ class TrainStepExecutor(StepExecutor):
     wired: multi-rank training steps launch eagerly).
 
         flat = FlatParams(kd.student); opt = FlatAdam(flat, lr=..., device_step=True)
-        step = TrainStepExecutor(kd, flat, opt, X, y)
+        step = TrainStepGraph(kd, flat, opt, X, y)      # hipGraphLaunch replay
         loss = step(X_next, y_next)        # one training step on the new batch
+
+    TrainStepExecutor: the same capture replayed by the C++ executor on four streams.
     """
 
-    def __init__(self, kd, flat, opt, X, y, warmup=1, nstreams=None):
+    def __init__(self, kd, flat, opt, X, y, warmup=1, **kw):
         import torch.distributed as dist
         if not getattr(opt, "device_step", False):
             raise ValueError("TrainStepExecutor needs FlatAdam(device_step=True): the step count "
@@ -226,7 +228,7 @@ class TrainStepExecutor(StepExecutor):
             raise NotImplementedError("TrainStepExecutor: multi-rank steps launch eagerly "
                                       "(no all-reduce inside the capture)")
         self.flat, self.opt = flat, opt
-        super().__init__(kd, X, y, warmup, nstreams)
+        super().__init__(kd, X, y, warmup, **kw)
 
     def _baked(self):
         # the trainable student parameters are the step's state, not baked constants
@@ -258,7 +260,7 @@ class TrainStepExecutor(StepExecutor):
             for t, v in zip(state, saved):
                 t.copy_(v)
         self.graph = None
-        g = torch.cuda.CUDAGraph(keep_graph=True)
+        g = torch.cuda.CUDAGraph(keep_graph=True) if self.keep_graph else torch.cuda.CUDAGraph()
         student = self.kd.student
         student.repack_in_capture = True
         self._tagging(True)
@@ -272,6 +274,11 @@ class TrainStepExecutor(StepExecutor):
         self.sig = self._sig()
         self.captures += 1
         self._after_capture()
+
+
+class TrainStepExecutor(TrainStepGraph, StepExecutor):
+    """TrainStepGraph replayed by the C++ step executor (clskd_exec_launch) on the step's four
+    streams instead of hipGraphLaunch."""
 
 
 class CapturedCall:

@@ -318,31 +318,40 @@ __global__ __launch_bounds__(512) void conv_halow_kernel(const HwArgs a) {
     }
     int t = 0, kch = ti * nchunk;  // kch: the workgroup's chunk count (halo buffer kch & 1)
     for (int s = 0; s < S; ++s, ++gs) {
-      // this step's slab and halo are visible; stage (gs + 2) % BST was last read in step gs - 1
-      const int ib = issue_next_slab();
-      const int ih = t == 0 ? issue_next_halo() : 0;
+      // this step's slab and halo are visible; stage (gs + 2) % BST was last read in step gs - 1.
+      // Order: fragments of k16 0 -> its 8 MFMAs -> fragments of k16 1 -> the DMA issue of
+      // later steps (its issue stalls hide under the queued MFMAs) -> the 8 MFMAs of k16 1
       const unsigned char* ws = wst + (gs % BST) * SLAB;
       const unsigned char* hb = hbuf + (kch & 1) * halo_bytes;
       const int pt = pb0 + ttab[t];  // the tap's halo pixel offset (LDS broadcast)
-#pragma unroll
-      for (int k16 = 0; k16 < 2; ++k16) {
+      bf16x8_t af[2][FM], bw[2][FN];
+      auto read_k16 = [&](int k16) {
         const int c = k16 * 2 + h;
-        bf16x8_t af[FM], bw[FN];
         // row block i's pixel = pt + rb_pix(i), rb_pix(i) a multiple of 16: same swizzle
         const unsigned char* a0 = hb + pt * 64 + ((c ^ swz(pt)) << 4);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
-          af[i] = *reinterpret_cast<const bf16x8_t*>(a0 + rb_pix(i) * 64);
+          af[k16][i] = *reinterpret_cast<const bf16x8_t*>(a0 + rb_pix(i) * 64);
 #pragma unroll
         for (int jj = 0; jj < FN; ++jj) {
           const int n = wn * (BN / WN) + jj * 32 + l32;
-          bw[jj] = *reinterpret_cast<const bf16x8_t*>(ws + n * 64 + ((c ^ swz(n)) << 4));
+          bw[k16][jj] = *reinterpret_cast<const bf16x8_t*>(ws + n * 64 + ((c ^ swz(n)) << 4));
         }
+      };
+      auto mfma_k16 = [&](int k16) {
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int jj = 0; jj < FN; ++jj) acc[i][jj] = mfma16<InT>(af[i], bw[jj], acc[i][jj]);
-      }
+          for (int jj = 0; jj < FN; ++jj) acc[i][jj] = mfma16<InT>(af[k16][i], bw[k16][jj], acc[i][jj]);
+      };
+      read_k16(0);
+      mfma_k16(0);
+      read_k16(1);
+      __builtin_amdgcn_sched_barrier(0);
+      const int ib = issue_next_slab();
+      const int ih = t == 0 ? issue_next_halo() : 0;
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_k16(1);
       // the next step's slab (issued one step ago) and, at a chunk's last tap, the next
       // chunk's halo (issued at its first tap) have landed; younger pieces stay in flight
       hw::wait_vm<MAXG + GB>(ib + ih + (t == 1 ? hprev : 0));

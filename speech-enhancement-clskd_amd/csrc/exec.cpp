@@ -476,9 +476,17 @@ extern "C" int clskd_exec_launch(clskd_exec* ex, void* stream) {
         else (void)hipStreamWaitEvent(st[jo.stream], ex->events[jo.idx], 0);
       }
       static const char* kinds[] = {"kernel", "memset", "memcpy", "wait", "record"};
-      char what[96];
-      snprintf(what, sizeof what, "launch (program op %zu: %s #%d, stream %d)", i,
-               op.kind >= 0 && op.kind < 5 ? kinds[op.kind] : "?", op.idx, op.stream);
+      char what[320];
+      int w = snprintf(what, sizeof what, "launch (program op %zu: %s #%d, stream %d)", i,
+                       op.kind < 5 ? kinds[op.kind] : "?", op.idx, op.stream);
+      if (op.kind == OP_MEMCPY && w > 0 && w < (int)sizeof what) {
+        const hipMemcpy3DParms& p = ex->memcpys[op.idx];
+        snprintf(what + w, sizeof what - w,
+                 " [src %p+%zu pitch %zu, dst %p+%zu pitch %zu, extent %zux%zux%zu, kind %d, "
+                 "arrays %p/%p]", p.srcPtr.ptr, p.srcPos.x, p.srcPtr.pitch, p.dstPtr.ptr,
+                 p.dstPos.x, p.dstPtr.pitch, p.extent.width, p.extent.height, p.extent.depth,
+                 (int)p.kind, (void*)p.srcArray, (void*)p.dstArray);
+      }
       return hip_fail(what, e);
     }
   }

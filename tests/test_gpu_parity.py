@@ -1007,6 +1007,9 @@ def test_conv_gemm8_against_torch(case, lp, engine, loop="phased"):
     segc, N, taps, sf, Fi, Fo, of_mul, of_add, out_bf16 = G8_CASES[case]
     if engine == "halow" and (len(taps) < 3 or loop == "pingpong"):
         pytest.skip("conv_halow takes tap-structured layers (>= 3 taps)")
+    if engine == "halow" and not out_bf16:
+        pytest.skip("conv_halow stages 32x32 output tiles in a halo buffer: fp32 outputs need "
+                    "a 32 KB halo (these cases' halos are smaller; they stay on conv_gemm8)")
     g = torch.Generator().manual_seed(len(case) * 13 + N)
     B, T = 3, 97
     segs_h = [torch.randn(B, Fi, T, c, generator=g).to(_LP[lp]) for c in segc]
