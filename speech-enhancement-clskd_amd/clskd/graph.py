@@ -203,29 +203,30 @@ class StepExecutor(StepGraph):
 class TrainStepGraph(StepGraph):
     """Configuration C3 as one captured step: ``kd.train_step`` — fwd+loss with the autograd
     tape, the HIP backward into the flat gradient buffer, Adam over the flat parameters
-    (distill.py:72-148, 202-204) — recorded once and replayed by the C++ step executor on the
-    step's four streams.  Every replay packs the student's weights from the parameters the
+    (distill.py:72-148, 202-204) — recorded once and replayed with hipGraphLaunch.  Every replay packs the student's weights from the parameters the
     previous replay's Adam wrote (DCCRN.repack_in_capture) and advances the optimizer's device
     step count (FlatAdam(device_step=True)), so N replays are N training steps, bitwise equal to
     N eager ``train_step`` calls with the same optimizer (tests/test_gpu_train_graph.py).  The
-    eager path spends ~16 ms of host time per step issuing ~1,000 launches; the executor issues
-    the captured step in a few.  Single process only (a collective inside the capture is not
-    wired: multi-rank training steps launch eagerly).
+    eager path spends ~16 ms of host time per step issuing ~1,000 launches; a replay is one
+    hipGraphLaunch.  Single process only (a collective inside the capture is not wired:
+    multi-rank training steps launch eagerly).
 
         flat = FlatParams(kd.student); opt = FlatAdam(flat, lr=..., device_step=True)
         step = TrainStepGraph(kd, flat, opt, X, y)      # hipGraphLaunch replay
         loss = step(X_next, y_next)        # one training step on the new batch
 
-    TrainStepExecutor: the same capture replayed by the C++ executor on four streams.
+    The C++ step executor cannot replay this capture: it holds ~60 one-dimensional memcpy nodes
+    (torch copies inside the backward) whose parameters hipGraphMemcpyNodeGetParams does not
+    return (ROCm 7.2: null destination, garbage extent); clskd_exec_create refuses such graphs.
     """
 
     def __init__(self, kd, flat, opt, X, y, warmup=1, **kw):
         import torch.distributed as dist
         if not getattr(opt, "device_step", False):
-            raise ValueError("TrainStepExecutor needs FlatAdam(device_step=True): the step count "
+            raise ValueError("TrainStepGraph needs FlatAdam(device_step=True): the step count "
                              "must live on the device to be replayed")
         if dist.is_initialized() and dist.get_world_size() > 1:
-            raise NotImplementedError("TrainStepExecutor: multi-rank steps launch eagerly "
+            raise NotImplementedError("TrainStepGraph: multi-rank steps launch eagerly "
                                       "(no all-reduce inside the capture)")
         self.flat, self.opt = flat, opt
         super().__init__(kd, X, y, warmup, **kw)
@@ -274,11 +275,6 @@ class TrainStepGraph(StepGraph):
         self.sig = self._sig()
         self.captures += 1
         self._after_capture()
-
-
-class TrainStepExecutor(TrainStepGraph, StepExecutor):
-    """TrainStepGraph replayed by the C++ step executor (clskd_exec_launch) on the step's four
-    streams instead of hipGraphLaunch."""
 
 
 class CapturedCall:

@@ -204,7 +204,7 @@ class DCCRN(nn.Module):
         # bf16 split-product MFMA for the fp32 convs), "bf16" / "fp16" (16-bit operands, fp32
         # accumulation).  STFT/iSTFT framing GEMMs run fp32 ("f32x3": split products).
         self.compute = "fp32"
-        # a captured training step (clskd.graph.TrainStepExecutor) records the packing of every
+        # a captured training step (clskd.graph.TrainStepGraph) records the packing of every
         # trainable parameter group, so each replay packs the weights its own optimizer step wrote
         self.repack_in_capture = False
 

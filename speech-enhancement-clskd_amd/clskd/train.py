@@ -57,7 +57,7 @@ class FlatAdam:
     """torch.optim.Adam semantics over a FlatParams buffer, one clskd_adam_step launch.
 
     device_step=True keeps the step count in device memory (`self.t`, int32) and advances it
-    in-stream (clskd_adam_step_dev), so a captured training step (clskd.graph.TrainStepExecutor)
+    in-stream (clskd_adam_step_dev), so a captured training step (clskd.graph.TrainStepGraph)
     replays with the right bias corrections; `step_count` then reads it back."""
 
     def __init__(self, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,

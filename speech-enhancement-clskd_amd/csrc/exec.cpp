@@ -223,6 +223,15 @@ extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, void* const*
         delete ex;
         return hip_fail("hipGraphMemcpyNodeGetParams", e);
       }
+      // ROCm 7.2 returns unusable parameters for one-dimensional memcpy nodes (the kind torch's
+      // copies record under capture: null destination, garbage extent); such a graph cannot be
+      // replayed node by node — refuse it (hipGraphLaunch replays it)
+      if (!p.dstArray && !p.dstPtr.ptr) {
+        delete ex;
+        set_error("exec_create: memcpy node %zu has unreadable parameters (a 1-D copy node); "
+                  "replay this graph with hipGraphLaunch", i);
+        return CLSKD_E_ARG;
+      }
       slot[i] = (int)ex->memcpys.size();
       ex->memcpys.push_back(p);
       clskd_exec::Flat f{nullptr, nullptr, 0, p.kind};

@@ -82,16 +82,16 @@ def test_spkd_perturbation_bound_holds():
             assert abs(L1 - L0) <= bnd, (trial, aligned, abs(L1 - L0), bnd)
 
 
-def test_train_executor_requires_device_step_optimizer():
-    """TrainStepExecutor replays the optimizer: a host-side step count would be frozen into the
+def test_train_graph_requires_device_step_optimizer():
+    """TrainStepGraph replays the optimizer: a host-side step count would be frozen into the
     capture, so it refuses FlatAdam(device_step=False) before touching the model."""
     import pytest
     import torch
-    from clskd.graph import TrainStepExecutor
+    from clskd.graph import TrainStepGraph
     from clskd.train import FlatAdam, FlatParams
     m = torch.nn.Linear(4, 3)
     flat = FlatParams(m)
     with pytest.raises(ValueError, match="device_step"):
-        TrainStepExecutor(None, flat, FlatAdam(flat), torch.zeros(1, 8), torch.zeros(1, 8))
+        TrainStepGraph(None, flat, FlatAdam(flat), torch.zeros(1, 8), torch.zeros(1, 8))
     opt = FlatAdam(flat, device_step=True)
     assert opt.step_count == 0 and len(opt.state()) == 4
