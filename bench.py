@@ -367,7 +367,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--abf-reinit", default="step", choices=["step", "once"])
     ap.add_argument("--launch", default=None, choices=["exec", "eager", "graph"],
-                    help="default: eager for C2 / C4, graph for C3 (--train) on one GPU.  "
+                    help="default: eager for C2 / C4, exec for C3 (--train) on one GPU.  "
                          "eager: launch the four-stream schedule from Python every "
                          "step (host enqueue ~4.1 ms under a ~5.6 ms device step: device-bound); "
                          "exec: capture the step once and replay it with the library's C++ "
@@ -424,11 +424,9 @@ def main():
     if args.spkd and args.train:
         raise SystemExit("--spkd is its own leg (no --train)")
     if args.launch is None:
-        # C3 on one GPU: the captured training step replayed by hipGraphLaunch (its eager host
+        # C3 on one GPU: the captured training step replayed by the C++ executor (its eager host
         # path issues ~1,000 launches per step); C2 / C4: eager
-        args.launch = "graph" if (args.train and world == 1) else "eager"
-    if args.train and args.launch == "exec":
-        args.launch = "graph"  # the training capture holds memcpy nodes the executor cannot replay
+        args.launch = "exec" if (args.train and world == 1) else "eager"
     if args.spkd or world > 1:
         # the C4 leg launches eagerly (its capture is not wired yet); multi-rank runs launch
         # eagerly too (no graph capture beside the RCCL communicator's watchdog)
@@ -465,17 +463,20 @@ def main():
     if args.train:
         from clskd.train import FlatAdam, FlatParams
         flat = FlatParams(kd.student)
-        opt = FlatAdam(flat, lr=cfg.learning_rate, device_step=args.launch == "graph")
+        opt = FlatAdam(flat, lr=cfg.learning_rate, device_step=args.launch in ("exec", "graph"))
 
         def eager_step(i):
             return kd.train_step((Xs[i % NBATCH], Ys[i % NBATCH]), flat, opt)
-        if args.launch == "graph":
-            # the captured training step replayed with hipGraphLaunch (clskd.graph.TrainStepGraph)
-            from clskd.graph import TrainStepGraph
-            graph = TrainStepGraph(kd, flat, opt, Xs[0], Ys[0])
+        if args.launch in ("exec", "graph"):
+            # the captured training step, replayed by the C++ executor (exec) or hipGraphLaunch
+            from clskd.graph import TrainStepExecutor, TrainStepGraph
+            if args.launch == "exec":
+                executor = captured = TrainStepExecutor(kd, flat, opt, Xs[0], Ys[0])
+            else:
+                graph = captured = TrainStepGraph(kd, flat, opt, Xs[0], Ys[0])
 
             def step(i):
-                return graph(Xs[i % NBATCH], Ys[i % NBATCH])
+                return captured(Xs[i % NBATCH], Ys[i % NBATCH])
         else:
             step = eager_step
     elif args.launch == "eager":

@@ -195,8 +195,15 @@ def pack_weight(w, K, compute="fp32"):
     if compute == "fp16":
         return w.to(torch.float16).contiguous()
     # always a fresh, 16-B-aligned tensor: never a view aliasing the parameter storage (which
-    # may sit at any offset of a flat parameter buffer, clskd.train.FlatParams)
-    return w.clone(memory_format=torch.contiguous_format)
+    # may sit at any offset of a flat parameter buffer, clskd.train.FlatParams).  On the device
+    # the copy is a kernel (clskd_axpy_f32, alpha 1: exact), not torch's clone: a D2D clone is a
+    # memcpy node in a captured step, which the step executor cannot replay (clskd.graph)
+    w = w.contiguous()
+    if not w.is_cuda or w.numel() == 0:
+        return w.clone(memory_format=torch.contiguous_format)
+    out = torch.empty(w.shape, dtype=torch.float32, device=w.device)
+    check(lib().clskd_axpy_f32(ptr(w), ptr(out), w.numel(), 1.0, 0, _stream()), "pack_weight copy")
+    return out
 
 
 def _dt(t):

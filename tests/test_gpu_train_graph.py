@@ -1,5 +1,6 @@
-"""Configuration C3 as a captured step (clskd.graph.TrainStepGraph): the training step — fwd+loss
-with the tape, HIP backward, Adam — recorded once and replayed by hipGraphLaunch must
+"""Configuration C3 as a captured step (clskd.graph.TrainStepExecutor / TrainStepGraph): the
+training step — fwd+loss with the tape, HIP backward, Adam — recorded once and replayed by the C++
+step executor or hipGraphLaunch must
 be the same computation as eager ``train_step`` calls: loss, every parameter, Adam's moments and
 step count bitwise equal after each of three steps on different batches (same kernels, same
 arguments, deterministic reductions).  Plus the device-step Adam kernel against the host-step
@@ -39,11 +40,13 @@ def test_adam_device_step_matches_host_step_and_torch():
     assert torch.equal(m_d, m_h) and torch.equal(v_d, v_h)
 
 
+@pytest.mark.parametrize("launch", ["exec", "graph"])
 @pytest.mark.parametrize("precision", ["mixed", "fp32"])
-def test_train_graph_matches_eager_train_steps(precision):
-    """TrainStepGraph (hipGraphLaunch replay of the captured training step) vs eager."""
+def test_train_graph_matches_eager_train_steps(precision, launch):
+    """TrainStepExecutor (the C++ step executor) / TrainStepGraph (hipGraphLaunch) replays of the
+    captured training step vs eager."""
     from clskd.data import synthetic_pairs
-    from clskd.graph import TrainStepGraph
+    from clskd.graph import TrainStepExecutor, TrainStepGraph
     from clskd.train import FlatAdam, FlatParams
     from test_gpu_parity import _kd
     batches = []
@@ -57,8 +60,10 @@ def test_train_graph_matches_eager_train_steps(precision):
         runs.append((flat, FlatAdam(flat, lr=6e-4, device_step=True)))
     (fe, oe), (fg, og) = runs
     assert torch.equal(fe.data, fg.data)
-    ex = TrainStepGraph(kd_g, fg, og, *batches[0])
+    ex = (TrainStepExecutor if launch == "exec" else TrainStepGraph)(kd_g, fg, og, *batches[0])
     assert og.step_count == 0 and torch.equal(fe.data, fg.data)  # warm-up state restored
+    if launch == "exec":
+        assert ex.info["memcpys"] == 0 and ex.info["kernels"] > 500, ex.info
     for i, (X, y) in enumerate(batches):
         le = kd_e.train_step((X, y), fe, oe)
         lg = ex(X, y)
