@@ -367,7 +367,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--abf-reinit", default="step", choices=["step", "once"])
     ap.add_argument("--launch", default=None, choices=["exec", "eager", "graph"],
-                    help="default: eager for C2 / C4, exec for C3 (--train) on one GPU.  "
+                    help="default: eager.  C3 (--train) also takes exec / graph (the captured "
+                         "training step, clskd.graph.TrainStepExecutor / TrainStepGraph).  "
                          "eager: launch the four-stream schedule from Python every "
                          "step (host enqueue ~4.1 ms under a ~5.6 ms device step: device-bound); "
                          "exec: capture the step once and replay it with the library's C++ "
@@ -424,9 +425,10 @@ def main():
     if args.spkd and args.train:
         raise SystemExit("--spkd is its own leg (no --train)")
     if args.launch is None:
-        # C3 on one GPU: the captured training step replayed by the C++ executor (its eager host
-        # path issues ~1,000 launches per step); C2 / C4: eager
-        args.launch = "exec" if (args.train and world == 1) else "eager"
+        # eager everywhere: the C3 step is device-bound (~20 ms of device work; its captured
+        # replays measured 23.5 ms with the C++ executor and 24.6 ms with hipGraphLaunch against
+        # 20.6 ms eager, gpurun_out r4p / DESIGN.md section 13)
+        args.launch = "eager"
     if args.spkd or world > 1:
         # the C4 leg launches eagerly (its capture is not wired yet); multi-rank runs launch
         # eagerly too (no graph capture beside the RCCL communicator's watchdog)
