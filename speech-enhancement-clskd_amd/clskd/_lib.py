@@ -252,6 +252,21 @@ def set_knob(name, value):
     return prev.value
 
 
+_GRID_KNOB = b"CLSKD_G8_GRID"
+
+
+def set_g8_grid(value):
+    """conv_gemm8's persistent-grid cap (CLSKD_G8_GRID; 0 = every CU).  It changes how tiles are
+    dealt to workgroups at launch, never which kernel runs or what it computes, so unlike
+    set_knob it leaves the cached dispatch decisions valid.  Returns the previous value."""
+    lib = load(require_gpu=False)
+    prev = C.c_int32(0)
+    check(lib.clskd_get_knob(_GRID_KNOB, C.byref(prev)), "get_knob CLSKD_G8_GRID")
+    if prev.value != value:
+        check(lib.clskd_set_knob(_GRID_KNOB, int(value)), "set_knob CLSKD_G8_GRID")
+    return prev.value
+
+
 # capture-time stream tagging (clskd.graph.StepExecutor): a callable run after every library
 # call while a step is being captured
 TAG_HOOK = None

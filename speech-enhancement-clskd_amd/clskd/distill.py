@@ -47,6 +47,24 @@ def _mark(label, stream):
 # A/B switch: CLSKD_STUDENT_SPLIT=0 keeps the student of precision 'mixed' on the exact fp32 engines
 _STUDENT_SPLIT = os.environ.get("CLSKD_STUDENT_SPLIT", "1") == "1"
 _SERIAL = os.environ.get("CLSKD_SERIAL_STREAMS") == "1"  # diagnostic: the whole step on one stream
+# conv_gemm8's persistent grid inside the concurrent four-stream step: 7/8 of the CUs (224 of
+# 256), so the wide teacher / ReviewKD GEMMs leave a CU per XCD group to the other streams'
+# kernels instead of queueing them behind a full-chip grid (measured 5.31-5.32 vs 5.37-5.39 ms
+# per C2 step, interleaved on one box; tools/grid_ab.sh).  The tile deal changes, not the tiles
+# or their K order: results are bitwise the full grid's (tests/test_gpu_parity.py).  0 = every
+# CU; a serialized step (the census: isolated kernel times) and taped training forwards keep the
+# full grid.
+_STEP_G8_GRID_FRAC = float(os.environ.get("CLSKD_STEP_G8_GRID_FRAC", "0.875"))
+_NCU = {}
+
+
+def _step_g8_grid(dev):
+    if _STEP_G8_GRID_FRAC <= 0 or _STEP_G8_GRID_FRAC >= 1:
+        return 0
+    n = _NCU.get(dev.index)
+    if n is None:
+        n = _NCU[dev.index] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return max(8, int(n * _STEP_G8_GRID_FRAC) // 8 * 8)
 
 
 class serialized_streams:
@@ -279,6 +297,20 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     under graph capture, tapes or serialised streams."""
     if not (isinstance(teacher, DCCRN) and isinstance(student, DCCRN)):
         raise TypeError("clskd_step expects clskd.DCCRN teacher and student")
+    if _SERIAL or tape or not X.is_cuda:
+        return _clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y,
+                           reinit, tape, teacher_ahead)
+    from . import _lib
+    prev = _lib.set_g8_grid(_step_g8_grid(X.device))
+    try:
+        return _clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y,
+                           reinit, tape, teacher_ahead)
+    finally:
+        _lib.set_g8_grid(prev)
+
+
+def _clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y, reinit, tape,
+                teacher_ahead):
     X0, y0 = X, y
     X = X.float()
     if X.dim() == 3:

@@ -39,7 +39,7 @@ struct KnobDef {
 };
 // order = KnobId
 static const KnobDef kKnobs[KNOB_COUNT] = {
-    {"CLSKD_G8", 1, false},          {"CLSKD_G8_GRID", 0, false},     {"CLSKD_HALO_GRID", 0, false},
+    {"CLSKD_G8", 1, false},          {"CLSKD_G8_GRID", 0, true},      {"CLSKD_HALO_GRID", 0, false},
     {"CLSKD_LSTM_NKS", 4, false},    {"CLSKD_LSTM_NKS32", 1, true},   {"CLSKD_WGRAD_WG", 4096, false},
     {"CLSKD_NO_HALO", 0, false},     {"CLSKD_BF16_WAVES", 8, false},  {"CLSKD_BF16_STAGES", 3, false},
     {"CLSKD_BF16_TILE", 0, false},   {"CLSKD_NO_POINTWISE", 0, false},

@@ -172,7 +172,7 @@ def test_dispatch_knobs_and_experiment_guard_without_gpu():
     # experiment knobs (timing-only modes, A/B dispatch switches, grid caps): a product library
     # holds them at their defaults and refuses any other value (every remaining
     # knob is parity-tested or gone from the product)
-    for name in ("CLSKD_LSTM128_TDIV", "CLSKD_LSTM32_TDIV", "CLSKD_G8", "CLSKD_G8_GRID",
+    for name in ("CLSKD_LSTM128_TDIV", "CLSKD_LSTM32_TDIV", "CLSKD_G8", "CLSKD_HALO_GRID",
                  "CLSKD_NO_HALO", "CLSKD_BF16_DEBUG_MODE", "CLSKD_G8_KORDER", "CLSKD_EXEC_GATE"):
         assert lib.clskd_get_knob(name.encode(), ctypes.byref(v)) == 0
         dflt = v.value
@@ -180,6 +180,9 @@ def test_dispatch_knobs_and_experiment_guard_without_gpu():
         assert lib.clskd_set_knob(name.encode(), dflt + 2) == -4, name
         assert b"CLSKD_EXPERIMENTS" in lib.clskd_last_error(), name
         assert lib.clskd_get_knob(name.encode(), ctypes.byref(v)) == 0 and v.value == dflt
+    # CLSKD_G8_GRID is a product knob since round 4 (clskd_step's concurrent-step grid cap,
+    # tests/test_gpu_parity.py::test_step_g8_grid_cap_is_bitwise_neutral)
+    assert _lib.set_g8_grid(224) == 0 and _lib.set_g8_grid(0) == 224
     # the removed knobs are unknown
     for name in (b"CLSKD_DIRECT_COOP", b"CLSKD_EXEC_PRIO", b"CLSKD_EXEC_PACE_NS"):
         assert lib.clskd_set_knob(name, 1) == -4 and b"unknown knob" in lib.clskd_last_error()

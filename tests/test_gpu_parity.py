@@ -629,6 +629,34 @@ def _kd(abf_seed=ABF_SEED):
     return kd
 
 
+def test_step_g8_grid_cap_is_bitwise_neutral():
+    """clskd_step caps conv_gemm8's persistent grid at 7/8 of the CUs inside the concurrent
+    step (distill._STEP_G8_GRID_FRAC): only the deal of tiles to workgroups changes, so every
+    loss slot, the student waveform and the BatchNorm running statistics are bitwise those of
+    the full-grid step."""
+    from clskd import distill
+    from clskd.data import synthetic_pairs
+    n, c = synthetic_pairs(4, 32000, seed=41)
+    X, y = torch.from_numpy(n).to(DEV), torch.from_numpy(c).to(DEV)
+    outs = []
+    prev = distill._STEP_G8_GRID_FRAC
+    try:
+        for frac in (0.0, 0.875, 0.5):
+            distill._STEP_G8_GRID_FRAC = frac
+            kd = _kd().set_precision("mixed")
+            o = kd.training_step((X, y), 0, return_parts=True)
+            torch.cuda.synchronize()
+            outs.append((torch.cat([o["loss"].reshape(1), o["spkd"], o["base"].reshape(1)]),
+                         o["student_wav"].clone(),
+                         [b.clone() for nme, b in kd.named_buffers() if "running" in nme]))
+    finally:
+        distill._STEP_G8_GRID_FRAC = prev
+    for loss, wav, bufs in outs[1:]:
+        assert torch.equal(loss, outs[0][0])
+        assert torch.equal(wav, outs[0][1])
+        assert all(torch.equal(a, b) for a, b in zip(bufs, outs[0][2]))
+
+
 @pytest.mark.parametrize("precision", ["fp32", "mixed"])
 def test_teacher_ahead_matches_serial_schedule(precision):
     """clskd_step(teacher_ahead=True): the teacher chain of step i+1 overlapping step i's tail
