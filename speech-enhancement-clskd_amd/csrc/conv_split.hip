@@ -431,7 +431,9 @@ static bool split_plan(const clskd_conv_desc& d, SplitArgs& a, int& nt, int& bk,
   const size_t tab = (size_t)2 * 128 * (16 + 16 + 8);
   const size_t lds = (bk == 64 ? 1 : 2) * 2 * (size_t)(128 + 32 * nt) * bk * 2 + tab + (size_t)(d.K / 4) * 8;
   const int per_cu = lds * 3 <= 160 * 1024 ? 3 : lds * 2 <= 160 * 1024 ? 2 : 1;
-  const int cap = per_cu * ncu;
+  // CLSKD_SPLIT_GRID caps the CUs the grid spans (experiments build: A/B inside the concurrent step)
+  const int gcap = knob(KNOB_SPLIT_GRID);
+  const int cap = per_cu * (gcap > 0 && gcap < ncu ? gcap : ncu);
   grid = a.ntiles < cap ? a.ntiles : cap;
   if (d.stats && grid > a.nblk128) return false;  // (never: BM = 128 rows a tile)
   return true;
