@@ -358,6 +358,27 @@ def run_c5(args, dev):
     print(json.dumps(out))
 
 
+def spawn_cmd(n, argv, port):
+    """The launcher command of a standalone multi-GPU run: torch.distributed.run, one rank per
+    GPU of this node, rendezvous on 127.0.0.1, each rank running this file with the same args."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def spawn_ranks(n, argv):
+    """Start the ranks as a child process group (no exec: nothing here has initialised the GPU,
+    but a child keeps the launcher's exit code ours to return).  Returns the worst exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host driver
+    return subprocess.run(spawn_cmd(n, argv, port), env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -410,10 +431,16 @@ def main():
     from clskd import dist as cdist
     rank, world, local_rank = cdist.env_rank()
     if args.gpus > 1 and world == 1:
-        raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    cdist.init("nccl", dev)
+        # standalone `bench.py --gpus N`: start the N ranks (one process per GPU) before anything
+        # here touches the GPU, relay their output (rank 0 prints the JSON line), exit with the
+        # launcher's code (non-zero when any rank failed)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    # test-only overrides (tests/test_gpu_bench_ddp.py runs two ranks on the one GPU of a box):
+    # CLSKD_DIST_BACKEND=gloo, CLSKD_BENCH_DEVICE=<index> for every rank
+    dev_index = int(os.environ.get("CLSKD_BENCH_DEVICE", local_rank))
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    cdist.init(os.environ.get("CLSKD_DIST_BACKEND", "nccl"), dev)
 
     from clskd import ops
     from clskd.data import synthetic_pairs
@@ -589,6 +616,17 @@ def main():
         census, census_steps = ktimes, args.steps
     el = cdist.max_over_ranks(el, dev)
     loss_v = float(loss.item())
+    param_hashes = None
+    if args.train:
+        # data-parallel consistency of the benched training step: every rank's student
+        # parameters after the last Adam step, hashed (identical on every rank when the gradient
+        # all-reduce and the optimizer agree)
+        import hashlib
+        h = hashlib.sha256(flat.data.detach().cpu().numpy().tobytes()).hexdigest()[:16]
+        param_hashes = [h]
+        if world > 1:
+            param_hashes = [None] * world
+            torch.distributed.all_gather_object(param_hashes, h)
     quality = None
     if not args.train and not args.spkd and args.precision == "mixed":
         # quality gate of the metric ("SI-SNR parity ±0.01 dB"): the timed step's student
@@ -765,6 +803,7 @@ def main():
                        if args.precision == "mixed" else "fp32 MFMA everywhere"},
             "roofline": roof,
             "quality": quality,
+            "param_hash_per_rank": param_hashes,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

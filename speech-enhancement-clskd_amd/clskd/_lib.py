@@ -240,6 +240,11 @@ def load(require_gpu=True):
 KNOB_EPOCH = 0
 
 
+def experiments():
+    """Whether the loaded library is the timing-experiments build (CLSKD_LIB=exp)."""
+    return bool(load(require_gpu=False).clskd_experiments_build())
+
+
 def set_knob(name, value):
     """Switch a dispatch knob of the loaded library (include/clskd.h: read from the environment
     once, then only through this call).  Returns the previous value."""

@@ -466,11 +466,14 @@ def _clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, 
                              if _MARKS is not None else None)
             _mark("teacher: done", tstream)
             if fused:
-                assert len(tg) == 11 and "g" in dg, len(tg)
+                # taps in run order: the nl encoder outputs, then the first nl - 1 decoder
+                # outputs (the last decoder layer is dead for the loss); any teacher depth
+                nl = len(teacher.kernel_num) - 1
+                assert len(tg) == 2 * nl - 1 and "g" in dg, (len(tg), nl)
                 d = dg["g"]
-                g_te = _SlabRefs([g.refs[0] for g in tg[:6]], tg[:6])
-                g_td = _SlabRefs([d.refs[0]] + [g.refs[0] for g in tg[6:]] + d.refs[1:],
-                                 (d, tg[6:]))
+                g_te = _SlabRefs([g.refs[0] for g in tg[:nl]], tg[:nl])
+                g_td = _SlabRefs([d.refs[0]] + [g.refs[0] for g in tg[nl:]] + d.refs[1:],
+                                 (d, tg[nl:]))
             else:  # eval-mode teacher: BatchNorm applied in place, Gram passes of their own
                 g_te = ops.GramSlabs([_gram_bftc(a) for a in tf["enc"]], B)
                 t_dec = [tf["dec_in"]] + tf["dec"][:5]

@@ -241,6 +241,14 @@ class TrainStepGraph(StepGraph):
     def _run(self):
         return self.kd.train_step((self.X, self.y), self.flat, self.opt)
 
+    def _replay(self):
+        super()._replay()
+        # the replay's Adam rewrote the parameters on the device: advance their version counters
+        # (as FlatAdam.step does eagerly) so caches keyed on (data_ptr, _version) — the student's
+        # packed weights, DCCRN._packed — rebuild on the next eager forward instead of serving
+        # weights packed before this replay
+        self.flat.bump_versions()
+
     def _capture(self):
         self._release()
         dev = self.X.device

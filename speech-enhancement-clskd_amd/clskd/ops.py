@@ -425,6 +425,20 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
         d.stats = stats.data_ptr() + 8 * stats_offset
     else:
         d.stats = None
+    if fold is not None:
+        try:
+            _launch_conv(L, d, pl)
+        except Exception:
+            # an earlier launch of this BatchNorm may already have added into the fold state:
+            # return it to zero so later steps do not inherit a dirty accumulator
+            bn_stats[0].abort()
+            raise
+    else:
+        _launch_conv(L, d, pl)
+    return out
+
+
+def _launch_conv(L, d, pl):
     if KernelTimer.active and not torch.cuda.is_current_stream_capturing() \
             and KernelTimer.wants(pl.name):
         e0 = torch.cuda.Event(enable_timing=True)
@@ -445,7 +459,6 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
         if pl.name is None:
             pl.name = L.clskd_conv_last_kernel().decode()
             pl.fn = L.clskd_conv_last_kernel_fn()
-    return out
 
 
 def conv_kernel_of_last_launch():
@@ -567,6 +580,15 @@ class BnStats:
         self.used += nblk
         assert self.used <= self.nblk, "BnStats: more partial blocks than rows / 128"
         return self.part, off
+
+    def abort(self):
+        """A launch of this BatchNorm failed: zero its fold accumulators and ticket (stream-
+        ordered), which only the finalizing launch would otherwise return to zero."""
+        states = self.bn.__dict__.get("_clskd_fold", {})
+        st = states.get((torch.device(self.dev).index, self.C))
+        if st is not None:
+            st[0].zero_()
+            st[1].zero_()
 
     def launched(self, fold):
         mode = "fold" if fold else "part"

@@ -104,6 +104,15 @@ __device__ __forceinline__ void bnfold_commit(const BnFoldArgs& f, int N, SQ sq,
   if (!f.finalize) return;  // uniform: an earlier launch of the layer only contributes
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics are performed
   __syncthreads();
+  // Ordering without an agent release/acquire: every access to the replicas and to the ticket is
+  // an 8-/4-B agent-scope atomic, performed at the memory side ("agent atomics both sides",
+  // MI355X_MICROARCH.md §Workgroup dispatch, Valid forms), and a no-return atomic stays counted
+  // in vmcnt until it is performed (§Global float atomics), so the vmcnt(0) + barrier above put
+  // every limb add of this workgroup before its ticket add.  An acq_rel ticket would lower to
+  // buffer_wbl2 sc1 + buffer_inv sc1 per workgroup — a write-back of the XCD L2 right after the
+  // conv's output tiles were stored (redraw: a 4 % step regression measured for a
+  // fence per workgroup) — and guard no non-atomic hand-off: the coefficients the last arriver
+  // writes are read by later kernels only (kernel boundary).
   if (tid == 0) {
     const unsigned t = __hip_atomic_fetch_add(f.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *flag = t == (unsigned)(nwg - 1);

@@ -50,7 +50,7 @@ static const KnobDef kKnobs[KNOB_COUNT] = {
     {"CLSKD_F32_SPLIT", 0, true},
     {"CLSKD_LSTM_PRIO", 0, true},
     {"CLSKD_SPLIT_BK", 0, true},
-    {"CLSKD_HALOW", 0, true},
+    {"CLSKD_HALOW", 0, false},
     {"CLSKD_SPLIT_GRID", 0, false},
     {"CLSKD_LSTM128_TDIV", 0, false},
     {"CLSKD_LSTM32_TDIV", 0, false}, {"CLSKD_BF16_DEBUG_MODE", 0, false}, {"CLSKD_SKIP", 0, false},

@@ -457,7 +457,9 @@ static int launch_big(const clskd_conv_desc& d, hipStream_t st) { return launch_
 // 4-wave tiles everywhere (A/B measurements).
 int launch_conv_halo(const clskd_conv_desc& d, hipStream_t st, bool* launched);
 int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched);
+#ifdef CLSKD_EXPERIMENTS
 int launch_conv_halow(const clskd_conv_desc& d, hipStream_t st, bool* launched);
+#endif
 
 int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
   const bool no_halo = knob(KNOB_NO_HALO) == 1;  // A/B switch: 1 keeps narrow layers on the engine
@@ -471,11 +473,13 @@ int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
     const int rc = experiment_guard("CLSKD_BF16_DEBUG_MODE", dbg);
     if (rc != CLSKD_OK) return rc;
   }
+#ifdef CLSKD_EXPERIMENTS
   if (dbg == 0 && knob(KNOB_G8) < 10) {  // the wide layers: halo tiles with streamed weights
     bool launched = false;
     const int rc = launch_conv_halow(d, st, &launched);
     if (rc != CLSKD_OK || launched) return rc;
   }
+#endif
   if (dbg == 0) {
     bool launched = false;
     const int rc = launch_conv_gemm8(d, st, &launched);

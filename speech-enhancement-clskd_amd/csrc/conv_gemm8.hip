@@ -617,6 +617,10 @@ template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DB
 static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   using namespace g8;
   constexpr int SB = (BM + BN) * 2 * BK;
+  if (d.bn_fold && d.N > BN) {  // the fold epilogue keeps one channel per tile column
+    set_error("conv2d(bf16 g8): folded BatchNorm needs N=%d <= the %d-column tile", d.N, BN);
+    return CLSKD_E_ARG;
+  }
   const size_t lds = NS * (size_t)SB + 2 * sizeof(RowTable<BM>) + (size_t)((d.N + 3) & ~3) * 4 +
                      (size_t)(d.K / 8) * 8;
   if (lds > 160 * 1024) {

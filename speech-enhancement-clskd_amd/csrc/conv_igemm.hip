@@ -346,7 +346,9 @@ namespace clskd {
 bool conv_halo_takes(const clskd_conv_desc& d);
 bool conv_halo_f32_takes(const clskd_conv_desc& d);
 bool conv_gemm8_takes(const clskd_conv_desc& d);
+#ifdef CLSKD_EXPERIMENTS
 bool conv_halow_takes(const clskd_conv_desc& d);
+#endif
 bool conv_pointwise_takes(const clskd_conv_desc& d);
 bool conv_split3_takes(const clskd_conv_desc& d, bool force);
 }  // namespace clskd
@@ -357,7 +359,9 @@ static bool fold_capable(const clskd_conv_desc& dd) {
   if (dd.wlayout == CLSKD_WLAYOUT_DIRECT || dd.accumulate) return false;
   if (is_lowp(dd.compute)) {
     if (conv_halo_takes(dd)) return true;
+#ifdef CLSKD_EXPERIMENTS
     if (conv_halow_takes(dd)) return true;
+#endif
     return conv_gemm8_takes(dd) && dd.N <= 256;  // one N-tile (256x256 / 256x128 instances)
   }
   const bool split = dd.compute == CLSKD_F32X3;

@@ -77,3 +77,40 @@ def test_train_graph_matches_eager_train_steps(precision, launch):
     # BatchNorm running statistics of the student (updated inside the replayed forward)
     for (k, a), b in zip(kd_e.student.state_dict().items(), kd_g.student.state_dict().values()):
         assert torch.equal(a, b), k
+
+
+@pytest.mark.parametrize("launch", ["exec", "graph"])
+def test_train_graph_replays_interleaved_with_eager_forwards(launch):
+    """Replay, eager eval forward, replay, eager eval forward: every eager forward of the trained
+    student must use the parameters the replays' Adam wrote (the packed-weight cache is keyed on
+    the parameters' version counters, which a replay bumps) — checked against a fresh copy of
+    the student (no caches) holding the same parameters."""
+    from clskd import config as cfg
+    from clskd.data import synthetic_pairs
+    from clskd.graph import TrainStepExecutor, TrainStepGraph
+    from clskd.model import DCCRN
+    from clskd.train import FlatAdam, FlatParams
+    from test_gpu_parity import _kd
+    n, c = synthetic_pairs(4, 16000, seed=41)
+    X, y = torch.from_numpy(n).to(DEV), torch.from_numpy(c).to(DEV)
+    xe = torch.from_numpy(synthetic_pairs(2, 16000, seed=42)[0]).to(DEV)
+    kd = _kd().set_precision("mixed")
+    flat = FlatParams(kd.student)
+    opt = FlatAdam(flat, lr=6e-4, device_step=True)
+    ex = (TrainStepExecutor if launch == "exec" else TrainStepGraph)(kd, flat, opt, X, y)
+    outs = []
+    for _ in range(2):
+        ex(X, y)
+        kd.student.eval()
+        with torch.no_grad():
+            got = kd.student(xe, is_feat=True).clone()
+            # a new student holding the same parameters and statistics: no packed-weight caches
+            fresh = DCCRN(masking_mode="E", use_clstm=True, **cfg.STUDENT).to(DEV)
+            fresh.load_state_dict(kd.student.state_dict())
+            fresh.compute = kd.student.compute
+            ref = fresh.eval()(xe, is_feat=True)
+        kd.student.train()
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref)
+        outs.append(got)
+    assert not torch.equal(outs[0], outs[1])  # the second replay changed the parameters

@@ -1,5 +1,6 @@
 """Host-side logic of the Python drop-in layer that needs no GPU: caches and bookkeeping."""
 import gc
+import os
 
 import torch
 
@@ -95,3 +96,19 @@ def test_train_graph_requires_device_step_optimizer():
         TrainStepGraph(None, flat, FlatAdam(flat), torch.zeros(1, 8), torch.zeros(1, 8))
     opt = FlatAdam(flat, device_step=True)
     assert opt.step_count == 0 and len(opt.state()) == 4
+
+
+def test_bench_standalone_multi_gpu_launch_command():
+    """`bench.py --gpus N` outside a launcher starts N ranks itself (torch.distributed.run as a
+    child, rendezvous on 127.0.0.1) with the same arguments."""
+    import importlib.util
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    cmd = bench.spawn_cmd(8, ["--gpus", "8", "--steps", "5"], 29512)
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert "--nproc-per-node=8" in cmd
+    i = cmd.index("--master-addr")
+    assert cmd[i + 1] == "127.0.0.1" and cmd[cmd.index("--master-port") + 1] == "29512"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "5"] and cmd[-5].endswith("bench.py")

@@ -1,0 +1,42 @@
+#!/bin/bash
+# Round-5 GPU call (from the repo root via gpurun).  STEPS selects what runs (space separated):
+#   suite   full GPU suite (+ the C3 gradient-parity table written to $O/c3_grad_parity.txt)
+#   bench   default C2 bench line;  train  C3 line;  spkd  C4 line;  c1 / c5
+#   trace   rocprofv3 kernel+marker trace of the bench command split at its roctx ranges
+#   pmc     FETCH_SIZE / WRITE_SIZE passes -> per-kernel HBM traffic
+#   tests:<pytest args>   a subset of the suite
+# Every GPU step has its own time limit; a failing step ends the call.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/${ITER:-r5}
+mkdir -p $O
+ok() { local rc=$1; if [ $rc -ne 0 ]; then echo "stop: rc=$rc ($2)"; exit $rc; fi; }
+T="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+for st in ${STEPS:-suite bench}; do
+  case $st in
+    suite)
+      rc=0; CLSKD_GRAD_PARITY_OUT=$O/c3_grad_parity.txt timeout -k 10 900 $T $R/tests -m gpu > $O/gpu_suite.log 2>&1 || rc=$?
+      tail -2 $O/gpu_suite.log; ok $rc suite;;
+    tests:*)
+      rc=0; timeout -k 10 600 $T -m gpu ${st#tests:} > $O/tests.log 2>&1 || rc=$?
+      tail -2 $O/tests.log; ok $rc tests;;
+    bench) rc=0; timeout -k 10 300 python $R/bench.py $BENCH_ARGS > $O/bench.log 2>&1 || rc=$?; ok $rc bench
+      grep '^{' $O/bench.log | cut -c1-400;;
+    train) rc=0; timeout -k 10 300 python $R/bench.py --train --no-cpu-baseline > $O/bench_train.log 2>&1 || rc=$?; ok $rc train
+      grep '^{' $O/bench_train.log | cut -c1-300;;
+    spkd) rc=0; timeout -k 10 300 python $R/bench.py --spkd --no-cpu-baseline > $O/bench_spkd.log 2>&1 || rc=$?; ok $rc spkd;;
+    c1) rc=0; timeout -k 10 300 python $R/bench.py --c1 > $O/bench_c1.log 2>&1 || rc=$?; ok $rc c1;;
+    c5) rc=0; timeout -k 10 300 python $R/bench.py --c5 > $O/bench_c5.log 2>&1 || rc=$?; ok $rc c5;;
+    trace)
+      ( cd /tmp && export TMPDIR=/tmp
+        rc=0; timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline $BENCH_ARGS > $O/trace.log 2>&1 || rc=$?; ok $rc trace ) || exit $?
+      python3 $R/tools/region_stats.py $O/trace/run 20 $O/region_stats.json > $O/region_stats.txt 2>&1 || true
+      grep '^{' $O/trace.log | cut -c1-300;;
+    pmc)
+      ( cd /tmp && export TMPDIR=/tmp
+        rc=0; timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/fetch.log 2>&1 || rc=$?; ok $rc fetch
+        rc=0; timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/write.log 2>&1 || rc=$?; ok $rc write ) || exit $?
+      python3 $R/tools/pmc_traffic.py $O/fetch/run_counter_collection.csv $O/write/run_counter_collection.csv $O/pmc_traffic.json > $O/traffic.txt;;
+    *) echo "unknown step $st"; exit 2;;
+  esac
+done
+echo r5-done
