@@ -56,6 +56,63 @@ __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_base) {
       : "memory");
 }
 
+// Tap-addressed pieces (TA): the buffer form of the LDS-DMA, four 1-KiB pieces per call.  Lane l
+// copies 16 B from rsrc.base + voff[l] to m0 + 16*l (out-of-range offsets, >= num_records = 2^31,
+// read as zeros: masked taps and N-tail weight rows cost no address arithmetic).  Piece p lands at
+// lds_base + O0 + p * OS; m0 is saved and restored around the group (the compiler does not
+// track it).
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+constexpr unsigned TA_OOB = 0x80000000u;
+__device__ __forceinline__ i32x4 ta_rsrc(uint64_t base) {
+  i32x4 r;
+  r[0] = (int)(uint32_t)base;
+  r[1] = (int)((uint32_t)(base >> 32) & 0xFFFFu);  // stride 0: raw buffer
+  r[2] = (int)TA_OOB;                               // num_records (bytes)
+  r[3] = 0x00020000;                                // gfx9 data format: 32 bits
+  return r;
+}
+template <int O0, int OS>
+__device__ __forceinline__ void bdma4(unsigned v0, unsigned v1, unsigned v2, unsigned v3, i32x4 rs,
+                                      unsigned lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_add_u32 m0, %1, %7\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %3, %2, 0 offen lds\n\t"
+      "s_add_u32 m0, %1, %8\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %4, %2, 0 offen lds\n\t"
+      "s_add_u32 m0, %1, %9\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %5, %2, 0 offen lds\n\t"
+      "s_add_u32 m0, %1, %10\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %6, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds_base), "s"(rs), "v"(v0), "v"(v1), "v"(v2), "v"(v3), "n"(O0), "n"(O0 + OS),
+        "n"(O0 + 2 * OS), "n"(O0 + 3 * OS)
+      : "memory");
+}
+
+template <int O0, int OS>
+__device__ __forceinline__ void bdma2(unsigned v0, unsigned v1, i32x4 rs, unsigned lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_add_u32 m0, %1, %5\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %3, %2, 0 offen lds\n\t"
+      "s_add_u32 m0, %1, %6\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %4, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds_base), "s"(rs), "v"(v0), "v"(v1), "n"(O0), "n"(O0 + OS)
+      : "memory");
+}
+
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
@@ -91,6 +148,7 @@ struct RowTable {
   int4 info[BM];     // fi0, ti0, valid, -
   int base[4][BM];   // per-segment element offset of the row
   int64_t orow[BM];  // output element offset (-1: past M)
+  unsigned inv[BM];  // TA: bit t * nseg + s set when tap t of segment s reads outside the input
 };
 
 }  // namespace g8
@@ -111,8 +169,12 @@ struct ConvArgsG8 {
 // 3 = neither, 4 = B operand only (no A gather), 5 = A operand only.  Correct-result variants:
 // 6 = s_setprio 1 around each substep's MFMA cluster, 7 = static priority 1 for waves 4-7, 8 = both;
 // 9 = no DMA wait inside the stream (timing only: DMA latency vs issue cost).
+// TA = 1 (tap-addressed pieces, round 5): for tap-structured layers (K = ntaps x ctot, every
+// K-tile inside one tap and segment) each piece's source is a per-(tile, piece) lane offset plus
+// a per-K-tile buffer base (kinfo table, uniform), with a per-row tap-validity mask instead of
+// per-piece 64-bit bounds arithmetic: ~12 VALU per K-tile instead of ~120.
 template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8,
-          int EB = 0, typename InT = __bf16, int PP = 0>
+          int EB = 0, typename InT = __bf16, int PP = 0, int TA = 0>
 __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 args) {
   using namespace g8;
   const clskd_conv_desc& d = args.d;
@@ -133,12 +195,15 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
   static_assert((BM / RPP) % NW == 0 && (BN / RPP) % NW == 0 && NGA >= 1, "DMA piece split");
   static_assert(PHI >= 1 && PHI <= NSUB && NSUB % 2 == 0, "issue substeps");
   static_assert(NS >= 2 && WM * BN * 16 <= SB, "statistics scratch fits one stage");
+  static_assert(!TA || (BK == 64 && NGA == 4 && (NGB == 4 || NGB == 2) && PHI == 2 && PP == 0 && DBG == 0),
+                "tap-addressed pieces: 256-row tiles, two issue substeps");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* stages = smem;
   RowTable<BM>* tabs = reinterpret_cast<RowTable<BM>*>(smem + NS * SB);  // [2]
   float* bias_l = reinterpret_cast<float*>(tabs + 2);                    // [N]
   int2* ctab = reinterpret_cast<int2*>(bias_l + ((d.N + 3) & ~3));       // [K/8]
+  int4* kinfo = reinterpret_cast<int4*>(ctab);  // TA: [K/BK] {A base lo, hi, mask bit, -}
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -189,15 +254,44 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
       for (int s = 0; s < 4; ++s)
         tb.base[s][tid] = (int)(bb * d.seg[s].sB + (int64_t)fi0 * d.seg[s].sF + (int64_t)ti0 * d.seg[s].sT);
       tb.orow[tid] = valid ? bb * d.oB + (int64_t)(fo * d.of_mul + d.of_add) * d.oF + (int64_t)to * d.oT : -1;
+      if constexpr (TA) {
+        unsigned m = 0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          if (t < d.ntaps) {
+#pragma unroll
+            for (int sg = 0; sg < 2; ++sg) {
+              if (sg < d.nseg) {
+                const int fi = fi0 + d.tap_df[t], ti = ti0 + d.tap_dt[t];
+                const bool ok = valid && (unsigned)fi < (unsigned)d.seg[sg].F && (unsigned)ti < (unsigned)d.seg[sg].T;
+                m |= (ok ? 0u : 1u) << (t * d.nseg + sg);
+              }
+            }
+          }
+        }
+        tb.inv[tid] = m;
+      }
     }
   };
 
   // ---- layer tables: K-chunk entries, bias; row tables of the first two tiles ---------------
-  for (int q = tid; q < d.K / 8; q += NT) {
-    const clskd_ktab_entry e = d.ktab[q * 8];
-    const int s = d.kseg[q * 8];
-    ctab[q] = make_int2(e.off, (int)(((unsigned)e.dF & 0xFFFFu) | (((unsigned)e.dT & 0xFFu) << 16) |
-                                     ((unsigned)s << 24)));
+  if constexpr (TA) {
+    // per packed K-tile: the A buffer base (segment pointer + the K-tile's first entry's element
+    // offset: tap displacement + channel) and the row-mask bit of its (tap, segment)
+    for (int q = tid; q < nk; q += NT) {
+      const clskd_ktab_entry e = d.ktab[q * BK];
+      const int s = d.kseg[q * BK];
+      const int t = (q * BK) / d.ctot;
+      const uint64_t a = (uint64_t)(uintptr_t)(s ? d.seg[1].ptr : d.seg[0].ptr) + (uint64_t)(int64_t)e.off * 2u;
+      kinfo[q] = make_int4((int)(uint32_t)a, (int)(uint32_t)(a >> 32), t * d.nseg + s, s);
+    }
+  } else {
+    for (int q = tid; q < d.K / 8; q += NT) {
+      const clskd_ktab_entry e = d.ktab[q * 8];
+      const int s = d.kseg[q * 8];
+      ctab[q] = make_int2(e.off, (int)(((unsigned)e.dF & 0xFFFFu) | (((unsigned)e.dT & 0xFFu) << 16) |
+                                       ((unsigned)s << 24)));
+    }
   }
   for (int n = tid; n < d.N; n += NT) bias_l[n] = d.bias ? d.bias[n] : 0.f;
   build_table(0, 0);
@@ -215,9 +309,28 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
   const int prow = lane / CPR;
   int a_ft[NGA], a_rb0[NGA], a_rb1[NGA];
   int b_n0 = 0, geo_tile = -1;
+  // TA: per piece the row's tap-invalid mask and byte offsets (chunk swizzle folded in) into
+  // each segment; the weight rows' byte offsets (out of range past N)
+  unsigned a_inv[NGA], a_vb0[NGA], a_vb1[NGA], b_vo[NGB];  // dead unless TA
   const unsigned short* wgt = reinterpret_cast<const unsigned short*>(d.weight);
   auto load_geometry = [&](int j) {
     const RowTable<BM>& tb = tabs[j & 1];
+    if constexpr (TA) {
+#pragma unroll
+      for (int i = 0; i < NGA; ++i) {
+        const int r = (i * NW + wave) * RPP + prow;
+        a_inv[i] = tb.inv[r];
+        a_vb0[i] = (unsigned)tb.base[0][r] * 2u + (unsigned)csrc * 16u;
+        a_vb1[i] = (unsigned)tb.base[1][r] * 2u + (unsigned)csrc * 16u;
+      }
+#pragma unroll
+      for (int i = 0; i < NGB; ++i) {
+        const int n = tile_nt(j) * BN + (i * NW + wave) * RPP + prow;
+        b_vo[i] = n < d.N ? ((unsigned)n * (unsigned)d.K + (unsigned)csrc * 8u) * 2u : TA_OOB;
+      }
+      geo_tile = j;
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NGA; ++i) {
       const int r = (i * NW + wave) * RPP + prow;
@@ -326,21 +439,66 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
   // are still in L2; the packed tap-major order came back to a row only after kt_cpt K-tiles.
   const int kt_taps = args.kt_taps, kt_cpt = args.kt_cpt;
   int it_tap = 0, it_cb = 0;
+  int it_tile = 0, kt_tile = 0;  // tile of the K-tile next_kt() returned (no division per K-tile)
   auto next_kt = [&]() {
     const int k = it_tap * kt_cpt + it_cb;
+    kt_tile = it_tile;
     if (++it_tap == kt_taps) {
       it_tap = 0;
-      if (++it_cb == kt_cpt) it_cb = 0;
+      if (++it_cb == kt_cpt) {
+        it_cb = 0;
+        ++it_tile;
+      }
     }
     return k;
   };
   // issue every piece of stream K-tile w into its stage (geometry moved to its tile first)
-  auto issue_all = [&](int w) {
-    const int jt = w / nk, kt = next_kt();
-    if (jt != geo_tile) load_geometry(jt);
-    const KEnt e = kdecode(ctab[kt * CPR + csrc]);
+  // TA: the uniform per-K-tile state (A / B buffer resources, mask bit, segment)
+  struct TaK {
+    i32x4 ra, rb;
+    unsigned bit;
+    bool s1;
+  };
+  auto ta_k = [&](int kt) -> TaK {
+    const int4 ki = kinfo[kt];
+    const unsigned lo = __builtin_amdgcn_readfirstlane(ki.x), hi = __builtin_amdgcn_readfirstlane(ki.y);
+    const unsigned bit = __builtin_amdgcn_readfirstlane(ki.z);
+    const unsigned s1 = __builtin_amdgcn_readfirstlane(ki.w);
+    TaK t;
+    t.ra = ta_rsrc(((uint64_t)hi << 32) | lo);
+    t.rb = ta_rsrc((uint64_t)(uintptr_t)wgt + (uint64_t)kt * (BK * 2));
+    t.bit = bit;
+    t.s1 = s1 != 0;
+    return t;
+  };
+  // TA: pieces of part p (0: the four A pieces, 1: the four B pieces) into stage sn
+  auto ta_issue = [&](int part, const TaK& k, int sn) {
+    const unsigned sl = stage_lds0 + sn * SB + wave * 1024;
+    if (part == 0) {
+      unsigned v[NGA];
 #pragma unroll
-    for (int g = 0; g < G; ++g) glds16((const void*)piece_src(g, kt, e), dst(g, w % NS));
+      for (int i = 0; i < NGA; ++i)
+        v[i] = (k.s1 ? a_vb1[i] : a_vb0[i]) | (((a_inv[i] >> k.bit) & 1u) << 31);
+      bdma4<0, NW * 1024>(v[0], v[1], v[2], v[3], k.ra, sl);
+    } else {
+      if constexpr (NGB == 4)
+        bdma4<BM * ROWB, NW * 1024>(b_vo[0], b_vo[1], b_vo[2 % NGB], b_vo[3 % NGB], k.rb, sl);
+      else
+        bdma2<BM * ROWB, NW * 1024>(b_vo[0], b_vo[1 % NGB], k.rb, sl);
+    }
+  };
+  auto issue_all = [&](int w) {
+    const int kt = next_kt(), jt = kt_tile;
+    if (jt != geo_tile) load_geometry(jt);
+    if constexpr (TA) {
+      const TaK k = ta_k(kt);
+      ta_issue(0, k, w % NS);
+      ta_issue(1, k, w % NS);
+    } else {
+      const KEnt e = kdecode(ctab[kt * CPR + csrc]);
+#pragma unroll
+      for (int g = 0; g < G; ++g) glds16((const void*)piece_src(g, kt, e), dst(g, w % NS));
+    }
   };
   if (DBG != 1 && DBG != 3) {
 #pragma unroll
@@ -414,14 +572,22 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
       const bool do_issue = wi < total && DBG != 1 && DBG != 3;
       int kti = 0;
       KEnt e{};
+      TaK tk{};
       if (do_issue) {
-        const int jt = wi / nk;
         kti = next_kt();
+        const int jt = kt_tile;
         if (jt != geo_tile) load_geometry(jt);
-        e = kdecode(ctab[kti * CPR + csrc]);
+        if constexpr (TA)
+          tk = ta_k(kti);
+        else
+          e = kdecode(ctab[kti * CPR + csrc]);
       }
       const int sn = wi % NS;
       auto issue = [&](int part) {
+        if constexpr (TA) {
+          if (part < PHI && do_issue) ta_issue(part, tk, sn);
+          return;
+        }
         if (part < PHI && do_issue) {
 #pragma unroll
           for (int g = part * GP; g < (part + 1) * GP && g < G; ++g) {
@@ -613,7 +779,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
 }
 
 template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8,
-          int EB = 0, typename InT = __bf16, int PP = 0>
+          int EB = 0, typename InT = __bf16, int PP = 0, int TA = 0>
 static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   using namespace g8;
   constexpr int SB = (BM + BN) * 2 * BK;
@@ -627,7 +793,7 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
     set_error("conv2d(bf16 g8): K=%d N=%d needs %zu B of LDS", d.K, d.N, lds);
     return CLSKD_E_SHAPE;
   }
-  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG, PF, NWV, EB, InT, PP>;
+  auto kern = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG, PF, NWV, EB, InT, PP, TA>;
   static bool attr_set = false;  // per instantiation
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -656,12 +822,29 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NWV * 64), lds, st, a);
   note_kernel_fn((const void*)kern);
   if constexpr (__is_same(InT, _Float16))
-    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d,f16%s>", BM, BN, WM, BK, NS, PHI,
-                type_name<OutT>(), DBG, PF, NWV, EB, PP ? ",pp" : "");
+    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d,f16%s%s>", BM, BN, WM, BK, NS, PHI,
+                type_name<OutT>(), DBG, PF, NWV, EB, PP ? ",pp" : "", TA ? ",ta" : "");
   else
-    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d%s>", BM, BN, WM, BK, NS, PHI,
-                type_name<OutT>(), DBG, PF, NWV, EB, PP ? ",bf16,pp" : "");
+    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d%s%s>", BM, BN, WM, BK, NS, PHI,
+                type_name<OutT>(), DBG, PF, NWV, EB, PP ? ",bf16,pp" : "", TA ? ",ta" : "");
   return CLSKD_OK;
+}
+
+// Tap-addressed pieces (TA) apply: a tap-structured K table whose every 64-deep K-tile lies
+// inside one tap and one segment, at most 32 (tap, segment) mask bits, and every row's / weight
+// row's byte offset below 2^31 (buffer offsets; 2^31 and above read as zeros).
+static bool g8_ta_ok(const clskd_conv_desc& d) {
+  if (knob(KNOB_G8_TA) == 0 || d.ntaps < 1 || d.ntaps > 16 || d.nseg < 1 || d.nseg > 2) return false;
+  if (d.ctot % 64 != 0 || (int64_t)d.ntaps * d.ctot != d.K) return false;
+  if (d.nseg == 2 && d.seg_c[0] % 64 != 0) return false;
+  for (int s = 0; s < d.nseg; ++s) {
+    const clskd_seg& g = d.seg[s];
+    if (g.sB < 0 || g.sF < 0 || g.sT < 0) return false;
+    const int64_t last = (int64_t)(d.B - 1) * g.sB + (int64_t)(d.Fo - 1) * d.stride_f * g.sF +
+                         (int64_t)(d.To - 1) * d.stride_t * g.sT + 64;
+    if (last * 2 >= ((int64_t)1 << 31) - 64) return false;
+  }
+  return (int64_t)d.N * d.K * 2 < ((int64_t)1 << 31) - 64;
 }
 
 // Entry from launch_conv_bf16 for N > 64 bf16 layers.  *launched = false leaves the layer to the
@@ -738,6 +921,13 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
   // default: BK 64, two stages, the K-tile boundary before the last substep (EB; 3-5 % on the
   // N = 256 layers against the boundary after it, CLSKD_G8=10)
   if (d.in_dtype == CLSKD_F16) {  // C4: IEEE-half operands (v_mfma_f32_32x32x16_f16)
+    if (g8_ta_ok(d)) {
+      if (d.N <= 128)
+        return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float, 0, 1, 8, 1, _Float16, 0, 1>(d, st)
+                   : launch_g8<256, 128, 4, 64, 2, 2, _Float16, 0, 1, 8, 1, _Float16, 0, 1>(d, st);
+      return f32 ? launch_g8<256, 256, 2, 64, 2, 2, float, 0, 1, 8, 1, _Float16, 0, 1>(d, st)
+                 : launch_g8<256, 256, 2, 64, 2, 2, _Float16, 0, 1, 8, 1, _Float16, 0, 1>(d, st);
+    }
     if (d.N <= 128)
       return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float, 0, 1, 8, 1, _Float16>(d, st)
                  : launch_g8<256, 128, 4, 64, 2, 2, _Float16, 0, 1, 8, 1, _Float16>(d, st);
@@ -755,6 +945,13 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
                : launch_g8<256, 256, 2, 64, 2, 2, __bf16, 0, 1, 8, 1, __bf16, 1>(d, st);
   }
 #endif
+  if (g8_ta_ok(d)) {
+    if (d.N <= 128)
+      return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float, 0, 1, 8, 1, __bf16, 0, 1>(d, st)
+                 : launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 1, 8, 1, __bf16, 0, 1>(d, st);
+    return f32 ? launch_g8<256, 256, 2, 64, 2, 2, float, 0, 1, 8, 1, __bf16, 0, 1>(d, st)
+               : launch_g8<256, 256, 2, 64, 2, 2, __bf16, 0, 1, 8, 1, __bf16, 0, 1>(d, st);
+  }
   if (d.N <= 128) {
     return f32 ? launch_g8<256, 128, 4, 64, 2, 2, float, 0, 1, 8, 1>(d, st)
                : launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 1, 8, 1>(d, st);

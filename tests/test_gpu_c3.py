@@ -19,8 +19,13 @@ per element); a student parameter's SPKD gradient crosses at most 2 x 6 such rou
 ReviewKD chain (forward activation + backward gradient per level), so its relative L2 error is
 of order u * sqrt(12) = 6.8e-3 from the ReviewKD chain, plus the relative change of M.  M is
 linear in the row-normalised Gram difference, whose relative error the loss-term check bounds
-at 5e-3.  REL_GRAD = 2e-2 covers the sum with a margin of ~2x for the worst parameter; the
-measured values are printed (tests/test_gpu_c3.py output) and recorded in DESIGN.md §9.
+at 5e-3.  That estimate (~1.2e-2 for the worst parameter) is an upper scale: measured on the
+MI355X (round 5, profiles/r5_c3_grad_parity.txt, every parameter listed) the worst relative L2
+error is 3.2e-3 (decoder.1.2.weight, a BatchNorm gain), the LSTM / projection parameters
+0.9-1.3e-3, the convolution weights <= 1e-3, and the loss 1.9e-5 relative.  The gates sit at
+about 2x the measured worst: REL_GRAD = 7e-3 (still below the u * sqrt(12) = 6.8e-3 + 5e-3
+derivation), REL_LOSS = 1e-4 (5x; the loss is a sum of 14 SPKD terms with independent bf16
+errors and the fp32 base loss).  Set CLSKD_GRAD_PARITY_OUT=<file> to record the table.
 """
 import os
 import socket
@@ -39,8 +44,8 @@ DEV = "cuda"
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 torch.set_num_threads(min(16, os.cpu_count() or 1))
 
-REL_GRAD = 2e-2
-REL_LOSS = 5e-3  # the total loss = base (fp32 path) + 14 SPKD terms (each <= 5e-3, test_gpu_c2_mixed)
+REL_GRAD = 7e-3  # measured worst 3.2e-3 (profiles/r5_c3_grad_parity.txt)
+REL_LOSS = 1e-4  # measured 1.9e-5; base (fp32 path) + 14 SPKD terms (each <= 5e-3, test_gpu_c2_mixed)
 
 
 def _rel(a, b):

@@ -1012,10 +1012,12 @@ G8_CASES = {
     "pw_k192_nk3_n256": ((192,), 256, [(0, 0)], 1, 9, 9, 1, 0, True),
     "enc5x2_fo4_n256": ((128,), 256, [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)], 2, 8, 4, 1, 0, True),
     "abf3x3_n200": ((64,), 200, [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], 1, 16, 16, 1, 0, False),
+    # K-tiles straddle taps (96 channels per tap): the per-chunk gather, never tap-addressed
+    "enc5x2_c96_n256": ((96,), 256, [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)], 2, 40, 20, 1, 0, True),
 }
 
 
-@pytest.mark.parametrize("engine", ["gemm8", "halow"])
+@pytest.mark.parametrize("engine", ["gemm8", "gemm8-noTA", "halow"])
 @pytest.mark.parametrize("lp", ["bf16", "fp16"])
 @pytest.mark.parametrize("case", sorted(G8_CASES))
 def test_conv_gemm8_against_torch(case, lp, engine, loop="phased"):
@@ -1067,6 +1069,7 @@ def test_conv_gemm8_against_torch(case, lp, engine, loop="phased"):
     st = torch.full((nblk * N * 2,), float("nan"), device=DEV, dtype=torch.float64)
     prev = _lib.set_knob("CLSKD_G8_PP", int(loop == "pingpong"))
     prev_hw = _lib.set_knob("CLSKD_HALOW", int(engine == "halow")) if _lib.experiments() else 0
+    prev_ta = _lib.set_knob("CLSKD_G8_TA", int(engine != "gemm8-noTA"))
     try:
         ops.conv([ops.seg_bftc(s.to(DEV)) for s in segs_h], taps, B, Fo, T, N, wp, bias.to(DEV),
                  out, ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add),
@@ -1076,9 +1079,15 @@ def test_conv_gemm8_against_torch(case, lp, engine, loop="phased"):
         _lib.set_knob("CLSKD_G8_PP", prev)
         if _lib.experiments():
             _lib.set_knob("CLSKD_HALOW", prev_hw)
-    prefix = "conv_gemm8" if engine == "gemm8" else "conv_halow"
-    assert kname.startswith(prefix) and (kname.endswith(",f16>") == (lp == "fp16")), kname
-    assert kname.endswith(",pp>") == (loop == "pingpong"), kname
+        _lib.set_knob("CLSKD_G8_TA", prev_ta)
+    prefix = "conv_halow" if engine == "halow" else "conv_gemm8"
+    assert kname.startswith(prefix) and ((",f16" in kname) == (lp == "fp16")), kname
+    assert (",pp" in kname) == (loop == "pingpong"), kname
+    # tap-addressed pieces: every 64-deep K-tile inside one tap and segment
+    ta = (engine == "gemm8" and loop != "pingpong" and sum(segc) % 64 == 0
+          and all(c % 64 == 0 for c in segc[:-1]))
+    if engine != "halow":
+        assert kname.endswith(",ta>") == ta, kname
     o = out.double().cpu()[:, of_add::of_mul]
     tol = _LP_TOL[lp] if out_bf16 else 1e-4
     np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=tol, atol=tol)

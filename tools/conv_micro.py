@@ -60,13 +60,44 @@ def make(kind, ci, co, fi, B=B, T=T, dev=None):
     return run, 2.0 * B * Fo * To * co * K, (B * Fo * To, co, K)
 
 
+def ab(a, dev, names):
+    """--ab KNOB=v1,v2: the knob's values interleaved over --rounds rounds in this one process
+    (cdna_hip_programming.md §5.4 rule 24); median and min per value."""
+    from clskd import _lib
+    knob, vals = a.ab.split("=")
+    vals = [int(v) for v in vals.split(",")]
+    for name in names:
+        run, fl, (M, N, K) = make(*CFGS[name], dev=dev)
+        res = {v: [] for v in vals}
+        for r in range(a.rounds):
+            for v in vals:
+                _lib.set_knob(knob, v)
+                for _ in range(2):
+                    run()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    run()
+                e1.record()
+                torch.cuda.synchronize()
+                res[v].append(e0.elapsed_time(e1) * 1e3 / a.iters)
+        line = " ".join(f"{knob}={v}: med {sorted(t)[len(t) // 2]:7.1f} min {min(t):7.1f} us "
+                        f"({fl / min(t) / 1e6:6.1f} TF/s)" for v, t in res.items())
+        print(f"{name:8s} M={M:7d} N={N:4d} K={K:5d}  {line}  [{ops.conv_kernel_of_last_launch()}]",
+              flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--only", default="")
+    ap.add_argument("--ab", default="", help="KNOB=v1,v2: interleaved A/B of a dispatch knob")
+    ap.add_argument("--rounds", type=int, default=5)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     names = [n for n in CFGS if not a.only or n in a.only.split(",")]
+    if a.ab:
+        return ab(a, dev, names)
     for name in names:
         run, fl, (M, N, K) = make(*CFGS[name], dev=dev)
         for _ in range(3):

@@ -36,6 +36,7 @@ for st in ${STEPS:-suite bench}; do
         rc=0; timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/fetch.log 2>&1 || rc=$?; ok $rc fetch
         rc=0; timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/write.log 2>&1 || rc=$?; ok $rc write ) || exit $?
       python3 $R/tools/pmc_traffic.py $O/fetch/run_counter_collection.csv $O/write/run_counter_collection.csv $O/pmc_traffic.json > $O/traffic.txt;;
+    micro) rc=0; timeout -k 10 300 python $R/tools/conv_micro.py $MICRO_ARGS > $O/micro.log 2>&1 || rc=$?; cat $O/micro.log; ok $rc micro;;
     *) echo "unknown step $st"; exit 2;;
   esac
 done
