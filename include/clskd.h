@@ -194,6 +194,15 @@ int clskd_conv2d_fwd(const clskd_conv_desc* d, void* stream);
 const char* clskd_conv_last_kernel(void);
 /* Host function (kernel stub address) of that kernel: the key clskd_exec_profile times by. */
 const void* clskd_conv_last_kernel_fn(void);
+/* 1 if that launch was a conv_gemm8 stream-K launch (round 5): the K-tile units of all tiles split
+ * evenly over the persistent grid, a tile shared by two workgroups finished by the later one
+ * (per-tile ticket, fp32 partial handed over write-through).  Deterministic for a fixed grid;
+ * CLSKD_G8_SK=0 keeps the data-parallel tile deal. */
+int32_t clskd_conv_last_stream_k(void);
+/* Allocate the stream-K workspace of `stream` (128 MiB partial slabs + tickets, zero at rest).
+ * Done implicitly by the first conv on a stream outside graph capture; hosts call it for a stream
+ * they are about to capture on, so captured and eager launches take the same path. */
+int clskd_stream_prepare(void* stream);
 /* Direct-path helpers: padded output width NP of the direct layout, and whether an (N, K)
  * GEMM is served by the direct kernel (returns 1) — hosts pack CLSKD_WLAYOUT_DIRECT weights
  * exactly when this is 1. */

@@ -105,6 +105,8 @@ SIGNATURES = {
     "clskd_last_error": (C.c_char_p, []),
     "clskd_conv_last_kernel": (C.c_char_p, []),
     "clskd_conv_last_kernel_fn": (_p, []),
+    "clskd_conv_last_stream_k": (_i32, []),
+    "clskd_stream_prepare": (_i32, [_p]),
     "clskd_version": (_i32, []),
     "clskd_set_knob": (_i32, [C.c_char_p, _i32]),
     "clskd_get_knob": (_i32, [C.c_char_p, C.POINTER(C.c_int32)]),

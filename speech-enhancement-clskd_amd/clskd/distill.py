@@ -95,7 +95,7 @@ def _side_stream(dev, which=0):
         return torch.cuda.current_stream(dev)
     key = (torch.device(dev).index, which)
     if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(device=dev)
+        _SIDE[key] = ops.prepare_stream(torch.cuda.Stream(device=dev))
     return _SIDE[key]
 
 

@@ -21,6 +21,7 @@ import os
 
 import torch
 
+from . import ops
 from .distill import KnowledgeDistillation
 
 
@@ -72,7 +73,7 @@ class StepGraph:
         # warm-up populates K tables and packed weights outside the graph; BN running statistics
         # are restored afterwards so capture leaves the model state as it found it
         saved = [b.clone() for b in _bn_buffers(self.kd)]
-        s = torch.cuda.Stream(device=dev)
+        s = ops.capture_stream(dev)  # prepared: warm-up and capture take the same conv paths
         s.wait_stream(cur)
         with torch.cuda.stream(s), torch.no_grad():
             for _ in range(self.warmup):
@@ -86,7 +87,7 @@ class StepGraph:
         g = torch.cuda.CUDAGraph(keep_graph=True) if self.keep_graph else torch.cuda.CUDAGraph()
         self._tagging(True)
         try:
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, stream=s):
                 self.out = self.kd.training_step((self.X, self.y), return_parts=True)
         finally:
             self._tagging(False)
@@ -260,7 +261,7 @@ class TrainStepGraph(StepGraph):
         # BatchNorm running statistics, the parameters, Adam's moments and step count
         state = _bn_buffers(self.kd) + self.opt.state()
         saved = [t.clone() for t in state]
-        s = torch.cuda.Stream(device=dev)
+        s = ops.capture_stream(dev)
         s.wait_stream(cur)
         with torch.cuda.stream(s):
             for _ in range(self.warmup):
@@ -276,7 +277,7 @@ class TrainStepGraph(StepGraph):
         student.repack_in_capture = True
         self._tagging(True)
         try:
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, stream=s):
                 self.out = dict(loss=self._run())
         finally:
             self._tagging(False)
@@ -311,7 +312,7 @@ class CapturedCall:
         self.inputs = [t.detach().clone() for t in inputs]
         dev = self.inputs[0].device
         cur = torch.cuda.current_stream(dev)
-        s = torch.cuda.Stream(device=dev)
+        s = ops.capture_stream(dev)
         s.wait_stream(cur)
         with torch.cuda.stream(s), torch.no_grad():
             for _ in range(warmup):
@@ -319,7 +320,7 @@ class CapturedCall:
         cur.wait_stream(s)
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph(keep_graph=True)
-        with torch.cuda.graph(self.graph), torch.no_grad():
+        with torch.cuda.graph(self.graph, stream=s), torch.no_grad():
             self.out = fn(*self.inputs)
         lib = _lib.load()
         h = C.c_void_p()

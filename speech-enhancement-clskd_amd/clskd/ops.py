@@ -461,6 +461,33 @@ def _launch_conv(L, d, pl):
             pl.fn = L.clskd_conv_last_kernel_fn()
 
 
+def prepare_stream(stream):
+    """Allocate the library's per-stream state (the conv_gemm8 stream-K workspace) for a torch
+    stream before a graph is captured on it: captured launches then take the same path as eager
+    ones (a stream without a workspace runs the data-parallel tile deal)."""
+    check(lib().clskd_stream_prepare(stream.cuda_stream), "stream_prepare")
+    return stream
+
+
+_CAPTURE_STREAMS = {}
+
+
+def capture_stream(device):
+    """One prepared stream per device for graph capture (torch.cuda.graph(..., stream=)) and the
+    capture's warm-up."""
+    idx = torch.device(device).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    s = _CAPTURE_STREAMS.get(idx)
+    if s is None:
+        s = _CAPTURE_STREAMS[idx] = prepare_stream(torch.cuda.Stream(device=idx))
+    return s
+
+
+def conv_last_stream_k():
+    """Whether this thread's last conv launch ran conv_gemm8's stream-K deal."""
+    return bool(lib().clskd_conv_last_stream_k())
+
+
 def conv_kernel_of_last_launch():
     """Kernel instance (rocprof name, 'base<args>') of this thread's last conv launch."""
     return lib().clskd_conv_last_kernel().decode()

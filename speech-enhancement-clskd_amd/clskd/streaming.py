@@ -228,7 +228,7 @@ class StreamingDCCRN:
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
         snap = self._snapshot()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, stream=ops.capture_stream(self.dev)):
             self._hop()
         self._restore(snap)   # capture only records: the hop counter must not advance
         self.graph = g

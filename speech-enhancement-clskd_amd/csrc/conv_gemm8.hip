@@ -29,6 +29,9 @@
 //    its L2.
 #include <stdlib.h>
 
+#include <mutex>
+#include <unordered_map>
+
 #include "bnfold.h"
 #include "common.h"
 
@@ -161,7 +164,20 @@ struct ConvArgsG8 {
   // tap count, kt_cpt = K-tiles per tap); kt_taps = 1, kt_cpt = K / 64 is the packed order.
   int kt_taps, kt_cpt;
   BnFoldArgs f;  // folded BatchNorm finalize (f.acc != nullptr; needs one N-tile: N <= BN)
+  // Stream-K (sk_cnt != nullptr): the ntiles x nk K-tile units are split into gridDim.x equal
+  // contiguous ranges; a tile whose units fall in two ranges (never more: ntiles >= grid) is
+  // finished by the workgroup that arrives second (per-tile ticket), which adds the other's
+  // fp32 partial (written through sc1 into its slot of sk_ws) — one commutative add, so the
+  // result does not depend on arrival order.  Tickets and ready flags are zero at rest.
+  float* sk_ws;        // [grid][2][BM * BN] partial accumulators, register order
+  unsigned* sk_ready;  // [grid][2]
+  unsigned* sk_cnt;    // [ntiles]
 };
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__device__ void sk_store4(f32x4v v, g8::i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4f32");
+__device__ f32x4v sk_load4(g8::i32x4 rsrc, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
+constexpr int SK_SC1 = 16;  // buffer cache-policy bits: sc1 (write-through / L1-bypassing, gfx950)
 
 // BM x BN tile, 8 waves as WM x WN, BK-deep K-tiles (64: 128-B LDS rows; 32: 64-B rows) in NS
 // LDS stages (NS - 1 K-tiles in flight), the DMA pieces of a K-tile issued over the first PHI
@@ -172,7 +188,9 @@ struct ConvArgsG8 {
 // TA = 1 (tap-addressed pieces, round 5): for tap-structured layers (K = ntaps x ctot, every
 // K-tile inside one tap and segment) each piece's source is a per-(tile, piece) lane offset plus
 // a per-K-tile buffer base (kinfo table, uniform), with a per-row tap-validity mask instead of
-// per-piece 64-bit bounds arithmetic: ~12 VALU per K-tile instead of ~120.
+// per-piece 64-bit bounds arithmetic: ~12 VALU per K-tile instead of ~120.  TA bit 1 (TA = 3):
+// the stream-K deal (ConvArgsG8::sk_cnt) compiled in; its bookkeeping costs registers, so only
+// the launches that split tiles run that instantiation.
 template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8,
           int EB = 0, typename InT = __bf16, int PP = 0, int TA = 0>
 __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 args) {
@@ -195,7 +213,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
   static_assert((BM / RPP) % NW == 0 && (BN / RPP) % NW == 0 && NGA >= 1, "DMA piece split");
   static_assert(PHI >= 1 && PHI <= NSUB && NSUB % 2 == 0, "issue substeps");
   static_assert(NS >= 2 && WM * BN * 16 <= SB, "statistics scratch fits one stage");
-  static_assert(!TA || (BK == 64 && NGA == 4 && (NGB == 4 || NGB == 2) && PHI == 2 && PP == 0 && DBG == 0),
+  static_assert(!(TA & 1) || (BK == 64 && NGA == 4 && (NGB == 4 || NGB == 2) && PHI == 2 && PP == 0 && DBG == 0),
                 "tap-addressed pieces: 256-row tiles, two issue substeps");
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -215,8 +233,24 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
 
   // ---- this workgroup's tile list (XCD-aware contiguous runs) ------------------------------
   const int grid = gridDim.x, b = blockIdx.x;
-  int t_first, t_step, ntl;
-  if ((grid & 7) == 0 && args.ntiles >= grid) {
+  int t_first = 0, t_step = 1, ntl;
+  const bool sk = (TA & 2) != 0 && PP == 0 && args.sk_cnt != nullptr;  // compile-time off unless TA bit 1
+  // stream-K: logical index (the workgroups of one XCD take consecutive ranges), the K-tile
+  // range [kb0, nk) of the first tile and [0, ke1) of the last
+  const int lidx = (grid & 7) == 0 ? (b & 7) * (grid >> 3) + (b >> 3) : b;
+  int kb0 = 0, ke1 = nk;
+  if (sk) {
+    const int64_t U = (int64_t)args.ntiles * nk;
+    const int64_t u0 = U * lidx / grid, u1 = U * (lidx + 1) / grid;
+    ntl = 0;
+    if (u1 > u0) {
+      t_first = (int)(u0 / nk);
+      kb0 = (int)(u0 - (int64_t)t_first * nk);
+      const int tl = (int)((u1 - 1) / nk);
+      ke1 = (int)(u1 - (int64_t)tl * nk);
+      ntl = tl - t_first + 1;
+    }
+  } else if ((grid & 7) == 0 && args.ntiles >= grid) {
     const int c = b & 7, s = b >> 3, cpx = grid >> 3;
     const int q = args.ntiles >> 3, r = args.ntiles & 7;
     const int len = q + (c < r ? 1 : 0), start = c * q + (c < r ? c : r);
@@ -254,7 +288,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
       for (int s = 0; s < 4; ++s)
         tb.base[s][tid] = (int)(bb * d.seg[s].sB + (int64_t)fi0 * d.seg[s].sF + (int64_t)ti0 * d.seg[s].sT);
       tb.orow[tid] = valid ? bb * d.oB + (int64_t)(fo * d.of_mul + d.of_add) * d.oF + (int64_t)to * d.oT : -1;
-      if constexpr (TA) {
+      if constexpr ((TA & 1) != 0) {
         unsigned m = 0;
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
@@ -275,7 +309,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
   };
 
   // ---- layer tables: K-chunk entries, bias; row tables of the first two tiles ---------------
-  if constexpr (TA) {
+  if constexpr ((TA & 1) != 0) {
     // per packed K-tile: the A buffer base (segment pointer + the K-tile's first entry's element
     // offset: tap displacement + channel) and the row-mask bit of its (tap, segment)
     for (int q = tid; q < nk; q += NT) {
@@ -315,7 +349,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
   const unsigned short* wgt = reinterpret_cast<const unsigned short*>(d.weight);
   auto load_geometry = [&](int j) {
     const RowTable<BM>& tb = tabs[j & 1];
-    if constexpr (TA) {
+    if constexpr ((TA & 1) != 0) {
 #pragma unroll
       for (int i = 0; i < NGA; ++i) {
         const int r = (i * NW + wave) * RPP + prow;
@@ -384,12 +418,15 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
 
   const int h = lane >> 5, l32 = lane & 31;
   f32x16 acc[FM][FN];
+  auto k_begin = [&](int j) { return j == 0 ? kb0 : 0; };  // K-tile range of tile j (stream-K)
+  auto k_end = [&](int j) { return j == ntl - 1 ? ke1 : nk; };
   auto init_acc = [&](int j) {
     const int nb = tile_nt(j) * BN;
+    const bool with_bias = k_begin(j) == 0;  // a split tile's bias is in its first piece only
 #pragma unroll
     for (int jj = 0; jj < FN; ++jj) {
       const int n = nb + wn * WC + jj * 32 + l32;
-      const float bv = n < d.N ? bias_l[n] : 0.f;
+      const float bv = (n < d.N && with_bias) ? bias_l[n] : 0.f;
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -432,13 +469,14 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
   };
 
   // ---- stream of K-tiles over the tile list: K-tile w belongs to tile w / nk ---------------------
-  const int total = ntl * nk;
+  int total = 0;
+  for (int j = 0; j < ntl; ++j) total += k_end(j) - k_begin(j);
   // packed K-tile of the next issued stream K-tile: the stream visits each tile's K-tiles
   // channel-block-major (tap q of block c = packed K-tile q * kt_cpt + c), so consecutive K-tiles
   // gather rows shifted by one tap — the rows the CU (and its XCD) fetched one K-tile earlier
   // are still in L2; the packed tap-major order came back to a row only after kt_cpt K-tiles.
   const int kt_taps = args.kt_taps, kt_cpt = args.kt_cpt;
-  int it_tap = 0, it_cb = 0;
+  int it_tap = kb0 % kt_taps, it_cb = kb0 / kt_taps;  // visit index kb0 (stream-K start)
   int it_tile = 0, kt_tile = 0;  // tile of the K-tile next_kt() returned (no division per K-tile)
   auto next_kt = [&]() {
     const int k = it_tap * kt_cpt + it_cb;
@@ -490,7 +528,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
   auto issue_all = [&](int w) {
     const int kt = next_kt(), jt = kt_tile;
     if (jt != geo_tile) load_geometry(jt);
-    if constexpr (TA) {
+    if constexpr ((TA & 1) != 0) {
       const TaK k = ta_k(kt);
       ta_issue(0, k, w % NS);
       ta_issue(1, k, w % NS);
@@ -565,7 +603,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
       }
       if (!lag) raw_barrier();  // re-align the groups: the epilogue runs in lockstep
     } else
-    for (int kt = 0; kt < nk; ++kt, ++gk) {
+    for (int kt = 0, nkj = k_end(j) - k_begin(j); kt < nkj; ++kt, ++gk) {
       const unsigned char* sa = stages + (gk % NS) * SB;
       // the K-tile issued during this one: stream gk + NS - 1
       const int wi = gk + NS - 1;
@@ -577,14 +615,14 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
         kti = next_kt();
         const int jt = kt_tile;
         if (jt != geo_tile) load_geometry(jt);
-        if constexpr (TA)
+        if constexpr ((TA & 1) != 0)
           tk = ta_k(kti);
         else
           e = kdecode(ctab[kti * CPR + csrc]);
       }
       const int sn = wi % NS;
       auto issue = [&](int part) {
-        if constexpr (TA) {
+        if constexpr ((TA & 1) != 0) {
           if (part < PHI && do_issue) ta_issue(part, tk, sn);
           return;
         }
@@ -608,7 +646,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
           g8::wait_vm<(NS - 2) * G>(min(NS - 2, total - 2 - gk) * G);
         }
         raw_barrier();
-        if (kt + 1 < nk) read_head(stages + ((gk + 1) % NS) * SB);
+        if (kt + 1 < nkj) read_head(stages + ((gk + 1) % NS) * SB);
       };
       // EB: the boundary sits before the last substep's MFMAs (its fragments are already in
       // registers), so the next K-tile's head reads return under those MFMAs instead of after
@@ -630,7 +668,86 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
     const RowTable<BM>& tb = tabs[j & 1];
     const int64_t m0 = (int64_t)tile_mt(j) * BM;
     const int n0 = tile_nt(j) * BN;
-    if (d.stats || fold) {  // fused BatchNorm statistics: one fp64 partial per 128 output rows
+    bool finish = true;
+    if (sk) {
+      // stream-K: a tile split between this range and a neighbouring one (lidx - 1 when this
+      // piece does not start at K-tile 0, else lidx + 1)
+      const bool split = k_begin(j) > 0 || k_end(j) < nk;
+      const int X = t_first + j;
+      const int other = k_begin(j) > 0 ? lidx - 1 : lidx + 1;
+      // slots: the piece at the start of a range (it does not begin at K-tile 0) uses slot 0, the
+      // piece at its end slot 1 (ranges are >= nk units long: never both in one tile)
+      const bool at_start = k_begin(j) > 0;
+      const int my_slot = lidx * 2 + (at_start ? 0 : 1);
+      const int o_slot = other * 2 + (at_start ? 1 : 0);
+      int* flag = reinterpret_cast<int*>(scratch);
+      bool last = true;
+      if (split) {
+        if (tid == 0) {
+          const unsigned t = __hip_atomic_fetch_add(args.sk_cnt + X, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *flag = t != 0;  // second arrival: finish the tile
+        }
+        raw_barrier();
+        last = *flag != 0;
+        raw_barrier();  // every wave has read the flag before the scratch stage is reused
+      }
+      const i32x4 wrs = ta_rsrc((uint64_t)(uintptr_t)args.sk_ws);
+      constexpr int SLAB = BM * BN * 4;
+      // a lane's 16-B chunk: lane * 16 (the only per-lane part) + a uniform (SGPR) offset
+      const int lvo = lane * 16;
+      auto soff = [&](int slot, int i, int jj, int q) {
+        return __builtin_amdgcn_readfirstlane(slot * SLAB + (((wave * FM + i) * FN + jj) * 4 + q) * 1024);
+      };
+      if (!last) {
+        // publish: write-through stores, every wave drained, then one ready flag
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              f32x4v v;
+              v[0] = acc[i][jj][4 * q];
+              v[1] = acc[i][jj][4 * q + 1];
+              v[2] = acc[i][jj][4 * q + 2];
+              v[3] = acc[i][jj][4 * q + 3];
+              sk_store4(v, wrs, lvo, soff(my_slot, i, jj, q), SK_SC1);
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        raw_barrier();
+        if (tid == 0) __hip_atomic_store(args.sk_ready + my_slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        finish = false;
+      } else if (split) {
+        // the other piece's ticket came first: its partial is published (or about to be: that
+        // workgroup is running and waits for nothing) — poll its flag, then sc1 loads
+        if (tid == 0) {
+          while (__hip_atomic_load(args.sk_ready + o_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+            __builtin_amdgcn_s_sleep(2);
+          __hip_atomic_store(args.sk_ready + o_slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(args.sk_cnt + X, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        raw_barrier();
+      }
+      // the add runs on every path (straight-line code: the accumulators stay in place): a tile
+      // finished here without a partial reads out-of-range offsets, i.e. zeros, and moves nothing
+      const int lsrc = (split && last) ? lvo : (int)TA_OOB;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+          for (int q = 0; q < 4; q += 2) {
+            const f32x4v v0 = sk_load4(wrs, lsrc, soff(o_slot, i, jj, q), SK_SC1);
+            const f32x4v v1 = sk_load4(wrs, lsrc, soff(o_slot, i, jj, q + 1), SK_SC1);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              acc[i][jj][4 * q + e] += v0[e];
+              acc[i][jj][4 * q + 4 + e] += v1[e];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+    }
+    if (finish && (d.stats || fold)) {  // fused BatchNorm statistics: one fp64 partial per 128 output rows
       constexpr int HALVES = BM / 128;
       constexpr int WPH = WM / HALVES;  // waves along M per 128-row half
       double* red = reinterpret_cast<double*>(scratch);  // [WM][BN][2]
@@ -707,7 +824,9 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
     static_assert(NW * UB <= SB, "epilogue staging");
     const bool vec = d.oNlo == 1 && d.nlo >= d.N && d.N % CH == 0 && (((uintptr_t)d.out) & 15) == 0 &&
                      d.oB % CH == 0 && d.oF % CH == 0 && d.oT % CH == 0;
-    if (vec) {
+    if (!finish) {
+      // the other piece's workgroup writes this tile
+    } else if (vec) {
       OutT* wt = reinterpret_cast<OutT*>(scratch + wave * UB);  // [32][32], this wave's
       constexpr int CPRW = 32 / CH;
 #pragma unroll
@@ -778,6 +897,46 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
   }
 }
 
+// ---- stream-K workspace: one per HIP stream (launches on one stream are ordered; two streams'
+// launches may run together, so they never share partial slabs, tickets or flags).  Allocated
+// at the first launch on a stream outside graph capture (or by clskd_stream_prepare); a launch
+// captured on a stream without one runs the data-parallel deal instead.
+constexpr int SK_MAX_GRID = 256, SK_MAX_TILES = 1 << 16;
+struct SkWs {
+  float* ws;           // [SK_MAX_GRID][2][256 * 256] fp32
+  unsigned* ready;     // [SK_MAX_GRID][2], then the tickets [SK_MAX_TILES]; zero at rest
+};
+// Whether this thread's last conv_gemm8 launch ran the stream-K deal (clskd_conv_last_stream_k).
+static thread_local int g_last_sk = 0;
+static void note_stream_k(bool on) { g_last_sk = on ? 1 : 0; }
+
+static std::mutex g_sk_mu;
+static std::unordered_map<hipStream_t, SkWs> g_sk;
+
+static const SkWs* sk_workspace(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lk(g_sk_mu);
+  auto it = g_sk.find(st);
+  if (it != g_sk.end()) return &it->second;
+  if (cs != hipStreamCaptureStatusNone) return nullptr;
+  SkWs w{};
+  const size_t wsb = (size_t)SK_MAX_GRID * 2 * 256 * 256 * 4, fb = (size_t)(SK_MAX_GRID * 2 + SK_MAX_TILES) * 4;
+  if (hipMalloc(&w.ws, wsb) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (hipMalloc(&w.ready, fb) != hipSuccess || hipMemsetAsync(w.ready, 0, fb, st) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFree(w.ws);
+    return nullptr;
+  }
+  return &(g_sk[st] = w);
+}
+
 template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8,
           int EB = 0, typename InT = __bf16, int PP = 0, int TA = 0>
 static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
@@ -813,20 +972,58 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   const int cap = knob(KNOB_G8_GRID) > 0 ? knob(KNOB_G8_GRID) : ncu;
   const int ncap = cap > 0 && cap < ncu ? cap : ncu;
   const int grid = ntiles <= ncap ? (int)ntiles : (ncap >= 8 ? (ncap & ~7) : ncap);
-  ConvArgsG8 a{d, (int)n_mt, (int)ntiles, 1, d.K / BK, make_bnfold(d)};
+  ConvArgsG8 a{d, (int)n_mt, (int)ntiles, 1, d.K / BK, make_bnfold(d), nullptr, nullptr, nullptr};
+  // stream-K when the data-parallel deal leaves a partial last round: the K-tile units split
+  // evenly over the grid.  Each workgroup hands one fp32 partial (BM x BN x 4 B) to a neighbour
+  // and takes one back; every workgroup does so at about the same time, so the grid moves
+  // grid x 2 partials through memory in two bursts (64 MB each for 256 x 256 tiles on 256 CUs):
+  // SK_COST = 12 K-tiles, fitted to the teacher layers (profiles/r5_g8_sk_ab.txt: enc3, 2.5
+  // rounds, measured 5 % slower with stream-K, enc4 / dec1 at 1.26 rounds 12-17 % faster)
+  // A capped grid (CLSKD_G8_GRID: the concurrent four-stream step) keeps the data-parallel deal:
+  // there the other streams' kernels fill the CUs a partial last round leaves idle, and the
+  // partial hand-off is extra memory traffic (measured: C2 step 5.36 vs 5.30 ms with stream-K,
+  // profiles/r5_g8_sk_ab.txt).  CLSKD_G8_SK=2 (tests) splits on any grid.
+  const int skm = knob(KNOB_G8_SK);
+  if (TA == 1 && (skm == 2 || (skm == 1 && ncap == ncu)) && grid >= 8 && grid <= SK_MAX_GRID && (grid & 7) == 0 &&
+      ntiles >= grid && ntiles <= SK_MAX_TILES && ntiles % grid != 0) {
+    constexpr int64_t SK_COST = 12;
+    const int64_t nk = d.K / BK;
+    // CLSKD_G8_SK=2 (tests, A/B): whenever the deal splits, whatever the cost model says
+    if (skm == 2 || cdiv(ntiles * nk, (int64_t)grid) + SK_COST < cdiv(ntiles, (int64_t)grid) * nk) {
+      if (const SkWs* w = sk_workspace(st)) {
+        a.sk_ws = w->ws;
+        a.sk_ready = w->ready;
+        a.sk_cnt = w->ready + SK_MAX_GRID * 2;
+      }
+    }
+  }
   // channel-block-major K order when every K-tile lies inside one tap (CLSKD_G8_KORDER=0: packed)
   if (knob(KNOB_G8_KORDER) != 0 && d.ntaps > 1 && d.ctot % BK == 0 && (int64_t)d.ntaps * d.ctot == d.K) {
     a.kt_taps = d.ntaps;
     a.kt_cpt = d.ctot / BK;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NWV * 64), lds, st, a);
-  note_kernel_fn((const void*)kern);
+  const void* kfn = (const void*)kern;
+  if constexpr (TA == 1) {
+    if (a.sk_cnt) {  // the stream-K instantiation
+      auto kern_sk = conv_gemm8_kernel<BM, BN, WM, BK, NS, PHI, OutT, DBG, PF, NWV, EB, InT, PP, 3>;
+      static bool attr_sk = false;
+      if (!attr_sk) {
+        (void)hipFuncSetAttribute((const void*)kern_sk, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_sk = true;
+      }
+      kfn = (const void*)kern_sk;
+      hipLaunchKernelGGL(kern_sk, dim3((unsigned)grid), dim3(NWV * 64), lds, st, a);
+    }
+  }
+  if (kfn == (const void*)kern) hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NWV * 64), lds, st, a);
+  note_kernel_fn(kfn);
   if constexpr (__is_same(InT, _Float16))
     note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d,f16%s%s>", BM, BN, WM, BK, NS, PHI,
-                type_name<OutT>(), DBG, PF, NWV, EB, PP ? ",pp" : "", TA ? ",ta" : "");
+                type_name<OutT>(), DBG, PF, NWV, EB, PP ? ",pp" : "", TA ? (a.sk_cnt ? ",ta,sk" : ",ta") : "");
   else
     note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d%s%s>", BM, BN, WM, BK, NS, PHI,
-                type_name<OutT>(), DBG, PF, NWV, EB, PP ? ",bf16,pp" : "", TA ? ",ta" : "");
+                type_name<OutT>(), DBG, PF, NWV, EB, PP ? ",bf16,pp" : "", TA ? (a.sk_cnt ? ",ta,sk" : ",ta") : "");
+  note_stream_k(a.sk_cnt != nullptr);
   return CLSKD_OK;
 }
 
@@ -961,3 +1158,9 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
 }
 
 }  // namespace clskd
+
+extern "C" int32_t clskd_conv_last_stream_k(void) { return clskd::g_last_sk; }
+
+extern "C" int clskd_stream_prepare(void* stream) {
+  return clskd::sk_workspace(reinterpret_cast<hipStream_t>(stream)) ? CLSKD_OK : CLSKD_E_HIP;
+}

@@ -60,10 +60,24 @@ def _bn(N, g):
     return bn
 
 
-@pytest.mark.parametrize("kind,N,dt", [("enc", 64, "bf16"), ("enc", 128, "bf16"),
-                                       ("enc", 256, "bf16"), ("abf", 32, "bf16"),
-                                       ("enc", 64, "f32"), ("enc", 32, "f32")])
-def test_bn_fold_against_torch(kind, N, dt):
+@pytest.mark.parametrize("kind,N,dt,grid", [("enc", 64, "bf16", 0), ("enc", 128, "bf16", 0),
+                                            ("enc", 256, "bf16", 0), ("abf", 32, "bf16", 0),
+                                            ("enc", 64, "f32", 0), ("enc", 32, "f32", 0),
+                                            ("enc", 256, "bf16", 16), ("enc", 128, "bf16", 24)])
+def test_bn_fold_against_torch(kind, N, dt, grid):
+    """grid > 0: conv_gemm8 on a capped persistent grid, where its stream-K deal splits tiles
+    between workgroups (the finishing workgroup folds the tile's statistics)."""
+    from clskd import _lib
+    prev_g = _lib.set_g8_grid(grid)
+    prev_sk = _lib.set_knob("CLSKD_G8_SK", 2 if grid else 1)  # 2: split even where not paying
+    try:
+        _bn_fold_check(kind, N, dt, grid)
+    finally:
+        _lib.set_g8_grid(prev_g)
+        _lib.set_knob("CLSKD_G8_SK", prev_sk)
+
+
+def _bn_fold_check(kind, N, dt, grid):
     from clskd import ops
     g = torch.Generator().manual_seed(N + (7 if dt == "f32" else 0) + (3 if kind == "abf" else 0))
     x, taps, (B, Fo, T, sf), wp, bias, ref = _conv_case(kind, N, dt, g)
@@ -80,6 +94,7 @@ def test_bn_fold_against_torch(kind, N, dt):
         st = ops.BnStats(bnd, N, B * Fo * T, 2, DEV, stats_out=(mv[0], mv[1]))
         ops.conv([ops.seg_bftc(x.to(DEV))], taps, B, Fo, T, N, wp, bias.to(DEV), out,
                  ops.OutMap(Fo * T * N, T * N, N), stride_f=sf, bn_stats=(st, True))
+        assert ops.conv_last_stream_k() == (grid > 0), "stream-K expected on the capped grid"
         coef = st.coefficients().clone()
         torch.cuda.synchronize()
         assert st.mode == "fold", f"{kind} N={N} {dt} did not dispatch to a folding engine"

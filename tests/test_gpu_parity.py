@@ -633,13 +633,16 @@ def test_step_g8_grid_cap_is_bitwise_neutral():
     """clskd_step caps conv_gemm8's persistent grid at 7/8 of the CUs inside the concurrent
     step (distill._STEP_G8_GRID_FRAC): only the deal of tiles to workgroups changes, so every
     loss slot, the student waveform and the BatchNorm running statistics are bitwise those of
-    the full-grid step."""
-    from clskd import distill
+    the full-grid step.  Checked on the data-parallel deal (CLSKD_G8_SK=0): with stream-K the
+    grid also sets where split tiles' K sums are cut (deterministic per grid, rounding-level
+    across grids: test_conv_gemm8_stream_k)."""
+    from clskd import _lib, distill
     from clskd.data import synthetic_pairs
     n, c = synthetic_pairs(4, 32000, seed=41)
     X, y = torch.from_numpy(n).to(DEV), torch.from_numpy(c).to(DEV)
     outs = []
     prev = distill._STEP_G8_GRID_FRAC
+    prev_sk = _lib.set_knob("CLSKD_G8_SK", 0)
     try:
         for frac in (0.0, 0.875, 0.5):
             distill._STEP_G8_GRID_FRAC = frac
@@ -651,6 +654,7 @@ def test_step_g8_grid_cap_is_bitwise_neutral():
                          [b.clone() for nme, b in kd.named_buffers() if "running" in nme]))
     finally:
         distill._STEP_G8_GRID_FRAC = prev
+        _lib.set_knob("CLSKD_G8_SK", prev_sk)
     for loss, wav, bufs in outs[1:]:
         assert torch.equal(loss, outs[0][0])
         assert torch.equal(wav, outs[0][1])
@@ -1139,3 +1143,82 @@ def _lstm_recurrence_check(H=32):
             h = torch.sigmoid(o) * torch.tanh(c)
             ref[ws, :, t] = h
     np.testing.assert_allclose(out.double().cpu().numpy(), ref.numpy(), rtol=2e-5, atol=2e-5)
+
+
+def _sk_expected(ntiles, nk, grid, force=False):
+    """conv_gemm8's stream-K rule (launch_g8): a partial last round and a gain of more than the
+    hand-off cost (12 K-tiles); CLSKD_G8_SK=2 forces it wherever the deal splits."""
+    return (grid >= 8 and grid % 8 == 0 and ntiles >= grid and ntiles % grid != 0
+            and (force or -(-ntiles * nk // grid) + 12 < -(-ntiles // grid) * nk))
+
+
+@pytest.mark.parametrize("grid", [40, 64])
+@pytest.mark.parametrize("lp", ["bf16", "fp16"])
+@pytest.mark.parametrize("case", ["enc5x2_n256", "dec_parity1_n128", "abf3x3_n200"])
+def test_conv_gemm8_stream_k(case, lp, grid):
+    """Stream-K deal of conv_gemm8 (round 5): the K-tile units of all tiles split evenly over a
+    persistent grid (capped here with CLSKD_G8_GRID so a small layer has a partial last round),
+    a tile shared by two workgroups finished by the later arrival with the earlier one's fp32
+    partial.  Against torch fp64 (outputs and fused statistics, the G8 tolerances), against the
+    data-parallel deal (CLSKD_G8_SK=0: the K sums only regroup, fp32 rounding), and bitwise
+    repeatable (a commutative add: arrival order does not matter)."""
+    from clskd import _lib, ops
+    segc, N, taps, sf, Fi, Fo, of_mul, of_add, out_bf16 = G8_CASES[case]
+    g = torch.Generator().manual_seed(7 + grid)
+    B, T = 4, 301
+    segs_h = [torch.randn(B, Fi, T, c, generator=g).to(_LP[lp]) for c in segc]
+    Cin = sum(segc)
+    K = len(taps) * Cin
+    w = torch.randn(N, len(taps), Cin, generator=g) * (0.5 / K ** 0.5)
+    bias = torch.randn(N, generator=g)
+    wp = ops.pack_weight(w.to(DEV), K, lp)
+    wq = wp[:, :K].float().cpu().double().view(N, len(taps), Cin)
+    x = torch.cat([s.double() for s in segs_h], 3)
+    ref = bias.double().view(1, 1, 1, N).expand(B, Fo, T, N).clone()
+    for ti, (dF, dT) in enumerate(taps):
+        fi = torch.arange(Fo) * sf + dF
+        tt = torch.arange(T) + dT
+        vf = (fi >= 0) & (fi < Fi)
+        vt = (tt >= 0) & (tt < T)
+        sub = torch.zeros(B, Fo, T, Cin, dtype=torch.float64)
+        sub[:, vf.nonzero()[:, 0][:, None], vt.nonzero()[:, 0][None, :]] = \
+            x[:, fi[vf][:, None], tt[vt][None, :]]
+        ref += torch.einsum("bftc,nc->bftn", sub, wq[:, ti])
+    Fout = Fo * of_mul
+    segs = [ops.seg_bftc(s.to(DEV)) for s in segs_h]
+    nblk = ops.conv_mblocks(B, Fo, T)
+    bn = 256 if N > 128 else 128
+    ntiles = -(-(B * Fo * T) // 256) * -(-N // bn)
+    expect_sk = _sk_expected(ntiles, K // 64, grid, force=True)
+
+    def run(sk):
+        out = torch.zeros(B, Fout, T, N, device=DEV, dtype=_LP[lp] if out_bf16 else torch.float32)
+        st = torch.full((nblk * N * 2,), float("nan"), device=DEV, dtype=torch.float64)
+        prev_sk = _lib.set_knob("CLSKD_G8_SK", 2 if sk else 0)  # 2: split even where not paying
+        prev_g = _lib.set_g8_grid(grid)
+        try:
+            ops.conv(segs, taps, B, Fo, T, N, wp, bias.to(DEV), out,
+                     ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add),
+                     stride_f=sf, stats=st)
+            used = ops.conv_last_stream_k()
+        finally:
+            _lib.set_knob("CLSKD_G8_SK", prev_sk)
+            _lib.set_g8_grid(prev_g)
+        torch.cuda.synchronize()
+        return out, st, used
+
+    o1, s1, used = run(True)
+    assert used == expect_sk, (ntiles, K // 64, grid)
+    o2, s2, _ = run(True)
+    assert torch.equal(o1, o2) and torch.equal(s1, s2), "stream-K must be bitwise repeatable"
+    o0, s0, used0 = run(False)
+    assert not used0
+    o = o1.double().cpu()[:, of_add::of_mul]
+    tol = _LP_TOL[lp] if out_bf16 else 1e-4
+    np.testing.assert_allclose(o.numpy(), ref.numpy(), rtol=tol, atol=tol)
+    if not out_bf16:  # fp32 outputs: only the K-sum grouping differs from the data-parallel deal
+        np.testing.assert_allclose(o1.cpu().numpy(), o0.cpu().numpy(), rtol=1e-5, atol=1e-5)
+    stc = s1.view(nblk, N, 2).cpu()
+    assert torch.isfinite(stc).all(), "every statistics slot must be written"
+    np.testing.assert_allclose(stc[:, :, 0].sum(0).numpy(), ref.sum((0, 1, 2)).numpy(), rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(stc[:, :, 1].sum(0).numpy(), (ref ** 2).sum((0, 1, 2)).numpy(), rtol=1e-5)
