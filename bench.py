@@ -388,19 +388,20 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--abf-reinit", default="step", choices=["step", "once"])
     ap.add_argument("--launch", default=None, choices=["exec", "eager", "graph"],
-                    help="default: eager.  C3 (--train) also takes exec / graph (the captured "
-                         "training step, clskd.graph.TrainStepExecutor / TrainStepGraph).  "
-                         "eager: launch the four-stream schedule from Python every "
-                         "step (host enqueue ~4.1 ms under a ~5.6 ms device step: device-bound); "
-                         "exec: capture the step once and replay it with the library's C++ "
-                         "multi-stream executor (clskd.graph.StepExecutor: ~1 ms host enqueue, but "
-                         "the replayed branches all start at the fork and slow the teacher chain: "
-                         "6.4-6.5 ms device); graph: hipGraphLaunch of the capture (ROCm's graph "
-                         "executor runs the branches one after another)")
+                    help="default: exec for C2 (one rank), eager for C3 / C4 / multi-rank.  "
+                         "C3 (--train) also takes exec / graph (the captured training step, "
+                         "clskd.graph.TrainStepExecutor / TrainStepGraph).  eager: launch the "
+                         "four-stream schedule from Python every step (host enqueue ~3.9 ms under "
+                         "a ~5.3 ms device step); exec: capture the step once and replay it with "
+                         "the library's C++ multi-stream executor — with the teacher_ahead "
+                         "overlap (two alternating captures, clskd.graph.AheadStepExecutor; "
+                         "--no-ahead: one capture, clskd.graph.StepExecutor): ~1.7 ms host "
+                         "enqueue, the eager device time; graph: hipGraphLaunch of the capture "
+                         "(ROCm's graph executor runs the branches one after another)")
     ap.add_argument("--graph", action="store_true", help="same as --launch graph")
     ap.add_argument("--no-ahead", dest="ahead", action="store_false",
-                    help="C2 eager: start each step's teacher chain after the previous step's "
-                         "join.  Default: the teacher chain of step i+1 overlaps step i's tail "
+                    help="C2 (eager and exec): start each step's teacher chain after the previous "
+                         "step's join.  Default: the teacher chain of step i+1 overlaps step i's tail "
                          "(clskd_step teacher_ahead, bitwise the serial schedule's results; "
                          "measured 0.6-1 %% faster: 5.35/5.37 vs 5.40/5.40 ms, 5.70 vs 5.76 ms)")
     ap.add_argument("--train", action="store_true",
@@ -453,10 +454,13 @@ def main():
     if args.spkd and args.train:
         raise SystemExit("--spkd is its own leg (no --train)")
     if args.launch is None:
-        # eager everywhere: the C3 step is device-bound (~20 ms of device work; its captured
-        # replays measured 23.5 ms with the C++ executor and 24.6 ms with hipGraphLaunch against
-        # 20.6 ms eager, gpurun_out r4p / DESIGN.md section 13)
-        args.launch = "eager"
+        # C2 (one rank): the step captured once and replayed by the C++ executor with the
+        # teacher_ahead overlap (clskd.graph.AheadStepExecutor): the eager device schedule at
+        # ~1.7 ms of host time per step instead of ~3.9 ms of Python launches (same-box A/B,
+        # profiles/r5_exec_ab.txt: 5.28 vs 5.28 ms per step).  C3 stays eager: its captured
+        # replays measured 23.5 ms (C++ executor) / 24.6 ms (hipGraphLaunch) against 20.6 ms
+        # eager (gpurun_out r4p / DESIGN.md section 13)
+        args.launch = "exec" if not (args.train or args.spkd) else "eager"
     if args.spkd or world > 1:
         # the C4 leg launches eagerly (its capture is not wired yet); multi-rank runs launch
         # eagerly too (no graph capture beside the RCCL communicator's watchdog)
@@ -517,7 +521,11 @@ def main():
     elif args.launch == "exec":
         from clskd.graph import StepExecutor
         if executor is None:
-            executor = StepExecutor(kd, Xs[0], Ys[0])
+            if args.ahead:  # the teacher_ahead overlap, replayed (two alternating captures)
+                from clskd.graph import AheadStepExecutor
+                executor = AheadStepExecutor(kd, Xs[0], Ys[0])
+            else:
+                executor = StepExecutor(kd, Xs[0], Ys[0])
 
         def step(i):
             return executor(Xs[i % NBATCH], Ys[i % NBATCH])
@@ -562,8 +570,9 @@ def main():
     if args.launch == "exec":
         # live HIP-event timing of the dominant instance inside the executor's launches
         n_dom = census[dominant][0]
-        ops.check(ops.lib().clskd_exec_profile(executor._ex, ops.KernelTimer.fns[dominant],
-                                               n_dom * args.steps), "exec_profile")
+        for e in getattr(executor, "ex", [executor]):
+            ops.check(ops.lib().clskd_exec_profile(e._ex, ops.KernelTimer.fns[dominant],
+                                                   n_dom * args.steps), "exec_profile")
 
     _gc_setting()
     # ---- timed region: exactly K steps, barrier + sync on both sides --------------------
@@ -583,8 +592,12 @@ def main():
     if args.launch == "exec":
         import ctypes
         tot, cnt = ctypes.c_double(0), ctypes.c_int32(0)
-        ops.check(ops.lib().clskd_exec_profile_read(executor._ex, ctypes.byref(tot),
-                                                    ctypes.byref(cnt)), "exec_profile_read")
+        for e in getattr(executor, "ex", [executor]):
+            t1, c1 = ctypes.c_double(0), ctypes.c_int32(0)
+            ops.check(ops.lib().clskd_exec_profile_read(e._ex, ctypes.byref(t1), ctypes.byref(c1)),
+                      "exec_profile_read")
+            tot.value += t1.value
+            cnt.value += c1.value
         fl = census[dominant][2] / census[dominant][0]
         ktimes = {dominant: [cnt.value, tot.value, fl * cnt.value]}
         timing = ("HIP events around every launch of the dominant conv kernel inside the timed "
@@ -698,19 +711,33 @@ def main():
             if tk is not None:
                 traffic = round(tk["hbm_bytes_per_launch"])
                 traffic_src = f"profiles/{TRAFFIC_FILE} (PMC FETCH_SIZE x2 + WRITE_SIZE, per launch)"
+        # achieved / frac: the ISOLATED rate — the dominant instance's average duration in the
+        # census step (its launches one at a time on one stream: the view a rocprofv3 kernel
+        # trace of the census range reproduces, tools/region_stats.py); the live rate inside the
+        # concurrent step (a launch's event span includes the time it shares the CUs with the
+        # other streams) is reported beside it as achieved_live / frac_live
+        iso_ms = census[name][1] / census[name][0] if name in census else avg_ms
+        iso_fl = census[name][2] / census[name][0] if name in census else flops / n_l
+        ach_iso = iso_fl / (iso_ms * 1e-3) / 1e12
         if hbm_bound:
-            ach_bw = byt / (avg_ms * 1e-3) / 1e9
+            ach_bw = byt / (iso_ms * 1e-3) / 1e9
+            live_bw = byt / (avg_ms * 1e-3) / 1e9
             roof = dict(bound="hbm", kernel=name, achieved=round(ach_bw, 1), peak=PEAK_HBM_GBPS,
                         unit="GB/s", frac=round(ach_bw / PEAK_HBM_GBPS, 4),
-                        achieved_tflops=round(achieved, 2))
+                        achieved_tflops=round(ach_iso, 2), achieved_live=round(live_bw, 1),
+                        frac_live=round(live_bw / PEAK_HBM_GBPS, 4))
         else:
-            roof = dict(bound="mfma", kernel=name, achieved=round(achieved, 2), peak=peak,
-                        unit="TFLOP/s", frac=round(achieved / peak, 4))
+            roof = dict(bound="mfma", kernel=name, achieved=round(ach_iso, 2), peak=peak,
+                        unit="TFLOP/s", frac=round(ach_iso / peak, 4),
+                        achieved_live=round(achieved, 2), frac_live=round(achieved / peak, 4))
         roof.update(traffic=traffic, traffic_source=traffic_src,
                     algorithmic_bytes_per_launch=round(byt) if byt else None,
                     arithmetic_intensity_flop_per_byte=round(intensity, 1) if intensity else None,
                     ridge_flop_per_byte=round(ridge, 1),
                     launches_per_step=n_l // args.steps, timing=timing,
+                    frac_basis=("isolated: census-step average duration (one stream, the timed "
+                                "steps' kernel instances); avg_launch_us / achieved_live: the "
+                                "same instance live in the timed concurrent steps"),
                     avg_launch_us=round(avg_ms * 1e3, 2),
                     algorithmic_gflop_per_launch=round(flops / n_l / 1e9, 3),
                     isolated_avg_launch_us=(round(census[name][1] / census[name][0] * 1e3, 2)
@@ -779,8 +806,11 @@ def main():
                                                        "i's ReviewKD/Gram/loss tail (teacher_ahead)"
                                                        if kd.teacher_ahead else "")
                                   if args.launch == "eager" else
-                                  "C++ step executor (clskd_exec_launch): the captured step "
-                                  "replayed on 4 HIP streams along its dependency edges "
+                                  "C++ step executor (clskd_exec_launch" +
+                                  ("_ahead: two captures alternating, each step's teacher chain "
+                                   "overlapping the previous step's tail" if args.ahead else "") +
+                                  "): the captured step replayed on 4 HIP streams along its "
+                                  "dependency edges "
                                   f"({executor.info['kernels']} kernels, "
                                   f"{executor.info['waits']} cross-stream waits per step)"
                                   if args.launch == "exec"

@@ -638,6 +638,13 @@ int clskd_exec_create(void* hip_graph, int32_t nstreams, void* const* side_strea
 int clskd_exec_tag(void* stream, int32_t tag);
 void clskd_exec_tag_reset(void);
 int clskd_exec_launch(clskd_exec* ex, void* stream);
+/* clskd_exec_launch with the side streams in ahead_mask (bit s = stream s >= 1) not waiting for
+ * the fork on `stream`: each waits for ahead_event instead (a hipEvent_t; NULL = no wait, the
+ * stream's own order only).  The teacher_ahead schedule of clskd_step (distill.py step i + 1's
+ * frozen-teacher chain overlapping step i's tail) for captured steps: two executors with their
+ * own static buffers alternate, each one's teacher stream waiting for the end of its own
+ * previous launch (clskd.graph.AheadStepExecutor). */
+int clskd_exec_launch_ahead(clskd_exec* ex, void* stream, uint32_t ahead_mask, void* ahead_event);
 int clskd_exec_info(const clskd_exec* ex, int32_t* info, int32_t n);
 /* Text listing of the replay program (one op per line: index, kind, stream, slot, and for kernel
  * ops the grid size, block size and kernel name) into buf (NUL-terminated, truncated at cap);

@@ -106,6 +106,7 @@ SIGNATURES = {
     "clskd_conv_last_kernel": (C.c_char_p, []),
     "clskd_conv_last_kernel_fn": (_p, []),
     "clskd_conv_last_stream_k": (_i32, []),
+    "clskd_exec_launch_ahead": (_i32, [_p, _p, C.c_uint32, _p]),
     "clskd_stream_prepare": (_i32, [_p]),
     "clskd_version": (_i32, []),
     "clskd_set_knob": (_i32, [C.c_char_p, _i32]),

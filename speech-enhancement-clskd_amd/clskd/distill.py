@@ -297,9 +297,12 @@ def clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y
     under graph capture, tapes or serialised streams."""
     if not (isinstance(teacher, DCCRN) and isinstance(student, DCCRN)):
         raise TypeError("clskd_step expects clskd.DCCRN teacher and student")
-    if _SERIAL or tape or not X.is_cuda:
+    if tape or not X.is_cuda:
         return _clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, y,
                            reinit, tape, teacher_ahead)
+    # the concurrent step's conv_gemm8 grid cap — also for the serialised census step
+    # (serialized_streams), so the census times exactly the kernel instances the timed steps run
+    # (a capped grid keeps the data-parallel tile deal: no stream-K)
     from . import _lib
     prev = _lib.set_g8_grid(_step_g8_grid(X.device))
     try:
@@ -335,10 +338,17 @@ def _clskd_step(teacher, student, review_encoder, review_decoder, stft_loss, X, 
         raise ValueError("clskd_step(teacher_ahead=True) needs fp32 contiguous [B, L] inputs "
                          "already resident on the device")
     spec_ev = None
-    if ahead:
+    # teacher_ahead under graph capture: the ahead LAYOUT (the spectrum on the teacher stream,
+    # the student waiting for it by event) with the teacher forked from the capture stream like
+    # every branch; clskd.graph.AheadStepExecutor replays two such captures alternately, each
+    # one's teacher stream waiting for the end of its own previous replay instead of the fork
+    if ahead or (teacher_ahead and capturing and not _SERIAL and not tape):
         # the teacher chain (spectrum included) waits for the join of step i-1, not step i
         tstream = _side_stream(dev, 2)
-        tstream.wait_event(ring["joins"][0])
+        if ahead:
+            tstream.wait_event(ring["joins"][0])
+        else:
+            tstream.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(tstream):
             spec = teacher.spectrum(X)
         spec_ev = torch.cuda.Event()

@@ -32,6 +32,10 @@ def _bn_buffers(kd):
 
 
 class StepGraph:
+    # capture in clskd_step's teacher_ahead layout (the spectrum on the teacher stream; replays
+    # by AheadStepExecutor)
+    ahead_layout = False
+
     def __init__(self, kd, X, y, warmup=1):
         if not isinstance(kd, KnowledgeDistillation):
             raise TypeError("StepGraph captures a clskd.distill.KnowledgeDistillation step")
@@ -55,7 +59,13 @@ class StepGraph:
         return [p for m in mods for p in m.parameters()]
 
     def _sig(self):
-        return tuple((p.data_ptr(), p._version) for p in self._baked())
+        # the baked parameter list is fixed per capture (module trees do not change): resolved
+        # once, so a replay's check is one pass over the tensors (no module traversal)
+        ps = getattr(self, "_baked_ps", None)
+        if ps is None or getattr(self, "_baked_for", None) != self.captures:
+            ps = self._baked_ps = tuple(self._baked())
+            self._baked_for = self.captures
+        return tuple([(p.data_ptr(), p._version) for p in ps])
 
     keep_graph = False
 
@@ -86,11 +96,14 @@ class StepGraph:
         self.graph = None
         g = torch.cuda.CUDAGraph(keep_graph=True) if self.keep_graph else torch.cuda.CUDAGraph()
         self._tagging(True)
+        prev_ahead = getattr(self.kd, "teacher_ahead", False)
+        self.kd.teacher_ahead = self.ahead_layout
         try:
             with torch.cuda.graph(g, stream=s):
                 self.out = self.kd.training_step((self.X, self.y), return_parts=True)
         finally:
             self._tagging(False)
+            self.kd.teacher_ahead = prev_ahead
         self.graph = g
         self.sig = self._sig()
         self.captures += 1
@@ -133,10 +146,11 @@ class StepExecutor(StepGraph):
 
     keep_graph = True
 
-    def __init__(self, kd, X, y, warmup=1, nstreams=None):
+    def __init__(self, kd, X, y, warmup=1, nstreams=None, ahead_layout=False):
         if nstreams is None:  # diagnostic override: CLSKD_EXEC_STREAMS (1 = serial replay)
             nstreams = int(os.environ.get("CLSKD_EXEC_STREAMS", "4"))
         self.nstreams = nstreams
+        self.ahead_layout = ahead_layout
         self._ex = None
         super().__init__(kd, X, y, warmup)
 
@@ -199,6 +213,60 @@ class StepExecutor(StepGraph):
             self._release()
         except Exception:
             pass
+
+
+class AheadStepExecutor:
+    """The C2 step replayed by the C++ executor with clskd_step's teacher_ahead overlap: step
+    i + 1's frozen-teacher chain runs while step i's ReviewKD / Gram / loss tail finishes.  Two
+    StepExecutors, each captured in the ahead layout with static buffers of its own, alternate;
+    an executor's teacher stream does not wait for the fork (the caller's stream, behind the
+    previous step's join) but for the end of its OWN previous replay — the last reader of its
+    buffers — and then takes the new batch on that stream (clskd_exec_launch_ahead).  Every
+    other branch forks from the caller's stream as before, so BatchNorm running statistics, ABF
+    re-draws and the loss stay step-ordered: the results are those of back-to-back eager steps
+    (tests/test_gpu_parity.py).  Host enqueue: one C-ABI call per step instead of ~140 Python
+    launches.
+
+        step = AheadStepExecutor(kd, X0, y0)
+        loss = step(X, y)      # inputs resident on the device; loss: that replay's output slot
+    """
+
+    def __init__(self, kd, X, y, warmup=1):
+        self.ex = [StepExecutor(kd, X, y, warmup, ahead_layout=True) for _ in range(2)]
+        if self.ex[0].nstreams != 4:
+            raise ValueError("AheadStepExecutor needs the four-stream replay")
+        self.done = [torch.cuda.Event(), torch.cuda.Event()]
+        self.i = 0
+        self.last = self.ex[0]
+        self.info = self.ex[0].info
+
+    @property
+    def out(self):
+        return self.last.out
+
+    def __call__(self, X=None, y=None):
+        from . import _lib
+        from .distill import _side_stream
+        e = self.ex[self.i]
+        if e._sig() != e.sig:
+            raise RuntimeError("AheadStepExecutor: a baked parameter changed; re-create it")
+        dev = e.X.device
+        main = torch.cuda.current_stream(dev)
+        t = _side_stream(dev, 2)  # the teacher stream: executor stream 3 (capture tag)
+        t.wait_event(self.done[self.i])
+        if X is not None:
+            with torch.cuda.stream(t):
+                e.X.copy_(X)
+                # the caller's resident batch is read on the teacher stream
+                X.record_stream(t)
+        if y is not None:
+            e.y.copy_(y.reshape(e.y.shape))
+        _lib.check(_lib.load().clskd_exec_launch_ahead(e._ex, _lib.stream_ptr(), 1 << 3, None),
+                   "exec_launch_ahead")
+        self.done[self.i].record(main)
+        self.last = e
+        self.i ^= 1
+        return e.out["loss"]
 
 
 class TrainStepGraph(StepGraph):

@@ -69,6 +69,7 @@ struct clskd_exec {
   std::vector<Flat> flat;
   std::vector<Op> program;
   size_t join_at = 0;  // program[join_at..]: every used side stream's join into stream 0
+  int ev_fork = -1;    // event slot of the fork (recorded on stream 0 first)
   int32_t n_nodes = 0, n_waits = 0, n_records = 0, n_empty = 0;
   int32_t per_stream[8] = {0};
   // optional live timing of one kernel (bench: the dominant instance): an event pair around
@@ -375,6 +376,7 @@ extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, void* const*
   for (size_t i = 0; i < n; ++i)
     if (needs_event[i]) ev_of[i] = nev++;
   const int ev_fork = nev++;
+  ex->ev_fork = ev_fork;
   const int ev_join0 = nev;
   nev += S - 1;
   ex->events.resize(nev, nullptr);
@@ -431,7 +433,12 @@ extern "C" int clskd_exec_create(void* hip_graph, int32_t nstreams, void* const*
 }
 
 extern "C" int clskd_exec_launch(clskd_exec* ex, void* stream) {
+  return clskd_exec_launch_ahead(ex, stream, 0, nullptr);
+}
+
+extern "C" int clskd_exec_launch_ahead(clskd_exec* ex, void* stream, uint32_t ahead_mask, void* ahead_event) {
   CLSKD_CHECK_ARG(ex, "exec_launch: null executor");
+  CLSKD_CHECK_ARG((ahead_mask & 1u) == 0, "exec_launch_ahead: stream 0 always follows the fork");
   hipStream_t st[8];
   st[0] = as_stream(stream);
   for (int s = 1; s < ex->nstreams; ++s) st[s] = ex->own[s - 1];
@@ -470,7 +477,14 @@ extern "C" int clskd_exec_launch(clskd_exec* ex, void* stream) {
         break;
       }
       case OP_WAIT:
-        e = hipStreamWaitEvent(s, ex->events[op.idx], 0);
+        if (i < ex->join_at && op.idx == ex->ev_fork && ((ahead_mask >> op.stream) & 1u)) {
+          // ahead stream: instead of the fork (the caller's stream, behind the previous launch's
+          // join), wait for the caller's event — e.g. the end of this executor's own previous
+          // launch, the last reader of its static buffers (none: the stream's own order only)
+          if (ahead_event) e = hipStreamWaitEvent(s, reinterpret_cast<hipEvent_t>(ahead_event), 0);
+        } else {
+          e = hipStreamWaitEvent(s, ex->events[op.idx], 0);
+        }
         break;
       case OP_RECORD:
         e = hipEventRecord(ex->events[op.idx], s);

@@ -693,6 +693,46 @@ def test_teacher_ahead_matches_serial_schedule(precision):
     assert torch.equal(ref, got), (ref - got).abs().max()
 
 
+@pytest.mark.parametrize("precision", ["fp32", "mixed"])
+def test_ahead_executor_matches_serial_schedule(precision):
+    """clskd.graph.AheadStepExecutor: two captures in the teacher_ahead layout replayed
+    alternately by the C++ executor, each one's teacher stream waiting for the end of its own
+    previous replay instead of the fork (clskd_exec_launch_ahead) — bitwise the per-step losses
+    (all 16 slots) and the student waveforms of the eager step-by-step schedule over five
+    back-to-back steps on distinct resident batches, and the same BatchNorm running statistics
+    afterwards (teacher and student, one update per step each)."""
+    from clskd.data import synthetic_pairs
+    from clskd.graph import AheadStepExecutor
+    batches = []
+    for k in range(5):
+        n, c = synthetic_pairs(4, 16000, seed=170 + k)
+        batches.append((torch.from_numpy(n).to(DEV), torch.from_numpy(c).to(DEV)))
+
+    def slots(o):
+        return torch.cat([o["loss"].reshape(1), o["sc"].reshape(1), o["base"].reshape(1),
+                          o["spkd"].reshape(-1)]).clone()
+
+    kd_e, kd_x = _kd().set_precision(precision), _kd().set_precision(precision)
+    ref, ref_w = [], []
+    with torch.no_grad():
+        for b in batches:
+            o = kd_e.training_step(b, 0, return_parts=True)
+            ref.append(slots(o))
+            ref_w.append(o["student_wav"].clone())
+    ex = AheadStepExecutor(kd_x, *batches[0])
+    got, got_w = [], []
+    for b in batches:
+        ex(*b)
+        got.append(slots(ex.out))
+        got_w.append(ex.out["student_wav"].clone())
+    torch.cuda.synchronize()
+    assert torch.equal(torch.stack(ref), torch.stack(got)), (torch.stack(ref) - torch.stack(got)).abs().max()
+    assert all(torch.equal(a, b) for a, b in zip(ref_w, got_w))
+    for (k, a), b in zip(kd_e.state_dict().items(), kd_x.state_dict().values()):
+        if "running" in k or "num_batches" in k:
+            assert torch.equal(a, b), k
+
+
 def test_teacher_ahead_toggled_between_steps():
     """switching teacher_ahead on and off between back-to-back steps with no
     synchronize in between.  A step after a non-ahead step must not run its teacher ahead (the

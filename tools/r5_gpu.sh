@@ -37,13 +37,15 @@ for st in ${STEPS:-suite bench}; do
         rc=0; timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/write.log 2>&1 || rc=$?; ok $rc write ) || exit $?
       python3 $R/tools/pmc_traffic.py $O/fetch/run_counter_collection.csv $O/write/run_counter_collection.csv $O/pmc_traffic.json > $O/traffic.txt;;
     micro) rc=0; timeout -k 10 300 python $R/tools/conv_micro.py $MICRO_ARGS > $O/micro.log 2>&1 || rc=$?; cat $O/micro.log; ok $rc micro;;
-    ab)  # same-box A/B of env settings on the C2 line: AB_CASES="A=1 B=2;A=0" (';'-separated)
+    ab)  # same-box A/B on the C2 line: AB_CASES="A=1 B=2;A=0 :: --launch exec" (';'-separated
+         # cases: env assignments, optionally '::' and extra bench.py arguments)
       IFS=';' read -ra CS <<< "$AB_CASES"
       for pass in 1 2 3; do
         i=0
         for c in "${CS[@]}"; do
           i=$((i+1)); rc=0
-          env $c timeout -k 10 200 python $R/bench.py --no-cpu-baseline --steps 20 --warmup 5 $BENCH_ARGS > $O/ab_c${i}_p$pass.log 2>&1 || rc=$?; ok $rc ab
+          ce=${c%%::*}; ca=""; [[ "$c" == *::* ]] && ca=${c#*::}
+          env $ce timeout -k 10 200 python $R/bench.py --no-cpu-baseline --steps 20 --warmup 5 $BENCH_ARGS $ca > $O/ab_c${i}_p$pass.log 2>&1 || rc=$?; ok $rc ab
           echo "[$c] pass $pass: $(grep '^{' $O/ab_c${i}_p$pass.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], "ms, host", d["host_enqueue_ms_per_step"], "frac", d["roofline"]["frac"], d["roofline"].get("isolated_avg_launch_us"))')"
         done
       done;;
@@ -54,6 +56,8 @@ for st in ${STEPS:-suite bench}; do
         rc=0; timeout -k 10 400 rocprofv3 --kernel-trace --marker-trace --stats --output-format csv -d $O/ttrace -o run -- python3 $R/bench.py --train --steps 10 --warmup 3 --no-cpu-baseline > $O/ttrace.log 2>&1 || rc=$?; ok $rc trace_train ) || exit $?
       python3 $R/tools/region_stats.py $O/ttrace/run 10 $O/train_region_stats.json > $O/train_region_stats.txt 2>&1 || true
       grep '^{' $O/ttrace.log | cut -c1-300;;
+    py:*) f=${st#py:}; f=${f//,/ }; rc=0; timeout -k 10 300 python $R/$f > $O/py_$(basename ${f%% *} .py).txt 2>&1 || rc=$?
+      tail -30 $O/py_$(basename ${f%% *} .py).txt; ok $rc py;;
     *) echo "unknown step $st"; exit 2;;
   esac
 done

@@ -1,5 +1,5 @@
 """MFMA-utilisation summary of the dominant conv_gemm8 instances from rocprofv3 PMC passes
-(tools/r4_first.sh: one pass per counter group, --kernel-include-regex conv_gemm8).
+(one rocprofv3 --pmc pass per counter group, --kernel-include-regex conv_gemm8; see tools/pmc_g8.sh).
 
     python tools/sq_summary.py out.json sq1/run_counter_collection.csv sq2/... sq3/...
 
