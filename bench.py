@@ -38,7 +38,7 @@ PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sp
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 B_PER_GPU = 16
 NBATCH = 4
-TRAFFIC_FILE = "r4_pmc_traffic.json"  # written by tools/pmc_traffic.py
+TRAFFIC_FILE = "r5_pmc_traffic.json"  # written by tools/pmc_traffic.py
 L = 64000
 
 
@@ -48,6 +48,25 @@ def _range_push(name):
 
 def _range_pop():
     torch.cuda.nvtx.range_pop()
+
+
+def dispatch_span_us(dev, n=64):
+    """HIP-event span of a near-empty launch (a 1-element fill) on the current stream: what an
+    event pair around a launch measures beyond the kernel's own duration (command-processor
+    packet processing and wave launch; rocprofv3's kernel-trace duration excludes it).  Median of
+    n back-to-back launches, after one warm-up."""
+    from clskd import ops
+    t = torch.empty(1, device=dev)
+    ops.fill(t, 0.0)
+    evs = []
+    for _ in range(n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ops.fill(t, 0.0)
+        e1.record()
+        evs.append((e0, e1))
+    torch.cuda.synchronize(dev)
+    return float(np.median([a.elapsed_time(b) for a, b in evs])) * 1e3
 
 
 def launches_per_step(kd, X, y):
@@ -549,6 +568,7 @@ def main():
     from clskd.distill import serialized_streams
     census = None
     serial_ms = None
+    disp_us = dispatch_span_us(dev)
     for i in range(args.warmup):
         last = i == args.warmup - 1 and not args.graph
         if last:
@@ -582,10 +602,15 @@ def main():
     _range_push("clskd_timed")
     if args.launch == "eager":
         ops.KernelTimer.start(only=dominant)
+    waited0 = getattr(executor, "throttle_s", 0.0) if executor is not None else 0.0
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(i)
     host_el = time.perf_counter() - t0  # host enqueue of K steps (no sync inside the loop)
+    # an executor bounds its run-ahead (clskd.graph.StepExecutor.inflight): the host time it
+    # spent waiting for the device at step boundaries is not enqueue work
+    host_wait = (getattr(executor, "throttle_s", 0.0) - waited0) if executor is not None else 0.0
+    host_el -= host_wait
     cdist.barrier(dev)
     el = time.perf_counter() - t0
     _range_pop()
@@ -716,8 +741,12 @@ def main():
         # trace of the census range reproduces, tools/region_stats.py); the live rate inside the
         # concurrent step (a launch's event span includes the time it shares the CUs with the
         # other streams) is reported beside it as achieved_live / frac_live
-        iso_ms = census[name][1] / census[name][0] if name in census else avg_ms
+        iso_span_ms = census[name][1] / census[name][0] if name in census else avg_ms
         iso_fl = census[name][2] / census[name][0] if name in census else flops / n_l
+        # the census times each launch with an event pair, which also spans the launch's dispatch
+        # (disp_us, measured above on an empty launch): the kernel's own duration — what a
+        # rocprofv3 kernel trace of the census range reports — is the span minus that
+        iso_ms = max(iso_span_ms - disp_us * 1e-3, 0.5 * iso_span_ms)
         ach_iso = iso_fl / (iso_ms * 1e-3) / 1e12
         if hbm_bound:
             ach_bw = byt / (iso_ms * 1e-3) / 1e9
@@ -735,13 +764,17 @@ def main():
                     arithmetic_intensity_flop_per_byte=round(intensity, 1) if intensity else None,
                     ridge_flop_per_byte=round(ridge, 1),
                     launches_per_step=n_l // args.steps, timing=timing,
-                    frac_basis=("isolated: census-step average duration (one stream, the timed "
-                                "steps' kernel instances); avg_launch_us / achieved_live: the "
-                                "same instance live in the timed concurrent steps"),
+                    frac_basis=("isolated: census-step average kernel duration (one stream, the "
+                                "timed steps' kernel instances): isolated_kernel_us = the HIP-event "
+                                "span isolated_avg_launch_us minus dispatch_span_us (the span of an "
+                                "empty launch); avg_launch_us / achieved_live: the same instance's "
+                                "event spans live in the timed concurrent steps"),
                     avg_launch_us=round(avg_ms * 1e3, 2),
                     algorithmic_gflop_per_launch=round(flops / n_l / 1e9, 3),
                     isolated_avg_launch_us=(round(census[name][1] / census[name][0] * 1e3, 2)
                                             if name in census else None),
+                    isolated_kernel_us=round(iso_ms * 1e3, 2),
+                    dispatch_span_us=round(disp_us, 2),
                     achieved_isolated=(round(census[name][2] / (census[name][1] * 1e-3) / 1e12, 2)
                                        if name in census else None),
                     conv_all_kernels=dict(
@@ -781,6 +814,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3),
             "host_enqueue_ms_per_step": round(host_el / args.steps * 1e3, 3),
+            "host_wait_ms_per_step": round(host_wait / args.steps * 1e3, 3),
             "launches_per_step": step_counts["kernels"] if step_counts else None,
             "launch_count_detail": (dict(step_counts, how="kernel nodes of one captured step "
                                          "(library + torch kernels)") if step_counts else None),

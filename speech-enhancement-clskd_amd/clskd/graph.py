@@ -204,9 +204,34 @@ class StepExecutor(StepGraph):
             _lib.load().clskd_exec_destroy(self._ex)
             self._ex = None
 
+    # Replays in flight on the device at most (CLSKD_EXEC_INFLIGHT, 0 = unbounded): before a
+    # launch the host waits for the end of the replay `inflight` launches back.  The executor
+    # enqueues a step in ~1 ms; unthrottled the host runs many steps ahead until a hardware
+    # queue's ring is full, and then blocks inside a launch in program order while the other
+    # streams' queues drain (head-of-line blocking); bounded, it waits at a step boundary.
+    inflight = int(os.environ.get("CLSKD_EXEC_INFLIGHT", "2"))
+
+    def _throttle(self):
+        import collections
+        import time
+        q = self.__dict__.setdefault("_done_q", collections.deque())
+        t0 = time.perf_counter()
+        while self.inflight > 0 and len(q) >= self.inflight:
+            q.popleft().synchronize()
+        # host time spent waiting here (not enqueue work): bench subtracts it
+        self.throttle_s = getattr(self, "throttle_s", 0.0) + time.perf_counter() - t0
+
+    def _mark_done(self):
+        if self.inflight > 0:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._done_q.append(ev)
+
     def _replay(self):
         from . import _lib
+        self._throttle()
         _lib.check(_lib.load().clskd_exec_launch(self._ex, _lib.stream_ptr()), "exec_launch")
+        self._mark_done()
 
     def __del__(self):
         try:
@@ -250,6 +275,14 @@ class AheadStepExecutor:
         e = self.ex[self.i]
         if e._sig() != e.sig:
             raise RuntimeError("AheadStepExecutor: a baked parameter changed; re-create it")
+        infl = StepExecutor.inflight
+        if infl > 0:  # bounded run-ahead (StepExecutor.inflight)
+            import time
+            self._q = getattr(self, "_q", [])
+            t0 = time.perf_counter()
+            while len(self._q) >= infl:
+                self._q.pop(0).synchronize()
+            self.throttle_s = getattr(self, "throttle_s", 0.0) + time.perf_counter() - t0
         dev = e.X.device
         main = torch.cuda.current_stream(dev)
         t = _side_stream(dev, 2)  # the teacher stream: executor stream 3 (capture tag)
@@ -264,6 +297,10 @@ class AheadStepExecutor:
         _lib.check(_lib.load().clskd_exec_launch_ahead(e._ex, _lib.stream_ptr(), 1 << 3, None),
                    "exec_launch_ahead")
         self.done[self.i].record(main)
+        if infl > 0:
+            ev = torch.cuda.Event()
+            ev.record(main)
+            self._q.append(ev)
         self.last = e
         self.i ^= 1
         return e.out["loss"]

@@ -1017,12 +1017,15 @@ static int launch_g8(const clskd_conv_desc& d, hipStream_t st) {
   }
   if (kfn == (const void*)kern) hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NWV * 64), lds, st, a);
   note_kernel_fn(kfn);
-  if constexpr (__is_same(InT, _Float16))
-    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d,f16%s%s>", BM, BN, WM, BK, NS, PHI,
-                type_name<OutT>(), DBG, PF, NWV, EB, PP ? ",pp" : "", TA ? (a.sk_cnt ? ",ta,sk" : ",ta") : "");
+  if constexpr (TA != 0)  // every template argument, as rocprofv3 names the instance (TA 3: stream-K)
+    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d,%s,%d,%d>", BM, BN, WM, BK, NS, PHI,
+                type_name<OutT>(), DBG, PF, NWV, EB, type_name<InT>(), PP, a.sk_cnt ? 3 : 1);
+  else if constexpr (__is_same(InT, _Float16))
+    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d,f16%s>", BM, BN, WM, BK, NS, PHI,
+                type_name<OutT>(), DBG, PF, NWV, EB, PP ? ",pp" : "");
   else
-    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d%s%s>", BM, BN, WM, BK, NS, PHI,
-                type_name<OutT>(), DBG, PF, NWV, EB, PP ? ",bf16,pp" : "", TA ? (a.sk_cnt ? ",ta,sk" : ",ta") : "");
+    note_kernel("conv_gemm8_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d,%d,%d%s>", BM, BN, WM, BK, NS, PHI,
+                type_name<OutT>(), DBG, PF, NWV, EB, PP ? ",bf16,pp" : "");
   note_stream_k(a.sk_cnt != nullptr);
   return CLSKD_OK;
 }
