@@ -46,6 +46,10 @@ def _mark(label, stream):
 
 # A/B switch: CLSKD_STUDENT_SPLIT=0 keeps the student of precision 'mixed' on the exact fp32 engines
 _STUDENT_SPLIT = os.environ.get("CLSKD_STUDENT_SPLIT", "1") == "1"
+# the training step of a 'mixed' student (C3): bit 0 — weight gradients on split products
+# (csrc/wgrad_x3.hip); bit 1 — the taped forward's and the backward's non-accumulating fp32 convs
+# too.  CLSKD_TRAIN_SPLIT=0 keeps the whole training step exact (A/B)
+_TRAIN_SPLIT = int(os.environ.get("CLSKD_TRAIN_SPLIT", "3"))
 _SERIAL = os.environ.get("CLSKD_SERIAL_STREAMS") == "1"  # diagnostic: the whole step on one stream
 # conv_gemm8's persistent grid inside the concurrent four-stream step: 7/8 of the CUs (224 of
 # 256), so the wide teacher / ReviewKD GEMMs leave a CU per XCD group to the other streams'
@@ -190,6 +194,7 @@ class KnowledgeDistillation(nn.Module):
         self.review_encoder.set_compute(c)
         self.review_decoder.set_compute(c)
         self.student.compute = "f32x3" if (precision == "mixed" and _STUDENT_SPLIT) else "fp32"
+        self.student.train_split = _TRAIN_SPLIT if self.student.compute == "f32x3" else 0
         return self
 
     def forward(self, x):
@@ -264,8 +269,10 @@ class KnowledgeDistillation(nn.Module):
     def backward_into(self, out, grads, accumulate=False, upstream=1.0):
         """Student gradients of upstream * out['loss'] into `grads` (parameter -> fp32 tensor)."""
         from .backward import clskd_backward
-        clskd_backward(out, self.student, self.review_encoder, self.review_decoder, grads,
-                       acc_params=accumulate, upstream=upstream)
+        ts = getattr(self.student, "train_split", 0)
+        with ops.split_products(bool(ts & 2), wgrad=bool(ts & 1)):
+            clskd_backward(out, self.student, self.review_encoder, self.review_decoder, grads,
+                           acc_params=accumulate, upstream=upstream)
 
     def train_step(self, batch, flat, opt):
         """One C3 training step without autograd bookkeeping: fwd+loss (tape) -> HIP backward

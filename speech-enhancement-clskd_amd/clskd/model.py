@@ -204,6 +204,7 @@ class DCCRN(nn.Module):
         # bf16 split-product MFMA for the fp32 convs), "bf16" / "fp16" (16-bit operands, fp32
         # accumulation).  STFT/iSTFT framing GEMMs run fp32 ("f32x3": split products).
         self.compute = "fp32"
+        self.train_split = 0  # KnowledgeDistillation.set_precision: split products in training
         # a captured training step (clskd.graph.TrainStepGraph) records the packing of every
         # trainable parameter group, so each replay packs the weights its own optimizer step wrote
         self.repack_in_capture = False
@@ -411,8 +412,10 @@ class DCCRN(nn.Module):
             tape=None, taps_only=False, mark=None, on_decoder_tap=None, gram_taps=None):
         """See _run.  compute 'f32x3' (the student in precision 'mixed'): the fp32 convs of a
         forward without a tape run as 3 x bf16 split products (CLSKD_F32X3); a taped (training)
-        forward stays on the exact fp32 engines its backward mirrors."""
-        with ops.split_products(self.compute == "f32x3" and tape is None):
+        forward too when train_split bit 1 is set (KnowledgeDistillation.set_precision), else on
+        the exact fp32 engines."""
+        split = self.compute == "f32x3" and (tape is None or bool(self.train_split & 2))
+        with ops.split_products(split):
             return self._run(x, train, bn_updates, spec, want_masks, on_encoder, tape, taps_only,
                              mark, on_decoder_tap, gram_taps)
 

@@ -335,18 +335,20 @@ _SPLIT = threading.local()
 
 
 class split_products:
-    """Context manager: fp32 conv launches of this thread ask for split-product MFMA."""
+    """Context manager: fp32 conv launches of this thread ask for split-product MFMA; weight
+    gradients (conv_wgrad) likewise when `wgrad` (default: the same as `on`)."""
 
-    def __init__(self, on):
+    def __init__(self, on, wgrad=None):
         self.on = bool(on)
+        self.wgrad = self.on if wgrad is None else bool(wgrad)
 
     def __enter__(self):
-        self.prev = getattr(_SPLIT, "on", False)
-        _SPLIT.on = self.on
+        self.prev = (getattr(_SPLIT, "on", False), getattr(_SPLIT, "wgrad", False))
+        _SPLIT.on, _SPLIT.wgrad = self.on, self.wgrad
         return self
 
     def __exit__(self, *exc):
-        _SPLIT.on = self.prev
+        _SPLIT.on, _SPLIT.wgrad = self.prev
         return False
 
 
@@ -1042,12 +1044,15 @@ def conv_wgrad(segs, taps, B, Fo, To, N, dy, omap, dw, dbias=None, dy_offset=0, 
     """Weight gradient of the conv launch conv(segs, taps, B, Fo, To, N, ..., omap): fp32
     segments (the forward inputs), dy read through the forward's output map at dy + dy_offset.
     dw: [N][Kp] fp32 (the packed-weight layout, Kp = K padded to 16); dbias: [N] or None.
-    accumulate adds into dw (and dbias, unless accumulate_bias says otherwise)."""
+    accumulate adds into dw (and dbias, unless accumulate_bias says otherwise).
+    Inside split_products(..., wgrad=True) the descriptor asks for 3 x bf16 split products
+    (CLSKD_F32X3: csrc/wgrad_x3.hip), else the exact fp32 engine runs."""
     addrs = [seg_addr(sg) for sg in segs]
     taps = tuple(taps)
     geoms = tuple(sg.geom for sg in segs)
+    split = getattr(_SPLIT, "wgrad", False)
     key = (geoms, taps, B, Fo, To, N, omap, stride_f, stride_t, dy.device.index,
-           tuple(a % 16 for a in addrs))
+           tuple(a % 16 for a in addrs), split)
     pl = _WGRAD_PLANS.get(key)
     if pl is None:
         assert all(sg.tensor.dtype == torch.float32 for sg in segs), "wgrad: fp32 segments"
@@ -1066,7 +1071,8 @@ def conv_wgrad(segs, taps, B, Fo, To, N, dy, omap, dw, dbias=None, dy_offset=0, 
         d.oB, d.oF, d.oT, d.oNhi, d.oNlo = omap.oB, omap.oF, omap.oT, omap.oNhi, omap.oNlo
         d.nlo = min(omap.nlo, 1 << 30)
         d.of_mul, d.of_add = omap.of_mul, omap.of_add
-        d.compute = d.in_dtype = d.out_dtype = _lib.F32
+        d.in_dtype = d.out_dtype = _lib.F32
+        d.compute = _lib.F32X3 if split else _lib.F32
         ws = int(lib().clskd_conv2d_wgrad_workspace(d))
         pl = (d, Kp, ws)
         _WGRAD_PLANS[key] = pl

@@ -24,6 +24,8 @@
 // buffered per tile.  The cross terms accumulate in a second register set (two independent
 // MFMA chains).  Epilogue: bias-initialised accumulators, fused BatchNorm statistics per
 // workgroup (fp64) as partials or as the folded finalize (bnfold.h).
+#include <mutex>
+#include <unordered_map>
 #include <stdlib.h>
 
 #include "bnfold.h"
@@ -73,7 +75,10 @@ struct SplitArgs {
 // NS LDS stages: 2 = the next K-tile is written to the other stage (one barrier per K-tile);
 // 1 = it is written in place after a second barrier (half the LDS: more workgroups per CU to
 // hide the register-staged gather's latency, which bounds this engine: ~1 µs per K-tile round)
-template <int NT, int NW, int BK, int NS>
+// PD = 2 (round 5): the gather of K-tile k + 2 is issued while K-tile k computes (two register
+// sets), so a K-tile's loads have a whole K-tile round more to land before they are split into
+// LDS — the engine waited about one gather latency per round at PD = 1 (needs >= 2 K-tiles)
+template <int NT, int NW, int BK, int NS, int PD = 1>
 __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs args) {
   using namespace sp3;
   const clskd_conv_desc& d = args.d;
@@ -183,8 +188,8 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
   const float* sp2 = d.seg[2].ptr;
   const float* sp3 = d.seg[3].ptr;
   const float* wgt = reinterpret_cast<const float*>(d.weight);
-  f32x4 ra[NRA], rb[NBL];
-  auto load_kt = [&](int kt) {
+  f32x4 ra[NRA], rb[NBL], ra2[NRA], rb2[NBL];  // ra2 / rb2: the second set (PD = 2)
+  auto load_kt = [&](int kt, f32x4 (&xa)[NRA], f32x4 (&xb)[NBL]) {
     const int2 ce = ctab[kt * QR + kq];
     const int sg = (int)((unsigned)ce.y >> 24);
     const int dF = (int)(short)(ce.y & 0xFFFF);
@@ -199,7 +204,7 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (rvl[i] && (unsigned)fi < (unsigned)Fb && (unsigned)ti < (unsigned)Tb)
         v = *reinterpret_cast<const f32x4*>(sp + (int64_t)(rbs + ce.x));
-      ra[i] = v;
+      xa[i] = v;
     }
 #pragma unroll
     for (int i = 0; i < NBL; ++i) {
@@ -208,17 +213,17 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (idx / QR < BN && n < d.N)
         v = *reinterpret_cast<const f32x4*>(wgt + (int64_t)n * d.K + kt * BK + (idx % QR) * 4);
-      rb[i] = v;
+      xb[i] = v;
     }
   };
   // split + write the registers into stage s: k-quad q of a row = 8 B inside chunk q >> 1
-  auto store_kt = [&](int s) {
+  auto store_kt = [&](int s, const f32x4 (&xa)[NRA], const f32x4 (&xb)[NBL]) {
 #pragma unroll
     for (int i = 0; i < NRA; ++i) {
       const int row = tid / QR + RSTEP * i;
       const int off = row * ROWB + (((kq >> 1) ^ swz<BK>(row)) << 4) + (kq & 1) * 8;
       s16x4 hi, lo;
-      split4(ra[i], hi, lo);
+      split4(xa[i], hi, lo);
       *reinterpret_cast<s16x4*>(&sA[s][0][off]) = hi;
       *reinterpret_cast<s16x4*>(&sA[s][1][off]) = lo;
     }
@@ -229,7 +234,7 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
       if (row < BN) {
         const int off = row * ROWB + (((q >> 1) ^ swz<BK>(row)) << 4) + (q & 1) * 8;
         s16x4 hi, lo;
-        split4(rb[i], hi, lo);
+        split4(xb[i], hi, lo);
         *reinterpret_cast<s16x4*>(&sB[s][0][off]) = hi;
         *reinterpret_cast<s16x4*>(&sB[s][1][off]) = lo;
       }
@@ -264,8 +269,13 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
 
   const int total = ntl * nk;
   load_geometry(0);
-  load_kt(next_kt());
-  store_kt(0);
+  load_kt(next_kt(), ra, rb);
+  store_kt(0, ra, rb);
+  if (PD == 2 && total > 1) {  // K-tile 1 into the second set
+    const int jn = 1 / nk;
+    if (jn != geo) load_geometry(jn);
+    load_kt(next_kt(), ra2, rb2);
+  }
   __syncthreads();
 
   const int arow = wave * 32 + l32;
@@ -279,11 +289,27 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
     for (int kt = 0; kt < nk; ++kt, ++gk) {
       const int s = NS == 2 ? (gk & 1) : 0;
       const bool pf = gk + 1 < total;
-      if (pf) {
-        const int jn = (gk + 1) / nk;
+      if constexpr (PD == 1) {
+        if (pf) {
+          const int jn = (gk + 1) / nk;
+          if (jn != geo) load_geometry(jn);
+          load_kt(next_kt(), ra, rb);
+        }
+      } else if (gk + 2 < total) {  // K-tile gk + 2 into the set K-tile gk came from
+        const int jn = (gk + 2) / nk;
         if (jn != geo) load_geometry(jn);
-        load_kt(next_kt());
+        if (gk & 1)
+          load_kt(next_kt(), ra2, rb2);
+        else
+          load_kt(next_kt(), ra, rb);
       }
+      // the set holding K-tile gk + 1 (PD = 2: loaded one K-tile round ago)
+      auto store_next = [&](int st) {
+        if (PD == 1 || (gk & 1))
+          store_kt(st, ra, rb);
+        else
+          store_kt(st, ra2, rb2);
+      };
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {  // 16-deep MFMA steps: chunk 2 ks + h of a row
         const int aoff = arow * ROWB + (((2 * ks + h) ^ swz<BK>(arow)) << 4);
@@ -319,11 +345,11 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
         }
       }
       if constexpr (NS == 2) {
-        if (pf) store_kt(s ^ 1);
+        if (pf) store_next(s ^ 1);
         __syncthreads();
       } else {
         __syncthreads();  // every wave is done reading the stage
-        if (pf) store_kt(0);
+        if (pf) store_next(0);
         __syncthreads();
       }
     }
@@ -394,7 +420,8 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
 }
 
 // Plan: which instance, grid and K order; false = not this kernel (the caller's engines run).
-static bool split_plan(const clskd_conv_desc& d, SplitArgs& a, int& nt, int& bk, int& grid) {
+static bool split_plan(const clskd_conv_desc& d, SplitArgs& a, int& nt, int& bk, int& grid,
+                       int* cus_out = nullptr) {
   if (d.compute != CLSKD_F32 || d.in_dtype != CLSKD_F32 || d.out_dtype != CLSKD_F32) return false;
   if (d.accumulate || d.wlayout != CLSKD_WLAYOUT_NK || !d.vec4) return false;
   if (d.K % 16 || (int64_t)(d.K / 4) * 8 > 32 * 1024) return false;  // K padded to 16 (host)
@@ -431,9 +458,12 @@ static bool split_plan(const clskd_conv_desc& d, SplitArgs& a, int& nt, int& bk,
   const size_t tab = (size_t)2 * 128 * (16 + 16 + 8);
   const size_t lds = (bk == 64 ? 1 : 2) * 2 * (size_t)(128 + 32 * nt) * bk * 2 + tab + (size_t)(d.K / 4) * 8;
   const int per_cu = lds * 3 <= 160 * 1024 ? 3 : lds * 2 <= 160 * 1024 ? 2 : 1;
-  // CLSKD_SPLIT_GRID caps the CUs the grid spans (experiments build: A/B inside the concurrent step)
+  // CLSKD_SPLIT_GRID caps the CUs the grid spans (A/B inside the concurrent step; tests: many
+  // tiles per workgroup, so K-tile prefetch crosses tiles)
   const int gcap = knob(KNOB_SPLIT_GRID);
-  const int cap = per_cu * (gcap > 0 && gcap < ncu ? gcap : ncu);
+  const int cus = gcap > 0 && gcap < ncu ? gcap : ncu;
+  if (cus_out) *cus_out = cus;
+  const int cap = per_cu * cus;
   grid = a.ntiles < cap ? a.ntiles : cap;
   if (d.stats && grid > a.nblk128) return false;  // (never: BM = 128 rows a tile)
   return true;
@@ -452,16 +482,51 @@ int launch_conv_split3(const clskd_conv_desc& d, hipStream_t st, bool* launched,
   *launched = false;
   if (!force && knob(KNOB_F32_SPLIT) != 1) return CLSKD_OK;
   SplitArgs a;
-  int nt = 0, bk = 0, grid = 0;
-  if (!split_plan(d, a, nt, bk, grid)) return CLSKD_OK;
+  int nt = 0, bk = 0, grid = 0, cus = 0;
+  if (!split_plan(d, a, nt, bk, grid, &cus)) return CLSKD_OK;
+  // CLSKD_SPLIT_OCC=1 (default): the grid holds only the workgroups the instance's register
+  // occupancy keeps resident (the plan counts LDS only: up to 3 per CU, while 208-404 VGPRs allow
+  // 1-2), so every workgroup is resident from the start and walks its tiles as one persistent
+  // stream (0: the LDS-sized grid; -0.02..-0.04 ms per C2 step, profiles/r5_split_pd_ab.txt)
+  const bool occ = knob(KNOB_SPLIT_OCC) == 1;
+  auto occ_cap = [&](const void* k, size_t lds) {
+    static std::mutex mu;
+    static std::unordered_map<const void*, int> per;
+    int nb;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      auto it = per.find(k);
+      if (it == per.end()) {
+        nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, lds) != hipSuccess || nb < 1) nb = 1;
+        per[k] = nb;
+      } else {
+        nb = it->second;
+      }
+    }
+    return grid < nb * cus ? grid : nb * cus;
+  };
   const size_t ctab_bytes = (size_t)(d.K / 4) * 8;
+  // CLSKD_SPLIT_PD=2: two K-tiles in flight where the stream has two — measured slower inside the
+  // C2 step (profiles/r5_split_pd_ab.txt: +0.07 ms even where occupancy is unchanged, +0.23 ms on
+  // every instance), so one (1) is the default
+  const bool pd2 = knob(KNOB_SPLIT_PD) == 2 && d.K / bk >= 2;
 #define SP3(NT_, BK_)                                                                  \
   do {                                                                                 \
     constexpr int NS_ = BK_ == 64 ? 1 : 2;                                             \
-    auto k = conv_split3_kernel<NT_, 4, BK_, NS_>;                                     \
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), ctab_bytes, st, a);                   \
-    note_kernel_fn((const void*)k);                                                    \
-    note_kernel("conv_split3_kernel<%d,4,%d,%d>", NT_, BK_, NS_);                      \
+    if (pd2) {                                                                         \
+      auto k = conv_split3_kernel<NT_, 4, BK_, NS_, 2>;                                \
+      if (occ) grid = occ_cap((const void*)k, ctab_bytes);                              \
+      hipLaunchKernelGGL(k, dim3(grid), dim3(256), ctab_bytes, st, a);                 \
+      note_kernel_fn((const void*)k);                                                  \
+      note_kernel("conv_split3_kernel<%d,4,%d,%d,2>", NT_, BK_, NS_);                  \
+    } else {                                                                           \
+      auto k = conv_split3_kernel<NT_, 4, BK_, NS_>;                                   \
+      if (occ) grid = occ_cap((const void*)k, ctab_bytes);                              \
+      hipLaunchKernelGGL(k, dim3(grid), dim3(256), ctab_bytes, st, a);                 \
+      note_kernel_fn((const void*)k);                                                  \
+      note_kernel("conv_split3_kernel<%d,4,%d,%d>", NT_, BK_, NS_);                    \
+    }                                                                                  \
   } while (0)
   if (bk == 64) {
     if (nt == 1) SP3(1, 64);

@@ -284,6 +284,12 @@ inline void wgrad_plan(const clskd_conv_desc& d, int& S, int64_t& rps) {
   S = (int)cdiv(M, rps);
 }
 
+// wgrad_x3.hip: the split-product engine for CLSKD_F32X3 descriptors (same partial layout)
+bool wgrad_x3_takes(const clskd_conv_desc& d);
+void wgrad_x3_plan(const clskd_conv_desc& d, int& S, int64_t& rps);
+void launch_wgrad_x3(const clskd_conv_desc& d, const float* dy, float* work, int S, int64_t rps,
+                     int want_bias, hipStream_t st);
+
 }  // namespace clskd
 
 using namespace clskd;
@@ -292,7 +298,10 @@ extern "C" int64_t clskd_conv2d_wgrad_workspace(const clskd_conv_desc* dp) {
   if (!dp) return -1;
   int S;
   int64_t rps;
-  wgrad_plan(*dp, S, rps);
+  if (wgrad_x3_takes(*dp))
+    wgrad_x3_plan(*dp, S, rps);
+  else
+    wgrad_plan(*dp, S, rps);
   return (int64_t)S * dp->N * dp->K + (int64_t)S * dp->N;
 }
 
@@ -306,7 +315,11 @@ extern "C" int clskd_conv2d_wgrad(const clskd_conv_desc* dp, const float* dy, fl
   CLSKD_CHECK_SHAPE(d.nseg >= 1 && d.nseg <= CLSKD_MAX_SEGS && d.K % 4 == 0, "conv2d_wgrad: nseg/K");
   int S;
   int64_t rps;
-  wgrad_plan(d, S, rps);
+  const bool x3 = wgrad_x3_takes(d);
+  if (x3)
+    wgrad_x3_plan(d, S, rps);
+  else
+    wgrad_plan(d, S, rps);
   const int64_t need = (int64_t)S * d.N * d.K + (int64_t)S * d.N;
   CLSKD_CHECK_SHAPE(work_elems >= need, "conv2d_wgrad: workspace %lld < %lld", (long long)work_elems,
                     (long long)need);
@@ -316,13 +329,17 @@ extern "C" int clskd_conv2d_wgrad(const clskd_conv_desc* dp, const float* dy, fl
                           d.seg[s].sF % 4 == 0 && d.seg[s].sT % 4 == 0,
                       "conv2d_wgrad: vec4 segment %d not 16-byte aligned", s);
   }
-  WgradArgs a{d, dy, work, rps, S, dbias ? 1 : 0};
   hipStream_t st = as_stream(stream);
-  dim3 grid(S, (unsigned)cdiv(d.N, WG_TN), (unsigned)cdiv(d.K, WG_TK));
-  if (d.vec4)
-    hipLaunchKernelGGL((conv_wgrad_f32<true>), grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_wgrad_f32<false>), grid, dim3(256), 0, st, a);
+  if (x3) {
+    launch_wgrad_x3(d, dy, work, S, rps, dbias ? 1 : 0, st);
+  } else {
+    WgradArgs a{d, dy, work, rps, S, dbias ? 1 : 0};
+    dim3 grid(S, (unsigned)cdiv(d.N, WG_TN), (unsigned)cdiv(d.K, WG_TK));
+    if (d.vec4)
+      hipLaunchKernelGGL((conv_wgrad_f32<true>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_wgrad_f32<false>), grid, dim3(256), 0, st, a);
+  }
   CLSKD_LAUNCH_CHECK("conv2d_wgrad");
   const int64_t per = (int64_t)d.N * d.K;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(per, 32)), dim3(256), 0, st, work, S,

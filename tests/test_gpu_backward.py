@@ -67,6 +67,76 @@ def test_conv_wgrad_and_accumulate_against_torch():
                                atol=1e-5)
 
 
+def _wgrad_ref(segs, taps, sf, Fo, dy):
+    """fp64 dW[n, tap, c] and dbias[n] of the implicit-GEMM conv (zero padding)."""
+    x = torch.cat([s.double() for s in segs], 3)
+    B, Fi, T, Cin = x.shape
+    dy = dy.double()
+    dw = torch.zeros(dy.shape[-1], len(taps), Cin, dtype=torch.float64)
+    for ti, (dF, dT) in enumerate(taps):
+        fi = torch.arange(Fo) * sf + dF
+        tt = torch.arange(T) + dT
+        vf = (fi >= 0) & (fi < Fi)
+        vt = (tt >= 0) & (tt < T)
+        sub = torch.zeros(B, Fo, T, Cin, dtype=torch.float64)
+        sub[:, vf.nonzero()[:, 0][:, None], vt.nonzero()[:, 0][None, :]] = \
+            x[:, fi[vf][:, None], tt[vt][None, :]]
+        dw[:, ti] = torch.einsum("bftn,bftc->nc", dy, sub)
+    return dw, dy.sum((0, 1, 2))
+
+
+X3_CASES = {
+    # name: (segment channels, N, taps, stride_f, B, Fi, Fo, T)
+    "n2_k96_2seg": ((16, 16), 2, [(dF, -kt) for dF in (1, 0, -1) for kt in (0, 1)], 1, 3, 20, 20, 301),
+    "n8_k20_cin2": ((2,), 8, [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)], 2, 2, 65, 33, 211),
+    "n16_k80": ((8,), 16, [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)], 2, 2, 64, 32, 301),
+    "n24_k384_2seg": ((32, 32), 24, [(dF, -kt) for dF in (1, 0, -1) for kt in (0, 1)], 1, 2, 9, 9, 157),
+    "n64_k320": ((32,), 64, [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)], 2, 2, 16, 8, 301),
+    "n100_k48": ((12,), 100, [(kf - 1, kt - 1) for kf in range(3) for kt in range(3)], 1, 1, 7, 7, 45),
+}
+
+
+@pytest.mark.parametrize("case", sorted(X3_CASES))
+def test_conv_wgrad_split_products_against_fp64(case):
+    """The split-product weight gradient (csrc/wgrad_x3.hip: descriptors of compute CLSKD_F32X3,
+    inside ops.split_products(..., wgrad=True)) against fp64 torch: every n-tile width (N 2 - 100,
+    two n-tiles at 100), vec4 and scalar gathers (Cin 2), polyphase two-segment decoder taps,
+    stride 2, several row splits (M up to 85 k) and partial chunks.  Bound: 3 x bf16 products
+    drop terms <= ~3 * 2^-18 relative each; the sums over 1e4-1e5 rows of random-sign terms stay
+    far inside rel L2 2e-5 (dbias sums the hi + lo parts exactly: 2e-6).  Bitwise repeatable."""
+    from clskd import ops
+    segc, N, taps, sf, B, Fi, Fo, T = X3_CASES[case]
+    g = torch.Generator().manual_seed(7)
+    segs = [torch.randn(B, Fi, T, c, generator=g) * 1.3 + 0.1 for c in segc]
+    dy = torch.randn(B, Fo, T, N, generator=g)
+    ref_w, ref_b = _wgrad_ref(segs, taps, sf, Fo, dy)
+    Cin = sum(segc)
+    Kp = -(-len(taps) * Cin // 16) * 16
+    dyd = dy.to(DEV)
+    dsegs = [ops.seg_bftc(s.to(DEV)) for s in segs]
+    outs = []
+    for _ in range(2):
+        dw = torch.full((N, Kp), float("nan"), device=DEV)
+        db = torch.full((N,), float("nan"), device=DEV)
+        with ops.split_products(False, wgrad=True):
+            ops.conv_wgrad(dsegs, taps, B, Fo, T, N, dyd, ops.OutMap(Fo * T * N, T * N, N), dw, db,
+                           stride_f=sf)
+        outs.append((dw.clone(), db.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    dw, db = outs[0]
+    got = dw[:, :len(taps) * Cin].reshape(N, len(taps), Cin)
+    assert torch.isfinite(dw).all()
+    ew, eb = _rel(_np(got), ref_w.numpy()), _rel(_np(db), ref_b.numpy())
+    print(f"{case}: rel L2 dW {ew:.2e} dbias {eb:.2e}")
+    assert ew < 2e-5, ew
+    assert eb < 2e-6, eb
+    # the exact engine on the same descriptor agrees to the split bound too
+    dwe = torch.empty(N, Kp, device=DEV)
+    ops.conv_wgrad(dsegs, taps, B, Fo, T, N, dyd, ops.OutMap(Fo * T * N, T * N, N), dwe, None,
+                   stride_f=sf)
+    assert _rel(_np(got), _np(dwe[:, :len(taps) * Cin].reshape(N, len(taps), Cin))) < 2e-5
+
+
 @pytest.mark.parametrize("H", [32, 128])
 def test_lstm_bwd_against_torch(H):
     """BPTT kernel: gate gradients for given dh, pre-activations rebuilt from the h history."""

@@ -66,6 +66,23 @@ def test_split_conv_against_torch(case, bk, split_on):
         _lib.set_knob("CLSKD_SPLIT_BK", prev_bk)
 
 
+@pytest.mark.parametrize("pd,grid,occ", [(1, 0, 0), (2, 0, 0), (2, 1, 0), (1, 1, 0), (2, 0, 1), (1, 1, 1)])
+@pytest.mark.parametrize("case", sorted(SPLIT_CASES))
+def test_split_conv_prefetch_depth(case, pd, grid, occ, split_on):
+    """Gather prefetch depth (CLSKD_SPLIT_PD: 1 K-tile ahead — the default — or 2 wherever the
+    K-tile count allows) with the grid capped to one CU (CLSKD_SPLIT_GRID=1): every workgroup walks
+    many tiles, so the prefetch of K-tiles k + 1 / k + 2 crosses tile boundaries.  CLSKD_SPLIT_OCC
+    1 (default) / 0: the grid of register-resident workgroups / of the LDS bound."""
+    from clskd import _lib
+    prev = {k: _lib.set_knob(k, v) for k, v in
+            (("CLSKD_SPLIT_PD", pd), ("CLSKD_SPLIT_GRID", grid), ("CLSKD_SPLIT_OCC", occ))}
+    try:
+        _split_case(case)
+    finally:
+        for k, v in prev.items():
+            _lib.set_knob(k, v)
+
+
 @pytest.mark.parametrize("case", sorted(SPLIT_CASES))
 def test_split_descriptor_against_torch(case):
     """The same layers asked for per descriptor (compute CLSKD_F32X3, ops.split_products: how the

@@ -51,6 +51,11 @@ for st in ${STEPS:-suite bench}; do
       done;;
     hostprof) rc=0; timeout -k 10 300 python $R/tools/host_profile.py --steps 20 --top 60 > $O/hostprof.txt 2>&1 || rc=$?; ok $rc hostprof
       head -3 $O/hostprof.txt;;
+    trace_train_exec)
+      ( cd /tmp && export TMPDIR=/tmp
+        rc=0; timeout -k 10 400 rocprofv3 --kernel-trace --marker-trace --stats --output-format csv -d $O/tetrace -o run -- python3 $R/bench.py --train --launch exec --steps 10 --warmup 3 --no-cpu-baseline > $O/tetrace.log 2>&1 || rc=$?; ok $rc trace_train_exec ) || exit $?
+      python3 $R/tools/region_stats.py $O/tetrace/run 10 $O/train_exec_region_stats.json > $O/train_exec_region_stats.txt 2>&1 || true
+      grep '^{' $O/tetrace.log | cut -c1-300;;
     trace_train)
       ( cd /tmp && export TMPDIR=/tmp
         rc=0; timeout -k 10 400 rocprofv3 --kernel-trace --marker-trace --stats --output-format csv -d $O/ttrace -o run -- python3 $R/bench.py --train --steps 10 --warmup 3 --no-cpu-baseline > $O/ttrace.log 2>&1 || rc=$?; ok $rc trace_train ) || exit $?
