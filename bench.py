@@ -860,7 +860,12 @@ def main():
                                      "student fp32 storage/accumulation with its fp32 convs as "
                                      "3 x bf16 split-product MFMA (CLSKD_F32X3, <= ~3*2^-18 per "
                                      "product; the reference trains with TF32 matmuls); "
-                                     "STFT, LSTM recurrence, BN, losses fp32"
+                                     "STFT, LSTM recurrence, BN, losses fp32" +
+                                     ({0: "; training step exact fp32",
+                                       1: "; weight gradients on split products",
+                                       3: "; taped forward, data and weight gradients on split "
+                                          "products"}.get(getattr(kd.student, "train_split", 0), "")
+                                      if args.train else "")
                                      if kd.student.compute == "f32x3" else
                                      "teacher+ReviewKD GEMMs bf16 MFMA operands / fp32 accumulate; "
                                      "student, STFT/iSTFT, LSTM recurrence, BN, losses fp32")

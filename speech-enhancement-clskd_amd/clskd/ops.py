@@ -291,9 +291,9 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
     d.oB, d.oF, d.oT, d.oNhi, d.oNlo = omap.oB, omap.oF, omap.oT, omap.oNhi, omap.oNlo
     d.nlo = min(omap.nlo, 1 << 30)
     d.of_mul, d.of_add = omap.of_mul, omap.of_add
-    # split products: fp32 layers of a split_products(True) forward (not the accumulating
-    # data-gradient sums of the backward)
-    d.compute = _lib.F32X3 if (split and in_dt == _lib.F32 and not accumulate) else in_dt
+    # split products: fp32 layers launched inside split_products(True) (the accumulating
+    # data-gradient sums of a split-product backward too)
+    d.compute = _lib.F32X3 if (split and in_dt == _lib.F32) else in_dt
     d.in_dtype = in_dt
     d.out_dtype = _dt(out)
     d.kvec = kvec

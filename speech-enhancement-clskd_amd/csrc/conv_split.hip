@@ -369,6 +369,7 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
         float v = acc[t][r];
         if constexpr (XACC) v += accx[t][r];
         if (nok && ro >= 0) {
+          if (d.accumulate) v += outp[ro + coff];  // data-gradient sums (no statistics then)
           sm += v;
           sq = fmaf(v, v, sq);
           outp[ro + coff] = v;
@@ -423,7 +424,8 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
 static bool split_plan(const clskd_conv_desc& d, SplitArgs& a, int& nt, int& bk, int& grid,
                        int* cus_out = nullptr) {
   if (d.compute != CLSKD_F32 || d.in_dtype != CLSKD_F32 || d.out_dtype != CLSKD_F32) return false;
-  if (d.accumulate || d.wlayout != CLSKD_WLAYOUT_NK || !d.vec4) return false;
+  if (d.wlayout != CLSKD_WLAYOUT_NK || !d.vec4) return false;
+  if (d.accumulate && (d.stats || d.bn_fold)) return false;  // (the exact engines refuse it too)
   if (d.K % 16 || (int64_t)(d.K / 4) * 8 > 32 * 1024) return false;  // K padded to 16 (host)
   if (d.nseg < 1 || d.nseg > 4 || d.stride_t < 1) return false;
   nt = d.N <= 32 ? 1 : d.N <= 64 ? 2 : 4;

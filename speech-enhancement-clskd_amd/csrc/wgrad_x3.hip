@@ -89,7 +89,9 @@ struct RowPos {
   }
 };
 
-template <int TN, bool VEC4>
+// DEPTH: 32-row chunks in flight per wave (1: the next chunk's gather under this chunk's MFMAs;
+// 2: two register sets, the gathers of the next two chunks in flight)
+template <int TN, bool VEC4, int DEPTH>
 __global__ __launch_bounds__(256) void conv_wgrad_x3(const WgradX3Args a) {
   const clskd_conv_desc& d = a.d;
   constexpr int QN = TN / 4;             // dY side: column quads per row
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(const WgradX3Args a) {
   // dY side: column quad nq (n = n0 + 4 nq .. + 3), rows RPL * (lane / QN) ..
   const int nq = lane % QN, dg = lane / QN;
 
-  float av[8][4], dv[RPL][4];
+  float av[8][4], dv[RPL][4], av2[8][4], dv2[RPL][4];  // av2 / dv2: the second set (DEPTH 2)
   f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
   const bool bias_lane = a.want_bias && blockIdx.z == 0;
 
@@ -154,7 +156,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(const WgradX3Args a) {
     coff[j] = cval[j] ? (int64_t)(n / d.nlo) * d.oNhi + (int64_t)(n % d.nlo) * d.oNlo : 0;
   }
 
-  auto gather = [&](unsigned rc) {  // chunk rows rc .. rc + 31 into av / dv
+  auto gather = [&](unsigned rc, float (&xa)[8][4], float (&xd)[RPL][4]) {  // chunk rows rc .. rc + 31
     {
       RowPos p;
       const unsigned m0 = rc + 8 * rg;
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(const WgradX3Args a) {
           f32x4 v = {0.f, 0.f, 0.f, 0.f};
           if (fok && ti >= 0 && ti < kT[0]) v = *reinterpret_cast<const f32x4*>(rp + rr * sTs);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) av[rr][j] = v[j];
+          for (int j = 0; j < 4; ++j) xa[rr][j] = v[j];
         }
       } else {
 #pragma unroll
@@ -184,7 +186,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(const WgradX3Args a) {
             if (valid && kvalid[0] && fi >= 0 && fi < kF[0] && ti >= 0 && ti < kT[0])
               v = *reinterpret_cast<const f32x4*>(qbase + p.b * ksB[0] + p.fo * sFs + p.to * sTs);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) av[rr][j] = v[j];
+            for (int j = 0; j < 4; ++j) xa[rr][j] = v[j];
           } else {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -193,7 +195,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(const WgradX3Args a) {
               if (valid && kvalid[j] && fi >= 0 && fi < kF[j] && ti >= 0 && ti < kT[j])
                 v = kp[j][p.b * ksB[j] + (int64_t)p.fo * d.stride_f * ksF[j] +
                           (int64_t)p.to * d.stride_t * ksT[j] + ke[j].off];
-              av[rr][j] = v;
+              xa[rr][j] = v;
             }
           }
           if (valid) p.next(d.Fo, d.To);
@@ -225,18 +227,19 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(const WgradX3Args a) {
           if (!fast) p.next(d.Fo, d.To);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) dv[rr][j] = v[j];
+        for (int j = 0; j < 4; ++j) xd[rr][j] = v[j];
         if (bias_lane) bsum += v;
       }
     }
   };
 
-  auto stage = [&]() {  // registers -> this wave's hi / lo planes, transposed (rows contiguous)
+  // registers -> this wave's hi / lo planes, transposed (rows contiguous)
+  auto stage = [&](const float (&xa)[8][4], const float (&xd)[RPL][4]) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       float col[8];
 #pragma unroll
-      for (int rr = 0; rr < 8; ++rr) col[rr] = av[rr][c];
+      for (int rr = 0; rr < 8; ++rr) col[rr] = xa[rr][c];
       s16x8 hi, lo;
       split_col<8>(col, hi, lo);
       const int off = (kq * 4 + c) * X3_CS + 8 * rg;
@@ -247,7 +250,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(const WgradX3Args a) {
     for (int c = 0; c < 4; ++c) {
       float col[RPL];
 #pragma unroll
-      for (int rr = 0; rr < RPL; ++rr) col[rr] = dv[rr][c];
+      for (int rr = 0; rr < RPL; ++rr) col[rr] = xd[rr][c];
       dvec hi, lo;
       split_col<RPL>(col, hi, lo);
       const int off = (nq * 4 + c) * X3_CS + RPL * dg;
@@ -263,13 +266,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(const WgradX3Args a) {
 #pragma unroll
     for (int j = 0; j < KB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  unsigned rc = r_begin + (unsigned)wave * X3_RB;
-  if (rc < r_end) gather(rc);
   const int l16 = lane & 15, lg = lane >> 4;
-  for (; rc < r_end; rc += 4 * X3_RB) {
-    stage();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: planes written
-    if (rc + 4 * X3_RB < r_end) gather(rc + 4 * X3_RB);  // in flight under the MFMAs
+  auto compute = [&]() {  // this wave's planes -> 3 x (NB x KB) MFMAs
     s16x8 bh[KB], bl[KB];
 #pragma unroll
     for (int j = 0; j < KB; ++j) {
@@ -289,6 +287,28 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(const WgradX3Args a) {
 #pragma unroll
       for (int j = 0; j < KB; ++j) acc[i][j] = mfma1632(al, bh[j], acc[i][j]);
     }
+  };
+
+  constexpr unsigned STEP = 4 * X3_RB;  // the workgroup's four waves take consecutive chunks
+  unsigned rc = r_begin + (unsigned)wave * X3_RB;
+  if (rc < r_end) gather(rc, av, dv);
+  if (DEPTH == 2 && rc + STEP < r_end) gather(rc + STEP, av2, dv2);
+  bool second = false;  // DEPTH 2: this chunk sits in the second set
+  for (; rc < r_end; rc += STEP) {
+    if (second)
+      stage(av2, dv2);
+    else
+      stage(av, dv);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: planes written
+    const unsigned nx = rc + DEPTH * STEP;  // refill the set just staged: in flight under the MFMAs
+    if (nx < r_end) {
+      if (second)
+        gather(nx, av2, dv2);
+      else
+        gather(nx, av, dv);
+    }
+    compute();
+    if (DEPTH == 2) second = !second;
   }
 
   // ---- the four waves' tiles added in LDS (fixed order), partial tile out: work[split][n][k] ----
@@ -322,6 +342,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(const WgradX3Args a) {
 
 inline int x3_tn(int N) { return N <= 16 ? 16 : N <= 32 ? 32 : 64; }
 
+template <int TN, bool VEC4, int DEPTH>
+void launch_x3(dim3 grid, hipStream_t st, const WgradX3Args& a) {
+  constexpr size_t lds = (size_t)4 * (2 * X3_TK * X3_CS + 2 * TN * X3_CS) * 2;
+  static_assert(lds >= (size_t)4 * TN * X3_TK * 4 + 4 * 64 * 16, "the reduction fits the planes");
+  const void* k = (const void*)conv_wgrad_x3<TN, VEC4, DEPTH>;
+  static const bool attr = lds <= 64 * 1024 ||
+      hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+  (void)attr;
+  hipLaunchKernelGGL((conv_wgrad_x3<TN, VEC4, DEPTH>), grid, dim3(256), lds, st, a);
+  note_kernel_fn(k);
+}
+
 }  // namespace
 
 // rows per split (a multiple of the 128 rows one workgroup round covers): about 1024 workgroups
@@ -343,33 +375,21 @@ bool wgrad_x3_takes(const clskd_conv_desc& d) {
 void launch_wgrad_x3(const clskd_conv_desc& d, const float* dy, float* work, int S, int64_t rps,
                      int want_bias, hipStream_t st) {
   WgradX3Args a{d, dy, work, (int)rps, S, want_bias};
+  const int depth = knob(KNOB_WGRAD_DEPTH) == 2 ? 2 : 1;
   const int tn = x3_tn(d.N);
   dim3 grid(S, (unsigned)cdiv(d.N, tn), (unsigned)cdiv(d.K, X3_TK));
-#define WX3(TN_)                                                                               \
-  do {                                                                                         \
-    constexpr size_t lds = (size_t)4 * (2 * X3_TK * X3_CS + 2 * TN_ * X3_CS) * 2;             \
-    static_assert(lds >= (size_t)4 * TN_ * X3_TK * 4 + 4 * 64 * 16, "reduction fits the planes"); \
-    if (d.vec4) {                                                                              \
-      auto k = conv_wgrad_x3<TN_, true>;                                                       \
-      static const bool attr = lds <= 64 * 1024 || hipFuncSetAttribute((const void*)k,          \
-          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;                  \
-      (void)attr;                                                                              \
-      hipLaunchKernelGGL(k, grid, dim3(256), lds, st, a);                                      \
-      note_kernel_fn((const void*)k);                                                          \
-    } else {                                                                                   \
-      auto k = conv_wgrad_x3<TN_, false>;                                                      \
-      static const bool attr = lds <= 64 * 1024 || hipFuncSetAttribute((const void*)k,          \
-          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;                  \
-      (void)attr;                                                                              \
-      hipLaunchKernelGGL(k, grid, dim3(256), lds, st, a);                                      \
-      note_kernel_fn((const void*)k);                                                          \
-    }                                                                                          \
-    note_kernel("conv_wgrad_x3<%d,%d>", TN_, d.vec4 ? 1 : 0);                                  \
-  } while (0)
-  if (tn == 16) WX3(16);
-  else if (tn == 32) WX3(32);
-  else WX3(64);
-#undef WX3
+  const bool v = d.vec4 != 0;
+  if (tn == 16) {
+    if (v) depth == 2 ? launch_x3<16, true, 2>(grid, st, a) : launch_x3<16, true, 1>(grid, st, a);
+    else depth == 2 ? launch_x3<16, false, 2>(grid, st, a) : launch_x3<16, false, 1>(grid, st, a);
+  } else if (tn == 32) {
+    if (v) depth == 2 ? launch_x3<32, true, 2>(grid, st, a) : launch_x3<32, true, 1>(grid, st, a);
+    else depth == 2 ? launch_x3<32, false, 2>(grid, st, a) : launch_x3<32, false, 1>(grid, st, a);
+  } else {
+    if (v) depth == 2 ? launch_x3<64, true, 2>(grid, st, a) : launch_x3<64, true, 1>(grid, st, a);
+    else depth == 2 ? launch_x3<64, false, 2>(grid, st, a) : launch_x3<64, false, 1>(grid, st, a);
+  }
+  note_kernel("conv_wgrad_x3<%d,%d,%d>", tn, v ? 1 : 0, depth);
 }
 
 }  // namespace clskd

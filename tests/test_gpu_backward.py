@@ -96,14 +96,25 @@ X3_CASES = {
 }
 
 
+@pytest.mark.parametrize("depth", [1, 2])
 @pytest.mark.parametrize("case", sorted(X3_CASES))
-def test_conv_wgrad_split_products_against_fp64(case):
+def test_conv_wgrad_split_products_against_fp64(case, depth):
     """The split-product weight gradient (csrc/wgrad_x3.hip: descriptors of compute CLSKD_F32X3,
     inside ops.split_products(..., wgrad=True)) against fp64 torch: every n-tile width (N 2 - 100,
     two n-tiles at 100), vec4 and scalar gathers (Cin 2), polyphase two-segment decoder taps,
     stride 2, several row splits (M up to 85 k) and partial chunks.  Bound: 3 x bf16 products
     drop terms <= ~3 * 2^-18 relative each; the sums over 1e4-1e5 rows of random-sign terms stay
-    far inside rel L2 2e-5 (dbias sums the hi + lo parts exactly: 2e-6).  Bitwise repeatable."""
+    far inside rel L2 2e-5 (dbias sums the fp32 values: 2e-6).  Bitwise repeatable.  depth: row
+    chunks in flight per wave (CLSKD_WGRAD_DEPTH)."""
+    from clskd import _lib, ops
+    prev = _lib.set_knob("CLSKD_WGRAD_DEPTH", depth)
+    try:
+        _x3_case(case)
+    finally:
+        _lib.set_knob("CLSKD_WGRAD_DEPTH", prev)
+
+
+def _x3_case(case):
     from clskd import ops
     segc, N, taps, sf, B, Fi, Fo, T = X3_CASES[case]
     g = torch.Generator().manual_seed(7)

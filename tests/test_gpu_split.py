@@ -92,7 +92,7 @@ def test_split_descriptor_against_torch(case):
         _split_case(case)
 
 
-def _split_case(case):
+def _split_case(case, accumulate=False):
     from clskd import ops
     segc, N, taps, sf, Fi, Fo, of_mul, of_add = SPLIT_CASES[case]
     g = torch.Generator().manual_seed(len(case) * 7 + N)
@@ -107,17 +107,19 @@ def _split_case(case):
     ref = _ref(segs, taps, sf, Fo, T, wq, bias)
     mag = _ref([s.abs() for s in segs], taps, sf, Fo, T, wq.abs(), bias.abs())
     Fout = Fo * of_mul
-    out = torch.zeros(B, Fout, T, N, device=DEV)
-    stats_on = N <= 128
+    prior = (torch.randn(B, Fout, T, N, generator=g) if accumulate else torch.zeros(B, Fout, T, N)).to(DEV)
+    out = prior.clone()
+    stats_on = N <= 128 and not accumulate
     nblk = ops.conv_mblocks(B, Fo, T)
     st = torch.full((nblk * N * 2,), float("nan"), device=DEV, dtype=torch.float64) if stats_on else None
     ops.conv([ops.seg_bftc(s.to(DEV)) for s in segs], taps, B, Fo, T, N, wp, bias.to(DEV), out,
-             ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add), stride_f=sf, stats=st)
+             ops.OutMap(Fout * T * N, T * N, N, of_mul=of_mul, of_add=of_add), stride_f=sf, stats=st,
+             accumulate=accumulate)
     kname = ops.conv_kernel_of_last_launch()
     if kname.startswith("conv_direct") or kname.startswith("conv_pointwise"):
         pytest.skip(f"{case}: dispatched to {kname} (not an MFMA layer)")
     assert kname.startswith("conv_split3_kernel"), kname
-    o = out.double().cpu()[:, of_add::of_mul]
+    o = (out.double() - prior.double()).cpu()[:, of_add::of_mul]
     err = (o - ref).abs()
     bound = 2e-5 * mag + 1e-7
     worst = float((err / bound).max())
@@ -125,7 +127,8 @@ def _split_case(case):
           f"median rel {float((err / mag.clamp_min(1e-30)).median()):.2e}")
     assert worst <= 1.0
     if of_mul > 1:
-        assert torch.all(out.cpu()[:, (of_add + 1) % of_mul::of_mul] == 0)
+        other = slice((of_add + 1) % of_mul, None, of_mul)
+        assert torch.equal(out.cpu()[:, other], prior.cpu()[:, other])
     if stats_on:
         stc = st.view(nblk, N, 2).cpu()
         assert torch.isfinite(stc).all(), "every statistics slot must be written"
@@ -133,6 +136,16 @@ def _split_case(case):
         np.testing.assert_allclose(S.numpy(), ref.sum((0, 1, 2)).numpy(), rtol=1e-5,
                                    atol=1e-5 * float(mag.sum((0, 1, 2)).max()))
         np.testing.assert_allclose(Q.numpy(), (ref * ref).sum((0, 1, 2)).numpy(), rtol=5e-5)
+
+
+@pytest.mark.parametrize("case", sorted(SPLIT_CASES))
+def test_split_conv_accumulate_against_torch(case):
+    """accumulate=True (out += conv: the data-gradient sums of a split-product backward, config C3
+    in precision 'mixed') on the split engine, asked for per descriptor: the increment against
+    fp64 at the split bound, the other polyphase parity rows untouched."""
+    from clskd import ops
+    with ops.split_products(True):
+        _split_case(case, accumulate=True)
 
 
 def test_split_bn_fold_against_torch(split_on):

@@ -1,6 +1,7 @@
 """Per-call census of the C3 backward's GEMM launches: every `ops.conv_wgrad` (weight gradient)
 and `ops.conv` (data gradient / forward) call of one eager training step, each bracketed by
-device synchronisation and HIP events, grouped by shape.  Diagnostic only (serialises the step).
+device synchronisation and HIP events (a sleep kernel ahead of the first event hides the host
+launch latency), grouped by shape.  Diagnostic only (serialises the step).
 
     python tools/bwd_census.py [--precision mixed] [--top 40]
 """
@@ -42,6 +43,9 @@ def main():
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s = torch.cuda.current_stream()
+            # keep the device busy while the host enqueues the call, so the event pair spans
+            # device time only (not the Python launch latency of a short launch)
+            torch.cuda._sleep(2_000_000)
             e0.record(s)
             r = fn(*a, **k)
             e1.record(s)

@@ -1,6 +1,7 @@
 """Weight-gradient microbenchmark on the C3 student's shapes (B=16, T=643/644: the layers of
 tools/bwd_census.py): the exact fp32 engine (conv_wgrad_f32) against the split-product engine
-(csrc/wgrad_x3.hip), `iters` back-to-back launches timed with HIP events.  Diagnostic only.
+(csrc/wgrad_x3.hip, one and two chunks in flight per wave: CLSKD_WGRAD_DEPTH), `iters`
+back-to-back launches timed with HIP events.  Diagnostic only.
 
     python tools/wgrad_micro.py [--iters 20] [--only n2_k96,n8_k20]
 """
@@ -39,7 +40,9 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     names = [n for n in CASES if not args.only or n in args.only.split(",")]
-    tot = {False: 0.0, True: 0.0}
+    from clskd import _lib
+    legs = [("f32", False, 1), ("x3", True, 1), ("x3d2", True, 2)]
+    tot = {lg[0]: 0.0 for lg in legs}
     for name in names:
         segc, N, taps, sf, Fi, Fo, T = CASES[name]
         B = args.B
@@ -52,7 +55,9 @@ def main():
         db = torch.empty(N, device=dev)
         om = ops.OutMap(Fo * T * N, T * N, N)
         row = []
-        for split in (False, True):
+        for leg, split, depth in legs:
+            _lib.set_knob("CLSKD_WGRAD_DEPTH", depth)
+
             def run():
                 with ops.split_products(False, wgrad=split):
                     ops.conv_wgrad(segs, taps, B, Fo, T, N, dy, om, dw, db, stride_f=sf)
@@ -66,10 +71,11 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / args.iters
-            tot[split] += us
-            row.append(f"{'x3' if split else 'f32'} {us:8.1f} us {2.0 * B * Fo * T * N * K / us / 1e6:7.1f} TF/s")
+            tot[leg] += us
+            row.append(f"{leg} {us:8.1f} us {2.0 * B * Fo * T * N * K / us / 1e6:6.1f} TF/s")
         print(f"{name:10s} M={B * Fo * T:8d} N={N:4d} K={K:5d}  " + "  ".join(row), flush=True)
-    print(f"total: f32 {tot[False]:.1f} us  x3 {tot[True]:.1f} us")
+    _lib.set_knob("CLSKD_WGRAD_DEPTH", 1)
+    print("total: " + "  ".join(f"{k} {v:.1f} us" for k, v in tot.items()))
 
 
 if __name__ == "__main__":
