@@ -47,9 +47,11 @@ def _mark(label, stream):
 # A/B switch: CLSKD_STUDENT_SPLIT=0 keeps the student of precision 'mixed' on the exact fp32 engines
 _STUDENT_SPLIT = os.environ.get("CLSKD_STUDENT_SPLIT", "1") == "1"
 # the training step of a 'mixed' student (C3): bit 0 — weight gradients on split products
-# (csrc/wgrad_x3.hip); bit 1 — the taped forward's and the backward's non-accumulating fp32 convs
-# too.  CLSKD_TRAIN_SPLIT=0 keeps the whole training step exact (A/B)
-_TRAIN_SPLIT = int(os.environ.get("CLSKD_TRAIN_SPLIT", "3"))
+# (csrc/wgrad_x3.hip, the default: 20.2 -> 19.0 ms per step); bit 1 — the taped forward's and the
+# backward's data-gradient fp32 convs too (measured +0.2 ms on top: the split engine displaces
+# the halo / pointwise kernels of the narrow layers).  CLSKD_TRAIN_SPLIT=0: the whole training
+# step exact (A/B, profiles/r5_train_split_ab.txt)
+_TRAIN_SPLIT = int(os.environ.get("CLSKD_TRAIN_SPLIT", "1"))
 _SERIAL = os.environ.get("CLSKD_SERIAL_STREAMS") == "1"  # diagnostic: the whole step on one stream
 # conv_gemm8's persistent grid inside the concurrent four-stream step: 7/8 of the CUs (224 of
 # 256), so the wide teacher / ReviewKD GEMMs leave a CU per XCD group to the other streams'

@@ -163,20 +163,37 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32(const WgradArgs a) {
     a.work[(int64_t)a.S * d.N * Kp + (int64_t)split * d.N + n0 + tid] = bacc;
 }
 
-// dw[i] (+)= sum_s work[s][i]: 32 elements x 8 lanes per block; lane l sums splits l, l+8, ...
-// then a fixed xor tree over the 8 lanes (deterministic for a given S)
+// dw[i] (+)= sum_s work[s][i]: 16 consecutive elements x 16 split lanes per block (a wave reads
+// four 64-B runs per load); split lane sl sums splits sl, sl + 16, ... (eight loads in flight per
+// round), then the 16 lane sums are added in a fixed order in LDS (deterministic for a given S).
+// Round 4's 32 x 8 layout read 8 splits of one element per 8 lanes (32-B pieces) and carried a
+// chain of S / 8 dependent loads: 16.8 us per launch in the C3 census.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ work, int S,
                                                           int64_t per, float* __restrict__ dw,
                                                           int accumulate) {
-  const int l = threadIdx.x & 7;
-  const int64_t i = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const int e = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int64_t i = (int64_t)blockIdx.x * 16 + e;
   float s = 0.f;
-  if (i < per)
-    for (int j = l; j < S; j += 8) s += work[(int64_t)j * per + i];
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  s += __shfl_xor(s, 4, 64);
-  if (l == 0 && i < per) dw[i] = accumulate ? dw[i] + s : s;
+  if (i < per) {
+    int j = sl;
+    for (; j + 7 * 16 < S; j += 8 * 16) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = work[(int64_t)(j + 16 * u) * per + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; j < S; j += 16) s += work[(int64_t)j * per + i];
+  }
+  __shared__ float red[16][17];
+  red[sl][e] = s;
+  __syncthreads();
+  if (sl == 0 && i < per) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][e];
+    dw[i] = accumulate ? dw[i] + t : t;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -342,10 +359,10 @@ extern "C" int clskd_conv2d_wgrad(const clskd_conv_desc* dp, const float* dy, fl
   }
   CLSKD_LAUNCH_CHECK("conv2d_wgrad");
   const int64_t per = (int64_t)d.N * d.K;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(per, 32)), dim3(256), 0, st, work, S,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(per, 16)), dim3(256), 0, st, work, S,
                      per, dw, accumulate & 1);
   if (dbias)
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(d.N, 32)), dim3(256), 0, st,
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(d.N, 16)), dim3(256), 0, st,
                        work + (int64_t)S * per, S, (int64_t)d.N, dbias, (accumulate >> 1) & 1);
   CLSKD_LAUNCH_CHECK("conv2d_wgrad_reduce");
   return CLSKD_OK;

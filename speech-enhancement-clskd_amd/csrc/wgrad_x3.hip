@@ -375,8 +375,13 @@ bool wgrad_x3_takes(const clskd_conv_desc& d) {
 void launch_wgrad_x3(const clskd_conv_desc& d, const float* dy, float* work, int S, int64_t rps,
                      int want_bias, hipStream_t st) {
   WgradX3Args a{d, dy, work, (int)rps, S, want_bias};
-  const int depth = knob(KNOB_WGRAD_DEPTH) == 2 ? 2 : 1;
   const int tn = x3_tn(d.N);
+  // chunks in flight per wave (CLSKD_WGRAD_DEPTH 1 / 2; 0 = by instance): two for the vec4
+  // gathers of the narrow tiles, where the second register set keeps the occupancy and the
+  // gather latency is what a chunk waits on (n2-n32: -18..-22 %); one for TN = 64 (328 VGPRs at
+  // two: one wave per SIMD, +40..50 %) and the scalar gathers (+70 %) (tools/wgrad_micro.py)
+  const int dk = knob(KNOB_WGRAD_DEPTH);
+  const int depth = dk == 1 || dk == 2 ? dk : (d.vec4 && tn <= 32 ? 2 : 1);
   dim3 grid(S, (unsigned)cdiv(d.N, tn), (unsigned)cdiv(d.K, X3_TK));
   const bool v = d.vec4 != 0;
   if (tn == 16) {

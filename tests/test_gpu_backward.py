@@ -96,7 +96,7 @@ X3_CASES = {
 }
 
 
-@pytest.mark.parametrize("depth", [1, 2])
+@pytest.mark.parametrize("depth", [0, 1, 2])
 @pytest.mark.parametrize("case", sorted(X3_CASES))
 def test_conv_wgrad_split_products_against_fp64(case, depth):
     """The split-product weight gradient (csrc/wgrad_x3.hip: descriptors of compute CLSKD_F32X3,
@@ -105,7 +105,7 @@ def test_conv_wgrad_split_products_against_fp64(case, depth):
     stride 2, several row splits (M up to 85 k) and partial chunks.  Bound: 3 x bf16 products
     drop terms <= ~3 * 2^-18 relative each; the sums over 1e4-1e5 rows of random-sign terms stay
     far inside rel L2 2e-5 (dbias sums the fp32 values: 2e-6).  Bitwise repeatable.  depth: row
-    chunks in flight per wave (CLSKD_WGRAD_DEPTH)."""
+    chunks in flight per wave (CLSKD_WGRAD_DEPTH; 0 = the per-instance default)."""
     from clskd import _lib, ops
     prev = _lib.set_knob("CLSKD_WGRAD_DEPTH", depth)
     try:

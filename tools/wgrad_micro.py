@@ -1,6 +1,7 @@
 """Weight-gradient microbenchmark on the C3 student's shapes (B=16, T=643/644: the layers of
 tools/bwd_census.py): the exact fp32 engine (conv_wgrad_f32) against the split-product engine
-(csrc/wgrad_x3.hip, one and two chunks in flight per wave: CLSKD_WGRAD_DEPTH), `iters`
+(csrc/wgrad_x3.hip, one / two chunks in flight per wave and the default per-instance pick:
+CLSKD_WGRAD_DEPTH 1 / 2 / 0), `iters`
 back-to-back launches timed with HIP events.  Diagnostic only.
 
     python tools/wgrad_micro.py [--iters 20] [--only n2_k96,n8_k20]
@@ -41,7 +42,7 @@ def main():
     dev = torch.device("cuda", 0)
     names = [n for n in CASES if not args.only or n in args.only.split(",")]
     from clskd import _lib
-    legs = [("f32", False, 1), ("x3", True, 1), ("x3d2", True, 2)]
+    legs = [("f32", False, 0), ("x3d1", True, 1), ("x3d2", True, 2), ("x3", True, 0)]
     tot = {lg[0]: 0.0 for lg in legs}
     for name in names:
         segc, N, taps, sf, Fi, Fo, T = CASES[name]
@@ -74,7 +75,7 @@ def main():
             tot[leg] += us
             row.append(f"{leg} {us:8.1f} us {2.0 * B * Fo * T * N * K / us / 1e6:6.1f} TF/s")
         print(f"{name:10s} M={B * Fo * T:8d} N={N:4d} K={K:5d}  " + "  ".join(row), flush=True)
-    _lib.set_knob("CLSKD_WGRAD_DEPTH", 1)
+    _lib.set_knob("CLSKD_WGRAD_DEPTH", 0)
     print("total: " + "  ".join(f"{k} {v:.1f} us" for k, v in tot.items()))
 
 
