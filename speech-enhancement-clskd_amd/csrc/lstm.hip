@@ -402,6 +402,126 @@ __global__ __launch_bounds__(NKS * H) void lstm_bwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// The same BPTT for H = 16 / 32 in ONE wave per (weight set, sequence): lane (u, ks) of the
+// S = 64 / H lanes of unit u.  Every lane of a unit forms the unit's gate gradients (redundant,
+// no divergence) and writes its share of them (S = 2: {i, f} / {g, o}; S = 4: one gate) to
+// dgates and LDS; after a wave-local LDS wait (no workgroup barrier: one wave, in-order LDS) each
+// lane multiplies its G / S gate rows of W_hh's column u with da and the S lanes combine by DPP
+// into (W_hh^T da_t)_u.  A step's operands (4 pre-activations, c_t, c_{t-1}, dh_in) are fetched
+// four steps ahead into a register ring, so the serial chain waits on no global load.  The
+// 4-wave kernel above spent ~820 ns per step (its barrier and the 8-lane reduction); this one is
+// bound by the chain's VALU / LDS latency (tools/lstm_micro.py).
+// ------------------------------------------------------------------------------------------
+template <int H>
+__global__ __launch_bounds__(64) void lstm_bwd_wave_kernel(
+    const float* __restrict__ pre, int64_t p_ws, int64_t p_seq, int64_t p_t,
+    const float* __restrict__ dh, int64_t d_ws, int64_t d_seq, int64_t d_t,
+    const float* __restrict__ whh, int T, float* __restrict__ cbuf,
+    float* __restrict__ dg, int64_t g_ws, int64_t g_seq, int64_t g_t) {
+  constexpr int G = 4 * H;
+  constexpr int S = 64 / H;  // lanes per unit
+  constexpr int GW = G / S;  // gate rows per lane in the W_hh^T reduction
+  static_assert((S == 2 || S == 4) && GW % 4 == 0, "lstm_bwd_wave: H = 16 or 32");
+  const int lane = threadIdx.x;
+  const int u = lane / S, ks = lane % S;
+  const int ws = blockIdx.y, seq = blockIdx.x;
+  __shared__ __attribute__((aligned(16))) float das[2][G];
+  f32x2l wc[GW / 2];  // packed pairs: the reduction runs as v_pk_fma_f32
+#pragma unroll
+  for (int j = 0; j < GW; ++j) wc[j / 2][j % 2] = whh[((int64_t)ws * G + ks * GW + j) * H + u];
+  const float* pp = pre + ws * p_ws + seq * p_seq + u;
+  const float* dp = dh + ws * d_ws + seq * d_seq + u;
+  float* cp = cbuf + ((int64_t)ws * gridDim.x + seq) * (int64_t)T * H + u;
+  float* gp = dg + ws * g_ws + seq * g_seq + u;
+  // phase 1: the cell scan, by every lane of the unit (identical values to the same address;
+  // each lane reads back only what it wrote itself)
+  {
+    float c = 0.f;
+#pragma unroll 4
+    for (int t = 0; t < T; ++t) {
+      const float* q = pp + (int64_t)t * p_t;
+      const float ig = sigm_fast(q[0]), fg = sigm_fast(q[H]);
+      const float gg = fmaf(2.f, sigm_fast(2.f * q[2 * H]), -1.f);
+      c = fg * c + ig * gg;
+      cp[(int64_t)t * H] = c;
+    }
+  }
+  struct Op {
+    float q0, q1, q2, q3, cc, cpv, dhin;
+  };
+  auto fetch = [&](int t, Op& o) {
+    if (t < 0) return;
+    const float* q = pp + (int64_t)t * p_t;
+    o.q0 = q[0];
+    o.q1 = q[H];
+    o.q2 = q[2 * H];
+    o.q3 = q[3 * H];
+    o.cc = cp[(int64_t)t * H];
+    o.cpv = t > 0 ? cp[(int64_t)(t - 1) * H] : 0.f;
+    o.dhin = dp[(int64_t)t * d_t];
+  };
+  float dc = 0.f, dhr = 0.f;
+  auto step = [&](int t, const Op& o) {
+    const int buf = t & 1;
+    const float ig = sigm_fast(o.q0), fg = sigm_fast(o.q1);
+    const float gg = fmaf(2.f, sigm_fast(2.f * o.q2), -1.f), og = sigm_fast(o.q3);
+    const float tc = tanh_fast(o.cc);
+    const float dht = o.dhin + dhr;
+    dc = fmaf(dht * og, 1.f - tc * tc, dc);
+    const float a_i = dc * gg * ig * (1.f - ig);
+    const float a_f = dc * o.cpv * fg * (1.f - fg);
+    const float a_g = dc * ig * (1.f - gg * gg);
+    const float a_o = dht * tc * og * (1.f - og);
+    dc *= fg;
+    float* go = gp + (int64_t)t * g_t;
+    if constexpr (S == 2) {  // lane 0 of the unit: gates i, f; lane 1: g, o
+      const float v0 = ks ? a_g : a_i, v1 = ks ? a_o : a_f;
+      das[buf][(2 * ks) * H + u] = v0;
+      das[buf][(2 * ks + 1) * H + u] = v1;
+      go[(2 * ks) * H] = v0;
+      go[(2 * ks + 1) * H] = v1;
+    } else {
+      const float v = ks == 0 ? a_i : ks == 1 ? a_f : ks == 2 ? a_g : a_o;
+      das[buf][ks * H + u] = v;
+      go[ks * H] = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: da of step t written
+    f32x2l a0 = {0.f, 0.f}, a1 = {0.f, 0.f};  // four independent chains, two per packed FMA
+    const f32x4* dv = reinterpret_cast<const f32x4*>(&das[buf][ks * GW]);
+#pragma unroll
+    for (int j = 0; j < GW / 4; ++j) {
+      const f32x4 v = dv[j];
+      const f32x2l v01 = {v[0], v[1]}, v23 = {v[2], v[3]};
+      a0 = wc[2 * j] * v01 + a0;
+      a1 = wc[2 * j + 1] * v23 + a1;
+    }
+    const f32x2l a = a0 + a1;
+    float s = a[0] + a[1];
+    s += dpp<DPP_XOR1>(s);
+    if constexpr (S == 4) s += dpp<DPP_XOR2>(s);
+    dhr = s;
+  };
+  Op o0{}, o1{}, o2{}, o3{};
+  fetch(T - 1, o0);
+  fetch(T - 2, o1);
+  fetch(T - 3, o2);
+  fetch(T - 4, o3);
+  for (int t = T - 1; t >= 0; t -= 4) {
+    step(t, o0);
+    fetch(t - 4, o0);
+    if (t - 1 < 0) break;
+    step(t - 1, o1);
+    fetch(t - 5, o1);
+    if (t - 2 < 0) break;
+    step(t - 2, o2);
+    fetch(t - 6, o2);
+    if (t - 3 < 0) break;
+    step(t - 3, o3);
+    fetch(t - 7, o3);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // One recurrence step with carried state (streaming inference, config C5): for every (weight
 // set, sequence), gates = gx + W_hh h, c = f c + i g, h = o tanh(c), with h and c updated in
 // place (h read into LDS before any write).  Same activation functions as the offline
@@ -521,6 +641,18 @@ extern "C" int clskd_lstm_bwd(const float* pre, int64_t p_ws, int64_t p_seq, int
 #define LSTM_BWD(H_, NKS_)                                                                     \
   hipLaunchKernelGGL((lstm_bwd_kernel<H_, NKS_>), grid, dim3(NKS_ * H_), 0, st, pre, p_ws, p_seq, \
                      p_t, dh, d_ws, d_seq, d_t, whh, T, cbuf, dgates, g_ws, g_seq, g_t)
+  // H = 16 / 32: the single-wave kernel unless CLSKD_LSTM_BWD_WAVE=0 (A/B)
+  const bool wave = knob(KNOB_LSTM_BWD_WAVE) != 0;
+  if (wave && (H == 16 || H == 32)) {
+    if (H == 16)
+      hipLaunchKernelGGL(lstm_bwd_wave_kernel<16>, grid, dim3(64), 0, st, pre, p_ws, p_seq, p_t, dh,
+                         d_ws, d_seq, d_t, whh, T, cbuf, dgates, g_ws, g_seq, g_t);
+    else
+      hipLaunchKernelGGL(lstm_bwd_wave_kernel<32>, grid, dim3(64), 0, st, pre, p_ws, p_seq, p_t, dh,
+                         d_ws, d_seq, d_t, whh, T, cbuf, dgates, g_ws, g_seq, g_t);
+    CLSKD_LAUNCH_CHECK("lstm_bwd");
+    return CLSKD_OK;
+  }
   switch (H) {
     case 16: LSTM_BWD(16, 8); break;
     case 32: LSTM_BWD(32, 8); break;

@@ -148,9 +148,20 @@ def _x3_case(case):
     assert _rel(_np(got), _np(dwe[:, :len(taps) * Cin].reshape(N, len(taps), Cin))) < 2e-5
 
 
-@pytest.mark.parametrize("H", [32, 128])
-def test_lstm_bwd_against_torch(H):
-    """BPTT kernel: gate gradients for given dh, pre-activations rebuilt from the h history."""
+@pytest.mark.parametrize("H,wave", [(16, 1), (32, 1), (32, 0), (128, 1)])
+def test_lstm_bwd_against_torch(H, wave):
+    """BPTT kernel: gate gradients for given dh, pre-activations rebuilt from the h history.
+    H = 16 / 32 run the single-wave kernel (wave 1, default; T = 57 ends mid register ring) or
+    the 4-wave one (CLSKD_LSTM_BWD_WAVE=0)."""
+    from clskd import _lib, ops
+    prev = _lib.set_knob("CLSKD_LSTM_BWD_WAVE", wave)
+    try:
+        _lstm_bwd_case(H)
+    finally:
+        _lib.set_knob("CLSKD_LSTM_BWD_WAVE", prev)
+
+
+def _lstm_bwd_case(H):
     from clskd import ops
     g = torch.Generator().manual_seed(2)
     nseq, T = 3, 57
