@@ -842,7 +842,8 @@ def main():
                                   if args.launch == "eager" else
                                   "C++ step executor (clskd_exec_launch" +
                                   ("_ahead: two captures alternating, each step's teacher chain "
-                                   "overlapping the previous step's tail" if args.ahead else "") +
+                                   "overlapping the previous step's tail"
+                                   if args.ahead and not args.train else "") +
                                   "): the captured step replayed on 4 HIP streams along its "
                                   "dependency edges "
                                   f"({executor.info['kernels']} kernels, "

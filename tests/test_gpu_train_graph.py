@@ -114,3 +114,38 @@ def test_train_graph_replays_interleaved_with_eager_forwards(launch):
         assert torch.equal(got, ref)
         outs.append(got)
     assert not torch.equal(outs[0], outs[1])  # the second replay changed the parameters
+
+
+def test_pack_maps_match_builds():
+    """The trained student's parameter groups are re-packed by one index_gather from the flat
+    parameter buffer (model._pack_group, maps probed on the first build): after Adam steps every
+    mapped group's outputs equal the torch packing of a fresh student holding the same
+    parameters, bitwise."""
+    from clskd import config as cfg
+    from clskd.data import synthetic_pairs
+    from clskd.model import DCCRN
+    from clskd.train import FlatAdam, FlatParams
+    from test_gpu_parity import _kd
+    n, c = synthetic_pairs(4, 16000, seed=43)
+    X, y = torch.from_numpy(n).to(DEV), torch.from_numpy(c).to(DEV)
+    kd = _kd().set_precision("mixed")
+    flat = FlatParams(kd.student)
+    opt = FlatAdam(flat, lr=6e-4)
+    for _ in range(3):
+        kd.train_step((X, y), flat, opt)
+    s = kd.student
+    mapped = [k for k, v in s._pmaps.items() if v]
+    assert len(mapped) >= 8, sorted(s._pmaps)
+    fresh = DCCRN(masking_mode="E", use_clstm=True, **cfg.STUDENT).to(DEV)
+    fresh.load_state_dict(s.state_dict())
+    flat.bump_versions()  # force the re-packs through the maps
+    calls = {"enc": "_enc_w", "dec": "_dec_w", "lstm": "_lstm_w"}
+    for key in mapped:
+        fn = calls[key[0]]
+        got = getattr(s, fn)(*key[1:])
+        ref = getattr(fresh, fn)(*key[1:])
+        got = [got] if isinstance(got, torch.Tensor) else list(got)
+        ref = [ref] if isinstance(ref, torch.Tensor) else list(ref)
+        assert len(got) == len(ref)
+        for a, b in zip(got, ref):
+            assert a.shape == b.shape and torch.equal(a, b), key
