@@ -475,11 +475,12 @@ def main():
     if args.launch is None:
         # C2 (one rank): the step captured once and replayed by the C++ executor with the
         # teacher_ahead overlap (clskd.graph.AheadStepExecutor): the eager device schedule at
-        # ~1.7 ms of host time per step instead of ~3.9 ms of Python launches (same-box A/B,
-        # profiles/r5_exec_ab.txt: 5.28 vs 5.28 ms per step).  C3 stays eager: its captured
-        # replays measured 23.5 ms (C++ executor) / 24.6 ms (hipGraphLaunch) against 20.6 ms
-        # eager (gpurun_out r4p / DESIGN.md section 13)
-        args.launch = "exec" if not (args.train or args.spkd) else "eager"
+        # ~0.6 ms of host time per step instead of ~3.9 ms of Python launches (same-box A/B,
+        # profiles/r5_exec_ab.txt: 5.28 vs 5.28 ms per step).  C3 (one rank): the captured
+        # training step replayed by the executor, one replay in flight (TrainStepExecutor):
+        # 17.8-18.0 ms at ~2.5 ms of host time against 18.15 ms eager with 14 ms of Python
+        # launches (profiles/r5_train_split_ab.txt)
+        args.launch = "exec" if not args.spkd else "eager"
     if args.spkd or world > 1:
         # the C4 leg launches eagerly (its capture is not wired yet); multi-rank runs launch
         # eagerly too (no graph capture beside the RCCL communicator's watchdog)

@@ -396,7 +396,13 @@ class TrainStepGraph(StepGraph):
 class TrainStepExecutor(TrainStepGraph, StepExecutor):
     """TrainStepGraph replayed by the C++ step executor (clskd_exec_launch) on the step's four
     streams instead of hipGraphLaunch (whose host cost grows with the node count: ~20 us per node
-    on ROCm 7.2, ~1,000 nodes here)."""
+    on ROCm 7.2, ~1,000 nodes here).
+
+    One replay in flight (CLSKD_EXEC_INFLIGHT, default 1 here): the host enqueues step i + 1 once
+    step i has finished.  Letting two training steps overlap measured slower — their memory-bound
+    backward kernels contend (19.8-20.0 vs 17.8-18.0 ms per step, profiles/r5_train_split_ab.txt)."""
+
+    inflight = int(os.environ.get("CLSKD_EXEC_INFLIGHT", "1"))
 
 
 class CapturedCall:
