@@ -699,6 +699,11 @@ def main():
     if world == 1 and not args.train and not args.spkd and not args.graph:
         # after the timed region: one capture of the step, its kernel nodes counted
         step_counts = launches_per_step(kd, Xs[0], Ys[0])
+    elif args.train and args.launch == "exec" and executor is not None:
+        # the captured training step the executor replays: its kernel nodes
+        step_counts = dict(kernels=int(executor.info["kernels"]),
+                           memsets=int(executor.info.get("memsets", 0)),
+                           memcpys=int(executor.info.get("memcpys", 0)))
 
     if rank == 0:
         frames = world * bsz * T * args.steps
