@@ -420,6 +420,16 @@ __global__ __launch_bounds__(NW * 64) void conv_split3_kernel(const SplitArgs ar
   }
 }
 
+// LDS stages of an instance: two (stores of K-tile k + 1 beside the MFMAs of k, one barrier per
+// K-tile) except the 64-deep tiles, which take one stage to fit two or three workgroups per CU —
+// unless CLSKD_SPLIT_NS2=1 (default) and nt >= 2: those instances keep one workgroup per CU
+// resident anyway (260-404 VGPRs), so their second stage costs no occupancy
+static int split_stages(int bk, int nt) {
+  if (bk != 64) return 2;
+  const int k = knob(KNOB_SPLIT_NS2);  // 2: every 64-deep instance (A/B: nt 1 drops to one WG/CU)
+  return (k == 1 && nt >= 2) || k == 2 ? 2 : 1;
+}
+
 // Plan: which instance, grid and K order; false = not this kernel (the caller's engines run).
 static bool split_plan(const clskd_conv_desc& d, SplitArgs& a, int& nt, int& bk, int& grid,
                        int* cus_out = nullptr) {
@@ -458,7 +468,8 @@ static bool split_plan(const clskd_conv_desc& d, SplitArgs& a, int& nt, int& bk,
   // 4-wave workgroups, as many per CU as LDS holds (up to three): more waves per SIMD hide more
   // of the gather latency
   const size_t tab = (size_t)2 * 128 * (16 + 16 + 8);
-  const size_t lds = (bk == 64 ? 1 : 2) * 2 * (size_t)(128 + 32 * nt) * bk * 2 + tab + (size_t)(d.K / 4) * 8;
+  const size_t lds = (size_t)split_stages(bk, nt) * 2 * (size_t)(128 + 32 * nt) * bk * 2 + tab +
+                     (size_t)(d.K / 4) * 8;
   const int per_cu = lds * 3 <= 160 * 1024 ? 3 : lds * 2 <= 160 * 1024 ? 2 : 1;
   // CLSKD_SPLIT_GRID caps the CUs the grid spans (A/B inside the concurrent step; tests: many
   // tiles per workgroup, so K-tile prefetch crosses tiles)
@@ -512,36 +523,33 @@ int launch_conv_split3(const clskd_conv_desc& d, hipStream_t st, bool* launched,
   // CLSKD_SPLIT_PD=2: two K-tiles in flight where the stream has two — measured slower inside the
   // C2 step (profiles/r5_split_pd_ab.txt: +0.07 ms even where occupancy is unchanged, +0.23 ms on
   // every instance), so one (1) is the default
-  const bool pd2 = knob(KNOB_SPLIT_PD) == 2 && d.K / bk >= 2;
-#define SP3(NT_, BK_)                                                                  \
-  do {                                                                                 \
-    constexpr int NS_ = BK_ == 64 ? 1 : 2;                                             \
-    if (pd2) {                                                                         \
-      auto k = conv_split3_kernel<NT_, 4, BK_, NS_, 2>;                                \
-      if (occ) grid = occ_cap((const void*)k, ctab_bytes);                              \
-      hipLaunchKernelGGL(k, dim3(grid), dim3(256), ctab_bytes, st, a);                 \
-      note_kernel_fn((const void*)k);                                                  \
-      note_kernel("conv_split3_kernel<%d,4,%d,%d,2>", NT_, BK_, NS_);                  \
-    } else {                                                                           \
-      auto k = conv_split3_kernel<NT_, 4, BK_, NS_>;                                   \
-      if (occ) grid = occ_cap((const void*)k, ctab_bytes);                              \
-      hipLaunchKernelGGL(k, dim3(grid), dim3(256), ctab_bytes, st, a);                 \
-      note_kernel_fn((const void*)k);                                                  \
-      note_kernel("conv_split3_kernel<%d,4,%d,%d>", NT_, BK_, NS_);                    \
-    }                                                                                  \
-  } while (0)
+  const int pd = knob(KNOB_SPLIT_PD) == 2 && d.K / bk >= 2 ? 2 : 1;
+  const int ns = split_stages(bk, nt);
+  auto go = [&](auto kern, int NT_, int BK_, int NS_) {
+    const void* k = (const void*)kern;
+    if (occ) grid = occ_cap(k, ctab_bytes);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), ctab_bytes, st, a);
+    note_kernel_fn(k);
+    if (pd == 2)
+      note_kernel("conv_split3_kernel<%d,4,%d,%d,2>", NT_, BK_, NS_);
+    else
+      note_kernel("conv_split3_kernel<%d,4,%d,%d>", NT_, BK_, NS_);
+  };
+#define SP3(NT_, BK_, NS_)                                                                  \
+  (pd == 2 ? go(conv_split3_kernel<NT_, 4, BK_, NS_, 2>, NT_, BK_, NS_)                     \
+           : go(conv_split3_kernel<NT_, 4, BK_, NS_, 1>, NT_, BK_, NS_))
   if (bk == 64) {
-    if (nt == 1) SP3(1, 64);
-    else if (nt == 2) SP3(2, 64);
-    else SP3(4, 64);
+    if (nt == 1) (ns == 2 ? SP3(1, 64, 2) : SP3(1, 64, 1));
+    else if (nt == 2) (ns == 2 ? SP3(2, 64, 2) : SP3(2, 64, 1));
+    else (ns == 2 ? SP3(4, 64, 2) : SP3(4, 64, 1));
   } else if (bk == 32) {
-    if (nt == 1) SP3(1, 32);
-    else if (nt == 2) SP3(2, 32);
-    else SP3(4, 32);
+    if (nt == 1) SP3(1, 32, 2);
+    else if (nt == 2) SP3(2, 32, 2);
+    else SP3(4, 32, 2);
   } else {
-    if (nt == 1) SP3(1, 16);
-    else if (nt == 2) SP3(2, 16);
-    else SP3(4, 16);
+    if (nt == 1) SP3(1, 16, 2);
+    else if (nt == 2) SP3(2, 16, 2);
+    else SP3(4, 16, 2);
   }
 #undef SP3
   *launched = true;

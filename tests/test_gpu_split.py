@@ -83,6 +83,20 @@ def test_split_conv_prefetch_depth(case, pd, grid, occ, split_on):
             _lib.set_knob(k, v)
 
 
+@pytest.mark.parametrize("ns2,grid", [(0, 0), (1, 0), (1, 1), (2, 0)])
+@pytest.mark.parametrize("case", sorted(SPLIT_CASES))
+def test_split_conv_lds_stages(case, ns2, grid, split_on):
+    """64-deep K-tiles on one LDS stage (CLSKD_SPLIT_NS2=0) or two (1, the default for the
+    instances of one resident workgroup per CU), also with many tiles per workgroup."""
+    from clskd import _lib
+    prev = {k: _lib.set_knob(k, v) for k, v in (("CLSKD_SPLIT_NS2", ns2), ("CLSKD_SPLIT_GRID", grid))}
+    try:
+        _split_case(case)
+    finally:
+        for k, v in prev.items():
+            _lib.set_knob(k, v)
+
+
 @pytest.mark.parametrize("case", sorted(SPLIT_CASES))
 def test_split_descriptor_against_torch(case):
     """The same layers asked for per descriptor (compute CLSKD_F32X3, ops.split_products: how the
