@@ -754,9 +754,13 @@ def main():
         # rocprofv3 kernel trace of the census range reports — is the span minus that
         iso_ms = max(iso_span_ms - disp_us * 1e-3, 0.5 * iso_span_ms)
         ach_iso = iso_fl / (iso_ms * 1e-3) / 1e12
+        # the live spans carry the same dispatch span: live_kernel_us is the kernel's own duration
+        # inside the concurrent step (rocprofv3's timed-range average of the instance)
+        live_ms = max(avg_ms - disp_us * 1e-3, 0.5 * avg_ms)
+        achieved = flops / n_l / (live_ms * 1e-3) / 1e12
         if hbm_bound:
             ach_bw = byt / (iso_ms * 1e-3) / 1e9
-            live_bw = byt / (avg_ms * 1e-3) / 1e9
+            live_bw = byt / (live_ms * 1e-3) / 1e9
             roof = dict(bound="hbm", kernel=name, achieved=round(ach_bw, 1), peak=PEAK_HBM_GBPS,
                         unit="GB/s", frac=round(ach_bw / PEAK_HBM_GBPS, 4),
                         achieved_tflops=round(ach_iso, 2), achieved_live=round(live_bw, 1),
@@ -773,9 +777,11 @@ def main():
                     frac_basis=("isolated: census-step average kernel duration (one stream, the "
                                 "timed steps' kernel instances): isolated_kernel_us = the HIP-event "
                                 "span isolated_avg_launch_us minus dispatch_span_us (the span of an "
-                                "empty launch); avg_launch_us / achieved_live: the same instance's "
-                                "event spans live in the timed concurrent steps"),
+                                "empty launch); live_kernel_us / achieved_live / frac_live: the same "
+                                "instance inside the timed concurrent steps, its event span "
+                                "avg_launch_us minus dispatch_span_us"),
                     avg_launch_us=round(avg_ms * 1e3, 2),
+                    live_kernel_us=round(live_ms * 1e3, 2),
                     algorithmic_gflop_per_launch=round(flops / n_l / 1e9, 3),
                     isolated_avg_launch_us=(round(census[name][1] / census[name][0] * 1e3, 2)
                                             if name in census else None),
