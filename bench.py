@@ -51,22 +51,20 @@ def _range_pop():
 
 
 def dispatch_span_us(dev, n=64):
-    """HIP-event span of a near-empty launch (a 1-element fill) on the current stream: what an
-    event pair around a launch measures beyond the kernel's own duration (command-processor
-    packet processing and wave launch; rocprofv3's kernel-trace duration excludes it).  Median of
-    n back-to-back launches, after one warm-up."""
-    from clskd import ops
+    """Event overhead of one event-timed launch: the span an event pair recorded around a launch
+    measures beyond the kernel's own duration (command-processor packet processing, wave
+    launch; a rocprofv3 kernel trace excludes it).  clskd_launch_timing_probe times n 1-element
+    fills both ways — events attached to the kernel's dispatch (hipExtLaunchKernel) and an event
+    pair around it — and the difference of the medians is the overhead (round 5 first subtracted
+    the whole fill span, which also removed the fill's own few microseconds)."""
+    import ctypes as C
+    from clskd import _lib
     t = torch.empty(1, device=dev)
-    ops.fill(t, 0.0)
-    evs = []
-    for _ in range(n):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        ops.fill(t, 0.0)
-        e1.record()
-        evs.append((e0, e1))
-    torch.cuda.synchronize(dev)
-    return float(np.median([a.elapsed_time(b) for a, b in evs])) * 1e3
+    out = (C.c_float * 2)()
+    _lib.check(_lib.load().clskd_launch_timing_probe(t.data_ptr(), n, out,
+                                                     torch.cuda.current_stream(dev).cuda_stream),
+               "launch_timing_probe")
+    return max(float(out[1]) - float(out[0]), 0.0)
 
 
 def launches_per_step(kd, X, y):
