@@ -64,6 +64,7 @@ def dispatch_span_us(dev, n=64):
     _lib.check(_lib.load().clskd_launch_timing_probe(t.data_ptr(), n, out,
                                                      torch.cuda.current_stream(dev).cuda_stream),
                "launch_timing_probe")
+    dispatch_span_us.probe = (round(float(out[0]), 2), round(float(out[1]), 2))
     return max(float(out[1]) - float(out[0]), 0.0)
 
 
@@ -785,6 +786,7 @@ def main():
                                             if name in census else None),
                     isolated_kernel_us=round(iso_ms * 1e3, 2),
                     dispatch_span_us=round(disp_us, 2),
+                    dispatch_probe_us=getattr(dispatch_span_us, "probe", None),
                     achieved_isolated=(round(census[name][2] / (census[name][1] * 1e-3) / 1e12, 2)
                                        if name in census else None),
                     conv_all_kernels=dict(

@@ -424,18 +424,22 @@ extern "C" int clskd_fill_f32(float* p, int64_t n, float value, void* stream) {
 extern "C" int clskd_launch_timing_probe(float* scratch, int32_t n, float* out, void* stream) {
   CLSKD_CHECK_ARG(scratch && out && n >= 1 && n <= 1024, "launch_timing_probe: bad argument");
   hipStream_t st = as_stream(stream);
-  std::vector<float> ext(n), span(n);
-  hipEvent_t e[4];
+  // issued back to back and synchronised once, like the census step's event-timed launches
+  // (an idle queue between launches adds wake-up latency the census never sees)
+  std::vector<hipEvent_t> e(4 * (size_t)n);
   for (auto& ev : e) CLSKD_CHECK_ARG(hipEventCreate(&ev) == hipSuccess, "launch_timing_probe: event");
   hipLaunchKernelGGL(fill_f32_kernel, dim3(1), dim3(64), 0, st, scratch, (int64_t)1, 0.f);  // warm
   for (int i = 0; i < n; ++i) {
-    hipEventRecord(e[2], st);
-    hipExtLaunchKernelGGL(fill_f32_kernel, dim3(1), dim3(64), 0, st, e[0], e[1], 0, scratch,
-                          (int64_t)1, 0.f);
-    hipEventRecord(e[3], st);
-    hipEventSynchronize(e[3]);
-    hipEventElapsedTime(&ext[i], e[0], e[1]);
-    hipEventElapsedTime(&span[i], e[2], e[3]);
+    hipEventRecord(e[4 * i + 2], st);
+    hipExtLaunchKernelGGL(fill_f32_kernel, dim3(1), dim3(64), 0, st, e[4 * i], e[4 * i + 1], 0,
+                          scratch, (int64_t)1, 0.f);
+    hipEventRecord(e[4 * i + 3], st);
+  }
+  hipStreamSynchronize(st);
+  std::vector<float> ext(n), span(n);
+  for (int i = 0; i < n; ++i) {
+    hipEventElapsedTime(&ext[i], e[4 * i], e[4 * i + 1]);
+    hipEventElapsedTime(&span[i], e[4 * i + 2], e[4 * i + 3]);
   }
   for (auto& ev : e) (void)hipEventDestroy(ev);
   CLSKD_LAUNCH_CHECK("launch_timing_probe");
