@@ -51,21 +51,26 @@ def _range_pop():
 
 
 def dispatch_span_us(dev, n=64):
-    """Event overhead of one event-timed launch: the span an event pair recorded around a launch
-    measures beyond the kernel's own duration (command-processor packet processing, wave
-    launch; a rocprofv3 kernel trace excludes it).  clskd_launch_timing_probe times n 1-element
-    fills both ways — events attached to the kernel's dispatch (hipExtLaunchKernel) and an event
-    pair around it — and the difference of the medians is the overhead (round 5 first subtracted
-    the whole fill span, which also removed the fill's own few microseconds)."""
-    import ctypes as C
-    from clskd import _lib
+    """Event overhead of one event-timed launch: what an event pair around a launch measures
+    beyond the kernel's own duration (command-processor packet processing and wave launch;
+    rocprofv3's kernel-trace duration excludes it).  The SMALLEST span of n back-to-back
+    1-element fills (after one warm-up): overhead plus a near-empty kernel.  Traced runs of this
+    round put the census spans 5.4-5.6 us above rocprof's durations of the same launches and a
+    fill's span 5.7 us above its own duration (profiles/README.md); a calibration against
+    dispatch-attached events (hipExtLaunchKernel) was tried and dropped: those events add packets
+    of their own and read 0-10 us depending on the tracer."""
+    from clskd import ops
     t = torch.empty(1, device=dev)
-    out = (C.c_float * 2)()
-    _lib.check(_lib.load().clskd_launch_timing_probe(t.data_ptr(), n, out,
-                                                     torch.cuda.current_stream(dev).cuda_stream),
-               "launch_timing_probe")
-    dispatch_span_us.probe = (round(float(out[0]), 2), round(float(out[1]), 2))
-    return max(float(out[1]) - float(out[0]), 0.0)
+    ops.fill(t, 0.0)
+    evs = []
+    for _ in range(n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ops.fill(t, 0.0)
+        e1.record()
+        evs.append((e0, e1))
+    torch.cuda.synchronize(dev)
+    return float(np.min([a.elapsed_time(b) for a, b in evs])) * 1e3
 
 
 def launches_per_step(kd, X, y):
@@ -786,7 +791,6 @@ def main():
                                             if name in census else None),
                     isolated_kernel_us=round(iso_ms * 1e3, 2),
                     dispatch_span_us=round(disp_us, 2),
-                    dispatch_probe_us=getattr(dispatch_span_us, "probe", None),
                     achieved_isolated=(round(census[name][2] / (census[name][1] * 1e-3) / 1e12, 2)
                                        if name in census else None),
                     conv_all_kernels=dict(

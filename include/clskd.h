@@ -500,11 +500,6 @@ int clskd_adam_step_dev(float* p, const float* g, float* m, float* v, int64_t n,
                         float beta1, float beta2, float eps, float weight_decay, int32_t* step,
                         float grad_scale, void* stream);
 int clskd_fill_f32(float* p, int64_t n, float value, void* stream);
-/* Timing calibration: n launches of a 1-element fill, each timed by events attached to the
- * kernel's own dispatch (hipExtLaunchKernel: the interval a kernel trace reports) and by an
- * ordinary event pair around it; out[0] / out[1] = the medians in us (synchronises `stream`).
- * No reference counterpart (benchmark plumbing). */
-int clskd_launch_timing_probe(float* scratch, int32_t n, float* out, void* stream);
 int clskd_axpy_f32(const float* x, float* y, int64_t n, float alpha, int32_t accumulate,
                    void* stream);
 

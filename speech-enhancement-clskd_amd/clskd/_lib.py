@@ -165,7 +165,6 @@ SIGNATURES = {
     "clskd_adam_step": (_i32, [_p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _f32, _p]),
     "clskd_adam_step_dev": (_i32, [_p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _p, _f32, _p]),
     "clskd_fill_f32": (_i32, [_p, _i64, _f32, _p]),
-    "clskd_launch_timing_probe": (_i32, [_p, _i32, _p, _p]),
     "clskd_axpy_f32": (_i32, [_p, _p, _i64, _f32, _i32, _p]),
     "clskd_bn_bwd_blocks": (_i32, [_i64, _i32]),
     "clskd_bn_bwd_workspace": (_i64, [_i32, _i32]),

@@ -17,9 +17,6 @@
 #include <stdlib.h>
 
 #include <algorithm>
-#include <vector>
-
-#include <hip/hip_ext.h>
 
 #include "common.h"
 
@@ -412,45 +409,6 @@ extern "C" int clskd_fill_f32(float* p, int64_t n, float value, void* stream) {
   if (n <= 0) return CLSKD_OK;
   hipLaunchKernelGGL(fill_f32_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, n, value);
   CLSKD_LAUNCH_CHECK("fill_f32");
-  return CLSKD_OK;
-}
-
-// Timing calibration (bench.py): n launches of a 1-element fill, each timed twice — by events the
-// runtime attaches to the kernel's own dispatch (hipExtLaunchKernelGGL start / stop: the kernel's
-// begin and end, the interval a rocprofv3 kernel trace reports) and by an ordinary event pair
-// recorded on the stream around it (what a caller's event-timed launch measures).  out[0] / out[1]
-// = medians in microseconds; out[1] - out[0] is the event overhead of one launch.  Synchronises
-// the stream; not for use under graph capture.
-extern "C" int clskd_launch_timing_probe(float* scratch, int32_t n, float* out, void* stream) {
-  CLSKD_CHECK_ARG(scratch && out && n >= 1 && n <= 1024, "launch_timing_probe: bad argument");
-  hipStream_t st = as_stream(stream);
-  // issued back to back and synchronised once, like the census step's event-timed launches
-  // (an idle queue between launches adds wake-up latency the census never sees)
-  std::vector<hipEvent_t> e(4 * (size_t)n);
-  for (auto& ev : e) CLSKD_CHECK_ARG(hipEventCreate(&ev) == hipSuccess, "launch_timing_probe: event");
-  hipLaunchKernelGGL(fill_f32_kernel, dim3(1), dim3(64), 0, st, scratch, (int64_t)1, 0.f);  // warm
-  // two separate series (the dispatch-attached events add packets of their own, so one launch
-  // is not timed both ways): kernel durations, then plain event spans
-  for (int i = 0; i < n; ++i)
-    hipExtLaunchKernelGGL(fill_f32_kernel, dim3(1), dim3(64), 0, st, e[4 * i], e[4 * i + 1], 0,
-                          scratch, (int64_t)1, 0.f);
-  for (int i = 0; i < n; ++i) {
-    hipEventRecord(e[4 * i + 2], st);
-    hipLaunchKernelGGL(fill_f32_kernel, dim3(1), dim3(64), 0, st, scratch, (int64_t)1, 0.f);
-    hipEventRecord(e[4 * i + 3], st);
-  }
-  hipStreamSynchronize(st);
-  std::vector<float> ext(n), span(n);
-  for (int i = 0; i < n; ++i) {
-    hipEventElapsedTime(&ext[i], e[4 * i], e[4 * i + 1]);
-    hipEventElapsedTime(&span[i], e[4 * i + 2], e[4 * i + 3]);
-  }
-  for (auto& ev : e) (void)hipEventDestroy(ev);
-  CLSKD_LAUNCH_CHECK("launch_timing_probe");
-  std::sort(ext.begin(), ext.end());
-  std::sort(span.begin(), span.end());
-  out[0] = ext[n / 2] * 1e3f;
-  out[1] = span[n / 2] * 1e3f;
   return CLSKD_OK;
 }
 
