@@ -446,7 +446,7 @@ def test_bn_bwd_against_torch(fold, prelu):
             outs.append((dx, dg, db, da))
     finally:
         _lib.set_knob("CLSKD_BN_BWD_FOLD", prev)
-    for t0, t1 in zip(outs[0], outs[1]):
+    for t0, t1 in list(zip(outs[0], outs[1]))[:4 if prelu else 3]:  # (da unwritten without PReLU)
         assert torch.equal(t0, t1)
     dx, dg, db, da = outs[0]
     assert _rel(_np(dx), xd.grad.numpy()) < 1e-5
