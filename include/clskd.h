@@ -199,11 +199,9 @@ const void* clskd_conv_last_kernel_fn(void);
  * (per-tile ticket, fp32 partial handed over write-through).  Deterministic for a fixed grid;
  * CLSKD_G8_SK=0 keeps the data-parallel tile deal. */
 int32_t clskd_conv_last_stream_k(void);
-/* Allocate the per-stream state of `stream`: the conv_gemm8 stream-K workspace (128 MiB partial
- * slabs + tickets) and the BatchNorm-backward fold accumulators (clskd_bn_bwd /
- * clskd_spkd_bn_bwd finalise in their reduce launch), all zero at rest.  Done implicitly by the
- * first use on a stream outside graph capture; hosts call it for a stream they are about to
- * capture on, so captured and eager launches take the same path. */
+/* Allocate the stream-K workspace of `stream` (128 MiB partial slabs + tickets, zero at rest).
+ * Done implicitly by the first conv on a stream outside graph capture; hosts call it for a stream
+ * they are about to capture on, so captured and eager launches take the same path. */
 int clskd_stream_prepare(void* stream);
 /* Direct-path helpers: padded output width NP of the direct layout, and whether an (N, K)
  * GEMM is served by the direct kernel (returns 1) — hosts pack CLSKD_WLAYOUT_DIRECT weights

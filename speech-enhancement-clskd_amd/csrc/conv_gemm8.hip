@@ -1164,12 +1164,6 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
 
 extern "C" int32_t clskd_conv_last_stream_k(void) { return clskd::g_last_sk; }
 
-namespace clskd {
-struct BnbState;
-const BnbState* bnb_state(hipStream_t st);  // norm_bwd.hip: the BatchNorm-backward fold state
-}  // namespace clskd
-
 extern "C" int clskd_stream_prepare(void* stream) {
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  return clskd::sk_workspace(st) && clskd::bnb_state(st) ? CLSKD_OK : CLSKD_E_HIP;
+  return clskd::sk_workspace(reinterpret_cast<hipStream_t>(stream)) ? CLSKD_OK : CLSKD_E_HIP;
 }

@@ -4,10 +4,7 @@
 // complex-LSTM output combine.  HBM-bound passes; statistics reductions in fp64 with fixed
 // orders (no float atomics), so every gradient is bitwise repeatable.
 #include <algorithm>
-#include <mutex>
-#include <unordered_map>
 
-#include "bnfold.h"
 #include "common.h"
 
 namespace clskd {
@@ -34,104 +31,12 @@ __device__ __forceinline__ f32x4 ld4<__bf16>(const __bf16* p) {
 //   dx = k1*dz + k2*x + k3   with k1 = gamma*rstd, k2 = -gamma*rstd^2*dgamma/n,
 //                              k3 = -gamma*rstd*dbeta/n + gamma*rstd^2*mean*dgamma/n
 // ------------------------------------------------------------------------------------------
-// ------------------------------------------------------------------------------------------
-// Folded finalize of the BatchNorm backward (round 5): the reduce launch also turns the batch
-// sums {sum dz, sum dz * xhat, sum over negative PReLU inputs} into the apply coefficients k,
-// dgamma / dbeta and dalpha — no bn_bwd_finalize / bn_bwd_alpha launches.  Same scheme as the
-// forward fold (bnfold.h): each block adds its fp64 per-channel values as exact int64 limbs with
-// agent-scope atomics into one of BNB_REPL replicas (integer addition: order-independent, so
-// bitwise repeatable), takes a ticket after its atomics are performed, and the last block reads
-// the replicas back with exchange(0) — leaving them zero for the next call on the stream — and
-// resets the ticket.  The state lives per stream (bnb_state); a launch captured on a stream
-// without one keeps the partials + finalize path.
-// ------------------------------------------------------------------------------------------
-constexpr int BNB_REPL = 8;
-constexpr int BNB_CMAX = 1024;
-
-struct BnbFold {
-  long long* acc;    // [REPL][C][3 values][3 limbs]; nullptr: write partials instead
-  unsigned* ticket;
-  int64_t rows;
-  int C;
-  const float* gamma;
-  const float* mean;
-  const float* var;
-  float eps;
-  float* dgamma;
-  float* dbeta;
-  float* k;          // [3][C]
-  float* dalpha;     // PReLU slope gradient or nullptr
-  int accumulate;
-};
-
-__device__ __forceinline__ void bnb_add(const BnbFold& f, int c, double B, double G, double A) {
-  long long* rep = f.acc + ((int64_t)(blockIdx.x % BNB_REPL) * f.C + c) * 9;
-  const double v[3] = {B, G, A};
-#pragma unroll
-  for (int w = 0; w < 3; ++w) {
-    long long q2, q1, q0;
-    bnf_limbs(v[w], q2, q1, q0);
-    __hip_atomic_fetch_add(rep + 3 * w, q2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(rep + 3 * w + 1, q1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(rep + 3 * w + 2, q0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// every thread of the block, after its bnb_add calls (uniform control flow)
-__device__ __forceinline__ void bnb_finish(const BnbFold& f) {
-  __shared__ int last;
-  __shared__ double asum[256];
-  const int tid = threadIdx.x;
-  // ordering as in bnfold_commit: no-return agent atomics stay in vmcnt until performed
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned tk = __hip_atomic_fetch_add(f.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = tk == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  double al = 0.0;
-  const double n = (double)f.rows;
-  for (int c = tid; c < f.C; c += blockDim.x) {
-    long long L[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
-    for (int r = 0; r < BNB_REPL; ++r) {
-      long long* p = f.acc + ((int64_t)r * f.C + c) * 9;
-#pragma unroll
-      for (int i = 0; i < 9; ++i)
-        L[i / 3][i % 3] += __hip_atomic_exchange(p + i, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const double SB = bnf_value(L[0][0], L[0][1], L[0][2]);
-    const double SG = bnf_value(L[1][0], L[1][1], L[1][2]);
-    const double SA = bnf_value(L[2][0], L[2][1], L[2][2]);
-    // the arithmetic of bn_bwd_finalize_kernel
-    const double rs = 1.0 / sqrt((double)f.var[c] + (double)f.eps);
-    const double g = f.gamma ? (double)f.gamma[c] : 1.0;
-    f.k[c] = (float)(g * rs);
-    f.k[f.C + c] = (float)(-g * rs * rs * SG / n);
-    f.k[2 * f.C + c] = (float)(-g * rs * SB / n + g * rs * rs * (double)f.mean[c] * SG / n);
-    if (f.dgamma) f.dgamma[c] = f.accumulate ? f.dgamma[c] + (float)SG : (float)SG;
-    if (f.dbeta) f.dbeta[c] = f.accumulate ? f.dbeta[c] + (float)SB : (float)SB;
-    al += SA;
-  }
-  if (f.dalpha) {  // channel sums, then the threads' totals in thread order
-    asum[tid] = al;
-    __syncthreads();
-    if (tid == 0) {
-      double s = 0.0;
-      for (int i = 0; i < (int)blockDim.x; ++i) s += asum[i];
-      f.dalpha[0] = f.accumulate ? f.dalpha[0] + (float)s : (float)s;
-    }
-  }
-  if (tid == 0) __hip_atomic_store(f.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <typename T>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const T* __restrict__ x, const float* __restrict__ dy, int64_t rows, int C, int64_t rpb,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ mean, const float* __restrict__ var, float eps,
-    const float* __restrict__ alpha, double* __restrict__ partial, const BnbFold fold) {
+    const float* __restrict__ alpha, double* __restrict__ partial) {
   const int CG = C >> 2;
   const int RP = 256 / CG;
   const int tid = threadIdx.x;
@@ -189,20 +94,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
         A[j] += red[t][8 + j];
       }
     }
-    if (fold.acc) {
+    double* p = partial + ((int64_t)blockIdx.x * C + tid * 4) * 3;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bnb_add(fold, tid * 4 + j, B[j], G[j], A[j]);
-    } else {
-      double* p = partial + ((int64_t)blockIdx.x * C + tid * 4) * 3;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        p[3 * j] = B[j];
-        p[3 * j + 1] = G[j];
-        p[3 * j + 2] = A[j];
-      }
+    for (int j = 0; j < 4; ++j) {
+      p[3 * j] = B[j];
+      p[3 * j + 1] = G[j];
+      p[3 * j + 2] = A[j];
     }
   }
-  if (fold.acc) bnb_finish(fold);
 }
 
 // one block per channel; writes dgamma/dbeta (accumulate optional), k[3][C], alpha_part[C]
@@ -674,7 +573,7 @@ __global__ __launch_bounds__(256) void spkd_bn_bwd_reduce_kernel(
     const T* __restrict__ raw, int64_t sB, int64_t P, int C, int B, int64_t ppb,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ Mc, const float* __restrict__ mean, const float* __restrict__ var,
-    float eps, double* __restrict__ partial, const BnbFold fold) {
+    float eps, double* __restrict__ partial) {
   const int CG = C >> 2;
   const int RP = 256 / CG;
   const int tid = threadIdx.x;
@@ -736,20 +635,14 @@ __global__ __launch_bounds__(256) void spkd_bn_bwd_reduce_kernel(
         G[j] += red[t][4 + j];
       }
     }
-    if (fold.acc) {
+    double* q = partial + ((int64_t)blockIdx.x * C + tid * 4) * 3;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bnb_add(fold, tid * 4 + j, Bv[j], G[j], 0.0);
-    } else {
-      double* q = partial + ((int64_t)blockIdx.x * C + tid * 4) * 3;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        q[3 * j] = Bv[j];
-        q[3 * j + 1] = G[j];
-        q[3 * j + 2] = 0.0;
-      }
+    for (int j = 0; j < 4; ++j) {
+      q[3 * j] = Bv[j];
+      q[3 * j + 1] = G[j];
+      q[3 * j + 2] = 0.0;
     }
   }
-  if (fold.acc) bnb_finish(fold);
 }
 
 template <typename T, typename OT, int BM>
@@ -802,64 +695,6 @@ inline unsigned grid_of(int64_t n, int64_t cap = 8192) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n, 256), cap));
 }
 
-// per-stream fold state (BnbFold.acc / ticket), zero at rest; allocated at the first use on a
-// stream outside graph capture or by clskd_stream_prepare
-struct BnbState {
-  long long* acc;
-  unsigned* ticket;
-};
-static std::mutex g_bnb_mu;
-static std::unordered_map<hipStream_t, BnbState> g_bnb;
-
-const BnbState* bnb_state(hipStream_t st) {
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  std::lock_guard<std::mutex> lk(g_bnb_mu);
-  auto it = g_bnb.find(st);
-  if (it != g_bnb.end()) return &it->second;
-  if (cs != hipStreamCaptureStatusNone) return nullptr;
-  BnbState s{};
-  const size_t ab = (size_t)BNB_REPL * BNB_CMAX * 9 * 8;
-  if (hipMalloc(&s.acc, ab + 64) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  s.ticket = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(s.acc) + ab);
-  if (hipMemsetAsync(s.acc, 0, ab + 64, st) != hipSuccess) {
-    (void)hipGetLastError();
-    (void)hipFree(s.acc);
-    return nullptr;
-  }
-  return &(g_bnb[st] = s);
-}
-
-// the fold for a launch on `st` (acc == nullptr: the partials + finalize path)
-static BnbFold bnb_fold(hipStream_t st, int64_t rows, int C, const float* gamma, const float* mean,
-                        const float* var, float eps, float* dgamma, float* dbeta, float* k,
-                        float* dalpha, int accumulate) {
-  BnbFold f{};
-  if (knob(KNOB_BN_BWD_FOLD) == 0 || C > BNB_CMAX) return f;
-  const BnbState* s = bnb_state(st);
-  if (!s) return f;
-  f.acc = s->acc;
-  f.ticket = s->ticket;
-  f.rows = rows;
-  f.C = C;
-  f.gamma = gamma;
-  f.mean = mean;
-  f.var = var;
-  f.eps = eps;
-  f.dgamma = dgamma;
-  f.dbeta = dbeta;
-  f.k = k;
-  f.dalpha = dalpha;
-  f.accumulate = accumulate;
-  return f;
-}
-
 }  // namespace clskd
 
 using namespace clskd;
@@ -888,23 +723,18 @@ extern "C" int clskd_bn_bwd(const void* x, const float* dy, int64_t rows, int32_
   float* k = reinterpret_cast<float*>(work + (int64_t)nblk * C * 3);
   double* apart = work + (int64_t)nblk * C * 3 + cdiv(3 * C, 2);
   const int64_t rpb = cdiv(rows, nblk);
-  const BnbFold fold = bnb_fold(st, rows, C, gamma, mean, var, eps, dgamma, dbeta, k,
-                                alpha ? dalpha : nullptr, accumulate_params);
   if (dtype == CLSKD_BF16)
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<__bf16>, dim3(nblk), dim3(256), 0, st,
-                       (const __bf16*)x, dy, rows, C, rpb, scale, shift, mean, var, eps, alpha, partial,
-                       fold);
+                       (const __bf16*)x, dy, rows, C, rpb, scale, shift, mean, var, eps, alpha, partial);
   else
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3(nblk), dim3(256), 0, st, (const float*)x,
-                       dy, rows, C, rpb, scale, shift, mean, var, eps, alpha, partial, fold);
-  if (!fold.acc) {
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, nblk, rows, C,
-                       gamma, mean, var, eps, dgamma, dbeta, k, alpha ? apart : nullptr,
+                       dy, rows, C, rpb, scale, shift, mean, var, eps, alpha, partial);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, nblk, rows, C,
+                     gamma, mean, var, eps, dgamma, dbeta, k, alpha ? apart : nullptr,
+                     accumulate_params);
+  if (alpha && dalpha)
+    hipLaunchKernelGGL(bn_bwd_alpha_kernel, dim3(1), dim3(64), 0, st, apart, C, dalpha,
                        accumulate_params);
-    if (alpha && dalpha)
-      hipLaunchKernelGGL(bn_bwd_alpha_kernel, dim3(1), dim3(64), 0, st, apart, C, dalpha,
-                         accumulate_params);
-  }
   const int64_t nq = rows * C / 4;
   if (dtype == CLSKD_BF16)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<__bf16>, dim3(grid_of(nq)), dim3(256), 0, st,
@@ -1016,11 +846,9 @@ extern "C" int clskd_spkd_bn_bwd(const void* raw, int32_t dtype, int64_t sB, int
   const int64_t ppb = cdiv(P, nblk);
   const int64_t nq = P * (C / 4);
   const unsigned ga = grid_of(nq, 16384);
-  const BnbFold fold = bnb_fold(st, (int64_t)B * P, C, gamma, mean, var, eps, dgamma, dbeta, k,
-                                nullptr, 0);
 #define SBB_RED(T_, BM_)                                                                            \
   hipLaunchKernelGGL((spkd_bn_bwd_reduce_kernel<T_, BM_>), dim3(nblk), dim3(256), 0, st,           \
-                     (const T_*)raw, sB, P, C, B, ppb, scale, shift, coef, mean, var, eps, partial, fold)
+                     (const T_*)raw, sB, P, C, B, ppb, scale, shift, coef, mean, var, eps, partial)
 #define SBB_APP(T_, OT_, BM_)                                                                        \
   hipLaunchKernelGGL((spkd_bn_bwd_apply_kernel<T_, OT_, BM_>), dim3(ga), dim3(256), 0, st,          \
                      (const T_*)raw, sB, P, C, B, scale, shift, coef, k, (OT_*)draw)
@@ -1030,9 +858,8 @@ extern "C" int clskd_spkd_bn_bwd(const void* raw, int32_t dtype, int64_t sB, int
   } else {
     if (big) SBB_RED(float, 32); else SBB_RED(float, 16);
   }
-  if (!fold.acc)
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, nblk,
-                       (int64_t)B * P, C, gamma, mean, var, eps, dgamma, dbeta, k, nullptr, 0);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, nblk,
+                     (int64_t)B * P, C, gamma, mean, var, eps, dgamma, dbeta, k, nullptr, 0);
   if (dtype == CLSKD_BF16) {
     if (draw_dtype == CLSKD_BF16) { if (big) SBB_APP(__bf16, __bf16, 32); else SBB_APP(__bf16, __bf16, 16); }
     else { if (big) SBB_APP(__bf16, float, 32); else SBB_APP(__bf16, float, 16); }

@@ -407,15 +407,11 @@ def test_streaming_matches_offline_eval_forward(graph):
     assert err <= 1e-5, err
 
 
-@pytest.mark.parametrize("fold", [1, 0])
 @pytest.mark.parametrize("prelu", [True, False])
-def test_bn_bwd_against_torch(fold, prelu):
-    """BatchNorm2d(train) [+ PReLU] backward (clskd_bn_bwd) against fp64 torch autograd: dx,
-    dgamma, dbeta, dalpha; with the finalize folded into the reduce launch (CLSKD_BN_BWD_FOLD=1,
-    the default: int64-limb atomics, last block finalises) and with the partials + finalize
-    launches (0).  The fold is bitwise repeatable and leaves its state at zero (a second call on
-    the same stream reproduces the first)."""
-    from clskd import _lib, ops
+def test_bn_bwd_against_torch(prelu):
+    """BatchNorm2d(train) [+ PReLU] backward (clskd_bn_bwd: reduce partials, finalize, apply)
+    against fp64 torch autograd: dx, dgamma, dbeta, dalpha; bitwise repeatable."""
+    from clskd import ops
     g = torch.Generator().manual_seed(11)
     rows, C, eps = 16 * 64 * 37, 32, 1e-5
     x = torch.randn(rows, C, generator=g) * 1.5 + 0.3
@@ -433,19 +429,15 @@ def test_bn_bwd_against_torch(fold, prelu):
     m, v = mean.detach().float(), var.detach().float()
     scale = (gamma / torch.sqrt(v + eps)).contiguous()
     shift = (beta - m * scale).contiguous()
-    prev = _lib.set_knob("CLSKD_BN_BWD_FOLD", fold)
-    try:
-        outs = []
-        for _ in range(2):
-            dx = torch.empty(rows, C, device=DEV)
-            dg = torch.empty(C, device=DEV)
-            db = torch.empty(C, device=DEV)
-            da = torch.empty(1, device=DEV)
-            ops.bn_bwd(x.to(DEV), dy.to(DEV), scale.to(DEV), shift.to(DEV), m.to(DEV), v.to(DEV), eps,
-                       gamma.to(DEV), a.to(DEV) if prelu else None, dx, dg, db, da if prelu else None)
-            outs.append((dx, dg, db, da))
-    finally:
-        _lib.set_knob("CLSKD_BN_BWD_FOLD", prev)
+    outs = []
+    for _ in range(2):
+        dx = torch.empty(rows, C, device=DEV)
+        dg = torch.empty(C, device=DEV)
+        db = torch.empty(C, device=DEV)
+        da = torch.empty(1, device=DEV)
+        ops.bn_bwd(x.to(DEV), dy.to(DEV), scale.to(DEV), shift.to(DEV), m.to(DEV), v.to(DEV), eps,
+                   gamma.to(DEV), a.to(DEV) if prelu else None, dx, dg, db, da if prelu else None)
+        outs.append((dx, dg, db, da))
     for t0, t1 in list(zip(outs[0], outs[1]))[:4 if prelu else 3]:  # (da unwritten without PReLU)
         assert torch.equal(t0, t1)
     dx, dg, db, da = outs[0]
