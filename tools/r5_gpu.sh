@@ -36,6 +36,18 @@ for st in ${STEPS:-suite bench}; do
         rc=0; timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/fetch.log 2>&1 || rc=$?; ok $rc fetch
         rc=0; timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/write.log 2>&1 || rc=$?; ok $rc write ) || exit $?
       python3 $R/tools/pmc_traffic.py $O/fetch/run_counter_collection.csv $O/write/run_counter_collection.csv $O/pmc_traffic.json > $O/traffic.txt;;
+    sq)  # MFMA utilisation / wait counters of the conv_gemm8 instances inside the C2 bench: three
+         # --pmc passes (the per-block slot limits), kernel filter, summarised by tools/sq_summary.py
+      ( cd /tmp && export TMPDIR=/tmp; i=0
+        for P in "GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES" \
+                 "SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_VALU_MFMA_MOPS_BF16" \
+                 "SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY"; do
+          i=$((i+1)); rc=0
+          timeout -s KILL 200 rocprofv3 --pmc $P --kernel-include-regex conv_gemm8 --output-format csv -d $O/sq$i -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/sq$i.log 2>&1 || rc=$?
+          ok $rc sq$i
+        done ) || exit $?
+      python3 $R/tools/sq_summary.py $O/g8_counters.json $O/sq1/run_counter_collection.csv $O/sq2/run_counter_collection.csv $O/sq3/run_counter_collection.csv > $O/sq_summary.txt 2>&1 || true
+      tail -5 $O/sq_summary.txt;;
     micro) rc=0; timeout -k 10 300 python $R/tools/conv_micro.py $MICRO_ARGS > $O/micro.log 2>&1 || rc=$?; cat $O/micro.log; ok $rc micro;;
     ab)  # same-box A/B on the C2 line: AB_CASES="A=1 B=2;A=0 :: --launch exec" (';'-separated
          # cases: env assignments, optionally '::' and extra bench.py arguments)

@@ -24,8 +24,14 @@ def instance(name):
         base = "conv_gemm8_kernel<256,128,4,64,2,2,"
     else:
         return name[:60]
-    out = "bf16" if "EDF16bLi0ELi1" in name else "float"
-    return f"{base}{out},0,1,8,1>"
+    # OutT follows the NS / PHI arguments (…ELi2ELi2E<OutT>…); round-5 names end with the
+    # tap-addressing / stream-K argument TA (…Li0ELi<TA>EEEv)
+    out = "bf16" if "ELi2ELi2EDF16b" in name else "float"
+    ta = ""
+    for v in ("1", "3"):
+        if name.endswith(f"Li0ELi{v}EEEvNS_10ConvArgsG8E"):
+            ta = f",bf16,0,{v}"
+    return f"{base}{out},0,1,8,1{ta}>"
 
 
 def main():
