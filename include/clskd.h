@@ -488,6 +488,21 @@ int clskd_conv2d_wgrad(const clskd_conv_desc* d, const float* dy, float* dw, flo
  * gradients back onto module parameters (complex [[Wr,-Wi],[Wi,Wr]] blocks, polyphase taps). */
 int clskd_index_gather(const float* src, const int32_t* idx, const float* sgn, int32_t J,
                        int64_t n, float* out, int32_t accumulate, void* stream);
+/* Several index gathers in one launch: job i computes out_i[e] (+)= sum_j sgn_i[e*J+j] *
+ * src_i[idx_i[e*J+j]] exactly as clskd_index_gather.  `jobs` is HOST memory (read at enqueue,
+ * n_jobs <= CLSKD_GATHER_JOBS_MAX); jobs must write disjoint outputs.  Used to apply a backward
+ * pass's packed-gradient -> parameter maps in one launch (clskd.backward). */
+#define CLSKD_GATHER_JOBS_MAX 48
+typedef struct {
+  const float* src;
+  const int32_t* idx;
+  const float* sgn;
+  float* out;
+  int64_t n;
+  int32_t J;
+  int32_t accumulate;
+} clskd_gather_job;
+int clskd_index_gather_jobs(const clskd_gather_job* jobs, int32_t n_jobs, void* stream);
 
 /* torch.optim.Adam step (distill.py:202-204) over a flat parameter buffer: g *= grad_scale
  * (e.g. 1/world for a summed all-reduce), L2 weight decay, bias corrections for `step` (1-based). */

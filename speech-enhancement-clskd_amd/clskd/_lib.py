@@ -101,6 +101,13 @@ assert C.sizeof(GramJob) == 88
 
 _p, _i32, _i64, _f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float
 
+GATHER_JOBS_MAX = 48  # include/clskd.h CLSKD_GATHER_JOBS_MAX
+
+
+class GatherJob(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("idx", C.c_void_p), ("sgn", C.c_void_p), ("out", C.c_void_p),
+                ("n", C.c_int64), ("J", C.c_int32), ("accumulate", C.c_int32)]
+
 SIGNATURES = {
     "clskd_last_error": (C.c_char_p, []),
     "clskd_conv_last_kernel": (C.c_char_p, []),
@@ -162,6 +169,7 @@ SIGNATURES = {
     "clskd_conv2d_wgrad_workspace": (_i64, [C.POINTER(ConvDesc)]),
     "clskd_conv2d_wgrad": (_i32, [C.POINTER(ConvDesc), _p, _p, _p, _p, _i64, _i32, _p]),
     "clskd_index_gather": (_i32, [_p, _p, _p, _i32, _i64, _p, _i32, _p]),
+    "clskd_index_gather_jobs": (_i32, [_p, _i32, _p]),
     "clskd_adam_step": (_i32, [_p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _f32, _p]),
     "clskd_adam_step_dev": (_i32, [_p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _p, _f32, _p]),
     "clskd_fill_f32": (_i32, [_p, _i64, _f32, _p]),

@@ -95,10 +95,19 @@ def unpack_maps(key, fn, shapes, Kp, dev):
     return out
 
 
+# Packed-gradient -> parameter scatters of one backward pass (acc = False: every parameter's
+# gradient is written once) are collected here and launched together at the end of the student's
+# backward (ops.index_gather_jobs: ~70 launches -> 2); None: launch each one at once
+_SCATTERS = None
+
+
 def _scatter(src, maps, grads, acc):
     for (idx, sgn), g in zip(maps, grads):
         if g is not None:
-            ops.index_gather(src, idx, sgn, g, accumulate=acc)
+            if _SCATTERS is not None and not acc:
+                _SCATTERS.append((src, idx, sgn, g))
+            else:
+                ops.index_gather(src, idx, sgn, g, accumulate=acc)
 
 
 # ------------------------------------------------------------------------------------------
@@ -141,6 +150,7 @@ def _tw(key, src, build):
 # gathering the real source reproduces the real build bitwise; entries that read other tensors
 # too, or change dtype, keep `build`.  CLSKD_TW_MAPS=0 disables the maps (A/B).
 _TW_MAPS_ON = os.environ.get("CLSKD_TW_MAPS", "1") == "1"
+_BATCH_SCATTERS = os.environ.get("CLSKD_BATCH_SCATTERS", "1") == "1"  # A/B: 0 = one launch each
 _TWMAP = {}
 
 
@@ -321,8 +331,7 @@ def dccrn_backward(m, tape, enc, dec, dec_in, lstm_io, g, pg, acc_params=False, 
         ops.conv_wgrad(segs, [(0, 0)], B, 1, T, P, g["dec_in"], omap, dw, db, dy_offset=half * Ch)
         maps = unpack_maps(("lin", P, H), lambda w: w, [(P, H)], wpp.shape[1], dev)
         _scatter(dw, maps, [pg.get(lin.weight)], acc_params)
-        if pg.get(lin.bias) is not None:
-            ops.index_gather(db, *_ident_map(P, dev), pg[lin.bias], accumulate=acc_params)
+        _scatter(db, [_ident_map(P, dev)], [pg.get(lin.bias)], acc_params)
         wt = _tw(("proj_t", id(m), half), wpp,
                  lambda: ops.pack_weight(wpp[:, :H].reshape(Ch, D4, H).permute(2, 1, 0).contiguous(),
                                          D4 * Ch))
@@ -643,5 +652,12 @@ def clskd_backward(res, student, review_encoder, review_decoder, pg, acc_params=
         main.wait_stream(s_dec)
         main.wait_stream(s_enc)
 
-    dccrn_backward(student, tp["s"], enc, dec, dec_in, sf["lstm_io"], g, pg, acc_params, join=join)
+    global _SCATTERS
+    _SCATTERS = [] if (_BATCH_SCATTERS and not acc_params) else None
+    try:
+        dccrn_backward(student, tp["s"], enc, dec, dec_in, sf["lstm_io"], g, pg, acc_params, join=join)
+        if _SCATTERS:
+            ops.index_gather_jobs(_SCATTERS)  # on main: every scattered gradient was made there
+    finally:
+        _SCATTERS = None
     return g

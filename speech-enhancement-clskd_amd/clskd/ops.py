@@ -1242,6 +1242,20 @@ def index_gather(src, idx, sgn, out, accumulate=False):
                                    _stream()), "index_gather")
 
 
+def index_gather_jobs(jobs):
+    """Several index gathers [(src, idx, sgn, out), ...] (no accumulation, disjoint outputs) in
+    clskd_index_gather_jobs launches of up to GATHER_JOBS_MAX jobs each, on the current stream."""
+    L = lib()
+    for i in range(0, len(jobs), _lib.GATHER_JOBS_MAX):
+        chunk = jobs[i:i + _lib.GATHER_JOBS_MAX]
+        arr = (_lib.GatherJob * len(chunk))()
+        for k, (src, idx, sgn, out) in enumerate(chunk):
+            assert out.numel() == idx.shape[0] and out.is_contiguous()
+            arr[k] = _lib.GatherJob(ptr(src), ptr(idx), ptr(sgn), ptr(out), idx.shape[0],
+                                    idx.shape[1], 0)
+        check(L.clskd_index_gather_jobs(arr, len(chunk), _stream()), "index_gather_jobs")
+
+
 def adam_step(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
     check(lib().clskd_adam_step(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, beta1, beta2, eps,
                                 weight_decay, step, grad_scale, _stream()), "adam")

@@ -218,6 +218,25 @@ __global__ __launch_bounds__(256) void index_gather_kernel(const float* __restri
   }
 }
 
+struct GatherJobsArg {
+  clskd_gather_job j[CLSKD_GATHER_JOBS_MAX];
+};
+
+// one job per blockIdx.y, grid-stride over its elements (the per-element arithmetic of
+// index_gather_kernel)
+__global__ __launch_bounds__(256) void index_gather_jobs_kernel(const GatherJobsArg a) {
+  const clskd_gather_job& jb = a.j[blockIdx.y];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < jb.n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int j = 0; j < jb.J; ++j) {
+      const int32_t q = jb.idx[i * jb.J + j];
+      if (q >= 0) s = fmaf(jb.sgn[i * jb.J + j], jb.src[q], s);
+    }
+    jb.out[i] = jb.accumulate ? jb.out[i] + s : s;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Adam (torch.optim.Adam semantics, distill.py:202-204): L2 weight decay folded into g,
 // bias corrections from the step count, eps added to sqrt(v)/sqrt(bc2).
@@ -375,6 +394,27 @@ extern "C" int clskd_index_gather(const float* src, const int32_t* idx, const fl
   hipLaunchKernelGGL(index_gather_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), src,
                      idx, sgn, J, n, out, accumulate);
   CLSKD_LAUNCH_CHECK("index_gather");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_index_gather_jobs(const clskd_gather_job* jobs, int32_t n_jobs, void* stream) {
+  CLSKD_CHECK_ARG(jobs && n_jobs >= 0 && n_jobs <= CLSKD_GATHER_JOBS_MAX,
+                  "index_gather_jobs: %d jobs (at most %d)", n_jobs, CLSKD_GATHER_JOBS_MAX);
+  if (n_jobs == 0) return CLSKD_OK;
+  GatherJobsArg a{};
+  int64_t nmax = 0;
+  for (int i = 0; i < n_jobs; ++i) {
+    const clskd_gather_job& jb = jobs[i];
+    CLSKD_CHECK_ARG(jb.src && jb.idx && jb.sgn && jb.out && jb.J >= 1 && jb.n >= 0,
+                    "index_gather_jobs: bad job %d", i);
+    a.j[i] = jb;
+    nmax = std::max<int64_t>(nmax, jb.n);
+  }
+  if (nmax == 0) return CLSKD_OK;
+  const unsigned gx = (unsigned)std::min<int64_t>(cdiv(nmax, 256), 512);
+  hipLaunchKernelGGL(index_gather_jobs_kernel, dim3(gx, (unsigned)n_jobs), dim3(256), 0,
+                     as_stream(stream), a);
+  CLSKD_LAUNCH_CHECK("index_gather_jobs");
   return CLSKD_OK;
 }
 

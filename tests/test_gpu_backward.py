@@ -446,3 +446,24 @@ def test_bn_bwd_against_torch(prelu):
     assert _rel(_np(db), bd.grad.numpy()) < 1e-5
     if prelu:
         assert _rel(_np(da), ad.grad.numpy()) < 1e-5
+
+
+def test_index_gather_jobs_matches_single_gathers():
+    """clskd_index_gather_jobs (the backward's batched packed-gradient -> parameter scatters)
+    equals one clskd_index_gather per job, bitwise, including more jobs than one launch takes."""
+    from clskd import _lib, ops
+    g = torch.Generator().manual_seed(3)
+    jobs, refs = [], []
+    for k in range(_lib.GATHER_JOBS_MAX + 7):
+        src = torch.randn(500 + 13 * k, generator=g).to(DEV)
+        n, J = 37 + 29 * k, 1 + k % 3
+        idx = torch.randint(-1, src.numel(), (n, J), generator=g, dtype=torch.int32).to(DEV)
+        sgn = (torch.randint(0, 2, (n, J), generator=g).float() * 2 - 1).to(DEV)
+        out = torch.full((n,), float("nan"), device=DEV)
+        ref = torch.empty(n, device=DEV)
+        ops.index_gather(src, idx, sgn, ref)
+        jobs.append((src, idx, sgn, out))
+        refs.append(ref)
+    ops.index_gather_jobs(jobs)
+    for (_, _, _, out), ref in zip(jobs, refs):
+        assert torch.equal(out, ref)
