@@ -88,8 +88,8 @@ __global__ __launch_bounds__(256) void abf_moments_kernel(const float* __restric
     for (int j = 0; j < 4; ++j) d2[p][j] = 0.0;
 #pragma unroll
   for (int t = 0; t < NT; ++t) d1[t] = 0.0;
-  // chunk c0's rows into x (every lane its row of each k-group, its channel of each tile)
-  auto load_chunk = [&](int c0, float (&x)[G][NT]) {
+  for (int c0 = r0 + wave * CH; c0 < r1; c0 += 4 * CH) {  // chunks dealt over the waves
+    float x[G][NT];
     int b, f, t;
     if (!g.contig) {
       g.split(c0, b, f, t);  // uniform
@@ -109,8 +109,6 @@ __global__ __launch_bounds__(256) void abf_moments_kernel(const float* __restric
 #pragma unroll
       for (int ti = 0; ti < NT; ++ti) x[gi][ti] = ok ? row[16 * ti + lch] : 0.f;
     }
-  };
-  auto compute_chunk = [&](const float (&x)[G][NT]) {
     f32x4 acc[NA][NP];
     float a1[NT];
 #pragma unroll
@@ -142,18 +140,6 @@ __global__ __launch_bounds__(256) void abf_moments_kernel(const float* __restric
       }
 #pragma unroll
     for (int ti = 0; ti < NT; ++ti) d1[ti] += (double)a1[ti];
-  };
-  // chunks dealt over the waves; the next chunk of a wave is loaded while this one computes
-  // (two register sets: the loop was one exposed load latency per chunk)
-  float xa[G][NT], xb[G][NT];
-  int c0 = r0 + wave * CH;
-  if (c0 < r1) load_chunk(c0, xa);
-  for (; c0 < r1; c0 += 8 * CH) {
-    if (c0 + 4 * CH < r1) load_chunk(c0 + 4 * CH, xb);
-    compute_chunk(xa);
-    if (c0 + 4 * CH >= r1) break;
-    if (c0 + 8 * CH < r1) load_chunk(c0 + 8 * CH, xa);
-    compute_chunk(xb);
   }
   // S1: the lanes holding one channel (4 row lanes; C = 8: 8 row lanes), fixed order
 #pragma unroll
