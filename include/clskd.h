@@ -223,10 +223,13 @@ int clskd_bn_stats_partial(const void* x, int64_t rows, int32_t C, double* parti
                            int32_t nblk, int32_t dtype, void* stream);
 /* clskd_bn_compact: level-2 reduction of [nblk][C][2] partials into [ceil(nblk/group)][C][2]
  * (fixed-order group sums).  Optional: clskd_bn_finalize reads any nblk directly (16-B loads,
- * eight in flight per lane), which is what the framework does — one launch per BatchNorm. */
+ * eight in flight per lane; above 1,024 rows after an in-place fold, below). */
 int clskd_bn_compact(const double* partial, int32_t nblk, int32_t C, int32_t group, double* out,
                      void* stream);
-int clskd_bn_finalize(const double* partial, int32_t nblk, int64_t rows, int32_t C,
+/* clskd_bn_finalize / clskd_bn_bwd_from_partials treat `partial` as scratch: above 1,024 rows
+ * they fold it in place to 512 rows first (fixed order, CLSKD_BN_PFOLD bit 2 / bit 1), so its
+ * contents are undefined after the call. */
+int clskd_bn_finalize(double* partial, int32_t nblk, int64_t rows, int32_t C,
                       const float* gamma, const float* beta, float eps,
                       float* running_mean, float* running_var, float momentum,
                       int32_t n_updates, float* scale, float* shift, float* mean_out,
@@ -554,7 +557,7 @@ int clskd_abf_fuse_bwd(const void* x1, const void* res, int32_t B, int32_t F, in
 int clskd_bn_bwd_from_partials(const void* x, const float* dy, int64_t rows, int32_t C,
                                const float* scale, const float* shift, const float* mean,
                                const float* var, float eps, const float* gamma,
-                               const double* partial, int32_t nblk, float* kbuf, float* dgamma,
+                               double* partial, int32_t nblk, float* kbuf, float* dgamma,
                                float* dbeta, float* dx, int32_t accumulate_dx, int32_t dtype,
                                void* stream);
 int clskd_nearest_down_sum(const float* g, int32_t B, int32_t F, int32_t T, int32_t Fr,

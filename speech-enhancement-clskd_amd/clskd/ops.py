@@ -66,6 +66,10 @@ class KernelTimer:
         return out  # name -> [launches, total_ms, total_flops]
 
 
+# accumulating launches on the direct kernel (A/B: CLSKD_DIRECT_ACC=0 keeps them on the engines)
+_DIRECT_ACC = os.environ.get("CLSKD_DIRECT_ACC", "1") != "0"
+
+
 @lru_cache(maxsize=4096)
 def _direct_policy(N, K):
     return bool(_lib.load(require_gpu=False).clskd_conv_direct_ok(N, K))
@@ -304,7 +308,9 @@ def _conv_plan(key, segs, geoms, taps, B, Fo, To, N, wpacked, bias, out, omap, s
             d.seg_c[i] = g.C
         for i, (dF, dT) in enumerate(taps):
             d.tap_df[i], d.tap_dt[i] = dF, dT
-    direct = direct_ok(N, Kp) and not (accumulate or mfma_only)
+    # accumulate (data-gradient sums): the direct kernel takes it for fp32 outputs too
+    direct = direct_ok(N, Kp) and not mfma_only and not (
+        accumulate and (out.dtype != torch.float32 or in_dt != _lib.F32 or not _DIRECT_ACC))
     d.accumulate = int(bool(accumulate))
     d.wlayout = _lib.WLAYOUT_DIRECT if direct else _lib.WLAYOUT_NK
     pl = _ConvPlan()
@@ -368,8 +374,8 @@ def conv(segs, taps, B, Fo, To, N, wpacked, bias, out, omap, out_offset=0, strid
     the fp32-MFMA engine (weights fp32, K % 16).  `out` may be fp32 or bf16 storage.
     The descriptor of each launch signature (geometry, taps, output map, dtypes, pointer
     alignment class) is built once (_conv_plan); a call patches only the pointers.
-    accumulate=True adds into `out` (fp32 engine; data-gradient sums); mfma_only skips the
-    direct-convolution kernel.
+    accumulate=True adds into `out` (fp32 engines or the direct kernel, fp32 out; data-gradient
+    sums); mfma_only skips the direct-convolution kernel.
     bn_stats=(BnStats, is_last): the launch produces (part of) a train-mode BatchNorm's batch
     statistics — folded into the launch when the dispatched kernel can (clskd_bn_fold), else as
     fused partials for BnStats.coefficients()."""

@@ -225,8 +225,14 @@ __global__ __launch_bounds__(128) void conv_direct_kernel(const DirectArgs args)
     for (int c = tid; c < rows * NP / CH; c += 128) {
       const int row = (c * CH) / NP, col = (c * CH) % NP;
       V v;
+      if (d.accumulate) {  // fp32 out only (host): data-gradient sums, out += conv
+        const V o = *reinterpret_cast<const V*>(dst + (int64_t)c * CH);
 #pragma unroll
-      for (int i = 0; i < CH; ++i) v[i] = (OutT)red[row * (NP + 1) + col + i];
+        for (int i = 0; i < CH; ++i) v[i] = (OutT)(red[row * (NP + 1) + col + i] + (float)o[i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) v[i] = (OutT)red[row * (NP + 1) + col + i];
+      }
       *reinterpret_cast<V*>(dst + (int64_t)c * CH) = v;
     }
     return;
@@ -244,19 +250,24 @@ __global__ __launch_bounds__(128) void conv_direct_kernel(const DirectArgs args)
 #pragma unroll
     for (int c = 0; c < NP; c += VW) {
       V v;
+      if (d.accumulate) {
+        const V o = *reinterpret_cast<const V*>(outp + ro + c);
 #pragma unroll
-      for (int i = 0; i < VW; ++i) v[i] = (OutT)acc[c + i];
+        for (int i = 0; i < VW; ++i) v[i] = (OutT)(acc[c + i] + (float)o[i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < VW; ++i) v[i] = (OutT)acc[c + i];
+      }
       *reinterpret_cast<V*>(outp + ro + c) = v;
     }
-  } else if (d.nlo >= NP) {
-#pragma unroll
-    for (int n = 0; n < NP; ++n)
-      if (n < d.N) outp[ro + (int64_t)n * d.oNlo] = (OutT)acc[n];
   } else {
 #pragma unroll
     for (int n = 0; n < NP; ++n) {
-      if (n < d.N)
-        outp[ro + (int64_t)(n / d.nlo) * d.oNhi + (int64_t)(n % d.nlo) * d.oNlo] = (OutT)acc[n];
+      if (n < d.N) {
+        const int64_t o = ro + (d.nlo >= NP ? (int64_t)n * d.oNlo
+                                            : (int64_t)(n / d.nlo) * d.oNhi + (int64_t)(n % d.nlo) * d.oNlo);
+        outp[o] = (OutT)(d.accumulate ? acc[n] + (float)outp[o] : acc[n]);
+      }
     }
   }
 }
@@ -273,7 +284,10 @@ static size_t direct_lds(const clskd_conv_desc& d, int NP, int G) {
 // it wins for the 2-channel output layers (2-3x), short-K narrow layers and the 2-channel-input
 // first encoder layer (K = 20 -> 32, N = 32: the fp32 engine's scalar gather path takes 135 us
 // there); with N >= 32 and real K, or N = 16 with long K, the MFMA engines are faster.
-// K <= 1024 bounds the LDS K table (16 KB).
+// K <= 1024 bounds the LDS K table (16 KB).  accumulate (out += conv, fp32 out, no statistics):
+// the data-gradient sums of the narrow decoder / encoder layers (C3 backward: the 2-channel
+// mask-gradient gather into the 8-channel decoder input took 195 us per segment on the fp32 MFMA
+// engine's scalar gather path).
 bool conv_direct_ok(int N, int K) {
   return N >= 1 && K >= 1 && K <= 1024 &&
          (N <= 4 || (N <= 16 && K <= 128) || (N <= 32 && K <= 32));
@@ -315,6 +329,8 @@ int launch_conv_direct(const clskd_conv_desc& d, hipStream_t st) {
   CLSKD_CHECK_SHAPE(conv_direct_ok(d.N, d.K), "conv2d(direct): N=%d K=%d outside the direct path",
                     d.N, d.K);
   CLSKD_CHECK_ARG(((uintptr_t)d.weight & 15) == 0, "conv2d(direct): weight must be 16-byte aligned");
+  CLSKD_CHECK_ARG(!d.accumulate || (d.out_dtype == CLSKD_F32 && !d.stats && !d.bn_fold),
+                  "conv2d(direct): accumulate takes an fp32 output and no statistics");
   int g = d.kvec;
   if (g == 0) g = is_lowp(d.in_dtype) ? 8 : (d.vec4 ? 4 : 1);
   CLSKD_CHECK_SHAPE(d.K % g == 0, "conv2d(direct): K=%d not a multiple of kvec %d", d.K, g);

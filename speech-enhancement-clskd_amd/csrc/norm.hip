@@ -463,6 +463,49 @@ __global__ __launch_bounds__(256) void bn_compact_kernel(const double* __restric
   }
 }
 
+// In-place level-2 fold of a [nblk][E] fp64 partial table (E = 2C forward {sum, sumsq}, 3C
+// backward {dbeta, dgamma, dalpha}): workgroup g of G sums rows g, g+G, g+2G, ... in that order and
+// overwrites row g.  Only workgroup g reads the rows = g (mod G), so the overwrite races nothing.
+// Lanes = (row lane, element): consecutive lanes read consecutive elements of a row (coalesced),
+// eight rows in flight per lane, then a fixed-order LDS combine over the row lanes.
+constexpr int PFOLD_G = 512;
+__global__ __launch_bounds__(256) void partial_fold_kernel(double* part, int nblk, int E, int G) {
+  const int g = blockIdx.x;
+  const int Ec = E < 256 ? E : 256;
+  const int RL = 256 / Ec;
+  const int tid = threadIdx.x;
+  const int rl = tid / Ec;
+  const int el = tid - rl * Ec;
+  const int nr = (nblk - g + G - 1) / G;  // rows g + k*G, k < nr
+  __shared__ double red[256];
+  for (int e0 = 0; e0 < E; e0 += Ec) {
+    const int e = e0 + el;
+    double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (rl < RL && e < E) {
+      int k = rl;
+      for (; k + 7 * RL < nr; k += 8 * RL) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s[u] += part[(int64_t)(g + (k + u * RL) * G) * E + e];
+      }
+      for (; k < nr; k += RL) s[0] += part[(int64_t)(g + k * G) * E + e];
+    }
+    red[tid] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    __syncthreads();
+    if (rl == 0 && e < E) {
+      double v = red[el];
+      for (int l = 1; l < RL; ++l) v += red[l * Ec + el];
+      part[(int64_t)g * E + e] = v;
+    }
+    __syncthreads();
+  }
+}
+
+int fold_partials(double* part, int nblk, int E, int bit, hipStream_t st) {
+  if (!(knob(KNOB_BN_PFOLD) & bit) || nblk <= 2 * PFOLD_G) return nblk;
+  hipLaunchKernelGGL(partial_fold_kernel, dim3(PFOLD_G), dim3(256), 0, st, part, nblk, E, PFOLD_G);
+  return PFOLD_G;
+}
+
 }  // namespace clskd
 
 using namespace clskd;
@@ -508,7 +551,7 @@ extern "C" int clskd_bn_compact(const double* partial, int32_t nblk, int32_t C, 
   return CLSKD_OK;
 }
 
-extern "C" int clskd_bn_finalize(const double* partial, int32_t nblk, int64_t rows, int32_t C,
+extern "C" int clskd_bn_finalize(double* partial, int32_t nblk, int64_t rows, int32_t C,
                                  const float* gamma, const float* beta, float eps,
                                  float* running_mean, float* running_var, float momentum,
                                  int32_t n_updates, float* scale, float* shift, float* mean_out,
@@ -517,6 +560,7 @@ extern "C" int clskd_bn_finalize(const double* partial, int32_t nblk, int64_t ro
   CLSKD_CHECK_SHAPE(C > 0 && nblk > 0 && rows > 0, "bn_finalize: shape");
   CLSKD_CHECK_ARG(((uintptr_t)partial & 15) == 0, "bn_finalize: partials must be 16-byte aligned");
   if (skip_kernel(SKIP_BN_FINALIZE)) return CLSKD_OK;
+  nblk = fold_partials(partial, nblk, 2 * C, 2, as_stream(stream));
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(BNF_T), 0, as_stream(stream), partial, nblk,
                      rows, C, gamma, beta, eps, running_mean, running_var, momentum, n_updates,
                      scale, shift, mean_out, var_out);

@@ -783,7 +783,7 @@ extern "C" int clskd_abf_fuse_bwd(const void* x1, const void* res, int32_t B, in
 extern "C" int clskd_bn_bwd_from_partials(const void* x, const float* dy, int64_t rows, int32_t C,
                                           const float* scale, const float* shift,
                                           const float* mean, const float* var, float eps,
-                                          const float* gamma, const double* partial, int32_t nblk,
+                                          const float* gamma, double* partial, int32_t nblk,
                                           float* kbuf, float* dgamma, float* dbeta, float* dx,
                                           int32_t accumulate_dx, int32_t dtype, void* stream) {
   CLSKD_CHECK_ARG(x && dy && scale && shift && mean && var && partial && kbuf && dx,
@@ -791,6 +791,7 @@ extern "C" int clskd_bn_bwd_from_partials(const void* x, const float* dy, int64_
   CLSKD_CHECK_SHAPE(rows > 0 && C >= 4 && C % 4 == 0 && nblk >= 1, "bn_bwd_from_partials: shape");
   CLSKD_CHECK_ARG(((uintptr_t)kbuf & 15) == 0, "bn_bwd_from_partials: kbuf must be 16-byte aligned");
   hipStream_t st = as_stream(stream);
+  nblk = fold_partials(partial, nblk, 3 * C, 1, st);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, nblk, rows, C,
                      gamma, mean, var, eps, dgamma, dbeta, kbuf, nullptr, 0);
   const int64_t nq = rows * C / 4;

@@ -98,6 +98,47 @@ def test_conv_direct_against_torch_and_engine(dt, C1, C2, N):
     _direct_case(dt, C1, C2, N)
 
 
+@pytest.mark.parametrize("C1,C2,N,omap", [(2, 0, 8, "plain"), (2, 0, 8, "poly"), (8, 0, 16, "plain"),
+                                            (4, 4, 2, "plain"), (2, 0, 3, "plain"), (4, 4, 8, "poly")])
+def test_conv_direct_accumulate_against_torch(C1, C2, N, omap):
+    """accumulate=True on the direct kernel (out += conv, fp32): the data-gradient sums of the
+    narrow decoder / encoder layers (backward.py's stride-2 mask-gradient gather, N = 8 / 16, K up
+    to 128).  Output maps: contiguous rows (the LDS-staged store), a polyphase parity (of_mul 2:
+    the per-row vector store) and N not a power of two (the scalar store).  Against fp64 torch
+    plus the prior contents; 1e-5 relative."""
+    from clskd import ops
+    g = torch.Generator().manual_seed(C1 * 100 + C2 * 10 + N)
+    B, F, T = 3, 33, 29
+    segs_h = [torch.randn(B, F, T, C1, generator=g)]
+    if C2:
+        segs_h.append(torch.randn(B, F, T, C2, generator=g))
+    Cin = C1 + C2
+    w = torch.randn(N, Cin, 5, 2, generator=g) * 0.2
+    taps = [(kf - 2, kt - 1) for kf in range(5) for kt in range(2)]
+    Fo = (F + 4 - 5) // 2 + 1
+    wp = ops.pack_weight(w.permute(0, 2, 3, 1).reshape(N, 10, Cin).to(DEV), 10 * Cin)
+    assert ops.direct_ok(N, wp.shape[1])
+    xin = torch.cat([x.double() for x in segs_h], 3).permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv2d(torch.nn.functional.pad(xin, (1, 0, 2, 2)), w.double(),
+                                     stride=(2, 1))[..., :T].permute(0, 2, 3, 1)
+    segs = [ops.seg_bftc(x.to(DEV)) for x in segs_h]
+    if omap == "poly":  # rows 2*fo + 1 of a [B][2*Fo][T][N] buffer
+        out = torch.randn(B, 2 * Fo, T, N, generator=g).to(DEV)
+        om = ops.OutMap(2 * Fo * T * N, T * N, N, of_mul=2, of_add=1)
+    else:
+        out = torch.randn(B, Fo, T, N, generator=g).to(DEV)
+        om = ops.OutMap(Fo * T * N, T * N, N)
+    prior = out.double().cpu()
+    ops.conv(segs, taps, B, Fo, T, N, wp, None, out, om, stride_f=2, accumulate=True)
+    assert ops.conv_kernel_of_last_launch().startswith("conv_direct_kernel")
+    exp = prior.clone()
+    if omap == "poly":
+        exp[:, 1::2] += ref
+    else:
+        exp += ref
+    np.testing.assert_allclose(out.double().cpu().numpy(), exp.numpy(), rtol=1e-5, atol=1e-5)
+
+
 def _direct_case(dt, C1, C2, N):
     from clskd import ops
     g = torch.Generator().manual_seed(C1 * 100 + C2 * 10 + N)
@@ -530,11 +571,54 @@ def test_bn_running_stats_two_updates():
             np.testing.assert_allclose(_np(sd[k[4:]]), fx[k], rtol=1e-4, atol=1e-6, err_msg=k)
 
 
-@pytest.mark.parametrize("nblk,C", [(3, 8), (256, 64), (2048, 16), (3000, 128)])
-def test_bn_finalize_reads_all_partials(nblk, C):
-    """clskd_bn_finalize alone (no level-2 compaction launch) on up to 3000 {sum, sumsq}
-    partials: scale / shift / batch mean / var and one running-stat update vs fp64 numpy."""
-    from clskd import ops
+@pytest.mark.parametrize("pfold", [0, 3])
+@pytest.mark.parametrize("nblk,C", [(3, 8), (256, 64), (2048, 16), (3000, 128), (12000, 8),
+                                    (1500, 100), (2100, 200)])
+def test_bn_finalize_reads_all_partials(nblk, C, pfold):
+    """clskd_bn_finalize alone (no level-2 compaction launch) on up to 12,000 {sum, sumsq}
+    partials, read directly (CLSKD_BN_PFOLD 0) or after the in-place fold to 512 rows (above
+    1,024 rows; 2C elements per row from 16 to 400: one and two element chunks per workgroup):
+    scale / shift / batch mean / var and one running-stat update vs fp64 numpy."""
+    from clskd import ops, _lib
+    _lib.set_knob("CLSKD_BN_PFOLD", pfold)
+    try:
+        _bn_finalize_case(ops, nblk, C)
+    finally:
+        _lib.set_knob("CLSKD_BN_PFOLD", 1)
+
+
+@pytest.mark.parametrize("nblk,C", [(16384, 64), (2000, 8), (700, 16)])
+def test_bn_bwd_from_partials_fold_matches_direct(nblk, C):
+    """clskd_bn_bwd_from_partials with its [nblk][C][3] partials folded in place first
+    (CLSKD_BN_PFOLD bit 1, above 1,024 rows) against the direct read: dx within fp64-sum
+    reassociation (1e-6 relative), and bitwise repeatable across calls."""
+    from clskd import ops, _lib
+    g = torch.Generator().manual_seed(nblk + C)
+    rows = 64 * nblk
+    x = torch.randn(rows, C, generator=g).to(DEV)
+    dy = torch.randn(rows, C, generator=g).to(DEV)
+    scale = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    shift = torch.randn(C, generator=g).to(DEV)
+    mean = (torch.randn(C, generator=g) * 0.1).to(DEV)
+    var = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    part0 = (torch.randn(nblk, C, 3, generator=g, dtype=torch.float64) * 10.0).to(DEV).reshape(-1)
+    outs = []
+    try:
+        for pf in (0, 1, 1):
+            _lib.set_knob("CLSKD_BN_PFOLD", pf)
+            dx = torch.empty_like(x)
+            ops.bn_bwd_from_partials(x, dy, scale, shift, mean, var, 1e-5, gamma, part0.clone(),
+                                     nblk, dx)
+            outs.append(dx)
+    finally:
+        _lib.set_knob("CLSKD_BN_PFOLD", 1)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(_np(outs[1]), _np(outs[0]), rtol=1e-6, atol=1e-6)
+    assert torch.equal(outs[1], outs[2])
+
+
+def _bn_finalize_case(ops, nblk, C):
     g = torch.Generator().manual_seed(nblk + C)
     rows = 1000 * nblk
     x = torch.randn(nblk, C, 2, generator=g, dtype=torch.float64)

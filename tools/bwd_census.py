@@ -1,7 +1,7 @@
 """Per-call census of the C3 backward's GEMM launches: every `ops.conv_wgrad` (weight gradient)
 and `ops.conv` (data gradient / forward) call of one eager training step, each bracketed by
 device synchronisation and HIP events (a sleep kernel ahead of the first event hides the host
-launch latency), grouped by shape.  Diagnostic only (serialises the step).
+launch latency), grouped by shape, call site and dispatched kernel.  Diagnostic only (serialises the step).
 
     python tools/bwd_census.py [--precision mixed] [--top 40]
 """
@@ -50,7 +50,10 @@ def main():
             r = fn(*a, **k)
             e1.record(s)
             torch.cuda.synchronize()
-            rec[(name,) + keyf(a, k)].append(e0.elapsed_time(e1) * 1e3)
+            f = sys._getframe(1)
+            site = f"{os.path.basename(f.f_code.co_filename)}:{f.f_lineno}"
+            kern = ops.conv_kernel_of_last_launch() if name == "conv" else ""
+            rec[(name,) + keyf(a, k) + (site, str(kern)[:60])].append(e0.elapsed_time(e1) * 1e3)
             return r
         return w
 

@@ -4,7 +4,7 @@
 #   bench   default C2 bench line;  train  C3 line;  spkd  C4 line;  c1 / c5
 #   trace   rocprofv3 kernel+marker trace of the bench command split at its roctx ranges
 #   pmc     FETCH_SIZE / WRITE_SIZE passes -> per-kernel HBM traffic
-#   tests:<pytest args>   a subset of the suite
+#   tests:<pytest args>   a subset of the suite (comma-separated)
 # Every GPU step has its own time limit; a failing step ends the call.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${ITER:-r5}
@@ -17,7 +17,7 @@ for st in ${STEPS:-suite bench}; do
       rc=0; CLSKD_GRAD_PARITY_OUT=$O/c3_grad_parity.txt timeout -k 10 900 $T $R/tests -m gpu > $O/gpu_suite.log 2>&1 || rc=$?
       tail -2 $O/gpu_suite.log; ok $rc suite;;
     tests:*)
-      rc=0; timeout -k 10 600 $T -m gpu ${st#tests:} > $O/tests.log 2>&1 || rc=$?
+      a=${st#tests:}; rc=0; timeout -k 10 600 $T -m gpu ${a//,/ } > $O/tests.log 2>&1 || rc=$?
       tail -2 $O/tests.log; ok $rc tests;;
     bench) rc=0; timeout -k 10 300 python $R/bench.py $BENCH_ARGS > $O/bench.log 2>&1 || rc=$?; ok $rc bench
       grep '^{' $O/bench.log | cut -c1-400;;
