@@ -255,6 +255,14 @@ int32_t clskd_bn_partial_blocks(int64_t rows, int32_t C);
 int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_seq, int64_t gx_t,
                          const float* whh, int32_t nws, int32_t nseq, int32_t T, int32_t H,
                          float* out, int64_t o_ws, int64_t o_seq, int64_t o_t, void* stream);
+/* Taped forward (training): as clskd_lstm_recurrent, and gx is overwritten in place with the gate
+ * pre-activations gx + W_hh h_{t-1} of every step — the `pre` input of clskd_lstm_bwd, so the
+ * backward does not recompute them with a GEMM over the saved history.  Only where
+ * clskd_lstm_pre_capable(H) (the single-wave H = 32 kernel; CLSKD_LSTM_PRE=0 turns it off). */
+int clskd_lstm_pre_capable(int32_t H);
+int clskd_lstm_recurrent_pre(float* gx, int64_t gx_ws, int64_t gx_seq, int64_t gx_t,
+                             const float* whh, int32_t nws, int32_t nseq, int32_t T, int32_t H,
+                             float* out, int64_t o_ws, int64_t o_seq, int64_t o_t, void* stream);
 
 /* One recurrence step with carried state (streaming inference, config C5): per (ws, seq),
  * gates = gx + W_hh h; c = f c + i g; h = o tanh(c) — h, c updated in place (strides s_ws,

@@ -136,6 +136,9 @@ SIGNATURES = {
     "clskd_mask_bdt": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _i32, _p]),
     "clskd_lstm_recurrent": (_i32, [_p, _i64, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _i64,
                                     _i64, _i64, _p]),
+    "clskd_lstm_recurrent_pre": (_i32, [_p, _i64, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _i64,
+                                    _i64, _i64, _p]),
+    "clskd_lstm_pre_capable": (_i32, [_i32]),
     "clskd_complex_combine": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p]),
     "clskd_complex_combine_dt": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i32, _p]),
     "clskd_lstm_cell": (_i32, [_p, _i64, _i64, _p, _i32, _i32, _i32, _p, _p, _i64, _i64, _p, _i64,

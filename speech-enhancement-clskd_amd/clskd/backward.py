@@ -346,13 +346,15 @@ def dccrn_backward(m, tape, enc, dec, dec_in, lstm_io, g, pg, acc_params=False, 
         wp, bias, whh = m._lstm_w(li, "fp32")[:3]
         dh = _empty((2, 2 * B, T, H), dev)
         ops.complex_combine_bwd(d_out[0], d_out[1], dh)
-        # gate pre-activations: gx + h_{t-1} W_hh^T over the saved history (in place in gx)
+        # gate pre-activations: gx + h_{t-1} W_hh^T over the saved history (in place in gx) —
+        # unless the taped forward's recurrence left them there (clskd_lstm_recurrent_pre)
         whp = _tw(("whh_p", id(m), li), whh,
                   lambda: torch.stack([ops.pack_weight(whh[ws].unsqueeze(1), H) for ws in (0, 1)]))
-        for ws in range(2):
-            hseg = Seg(hs, ws * 2 * B * T * H, SegGeom(H, T * H, 0, H, 1, T))
-            ops.conv([hseg], [(0, -1)], 2 * B, 1, T, 4 * H, whp[ws], None, gx,
-                     OutMap(T * 8 * H, 0, 8 * H), out_offset=ws * 4 * H, accumulate=True)
+        if not lt.get("pre", False):
+            for ws in range(2):
+                hseg = Seg(hs, ws * 2 * B * T * H, SegGeom(H, T * H, 0, H, 1, T))
+                ops.conv([hseg], [(0, -1)], 2 * B, 1, T, 4 * H, whp[ws], None, gx,
+                         OutMap(T * 8 * H, 0, 8 * H), out_offset=ws * 4 * H, accumulate=True)
         dg = _empty((2, B, T, 8 * H), dev)
         st = (4 * H, T * 8 * H, 8 * H)
         ops.lstm_bwd(gx, st, dh, (2 * B * T * H, T * H, H), whh, 2, 2 * B, T, H, dg, st)

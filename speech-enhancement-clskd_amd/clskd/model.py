@@ -606,10 +606,12 @@ class DCCRN(nn.Module):
                 ops.conv(segs, taps, B, 1, T, 8 * H, wp, bias, gx[half],
                          OutMap(T * 8 * H, 0, 8 * H))
             hs = torch.empty(2, 2 * B, T, H, **f32)
-            ops.lstm_recurrent(gx, 4 * H, T * 8 * H, 8 * H, whh, 2, 2 * B, T, H, hs,
-                               2 * B * T * H, T * H, H)
+            # taped: the recurrence leaves the gate pre-activations in gx (the backward's `pre`)
+            pre = tape is not None and ops.lstm_pre_capable(H)
+            (ops.lstm_recurrent_pre if pre else ops.lstm_recurrent)(
+                gx, 4 * H, T * 8 * H, 8 * H, whh, 2, 2 * B, T, H, hs, 2 * B * T * H, T * H, H)
             if tape is not None:
-                tape.setdefault("lstm", []).append(dict(gx=gx, hs=hs, r_in=r_in))
+                tape.setdefault("lstm", []).append(dict(gx=gx, hs=hs, r_in=r_in, pre=pre))
             # a 16-bit model (the frozen teacher in precision 'mixed' / 'fp16') stores the layer
             # output as the 16-bit operand of the next layer's input GEMM and the projection
             # (one rounding, as every other teacher activation); fp32 models and taped

@@ -670,6 +670,19 @@ def lstm_recurrent(gx, gx_ws, gx_seq, gx_t, whh, nws, nseq, T, H, out, o_ws, o_s
     return out
 
 
+def lstm_pre_capable(H):
+    """Whether lstm_recurrent_pre runs for hidden size H (else: lstm_recurrent + the backward's
+    pre-activation recompute)."""
+    return bool(lib().clskd_lstm_pre_capable(H))
+
+
+def lstm_recurrent_pre(gx, gx_ws, gx_seq, gx_t, whh, nws, nseq, T, H, out, o_ws, o_seq, o_t):
+    """lstm_recurrent that also overwrites gx with the gate pre-activations (taped forward)."""
+    check(lib().clskd_lstm_recurrent_pre(ptr(gx), gx_ws, gx_seq, gx_t, ptr(whh), nws, nseq, T, H,
+                                         ptr(out), o_ws, o_seq, o_t, _stream()), "lstm_pre")
+    return out
+
+
 def lstm_cell(gx, gx_ws, gx_seq, whh, nws, nseq, H, h, c, s_ws, s_seq, out, o_ws, o_seq):
     """One LSTM step with carried (h, c), updated in place (clskd_lstm_cell)."""
     check(lib().clskd_lstm_cell(ptr(gx), gx_ws, gx_seq, ptr(whh), nws, nseq, H, ptr(h), ptr(c),

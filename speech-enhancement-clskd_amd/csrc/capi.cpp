@@ -60,6 +60,7 @@ static const KnobDef kKnobs[KNOB_COUNT] = {
     {"CLSKD_LSTM_BWD_WAVE", 1, true},
     {"CLSKD_SPLIT_NS2", 1, true},
     {"CLSKD_BN_PFOLD", 1, true},
+    {"CLSKD_LSTM_PRE", 1, true},
     {"CLSKD_LSTM128_TDIV", 0, false},
     {"CLSKD_LSTM32_TDIV", 0, false}, {"CLSKD_BF16_DEBUG_MODE", 0, false}, {"CLSKD_SKIP", 0, false},
     {"CLSKD_H32_DEBUG_MODE", 0, false},

@@ -183,11 +183,15 @@ __global__ __launch_bounds__(NKS * H) void lstm_recurrent_kernel(
 // barrier), the S slices of a unit reduce with log2(S) DPP adds, lane s < 4 of a unit applies
 // gate(s) as in the k-sliced kernel, lane 0 keeps the cell, and h_t goes straight to `out`
 // (one 4*H-byte store per step).  Inputs prefetched two steps ahead.
+// pre (optional, may alias gx): the gate pre-activations gx + W_hh h_{t-1} of every step, in
+// gx's layout — what the backward's gate derivatives need (clskd_lstm_bwd `pre`); each lane
+// stores the pre-activations it formed, at the addresses its gate inputs came from (two steps
+// after they were read, so writing over gx in place is safe).
 template <int H>
 __global__ __launch_bounds__(64) void lstm_wave_kernel(
-    const float* __restrict__ gx, int64_t gx_ws, int64_t gx_seq, int64_t gx_t,
+    const float* gx, int64_t gx_ws, int64_t gx_seq, int64_t gx_t,
     const float* __restrict__ whh, int T, float* __restrict__ out, int64_t o_ws, int64_t o_seq,
-    int64_t o_t, int prio) {
+    int64_t o_t, int prio, float* pre) {
   if (prio) __builtin_amdgcn_s_setprio(3);
   constexpr int S = 64 / H;   // k-slices per unit
   constexpr int KW = H / S;   // k-slice width
@@ -208,6 +212,7 @@ __global__ __launch_bounds__(64) void lstm_wave_kernel(
   float cstate = 0.f;
   // this lane's gates: S = 4 -> gate ks; S = 2 -> gates ks, ks + 2
   const float* gp = gx + ws * gx_ws + seq * gx_seq + u;
+  float* pp = pre ? pre + ws * gx_ws + seq * gx_seq + u : nullptr;
   float* op = out + ws * o_ws + seq * o_seq + u;
   auto load_g = [&](int t, float& g0, float& g1) {
     const float* q = gp + (int64_t)min(t, T - 1) * gx_t;
@@ -248,6 +253,7 @@ __global__ __launch_bounds__(64) void lstm_wave_kernel(
       const float p01 = (ks & 1) ? pre[1] : pre[0];
       const float p23 = (ks & 1) ? pre[3] : pre[2];
       const float pg = ((ks & 2) ? p23 : p01) + g0;
+      if (pp) pp[(int64_t)t * gx_t + ks * H] = pg;
       const float k = ks == 2 ? 2.f : 1.f;
       const float act = fmaf(k, sigm_fast(k * pg), ks == 2 ? -1.f : 0.f);
       ig = act;
@@ -258,6 +264,10 @@ __global__ __launch_bounds__(64) void lstm_wave_kernel(
       // lane 0: i (sig) and g (tanh); lane 1: f (sig) and o (sig)
       const float pa = (ks ? pre[1] : pre[0]) + g0;
       const float pb = (ks ? pre[3] : pre[2]) + g1;
+      if (pp) {
+        pp[(int64_t)t * gx_t + ks * H] = pa;
+        pp[(int64_t)t * gx_t + (ks + 2) * H] = pb;
+      }
       const float a0 = sigm_fast(pa);
       const float kb = ks ? 1.f : 2.f;
       const float a1 = fmaf(kb, sigm_fast(kb * pb), ks ? 0.f : -1.f);
@@ -563,6 +573,10 @@ __global__ __launch_bounds__(4 * H) void lstm_cell_kernel(const float* __restric
 
 using namespace clskd;
 
+extern "C" int clskd_lstm_pre_capable(int32_t H) {
+  return H == 32 && knob(KNOB_LSTM_NKS32) == 1 && knob(KNOB_LSTM_PRE) != 0 ? 1 : 0;
+}
+
 extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_seq, int64_t gx_t,
                                     const float* whh, int32_t nws, int32_t nseq, int32_t T,
                                     int32_t H, float* out, int64_t o_ws, int64_t o_seq,
@@ -606,7 +620,7 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
       else if (nks32 == 2) LSTM_LAUNCH(32, 2);
       else if (nks32 == 8) LSTM_LAUNCH(32, 8);
       else hipLaunchKernelGGL(lstm_wave_kernel<32>, grid, dim3(64), 0, st, gx, gx_ws, gx_seq, gx_t,
-                              whh, T, out, o_ws, o_seq, o_t, prio);
+                              whh, T, out, o_ws, o_seq, o_t, prio, (float*)nullptr);
       break;
     case 64:
       LSTM_LAUNCH(64, 4);
@@ -626,6 +640,22 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
   }
 #undef LSTM_LAUNCH
   CLSKD_LAUNCH_CHECK("lstm_recurrent");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_lstm_recurrent_pre(float* gx, int64_t gx_ws, int64_t gx_seq, int64_t gx_t,
+                                        const float* whh, int32_t nws, int32_t nseq, int32_t T,
+                                        int32_t H, float* out, int64_t o_ws, int64_t o_seq,
+                                        int64_t o_t, void* stream) {
+  CLSKD_CHECK_ARG(gx && whh && out, "lstm_pre: null pointer");
+  CLSKD_CHECK_SHAPE(nws >= 1 && nseq >= 1 && T >= 1, "lstm_pre: empty shape");
+  CLSKD_CHECK_ARG(((uintptr_t)whh & 15) == 0, "lstm_pre: whh must be 16-byte aligned");
+  CLSKD_CHECK_SHAPE(clskd_lstm_pre_capable(H), "lstm_pre: H=%d runs on a kernel without the "
+                    "pre-activation output (clskd_lstm_pre_capable)", H);
+  hipLaunchKernelGGL(lstm_wave_kernel<32>, dim3(nseq, nws), dim3(64), 0, as_stream(stream), gx,
+                     gx_ws, gx_seq, gx_t, whh, T, out, o_ws, o_seq, o_t,
+                     knob(KNOB_LSTM_PRIO) == 1 ? 1 : 0, gx);
+  CLSKD_LAUNCH_CHECK("lstm_recurrent_pre");
   return CLSKD_OK;
 }
 

@@ -467,3 +467,29 @@ def test_index_gather_jobs_matches_single_gathers():
     ops.index_gather_jobs(jobs)
     for (_, _, _, out), ref in zip(jobs, refs):
         assert torch.equal(out, ref)
+
+
+def test_lstm_recurrent_pre_writes_gate_preactivations():
+    """clskd_lstm_recurrent_pre (the taped forward of the student's H = 32 layers): h identical
+    to clskd_lstm_recurrent bit for bit, and gx overwritten with the gate pre-activations
+    gx + W_hh h_{t-1} (h_{-1} = 0) of every step — against fp64 torch from the returned h
+    history, 1e-5 relative (what the backward otherwise recomputed with a GEMM)."""
+    from clskd import ops
+    H, B, T = 32, 3, 37
+    if not ops.lstm_pre_capable(H):
+        pytest.skip("pre-activation output disabled (CLSKD_LSTM_PRE=0)")
+    g = torch.Generator().manual_seed(5)
+    gx = torch.randn(2, 2 * B, T, 4 * H, generator=g).to(DEV)
+    whh = (torch.randn(2, 4 * H, H, generator=g) * 0.3).to(DEV)
+    st = (2 * B * T * 4 * H, T * 4 * H, 4 * H)
+    hs1 = torch.empty(2, 2 * B, T, H, device=DEV)
+    hs2 = torch.empty_like(hs1)
+    gx2 = gx.clone()
+    ops.lstm_recurrent(gx, *st, whh, 2, 2 * B, T, H, hs1, 2 * B * T * H, T * H, H)
+    ops.lstm_recurrent_pre(gx2, *st, whh, 2, 2 * B, T, H, hs2, 2 * B * T * H, T * H, H)
+    torch.cuda.synchronize()
+    assert torch.equal(hs1, hs2)
+    h = hs1.double().cpu()
+    hprev = torch.cat([torch.zeros(2, 2 * B, 1, H, dtype=torch.float64), h[:, :, :-1]], 2)
+    exp = gx.double().cpu() + torch.einsum("wstk,wgk->wstg", hprev, whh.double().cpu())
+    np.testing.assert_allclose(gx2.double().cpu().numpy(), exp.numpy(), rtol=1e-5, atol=1e-5)
