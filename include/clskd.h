@@ -131,8 +131,9 @@ typedef struct {
   int32_t seg_c[CLSKD_MAX_SEGS];
   int16_t tap_df[16];
   int16_t tap_dt[16];
-  /* 1: out += result (read-modify-write, fp32 `out`, MFMA engines with wlayout NK and fp32
-     compute only) — lets several data-gradient contributions of one tensor sum in place. */
+  /* 1: out += result (read-modify-write, fp32 `out`, fp32 compute, no statistics: the fp32 MFMA
+     engines with wlayout NK, or the direct kernel with wlayout DIRECT for narrow N / short K) —
+     lets several data-gradient contributions of one tensor sum in place. */
   int32_t accumulate;
   int32_t reserved_;
   /* Optional folded BatchNorm finalize (HOST pointer, read at launch; NULL = none): the launch
