@@ -124,12 +124,11 @@ def host_cpu_info():
     return model, total, usable
 
 
-def cpu_baseline(n_timed=3, n_warm=3):
+def cpu_baseline(n_timed=10, n_warm=3):
     """The CPU oracle (fp32 PyTorch-CPU restatement of the reference, oracle/ref_cpu.py) timed on
     this host following BASELINE.md §2: every usable host core, the same seeded B=16 x 4 s
-    workload as the GPU leg, warm-up iterations, then the median of `n_timed` full B=16 steps.
-    The warm-ups run at B=4 (thread pools and allocator warmed on the same code path at a
-    quarter of the cost) so the default bench stays within a few minutes."""
+    workload as the GPU leg, 3 warm-up steps and the median of 10 timed steps — all full B=16
+    steps (round 5 warmed up at B=4, which left the first timed B=16 step cold: 9.5 vs 7.5 s)."""
     from oracle import ref_cpu as R
     from clskd.data import synthetic_pairs
     from clskd.weights import ABF_SEED, STUDENT_SEED, TEACHER_SEED, recipe_state_dict
@@ -146,7 +145,7 @@ def cpu_baseline(n_timed=3, n_warm=3):
     times = []
     with torch.no_grad():
         for _ in range(n_warm):
-            R.clskd_step(pt, ps, pa, X[:4], Y[:4])
+            R.clskd_step(pt, ps, pa, X, Y)
         for _ in range(n_timed):
             t0 = time.perf_counter()
             R.clskd_step(pt, ps, pa, X, Y)
@@ -157,7 +156,7 @@ def cpu_baseline(n_timed=3, n_warm=3):
                 batch=Bc, host_cpus=total, cpu_model=model,
                 step_s=[round(t, 3) for t in times],
                 sample=f"oracle/ref_cpu.clskd_step on the bench workload (B={Bc} x 4 s @16 kHz, "
-                       f"same step as the GPU leg): {n_warm} warm-up steps (B=4), median of "
+                       f"same step as the GPU leg): {n_warm} warm-up steps (B={Bc}), median of "
                        f"{n_timed} timed B={Bc} steps, fp32, torch CPU {threads} threads = every "
                        f"CPU this job may use ({total} logical CPUs on the host), {model}")
 
@@ -407,7 +406,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU-oracle B=16 steps (median)")
+    ap.add_argument("--cpu-steps", type=int, default=10,
+                    help="timed CPU-oracle B=16 steps (median; BASELINE.md §2: 10)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--abf-reinit", default="step", choices=["step", "once"])
     ap.add_argument("--launch", default=None, choices=["exec", "eager", "graph"],
@@ -477,18 +477,19 @@ def main():
     if args.spkd and args.train:
         raise SystemExit("--spkd is its own leg (no --train)")
     if args.launch is None:
-        # C2 (one rank): the step captured once and replayed by the C++ executor with the
-        # teacher_ahead overlap (clskd.graph.AheadStepExecutor): the eager device schedule at
-        # ~0.6 ms of host time per step instead of ~3.9 ms of Python launches (same-box A/B,
-        # profiles/r5_exec_ab.txt: 5.28 vs 5.28 ms per step).  C3 (one rank): the captured
-        # training step replayed by the executor, one replay in flight (TrainStepExecutor):
-        # 17.8-18.0 ms at ~2.5 ms of host time against 18.15 ms eager with 14 ms of Python
-        # launches (profiles/r5_train_split_ab.txt)
+        # C2: the step captured once and replayed by the C++ executor with the teacher_ahead
+        # overlap (clskd.graph.AheadStepExecutor): the eager device schedule at ~0.6 ms of host
+        # time per step instead of ~3.9 ms of Python launches (same-box A/B,
+        # profiles/r5_exec_ab.txt: 5.28 vs 5.28 ms per step).  C3: the captured training step
+        # replayed by the executor, one replay in flight (TrainStepExecutor): 17.8-18.0 ms at
+        # ~2.5 ms of host time against 18.15 ms eager with 14 ms of Python launches
+        # (profiles/r5_train_split_ab.txt).  Every rank count runs the same launch path (round
+        # 6): with N > 1 ranks the C2 step has no exchange, and the C3 replay (fwd+loss +
+        # backward) is followed by the flat-gradient all-reduce and the Adam launch
+        # (clskd.graph.TrainStepGraph, collective mode)
         args.launch = "exec" if not args.spkd else "eager"
-    if args.spkd or world > 1:
-        # the C4 leg launches eagerly (its capture is not wired yet); multi-rank runs launch
-        # eagerly too (no graph capture beside the RCCL communicator's watchdog)
-        args.launch = "eager"
+    if args.spkd and args.launch != "eager":
+        raise SystemExit("--spkd (C4) launches eagerly")
     args.graph = args.launch == "graph"
     bsz = B_SPKD if args.spkd else B_PER_GPU
     kd = build_kd(dev, args.abf_reinit, args.precision, spkd=args.spkd)
@@ -521,7 +522,9 @@ def main():
     if args.train:
         from clskd.train import FlatAdam, FlatParams
         flat = FlatParams(kd.student)
-        opt = FlatAdam(flat, lr=cfg.learning_rate, device_step=args.launch in ("exec", "graph"))
+        # the step count on the device for every launch path (a captured step replays it), so
+        # eager and replayed steps run the same Adam kernel (bitwise comparable)
+        opt = FlatAdam(flat, lr=cfg.learning_rate, device_step=True)
 
         def eager_step(i):
             return kd.train_step((Xs[i % NBATCH], Ys[i % NBATCH]), flat, opt)

@@ -204,6 +204,16 @@ int32_t clskd_conv_last_stream_k(void);
  * Done implicitly by the first conv on a stream outside graph capture; hosts call it for a stream
  * they are about to capture on, so captured and eager launches take the same path. */
 int clskd_stream_prepare(void* stream);
+/* Stream-K workspaces of one graph capture (round 6).  A launch made while its stream is being
+ * captured never uses the stream's own workspace (the graph is replayed on other streams, and two
+ * graphs captured on one stream may replay concurrently); it uses the workspace the capturing
+ * thread's bound scope holds for that stream, or runs the data-parallel tile deal when there is
+ * none.  begin (outside capture): allocate a zeroed workspace for each of `streams` and bind the
+ * scope to the calling thread; end: unbind (after the capture); free: release it once no replay
+ * of the graph is queued or will be launched again. */
+int clskd_capture_scope_begin(void* const* streams, int32_t nstreams, void** scope);
+int clskd_capture_scope_end(void* scope);
+int clskd_capture_scope_free(void* scope);
 /* Direct-path helpers: padded output width NP of the direct layout, and whether an (N, K)
  * GEMM is served by the direct kernel (returns 1) — hosts pack CLSKD_WLAYOUT_DIRECT weights
  * exactly when this is 1. */

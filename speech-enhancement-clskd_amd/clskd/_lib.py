@@ -115,6 +115,9 @@ SIGNATURES = {
     "clskd_conv_last_stream_k": (_i32, []),
     "clskd_exec_launch_ahead": (_i32, [_p, _p, C.c_uint32, _p]),
     "clskd_stream_prepare": (_i32, [_p]),
+    "clskd_capture_scope_begin": (_i32, [_p, _i32, _p]),
+    "clskd_capture_scope_end": (_i32, [_p]),
+    "clskd_capture_scope_free": (_i32, [_p]),
     "clskd_version": (_i32, []),
     "clskd_set_knob": (_i32, [C.c_char_p, _i32]),
     "clskd_get_knob": (_i32, [C.c_char_p, C.POINTER(C.c_int32)]),

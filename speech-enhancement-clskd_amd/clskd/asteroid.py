@@ -165,10 +165,12 @@ class DCCRNet_mini(nn.Module):
     def _packed(self, key, params, build):
         ent = self._wcache.get(key)
         ver = _pv(*params)
-        if ent is None or ent[0] != ver:
+        tok = ops.capture_token()  # entries built inside a capture serve that capture only
+        if ent is None or ent[0] != ver or not ops.cache_entry_usable(ent[2], tok):
             with torch.no_grad():
-                ent = (ver, build())
+                ent = (ver, build(), tok)
             self._wcache[key] = ent
+        ops.capture_keep(ent[1], tok)
         return ent[1]
 
     def _enc_w(self, i):

@@ -127,8 +127,10 @@ def _tw(key, src, build):
     source died are dropped on every insert, and the cache is bounded (oldest first), so freed
     models do not keep device copies of their weights alive."""
     k = (src.data_ptr(), src._version)
+    tok = ops.capture_token()  # entries built inside a capture serve that capture only
     ent = _TW.get(key)
-    if ent is not None and ent[0] == k and ent[2]() is src:
+    if ent is not None and ent[0] == k and ent[2]() is src and ops.cache_entry_usable(ent[3], tok):
+        ops.capture_keep(ent[1], tok)
         return ent[1]
     with torch.no_grad():
         w = _tw_build(key, src, build)
@@ -138,7 +140,8 @@ def _tw(key, src, build):
         del _TW[dead]
     while len(_TW) >= _TW_MAX:
         del _TW[next(iter(_TW))]
-    _TW[key] = (k, w, weakref.ref(src))
+    _TW[key] = (k, w, weakref.ref(src), tok)
+    ops.capture_keep(w, tok)
     return w
 
 
@@ -186,6 +189,10 @@ def _tw_probe(src, build, w, sig):
     if wp.shape != w.shape or wp.dtype != f32:
         return False
     v = wp.reshape(-1)
+    # a build that reads tensors other than `src` (or is not a ±1 selection) yields values that
+    # are not source indices: reject the map before any gather could read out of bounds
+    if not ops.probe_values_are_indices(v, src.numel()):
+        return False
     idx = torch.where(v != 0, v.abs() - 1, torch.full_like(v, -1)).to(torch.int32).reshape(-1, 1)
     sgn = torch.sign(v).reshape(-1, 1).contiguous()
     out = torch.empty(w.shape, dtype=f32, device=w.device)

@@ -231,13 +231,14 @@ class ABF(nn.Module):
         if ent is not None:
             w1p, w2p, _ = ent[1]
             torch.autograd.graph.increment_version([w1p, w2p])  # invalidates derived layouts
-            self._wcache["w"] = (_pv(*ps) + ent[0][-2:], ent[1])
+            self._wcache["w"] = (_pv(*ps) + ent[0][-2:],) + tuple(ent[1:])
 
     def _weights(self, in_dtype):
         ps = self._params()
         ver = _pv(*ps) + (self.compute, in_dtype)
         ent = self._wcache.get("w")
-        if ent is None or ent[0] != ver:
+        tok = ops.capture_token()  # entries built inside a capture serve that capture only
+        if ent is None or ent[0] != ver or not ops.cache_entry_usable(ent[2] if len(ent) > 2 else None, tok):
             with torch.no_grad():
                 c1 = "bf16" if in_dtype == torch.bfloat16 else "fp32"
                 w1 = self.conv1[0].weight  # [mid, in, 1, 1]
@@ -249,8 +250,9 @@ class ABF(nn.Module):
                 if self.att_conv is not None:
                     att = (self.att_conv[0].weight.reshape(2, -1).float().contiguous(),
                            self.att_conv[0].bias.float().contiguous())
-            ent = (ver, (w1p, w2p, att))
+            ent = (ver, (w1p, w2p, att), tok)
             self._wcache["w"] = ent
+        ops.capture_keep(ent[1], tok)
         return ent[1]
 
     def forward_bftc(self, x, y=None, shape=None, out_shape=None, train=None, defer_bn=False,

@@ -95,13 +95,15 @@ class StepGraph:
                 b.copy_(v)
         self.graph = None
         g = torch.cuda.CUDAGraph(keep_graph=True) if self.keep_graph else torch.cuda.CUDAGraph()
+        scope = self._new_scope(s)
         self._tagging(True)
         prev_ahead = getattr(self.kd, "teacher_ahead", False)
         self.kd.teacher_ahead = self.ahead_layout
         try:
-            with torch.cuda.graph(g, stream=s):
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                 self.out = self.kd.training_step((self.X, self.y), return_parts=True)
         finally:
+            scope.end()
             self._tagging(False)
             self.kd.teacher_ahead = prev_ahead
         self.graph = g
@@ -111,6 +113,17 @@ class StepGraph:
 
     def _after_capture(self):
         pass
+
+    def _new_scope(self, s):
+        """The stream-K workspaces of the capture about to start (ops.CaptureScope): one per stream
+        the step launches on; the previous capture's (its graph is being replaced) are freed."""
+        from .distill import _side_stream
+        old = getattr(self, "_scope", None)
+        if old is not None:
+            old.free()
+        dev = self.X.device
+        self._scope = ops.CaptureScope([s] + [_side_stream(dev, w) for w in (0, 1, 2)])
+        return self._scope
 
     def _tagging(self, on):
         pass
@@ -260,6 +273,11 @@ class AheadStepExecutor:
         self.ex = [StepExecutor(kd, X, y, warmup, ahead_layout=True) for _ in range(2)]
         if self.ex[0].nstreams != 4:
             raise ValueError("AheadStepExecutor needs the four-stream replay")
+        if os.environ.get("CLSKD_EXEC_OWN_STREAMS") == "1":
+            # the batch copy below is ordered only with the step's own teacher stream (executor
+            # stream 3 when the executor replays on the step's streams)
+            raise ValueError("AheadStepExecutor replays on the step's own streams "
+                             "(unset CLSKD_EXEC_OWN_STREAMS)")
         self.done = [torch.cuda.Event(), torch.cuda.Event()]
         self.i = 0
         self.last = self.ex[0]
@@ -275,6 +293,12 @@ class AheadStepExecutor:
         e = self.ex[self.i]
         if e._sig() != e.sig:
             raise RuntimeError("AheadStepExecutor: a baked parameter changed; re-create it")
+        if X is not None and X.shape != e.X.shape:
+            raise ValueError(f"AheadStepExecutor captured inputs of shape {tuple(e.X.shape)}, "
+                             f"got {tuple(X.shape)}")
+        if y is not None and y.numel() != e.y.numel():
+            raise ValueError(f"AheadStepExecutor captured targets of {e.y.numel()} elements, "
+                             f"got {tuple(y.shape)}")
         infl = StepExecutor.inflight
         if infl > 0:  # bounded run-ahead (StepExecutor.inflight)
             import time
@@ -314,8 +338,15 @@ class TrainStepGraph(StepGraph):
     step count (FlatAdam(device_step=True)), so N replays are N training steps, bitwise equal to
     N eager ``train_step`` calls with the same optimizer (tests/test_gpu_train_graph.py).  The
     eager path spends ~16 ms of host time per step issuing ~1,000 launches; a replay is one
-    hipGraphLaunch.  Single process only (a collective inside the capture is not wired:
-    multi-rank training steps launch eagerly).
+    hipGraphLaunch.
+
+    Multi-rank (round 6): the gradient all-reduce is not captured.  With a process group of more
+    than one rank (or ``collective=True``) the capture holds fwd+loss and the backward only; every
+    replay is followed by the one flat-gradient all-reduce (clskd.train.allreduce_grads: RCCL,
+    gloo in tests) and the Adam launch, issued on the caller's stream — the eager step's order, so
+    a replayed step is bitwise the eager ``train_step`` (tests/test_gpu_bench_ddp.py).  Captures
+    use torch's thread-local capture mode, so the process group's watchdog thread may query its
+    own streams while the step is being recorded.
 
         flat = FlatParams(kd.student); opt = FlatAdam(flat, lr=..., device_step=True)
         step = TrainStepGraph(kd, flat, opt, X, y)      # hipGraphLaunch replay
@@ -328,14 +359,14 @@ class TrainStepGraph(StepGraph):
     refuses graphs that hold one.
     """
 
-    def __init__(self, kd, flat, opt, X, y, warmup=1, **kw):
+    def __init__(self, kd, flat, opt, X, y, warmup=1, collective=None, **kw):
         import torch.distributed as dist
         if not getattr(opt, "device_step", False):
             raise ValueError("TrainStepGraph needs FlatAdam(device_step=True): the step count "
                              "must live on the device to be replayed")
-        if dist.is_initialized() and dist.get_world_size() > 1:
-            raise NotImplementedError("TrainStepGraph: multi-rank steps launch eagerly "
-                                      "(no all-reduce inside the capture)")
+        if collective is None:
+            collective = dist.is_initialized() and dist.get_world_size() > 1
+        self.collective = bool(collective)
         self.flat, self.opt = flat, opt
         super().__init__(kd, X, y, warmup, **kw)
 
@@ -345,10 +376,22 @@ class TrainStepGraph(StepGraph):
         return [p for p in super()._baked() if id(p) not in trainable]
 
     def _run(self):
+        if self.collective:  # the captured part: fwd+loss with the tape and the backward
+            out = self.kd.forward_with_tape(self.X, self.y)
+            self.kd.backward_into(out, self.flat.grad_dict())
+            return out["loss"]
         return self.kd.train_step((self.X, self.y), self.flat, self.opt)
+
+    def _finish(self):
+        """The uncaptured tail of a multi-rank step (kd.train_step's): all-reduce + Adam."""
+        from .train import allreduce_grads
+        scale = allreduce_grads(self.flat)
+        self.opt.step(grad_scale=scale)
 
     def _replay(self):
         super()._replay()
+        if self.collective:
+            self._finish()
         # the replay's Adam rewrote the parameters on the device: advance their version counters
         # (as FlatAdam.step does eagerly) so caches keyed on (data_ptr, _version) — the student's
         # packed weights, DCCRN._packed — rebuild on the next eager forward instead of serving
@@ -371,6 +414,8 @@ class TrainStepGraph(StepGraph):
         with torch.cuda.stream(s):
             for _ in range(self.warmup):
                 self._run()
+                if self.collective:
+                    self._finish()
         cur.wait_stream(s)
         torch.cuda.synchronize(dev)
         with torch.no_grad():
@@ -380,11 +425,13 @@ class TrainStepGraph(StepGraph):
         g = torch.cuda.CUDAGraph(keep_graph=True) if self.keep_graph else torch.cuda.CUDAGraph()
         student = self.kd.student
         student.repack_in_capture = True
+        scope = self._new_scope(s)
         self._tagging(True)
         try:
-            with torch.cuda.graph(g, stream=s):
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                 self.out = dict(loss=self._run())
         finally:
+            scope.end()
             self._tagging(False)
             student.repack_in_capture = False
         self.graph = g
@@ -431,8 +478,13 @@ class CapturedCall:
         cur.wait_stream(s)
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph(keep_graph=True)
-        with torch.cuda.graph(self.graph, stream=s), torch.no_grad():
-            self.out = fn(*self.inputs)
+        self._scope = ops.CaptureScope([s])
+        try:
+            with torch.cuda.graph(self.graph, stream=s, capture_error_mode="thread_local"), \
+                    torch.no_grad():
+                self.out = fn(*self.inputs)
+        finally:
+            self._scope.end()
         lib = _lib.load()
         h = C.c_void_p()
         _lib.check(lib.clskd_exec_create(C.c_void_p(self.graph.raw_cuda_graph()), nstreams, None,

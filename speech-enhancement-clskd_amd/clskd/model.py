@@ -234,6 +234,10 @@ def _probe_pack_map(params, build, out):
     # each element's non-zero terms in parameter order, padded with idx -1
     order = torch.argsort((~nz).to(torch.int8), dim=1, stable=True)[:, :J]
     v = torch.gather(T, 1, order)
+    # values that are not flat indices of `root` (a build that reads other tensors, or one that is
+    # not a ±1 selection): reject before the gather could read out of bounds
+    if not ops.probe_values_are_indices(v, root.numel()):
+        return False
     idx = torch.where(v != 0, v.abs() - 1, torch.full_like(v, -1)).to(torch.int32).contiguous()
     sgn = torch.sign(v).contiguous()
     buf = torch.empty(total, dtype=torch.float32, device=dev)
@@ -350,12 +354,14 @@ class DCCRN(nn.Module):
             params = pg
         ent = self._wcache.get(key)
         ver = _pv(*params)
-        if ent is None or ent[0] != ver or (
-                self.repack_in_capture and torch.cuda.is_current_stream_capturing()
+        tok = ops.capture_token()  # entries built inside a capture serve that capture only
+        if ent is None or ent[0] != ver or not ops.cache_entry_usable(ent[2], tok) or (
+                self.repack_in_capture and tok is not None
                 and any(p.requires_grad for p in params)):
             with torch.no_grad():
-                ent = (_pv(*params), _pack_group(self._pmaps, key, params, build))
+                ent = (_pv(*params), _pack_group(self._pmaps, key, params, build), tok)
             self._wcache[key] = ent
+        ops.capture_keep(ent[1], tok)
         return ent[1]
 
     def _layer_refs(self):

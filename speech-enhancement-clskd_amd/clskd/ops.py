@@ -92,10 +92,13 @@ def direct_weight(wpacked):
     """[N][Kp] packed weight -> the direct kernel's k-major layout (CLSKD_WLAYOUT_DIRECT):
     fp32 [Kp][NP]; bf16 [Kp/2][NP][2].  Cached per packed tensor (pointer + version; the cache
     holds the source alive so a pointer is never reused while its entry exists)."""
-    key = (wpacked.data_ptr(), wpacked._version, tuple(wpacked.shape), wpacked.dtype)
+    tok = capture_token()
+    # an entry built inside a capture holds its values only in that graph's replays (key below)
+    key = (wpacked.data_ptr(), wpacked._version, tuple(wpacked.shape), wpacked.dtype, id(tok))
     ent = _DIRECT_W.get(key)
-    if ent is not None:
+    if ent is not None and ent[2] is tok:
         _DIRECT_W.move_to_end(key)
+        capture_keep(ent, tok)
         return ent[1]
     N, Kp = wpacked.shape
     NP = direct_np(N)
@@ -110,7 +113,8 @@ def direct_weight(wpacked):
     # capture — the BN partials of the very launch that reads these weights (a race in every
     # replay; the eager path always hit this cache).  A capture-built entry keeps its graph-pool
     # block alive; the captured repack rewrites the same values on every replay.
-    _DIRECT_W[key] = (wpacked, wd)
+    _DIRECT_W[key] = ent = (wpacked, wd, tok)
+    capture_keep(ent, tok)
     while len(_DIRECT_W) > 512:
         _DIRECT_W.popitem(last=False)
     return wd
@@ -475,6 +479,99 @@ def prepare_stream(stream):
     ones (a stream without a workspace runs the data-parallel tile deal)."""
     check(lib().clskd_stream_prepare(stream.cuda_stream), "stream_prepare")
     return stream
+
+
+def probe_values_are_indices(v, numel):
+    """Whether the output of a packing build evaluated on (flat index + 1)-valued parameters can be
+    read as a ±(index + 1) selection map of a `numel`-element source: every value an exact
+    integer of magnitude <= numel (0 = no source element).  The probes (model._probe_pack_map,
+    backward._tw_probe) check this before launching an index_gather built from the values."""
+    if v.numel() == 0:
+        return True
+    if not bool(torch.isfinite(v).all()):
+        return False
+    a = v.abs()
+    # float32 holds every integer up to 2^24 exactly: larger sources cannot be probed this way
+    return numel < (1 << 24) and bool((v == v.round()).all()) and float(a.max()) <= numel
+
+
+# ---- caches under graph capture ------------------------------------------------------------
+# Weight-layout caches (DCCRN._packed, ABF._weights, backward._tw, direct_weight) hold device
+# tensors keyed on their sources' (pointer, version).  Two hazards come with graph capture:
+#  (1) an entry BUILT while a graph is being captured holds nothing until that graph replays —
+#      served to an eager launch (e.g. bench.py's census step right after the capture, or any
+#      eager step before the first replay) it is garbage;
+#  (2) an entry a capture READS must outlive the graph, even when an eager rebuild later replaces
+#      it in the cache.
+# So every entry records the capture it was built in (capture_token(): None = eager), a lookup
+# reuses an entry only from its own capture or from eager code, and every value a capture reads
+# is appended to that capture's keep-alive list (CaptureScope.keep, owned with the graph).
+_CAPTURE_TOKEN = None  # the CaptureScope being recorded on this process's capturing thread
+_ANON_CAPTURE = object()  # a capture without a CaptureScope (nothing kept alive for it)
+
+
+def capture_token():
+    """None outside graph capture; else the identity of the capture being recorded."""
+    if not (torch.cuda.is_initialized() and torch.cuda.is_current_stream_capturing()):
+        return None
+    return _CAPTURE_TOKEN if _CAPTURE_TOKEN is not None else _ANON_CAPTURE
+
+
+def cache_entry_usable(built_token, token):
+    """Whether a cache entry built under `built_token` may serve a lookup under `token`."""
+    return built_token is None or built_token is token
+
+
+def capture_keep(obj, token):
+    """Keep `obj` alive as long as the graph being captured under `token`."""
+    if token is not None and token is not _ANON_CAPTURE:
+        token.keep.append(obj)
+
+
+class CaptureScope:
+    """One graph capture's library state: the conv_gemm8 stream-K workspaces
+    (clskd_capture_scope_begin, include/clskd.h) — created just before ``torch.cuda.graph(...)``
+    with every stream the capture launches on, ended right after it, freed together with the
+    graph (without a scope a captured launch runs the data-parallel tile deal, and its replays
+    would differ in the last bits from the eager launches of a prepared stream, which split
+    tiles) — and the cache token / keep-alive list above."""
+
+    def __init__(self, streams):
+        import ctypes as C
+        global _CAPTURE_TOKEN
+        if _CAPTURE_TOKEN is not None:
+            raise RuntimeError("CaptureScope: another capture is being recorded")
+        self._lib = lib()
+        ptrs = (C.c_void_p * len(streams))(*[s.cuda_stream for s in streams])
+        h = C.c_void_p()
+        check(self._lib.clskd_capture_scope_begin(ptrs, len(streams), C.byref(h)), "capture_scope_begin")
+        self.h, self.bound = h, True
+        self.keep = []
+        _CAPTURE_TOKEN = self
+
+    def end(self):
+        global _CAPTURE_TOKEN
+        if self.bound:
+            self.bound = False
+            if _CAPTURE_TOKEN is self:
+                _CAPTURE_TOKEN = None
+            check(self._lib.clskd_capture_scope_end(self.h), "capture_scope_end")
+
+    def free(self):
+        """Release the workspaces and kept tensors: the graph captured under this scope must not
+        run again."""
+        self.end()
+        if self.h is not None and self.h.value:
+            torch.cuda.synchronize()  # no replay using them may still be queued
+            check(self._lib.clskd_capture_scope_free(self.h), "capture_scope_free")
+        self.h = None
+        self.keep = []
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 _CAPTURE_STREAMS = {}

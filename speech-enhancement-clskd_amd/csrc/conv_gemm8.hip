@@ -191,6 +191,10 @@ constexpr int SK_SC1 = 16;  // buffer cache-policy bits: sc1 (write-through / L1
 // per-piece 64-bit bounds arithmetic: ~12 VALU per K-tile instead of ~120.  TA bit 1 (TA = 3):
 // the stream-K deal (ConvArgsG8::sk_cnt) compiled in; its bookkeeping costs registers, so only
 // the launches that split tiles run that instantiation.
+// DBG >= 16 (round 6, TA instances, experiments library only): ablation flags ABL = DBG - 16 —
+// 1 no LDS-DMA, 2 no MFMA, 4 no fragment reads (opaque registers), 8 no epilogue (statistics and
+// stores), 16 A pieces only, 32 B pieces only, 64 no DMA wait inside the stream, 128 no output
+// stores (statistics kept), 256 no statistics (stores kept).  Wrong results.
 template <int BM, int BN, int WM, int BK, int NS, int PHI, typename OutT, int DBG = 0, int PF = 1, int NWV = 8,
           int EB = 0, typename InT = __bf16, int PP = 0, int TA = 0>
 __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 args) {
@@ -213,8 +217,14 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
   static_assert((BM / RPP) % NW == 0 && (BN / RPP) % NW == 0 && NGA >= 1, "DMA piece split");
   static_assert(PHI >= 1 && PHI <= NSUB && NSUB % 2 == 0, "issue substeps");
   static_assert(NS >= 2 && WM * BN * 16 <= SB, "statistics scratch fits one stage");
-  static_assert(!(TA & 1) || (BK == 64 && NGA == 4 && (NGB == 4 || NGB == 2) && PHI == 2 && PP == 0 && DBG == 0),
+  static_assert(!(TA & 1) || (BK == 64 && NGA == 4 && (NGB == 4 || NGB == 2) && PHI == 2 && PP == 0 &&
+                               (DBG == 0 || DBG >= 16)),
                 "tap-addressed pieces: 256-row tiles, two issue substeps");
+  constexpr int ABL = DBG >= 16 ? DBG - 16 : 0;
+  constexpr bool NO_DMA = DBG == 1 || DBG == 3 || (ABL & 1);
+  constexpr bool NO_MFMA = DBG == 2 || DBG == 3 || (ABL & 2);
+  constexpr bool NO_FRAG = (ABL & 4) != 0;
+  constexpr bool NO_EPI = (ABL & 8) != 0;
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* stages = smem;
@@ -438,6 +448,13 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
   // fragment reads of substep s (k = 16s .. 16s+15) of the stage at `sa`
   auto swz = [](int row) { return BK == 64 ? ((row >> 1) & 7) : ((row >> 2) & 3); };
   auto read_frags = [&](const unsigned char* sa, int s, bf16x8s (&af)[FM], bf16x8s (&bfr)[FN]) {
+    if constexpr (NO_FRAG) {  // ablation: opaque registers instead of LDS reads
+#pragma unroll
+      for (int i = 0; i < FM; ++i) asm volatile("" : "=v"(af[i]));
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) asm volatile("" : "=v"(bfr[jj]));
+      return;
+    }
     const unsigned char* sb = sa + BM * ROWB;
     const int c = 2 * s + h;
 #pragma unroll
@@ -452,7 +469,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
     }
   };
   auto mfmas = [&](const bf16x8s (&af)[FM], const bf16x8s (&bfr)[FN]) {
-    if constexpr (DBG != 2 && DBG != 3) {
+    if constexpr (!NO_MFMA) {
       if constexpr (DBG == 6 || DBG == 8) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -538,7 +555,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
       for (int g = 0; g < G; ++g) glds16((const void*)piece_src(g, kt, e), dst(g, w % NS));
     }
   };
-  if (DBG != 1 && DBG != 3) {
+  if (!NO_DMA) {
 #pragma unroll
     for (int w = 0; w < NS - 1; ++w)
       if (w < total) issue_all(w);
@@ -607,7 +624,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
       const unsigned char* sa = stages + (gk % NS) * SB;
       // the K-tile issued during this one: stream gk + NS - 1
       const int wi = gk + NS - 1;
-      const bool do_issue = wi < total && DBG != 1 && DBG != 3;
+      const bool do_issue = wi < total && !NO_DMA;
       int kti = 0;
       KEnt e{};
       TaK tk{};
@@ -623,7 +640,8 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
       const int sn = wi % NS;
       auto issue = [&](int part) {
         if constexpr ((TA & 1) != 0) {
-          if (part < PHI && do_issue) ta_issue(part, tk, sn);
+          if (part < PHI && do_issue && !((ABL & 16) && part == 1) && !((ABL & 32) && part == 0))
+            ta_issue(part, tk, sn);
           return;
         }
         if (part < PHI && do_issue) {
@@ -639,7 +657,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
       // the next K-tile's pieces (this wave's) landed — younger K-tiles stay in flight; then
       // every wave's are visible and every wave is done reading this K-tile's stage
       auto k_boundary = [&]() {
-        if (DBG == 9 && gk + 1 < total) {  // timing only: never wait for the DMA inside the stream
+        if ((DBG == 9 || (ABL & 64)) && gk + 1 < total) {  // timing only: never wait for the DMA inside the stream
         } else if ((DBG >= 4 && DBG <= 5) || gk + 1 >= total) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
@@ -747,7 +765,7 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
             __builtin_amdgcn_sched_barrier(0);
           }
     }
-    if (finish && (d.stats || fold)) {  // fused BatchNorm statistics: one fp64 partial per 128 output rows
+    if (finish && (d.stats || fold) && !NO_EPI && !(ABL & 256)) {  // fused BatchNorm statistics: one fp64 partial per 128 output rows
       constexpr int HALVES = BM / 128;
       constexpr int WPH = WM / HALVES;  // waves along M per 128-row half
       double* red = reinterpret_cast<double*>(scratch);  // [WM][BN][2]
@@ -824,8 +842,8 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
     static_assert(NW * UB <= SB, "epilogue staging");
     const bool vec = d.oNlo == 1 && d.nlo >= d.N && d.N % CH == 0 && (((uintptr_t)d.out) & 15) == 0 &&
                      d.oB % CH == 0 && d.oF % CH == 0 && d.oT % CH == 0;
-    if (!finish) {
-      // the other piece's workgroup writes this tile
+    if (!finish || NO_EPI || (ABL & 128)) {
+      // the other piece's workgroup writes this tile (or the ablation skips the stores)
     } else if (vec) {
       OutT* wt = reinterpret_cast<OutT*>(scratch + wave * UB);  // [32][32], this wave's
       constexpr int CPRW = 32 / CH;
@@ -899,8 +917,14 @@ __global__ __launch_bounds__(NWV * 64) void conv_gemm8_kernel(const ConvArgsG8 a
 
 // ---- stream-K workspace: one per HIP stream (launches on one stream are ordered; two streams'
 // launches may run together, so they never share partial slabs, tickets or flags).  Allocated
-// at the first launch on a stream outside graph capture (or by clskd_stream_prepare); a launch
-// captured on a stream without one runs the data-parallel deal instead.
+// at the first launch on a stream outside graph capture (or by clskd_stream_prepare).  A launch
+// made during graph capture never takes the stream's own workspace: a graph's replays run on
+// other streams (the executor's, hipGraphLaunch's) and two graphs captured on one stream may be
+// replayed concurrently (clskd.graph.AheadStepExecutor), so a workspace baked into a capture no
+// longer belongs to one stream's ordered launches.  A capture gets workspaces of its own instead:
+// clskd_capture_scope_begin (before the capture starts) allocates one per stream the capture will
+// launch on and binds them to the calling thread; launches captured on another stream, or with no
+// scope bound, run the data-parallel deal.  The scope's owner frees it with the graph.
 constexpr int SK_MAX_GRID = 256, SK_MAX_TILES = 1 << 16;
 struct SkWs {
   float* ws;           // [SK_MAX_GRID][2][256 * 256] fp32
@@ -912,6 +936,30 @@ static void note_stream_k(bool on) { g_last_sk = on ? 1 : 0; }
 
 static std::mutex g_sk_mu;
 static std::unordered_map<hipStream_t, SkWs> g_sk;
+// a graph capture's own workspaces (clskd_capture_scope_begin), bound to the capturing thread
+struct SkScope {
+  std::unordered_map<hipStream_t, SkWs> ws;
+};
+static thread_local SkScope* g_sk_scope = nullptr;
+
+// zero at rest: the flags and tickets are cleared before the workspace is handed out
+static bool sk_alloc(SkWs& w, hipStream_t st, bool sync) {
+  const size_t wsb = (size_t)SK_MAX_GRID * 2 * 256 * 256 * 4, fb = (size_t)(SK_MAX_GRID * 2 + SK_MAX_TILES) * 4;
+  w = SkWs{};
+  if (hipMalloc(&w.ws, wsb) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (hipMalloc(&w.ready, fb) != hipSuccess || hipMemsetAsync(w.ready, 0, fb, st) != hipSuccess ||
+      (sync && hipStreamSynchronize(st) != hipSuccess)) {
+    (void)hipGetLastError();
+    (void)hipFree(w.ws);
+    if (w.ready) (void)hipFree(w.ready);
+    w = SkWs{};
+    return false;
+  }
+  return true;
+}
 
 static const SkWs* sk_workspace(hipStream_t st) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -919,21 +967,16 @@ static const SkWs* sk_workspace(hipStream_t st) {
     (void)hipGetLastError();
     return nullptr;
   }
+  if (cs != hipStreamCaptureStatusNone) {  // the capture's own workspace, if it has one
+    if (!g_sk_scope) return nullptr;
+    auto it = g_sk_scope->ws.find(st);
+    return it == g_sk_scope->ws.end() ? nullptr : &it->second;
+  }
   std::lock_guard<std::mutex> lk(g_sk_mu);
   auto it = g_sk.find(st);
   if (it != g_sk.end()) return &it->second;
-  if (cs != hipStreamCaptureStatusNone) return nullptr;
   SkWs w{};
-  const size_t wsb = (size_t)SK_MAX_GRID * 2 * 256 * 256 * 4, fb = (size_t)(SK_MAX_GRID * 2 + SK_MAX_TILES) * 4;
-  if (hipMalloc(&w.ws, wsb) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  if (hipMalloc(&w.ready, fb) != hipSuccess || hipMemsetAsync(w.ready, 0, fb, st) != hipSuccess) {
-    (void)hipGetLastError();
-    (void)hipFree(w.ws);
-    return nullptr;
-  }
+  if (!sk_alloc(w, st, false)) return nullptr;
   return &(g_sk[st] = w);
 }
 
@@ -1070,7 +1113,22 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
   const bool f32 = d.out_dtype == CLSKD_F32;
   *launched = true;
 #ifdef CLSKD_EXPERIMENTS
-  if (mode >= 10 && !f32 && d.in_dtype == CLSKD_BF16) {
+  if (mode >= 100 && !f32 && d.in_dtype == CLSKD_BF16 && g8_ta_ok(d)) {
+    // TA ablations (round 6): CLSKD_G8 = 100 + ABL flags (see the kernel's DBG >= 16 note)
+#define G8A(ABL_)                                                                               \
+  case ABL_:                                                                                    \
+    if (d.N <= 128) return launch_g8<256, 128, 4, 64, 2, 2, __bf16, 16 + ABL_, 1, 8, 1, __bf16, 0, 1>(d, st); \
+    return launch_g8<256, 256, 2, 64, 2, 2, __bf16, 16 + ABL_, 1, 8, 1, __bf16, 0, 1>(d, st);
+    switch (mode - 100) {
+      G8A(0) G8A(1) G8A(2) G8A(3) G8A(4) G8A(6) G8A(7) G8A(8) G8A(11) G8A(15) G8A(16) G8A(32) G8A(64)
+      G8A(128) G8A(256)
+      default:
+        set_error("CLSKD_G8=%d: unknown ablation", mode);
+        return CLSKD_E_ARG;
+    }
+#undef G8A
+  }
+  if (mode >= 10 && mode < 100 && !f32 && d.in_dtype == CLSKD_BF16) {
     const int cfg = mode / 10, dbg = mode % 10;
 #define G8X(BM_, BN_, WM_, BK_, NS_, PHI_)                                    \
   switch (dbg) {                                                              \
@@ -1166,4 +1224,49 @@ extern "C" int32_t clskd_conv_last_stream_k(void) { return clskd::g_last_sk; }
 
 extern "C" int clskd_stream_prepare(void* stream) {
   return clskd::sk_workspace(reinterpret_cast<hipStream_t>(stream)) ? CLSKD_OK : CLSKD_E_HIP;
+}
+
+extern "C" int clskd_capture_scope_begin(void* const* streams, int32_t nstreams, void** scope) {
+  using namespace clskd;
+  CLSKD_CHECK_ARG(scope && nstreams >= 0 && (nstreams == 0 || streams), "capture_scope_begin: bad arguments");
+  CLSKD_CHECK_ARG(g_sk_scope == nullptr, "capture_scope_begin: a scope is already bound to this thread");
+  auto* sc = new SkScope();
+  for (int i = 0; i < nstreams; ++i) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(streams[i]);
+    if (sc->ws.count(st)) continue;
+    SkWs w{};
+    if (!sk_alloc(w, st, true)) {
+      for (auto& kv : sc->ws) {
+        (void)hipFree(kv.second.ws);
+        (void)hipFree(kv.second.ready);
+      }
+      delete sc;
+      set_error("capture_scope_begin: workspace allocation failed");
+      return CLSKD_E_HIP;
+    }
+    sc->ws[st] = w;
+  }
+  g_sk_scope = sc;
+  *scope = sc;
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_capture_scope_end(void* scope) {
+  using namespace clskd;
+  CLSKD_CHECK_ARG(scope && g_sk_scope == scope, "capture_scope_end: not the scope bound to this thread");
+  g_sk_scope = nullptr;
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_capture_scope_free(void* scope) {
+  using namespace clskd;
+  if (!scope) return CLSKD_OK;
+  auto* sc = reinterpret_cast<SkScope*>(scope);
+  CLSKD_CHECK_ARG(g_sk_scope != sc, "capture_scope_free: the scope is still bound (call capture_scope_end)");
+  for (auto& kv : sc->ws) {
+    (void)hipFree(kv.second.ws);
+    (void)hipFree(kv.second.ready);
+  }
+  delete sc;
+  return CLSKD_OK;
 }

@@ -80,6 +80,32 @@ def test_train_graph_matches_eager_train_steps(precision, launch):
 
 
 @pytest.mark.parametrize("launch", ["exec", "graph"])
+def test_eager_train_step_right_after_capture(launch):
+    """An eager training step between the capture and the first replay (bench.py's census step)
+    must not read the packed weights the capture built (they hold nothing until a replay): the
+    capture advances the parameters' versions.  Eager, replay, eager — bitwise the all-eager
+    sequence on a second model."""
+    from clskd.data import synthetic_pairs
+    from clskd.graph import TrainStepExecutor, TrainStepGraph
+    from clskd.train import FlatAdam, FlatParams
+    from test_gpu_parity import _kd
+    batches = []
+    for seed in (51, 52, 53):
+        n, c = synthetic_pairs(4, 16000, seed=seed)
+        batches.append((torch.from_numpy(n).to(DEV), torch.from_numpy(c).to(DEV)))
+    kd_e, kd_g = _kd().set_precision("mixed"), _kd().set_precision("mixed")
+    (fe, oe), (fg, og) = [(f, FlatAdam(f, lr=6e-4, device_step=True))
+                          for f in (FlatParams(kd_e.student), FlatParams(kd_g.student))]
+    ex = (TrainStepExecutor if launch == "exec" else TrainStepGraph)(kd_g, fg, og, *batches[0])
+    for i, (X, y) in enumerate(batches):
+        le = kd_e.train_step((X, y), fe, oe)
+        lg = ex(X, y) if i == 1 else kd_g.train_step((X, y), fg, og)
+        torch.cuda.synchronize()
+        assert lg.item() == le.item(), (i, lg.item(), le.item())
+        assert torch.equal(fg.data, fe.data), i
+
+
+@pytest.mark.parametrize("launch", ["exec", "graph"])
 def test_train_graph_replays_interleaved_with_eager_forwards(launch):
     """Replay, eager eval forward, replay, eager eval forward: every eager forward of the trained
     student must use the parameters the replays' Adam wrote (the packed-weight cache is keyed on
