@@ -38,7 +38,10 @@ PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sp
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 B_PER_GPU = 16
 NBATCH = 4
-TRAFFIC_FILE = "r5_pmc_traffic.json"  # written by tools/pmc_traffic.py
+# per-kernel HBM traffic of the PMC passes (tools/pmc_traffic.py): the C2 leg's, and the C3 leg's
+# own passes (round 6: a C3 line never borrows the C2 file's same-named, different-shape launches)
+TRAFFIC_FILE = "r6_pmc_traffic.json"
+TRAFFIC_FILE_TRAIN = "r6_train_pmc_traffic.json"
 L = 64000
 
 
@@ -124,11 +127,12 @@ def host_cpu_info():
     return model, total, usable
 
 
-def cpu_baseline(n_timed=10, n_warm=3):
+def cpu_baseline(n_timed=10, n_warm=3, spkd=False):
     """The CPU oracle (fp32 PyTorch-CPU restatement of the reference, oracle/ref_cpu.py) timed on
     this host following BASELINE.md §2: every usable host core, the same seeded B=16 x 4 s
     workload as the GPU leg, 3 warm-up steps and the median of 10 timed steps — all full B=16
-    steps (round 5 warmed up at B=4, which left the first timed B=16 step cold: 9.5 vs 7.5 s)."""
+    steps (round 5 warmed up at B=4, which left the first timed B=16 step cold: 9.5 vs 7.5 s).
+    spkd: configuration C4's step (oracle/ref_cpu.spkd_output_step, B=32 x 4 s) instead."""
     from oracle import ref_cpu as R
     from clskd.data import synthetic_pairs
     from clskd.weights import ABF_SEED, STUDENT_SEED, TEACHER_SEED, recipe_state_dict
@@ -139,23 +143,25 @@ def cpu_baseline(n_timed=10, n_warm=3):
     ps = R.to_torch_params(recipe_state_dict(cfg.dccrn_param_shapes(**cfg.STUDENT), STUDENT_SEED))
     pa = R.to_torch_params(recipe_state_dict(
         {**cfg.review_param_shapes("encoder"), **cfg.review_param_shapes("decoder")}, ABF_SEED))
-    Bc = B_PER_GPU
+    Bc = B_SPKD if spkd else B_PER_GPU
     noisy, clean = synthetic_pairs(Bc, L, seed=99)
     X, Y = torch.from_numpy(noisy), torch.from_numpy(clean)
+    fn = (lambda: R.spkd_output_step(pt, ps, X, Y)) if spkd else (lambda: R.clskd_step(pt, ps, pa, X, Y))
     times = []
     with torch.no_grad():
         for _ in range(n_warm):
-            R.clskd_step(pt, ps, pa, X, Y)
+            fn()
         for _ in range(n_timed):
             t0 = time.perf_counter()
-            R.clskd_step(pt, ps, pa, X, Y)
+            fn()
             times.append(time.perf_counter() - t0)
     med = float(np.median(times))
     frames = Bc * cfg.n_frames(L)
     return dict(value=round(frames / med, 2), unit="frames/s", cores=threads, kind="port",
                 batch=Bc, host_cpus=total, cpu_model=model,
                 step_s=[round(t, 3) for t in times],
-                sample=f"oracle/ref_cpu.clskd_step on the bench workload (B={Bc} x 4 s @16 kHz, "
+                sample=f"oracle/ref_cpu.{'spkd_output_step' if spkd else 'clskd_step'} on the "
+                       f"bench workload (B={Bc} x 4 s @16 kHz, "
                        f"same step as the GPU leg): {n_warm} warm-up steps (B={Bc}), median of "
                        f"{n_timed} timed B={Bc} steps, fp32, torch CPU {threads} threads = every "
                        f"CPU this job may use ({total} logical CPUs on the host), {model}")
@@ -406,8 +412,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--cpu-steps", type=int, default=10,
-                    help="timed CPU-oracle B=16 steps (median; BASELINE.md §2: 10)")
+    ap.add_argument("--cpu-steps", type=int, default=None,
+                    help="timed CPU-oracle steps (median; BASELINE.md §2: 10 for C2; C4 default 3 "
+                         "timed after 1 warm-up: a bounded sample of its B=32 step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--abf-reinit", default="step", choices=["step", "once"])
     ap.add_argument("--launch", default=None, choices=["exec", "eager", "graph"],
@@ -487,9 +494,7 @@ def main():
         # 6): with N > 1 ranks the C2 step has no exchange, and the C3 replay (fwd+loss +
         # backward) is followed by the flat-gradient all-reduce and the Adam launch
         # (clskd.graph.TrainStepGraph, collective mode)
-        args.launch = "exec" if not args.spkd else "eager"
-    if args.spkd and args.launch != "eager":
-        raise SystemExit("--spkd (C4) launches eagerly")
+        args.launch = "exec"
     args.graph = args.launch == "graph"
     bsz = B_SPKD if args.spkd else B_PER_GPU
     kd = build_kd(dev, args.abf_reinit, args.precision, spkd=args.spkd)
@@ -548,7 +553,9 @@ def main():
     elif args.launch == "exec":
         from clskd.graph import StepExecutor
         if executor is None:
-            if args.ahead:  # the teacher_ahead overlap, replayed (two alternating captures)
+            if args.spkd:  # C4: the captured two-stream step (round 6), one capture
+                executor = StepExecutor(kd, Xs[0], Ys[0])
+            elif args.ahead:  # the teacher_ahead overlap, replayed (two alternating captures)
                 from clskd.graph import AheadStepExecutor
                 executor = AheadStepExecutor(kd, Xs[0], Ys[0])
             else:
@@ -595,12 +602,26 @@ def main():
             step(i)
     torch.cuda.synchronize()
     dominant = max(census.items(), key=lambda kv: kv[1][1])[0] if census else None
+    census_all, dom_fn = None, None
     if args.launch == "exec":
+        # one more untimed step: the captured step replayed in program order on ONE stream with
+        # every kernel node event-timed (clskd_exec_census) — the isolated duration of EVERY
+        # kernel, library and torch alike; the dominant instance is the one with the largest
+        # total, whatever kernel family it is (round 6: the C3 line no longer picks among conv
+        # launches only)
+        from clskd.graph import kernel_name
+        _range_push("clskd_exec_census")
+        kc = args.warmup % NBATCH
+        census_all = (executor.census(Xs[kc], Ys[kc]) if hasattr(executor, "ex")
+                      else executor.census())
+        _range_pop()
+        conv_of_fn = {fn: nm for nm, fn in ops.KernelTimer.fns.items()}
+        dom_fn = max(census_all, key=lambda f: census_all[f][1])
+        dominant = conv_of_fn.get(dom_fn) or ops.canonical_kernel_name(kernel_name(dom_fn))
         # live HIP-event timing of the dominant instance inside the executor's launches
-        n_dom = census[dominant][0]
+        n_dom = census_all[dom_fn][0]
         for e in getattr(executor, "ex", [executor]):
-            ops.check(ops.lib().clskd_exec_profile(e._ex, ops.KernelTimer.fns[dominant],
-                                                   n_dom * args.steps), "exec_profile")
+            ops.check(ops.lib().clskd_exec_profile(e._ex, dom_fn, n_dom * args.steps), "exec_profile")
 
     _gc_setting()
     # ---- timed region: exactly K steps, barrier + sync on both sides --------------------
@@ -631,13 +652,18 @@ def main():
                       "exec_profile_read")
             tot.value += t1.value
             cnt.value += c1.value
-        fl = census[dominant][2] / census[dominant][0]
+        if dominant in census:  # a conv instance: FLOPs from the eager census step
+            fl = census[dominant][2] / census[dominant][0]
+        else:  # another kernel family: the algorithmic work its wrapper noted (census step)
+            w = ops.KernelTimer.work.get(dominant)
+            fl = w[2] / w[0] if w else 0.0
         ktimes = {dominant: [cnt.value, tot.value, fl * cnt.value]}
-        timing = ("HIP events around every launch of the dominant conv kernel inside the timed "
-                  "region, recorded by the step executor on the kernel's own stream (4 concurrent "
+        timing = ("HIP events around every launch of the dominant kernel inside the timed "
+                  "region, recorded by the step executor on the kernel's own stream (concurrent "
                   "streams: a launch's event span includes time it shares the CUs); dominant = "
-                  "largest total isolated time in the census step (the last warm-up step run "
-                  "eagerly on one stream, every conv launch timed: conv_all_kernels)")
+                  "largest total isolated time over EVERY kernel node of one executor census "
+                  "replay (clskd_exec_census: the captured step on one stream, each node "
+                  "event-timed: all_kernels_isolated)")
         census_steps = 1
     elif (not args.graph):
         ktimes = ops.KernelTimer.stop()
@@ -727,7 +753,10 @@ def main():
 
         def _bytes(kname):  # compulsory bytes per launch (census: input + weights + output once)
             nb = ops.KernelTimer.nbytes.get(kname)
-            return nb[1] / nb[0] if nb else None
+            if nb:
+                return nb[1] / nb[0]
+            w = ops.KernelTimer.work.get(kname)  # non-conv kernels: their wrappers' note_work
+            return w[1] / w[0] if w and w[1] > 0 else None
 
         peak = _peak(name)
         byt = _bytes(name)
@@ -737,25 +766,33 @@ def main():
         ridge = peak * 1e12 / (PEAK_HBM_GBPS * 1e9)
         hbm_bound = intensity is not None and intensity < ridge
         traffic, traffic_src = None, None
-        tpath = os.path.join(REPO, "profiles", TRAFFIC_FILE)
-        if os.path.exists(tpath) and not args.spkd:  # the PMC passes profile the C2 leg
+        tfile = TRAFFIC_FILE_TRAIN if args.train else TRAFFIC_FILE
+        tpath = os.path.join(REPO, "profiles", tfile)
+        if os.path.exists(tpath) and not args.spkd:  # PMC passes of this leg's own bench command
             kern = json.load(open(tpath))["kernels"]
             tk = kern.get(name)
-            if tk is None:  # rocprof names carry the template arguments the census name omits
-                more = [k for k in kern if k.startswith(name[:-1] + ",")]
-                best = [k for k in more if k.count(",") == name.count(",") + 1]
-                more = best if best else more
-                tk = kern[more[0]] if len(more) == 1 else None
+            if tk is None:  # match in one canonical spelling (rocprof vs demangled vs census)
+                cn = ops.canonical_kernel_name(name)
+                same = [k for k in kern if ops.canonical_kernel_name(k) == cn]
+                if not same:  # rocprof names carry template arguments the census name omits
+                    same = [k for k in kern if ops.canonical_kernel_name(k).startswith(cn[:-1] + ",")]
+                    best = [k for k in same if k.count(",") == name.count(",") + 1]
+                    same = best if best else same
+                tk = kern[same[0]] if len(same) == 1 else None
             if tk is not None:
                 traffic = round(tk["hbm_bytes_per_launch"])
-                traffic_src = f"profiles/{TRAFFIC_FILE} (PMC FETCH_SIZE x2 + WRITE_SIZE, per launch)"
+                traffic_src = f"profiles/{tfile} (PMC FETCH_SIZE x2 + WRITE_SIZE, per launch)"
         # achieved / frac: the ISOLATED rate — the dominant instance's average duration in the
         # census step (its launches one at a time on one stream: the view a rocprofv3 kernel
         # trace of the census range reproduces, tools/region_stats.py); the live rate inside the
         # concurrent step (a launch's event span includes the time it shares the CUs with the
         # other streams) is reported beside it as achieved_live / frac_live
-        iso_span_ms = census[name][1] / census[name][0] if name in census else avg_ms
-        iso_fl = census[name][2] / census[name][0] if name in census else flops / n_l
+        if census_all is not None and dom_fn in census_all:  # the executor census (every kernel)
+            iso_span_ms = census_all[dom_fn][1] / census_all[dom_fn][0]
+            iso_fl = flops / n_l
+        else:
+            iso_span_ms = census[name][1] / census[name][0] if name in census else avg_ms
+            iso_fl = census[name][2] / census[name][0] if name in census else flops / n_l
         # the census times each launch with an event pair, which also spans the launch's dispatch
         # (disp_us, measured above on an empty launch): the kernel's own duration — what a
         # rocprofv3 kernel trace of the census range reports — is the span minus that
@@ -765,7 +802,8 @@ def main():
         # inside the concurrent step (rocprofv3's timed-range average of the instance)
         live_ms = max(avg_ms - disp_us * 1e-3, 0.5 * avg_ms)
         achieved = flops / n_l / (live_ms * 1e-3) / 1e12
-        if hbm_bound:
+        if hbm_bound or (byt and not flops):
+            hbm_bound = True
             ach_bw = byt / (iso_ms * 1e-3) / 1e9
             live_bw = byt / (live_ms * 1e-3) / 1e9
             roof = dict(bound="hbm", kernel=name, achieved=round(ach_bw, 1), peak=PEAK_HBM_GBPS,
@@ -790,12 +828,24 @@ def main():
                     avg_launch_us=round(avg_ms * 1e3, 2),
                     live_kernel_us=round(live_ms * 1e3, 2),
                     algorithmic_gflop_per_launch=round(flops / n_l / 1e9, 3),
-                    isolated_avg_launch_us=(round(census[name][1] / census[name][0] * 1e3, 2)
-                                            if name in census else None),
+                    isolated_avg_launch_us=round(iso_span_ms * 1e3, 2),
                     isolated_kernel_us=round(iso_ms * 1e3, 2),
                     dispatch_span_us=round(disp_us, 2),
-                    achieved_isolated=(round(census[name][2] / (census[name][1] * 1e-3) / 1e12, 2)
-                                       if name in census else None),
+                    # the isolated rate WITHOUT the dispatch-span correction (the basis of
+                    # rounds 1-4's frac): the event span of the launch, dispatch included
+                    achieved_isolated=round(iso_fl / (iso_span_ms * 1e-3) / 1e12, 2),
+                    frac_isolated_span=round(iso_fl / (iso_span_ms * 1e-3) / 1e12 / peak, 4)
+                    if not hbm_bound else round(byt / (iso_span_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
+                    all_kernels_isolated=(dict(
+                        note="executor census replay (clskd_exec_census): every kernel node of the "
+                             "captured step on one stream, event-timed; top 25 by total",
+                        ms_per_step=round(sum(v[1] for v in census_all.values()), 3),
+                        per_kernel={
+                            (conv_of_fn.get(f) or ops.canonical_kernel_name(kernel_name(f))):
+                                dict(launches=v[0], avg_us=round(v[1] / v[0] * 1e3, 1),
+                                     total_ms=round(v[1], 3))
+                            for f, v in sorted(census_all.items(), key=lambda kv: -kv[1][1])[:25]})
+                        if census_all else None),
                     conv_all_kernels=dict(
                         steps=census_steps,
                         note=("census step on one stream: isolated kernel durations"
@@ -811,8 +861,11 @@ def main():
                                                    _peak(k) * 1e12 / (PEAK_HBM_GBPS * 1e9) else "mfma"))
                                     for k, v in sorted(census.items(), key=lambda kv: -kv[1][1])}))
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and not args.train and not args.spkd:
-            cpu = cpu_baseline(args.cpu_steps)
+        if world == 1 and not args.no_cpu_baseline and not args.train:
+            if args.spkd:
+                cpu = cpu_baseline(args.cpu_steps or 3, n_warm=1, spkd=True)
+            else:
+                cpu = cpu_baseline(args.cpu_steps or 10)
             # GPU / CPU-oracle ratio on the same workload.  `vs_baseline` stays null: it is
             # reserved for a published number for this metric, and BASELINE.md has none
             cpu["gpu_over_cpu"] = round(frames / el / cpu["value"], 1)
@@ -852,17 +905,17 @@ def main():
                        "global_batch": world * bsz, "per_gpu_batch": bsz,
                        "clip_samples": L, "frames_per_clip": T, "parallelism": f"dp{world}",
                        "abf_reinit": args.abf_reinit, "loss": round(loss_v, 6),
-                       "launch": ("eager, 2 HIP streams (caller: teacher; side: student + "
-                                  "MRSTFT)" if args.spkd else
-                                  "eager, 4 HIP streams (caller, teacher, student, ReviewKD-"
-                                  "encoder/MRSTFT)" + ("; teacher chain of step i+1 overlaps step "
-                                                       "i's ReviewKD/Gram/loss tail (teacher_ahead)"
-                                                       if kd.teacher_ahead else "")
+                       "launch": (("eager, 2 HIP streams (caller: teacher; side: student + "
+                                   "MRSTFT)" if args.spkd else
+                                   "eager, 4 HIP streams (caller, teacher, student, ReviewKD-"
+                                   "encoder/MRSTFT)" + ("; teacher chain of step i+1 overlaps step "
+                                                        "i's ReviewKD/Gram/loss tail (teacher_ahead)"
+                                                        if kd.teacher_ahead else ""))
                                   if args.launch == "eager" else
                                   "C++ step executor (clskd_exec_launch" +
                                   ("_ahead: two captures alternating, each step's teacher chain "
                                    "overlapping the previous step's tail"
-                                   if args.ahead and not args.train else "") +
+                                   if args.ahead and not args.train and not args.spkd else "") +
                                   "): the captured step replayed on 4 HIP streams along its "
                                   "dependency edges "
                                   f"({executor.info['kernels']} kernels, "

@@ -271,9 +271,12 @@ int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_seq, int64_t
  * backward does not recompute them with a GEMM over the saved history.  Only where
  * clskd_lstm_pre_capable(H) (the single-wave H = 32 kernel; CLSKD_LSTM_PRE=0 turns it off). */
 int clskd_lstm_pre_capable(int32_t H);
+/* cbuf (optional, round 6): nws*nseq*T*H floats, [ws][seq][t][j] — the cell states c_t are stored
+ * too, so clskd_lstm_bwd (c_ready = 1) skips its serial cell-state scan. */
 int clskd_lstm_recurrent_pre(float* gx, int64_t gx_ws, int64_t gx_seq, int64_t gx_t,
                              const float* whh, int32_t nws, int32_t nseq, int32_t T, int32_t H,
-                             float* out, int64_t o_ws, int64_t o_seq, int64_t o_t, void* stream);
+                             float* out, int64_t o_ws, int64_t o_seq, int64_t o_t, float* cbuf,
+                             void* stream);
 
 /* One recurrence step with carried state (streaming inference, config C5): per (ws, seq),
  * gates = gx + W_hh h; c = f c + i g; h = o tanh(c) — h, c updated in place (strides s_ws,
@@ -606,11 +609,13 @@ int clskd_complex_combine_bwd(const float* dreal, const float* dimag, int32_t B,
  * pre-activations [nws][nseq][T][4H] (strided like gx; rebuild them as gx + h_{t-1} W_hh^T with
  * one accumulate conv over the saved h history), dh: dL/dh_t, whh [nws][4H][H].  Writes the
  * gate pre-activation gradients dgates (strided like gx) — whose conv-engine wgrad / dgrad give
- * dW_ih, db, dx and (over the shifted h history) dW_hh.  cbuf: nws*nseq*T*H floats (cell states). */
+ * dW_ih, db, dx and (over the shifted h history) dW_hh.  cbuf: nws*nseq*T*H floats (cell states):
+ * c_ready = 1 when clskd_lstm_recurrent_pre stored them there (the single-wave H = 16 / 32 kernel
+ * then skips its cell-state scan), 0: scratch the kernel fills itself. */
 int clskd_lstm_bwd(const float* pre, int64_t p_ws, int64_t p_seq, int64_t p_t, const float* dh,
                    int64_t d_ws, int64_t d_seq, int64_t d_t, const float* whh, int32_t nws,
-                   int32_t nseq, int32_t T, int32_t H, float* cbuf, float* dgates, int64_t g_ws,
-                   int64_t g_seq, int64_t g_t, void* stream);
+                   int32_t nseq, int32_t T, int32_t H, float* cbuf, int32_t c_ready, float* dgates,
+                   int64_t g_ws, int64_t g_seq, int64_t g_t, void* stream);
 
 /* SPKD backward (framework.py:150-172).  clskd_spkd_grad_ranges: per pair (slab ranges as in
  * clskd_spkd_finalize_ranges) M = dG + dG^T [pair][B][B] where dG = d(scale * loss)/d(z z^T)
@@ -694,6 +699,15 @@ void clskd_exec_destroy(clskd_exec* ex);
  * synchronize) returns the summed event spans and the number of timed launches. */
 int clskd_exec_profile(clskd_exec* ex, const void* fn, int32_t max_launches);
 int clskd_exec_profile_read(clskd_exec* ex, double* total_ms, int32_t* count);
+/* Per-kernel census of one replay (round 6): the captured step run once in program order on ONE
+ * stream (the caller's), an event pair around every kernel node; fns[i] / ms[i] = host function
+ * and duration of the i-th kernel node (cap >= the node count, exec_info slot 1; *n = the count).
+ * The isolated per-kernel view of a rocprofv3 trace of a serialised step — bench.py picks the
+ * dominant kernel instance over ALL kernels from it.  A real step; synchronises the stream. */
+int clskd_exec_census(clskd_exec* ex, void* stream, int32_t cap, const void** fns, float* ms, int32_t* n);
+/* Demangled name of a kernel host function into buf (NUL-terminated, truncated at cap); returns
+ * the full length, -1 if HIP does not know the function. */
+int32_t clskd_kernel_name(const void* fn, char* buf, int32_t cap);
 /* Per-stream milestones (diagnostic): with marks on, every launch records a timing event before
  * the fork and at each stream's tail; clskd_exec_marks_read (after a synchronize) returns per
  * stream the mean tail time after the fork in ms over the last <= 64 launches (n >= nstreams). */

@@ -10,8 +10,11 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # CLSKD_LIB=exp selects the timing-experiments build (clskd.build: never the product library)
-LIB_PATH = os.path.join(_HERE, "libclskd_hip_exp.so" if os.environ.get("CLSKD_LIB") == "exp"
-                        else "libclskd_hip.so")
+# (or a .so file next to this one: a saved earlier build for a same-box A/B, tools/ only)
+_LIB_ENV = os.environ.get("CLSKD_LIB", "")
+LIB_PATH = os.path.join(_HERE, "libclskd_hip_exp.so" if _LIB_ENV == "exp"
+                        else (os.path.basename(_LIB_ENV) if _LIB_ENV.endswith(".so")
+                              else "libclskd_hip.so"))
 
 MAX_SEGS = 4
 F32, BF16, F16 = 0, 1, 2
@@ -116,6 +119,8 @@ SIGNATURES = {
     "clskd_exec_launch_ahead": (_i32, [_p, _p, C.c_uint32, _p]),
     "clskd_stream_prepare": (_i32, [_p]),
     "clskd_capture_scope_begin": (_i32, [_p, _i32, _p]),
+    "clskd_exec_census": (_i32, [_p, _p, _i32, _p, _p, _p]),
+    "clskd_kernel_name": (_i32, [_p, _p, _i32]),
     "clskd_capture_scope_end": (_i32, [_p]),
     "clskd_capture_scope_free": (_i32, [_p]),
     "clskd_version": (_i32, []),
@@ -140,7 +145,7 @@ SIGNATURES = {
     "clskd_lstm_recurrent": (_i32, [_p, _i64, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _i64,
                                     _i64, _i64, _p]),
     "clskd_lstm_recurrent_pre": (_i32, [_p, _i64, _i64, _i64, _p, _i32, _i32, _i32, _i32, _p, _i64,
-                                    _i64, _i64, _p]),
+                                        _i64, _i64, _p, _p]),
     "clskd_lstm_pre_capable": (_i32, [_i32]),
     "clskd_complex_combine": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p]),
     "clskd_complex_combine_dt": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i32, _p]),
@@ -196,7 +201,7 @@ SIGNATURES = {
     "clskd_stft_mag_loss_bwd": (_i32, [_p, _p, _i64, _i32, _i32, _f32, _p, _i32, _p]),
     "clskd_complex_combine_bwd": (_i32, [_p, _p, _i32, _i64, _p, _p]),
     "clskd_lstm_bwd": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _i64, _i64, _p, _i32, _i32, _i32,
-                              _i32, _p, _p, _i64, _i64, _i64, _p]),
+                              _i32, _p, _i32, _p, _i64, _i64, _i64, _p]),
     "clskd_spkd_grad_ranges": (_i32, [C.POINTER(C.c_void_p), C.POINTER(C.c_int32),
                                       C.POINTER(C.c_void_p), C.POINTER(C.c_int32), _i32, _i32,
                                       _i32, _f32, _p, _p]),

@@ -364,7 +364,8 @@ def dccrn_backward(m, tape, enc, dec, dec_in, lstm_io, g, pg, acc_params=False, 
                          OutMap(T * 8 * H, 0, 8 * H), out_offset=ws * 4 * H, accumulate=True)
         dg = _empty((2, B, T, 8 * H), dev)
         st = (4 * H, T * 8 * H, 8 * H)
-        ops.lstm_bwd(gx, st, dh, (2 * B * T * H, T * H, H), whh, 2, 2 * B, T, H, dg, st)
+        ops.lstm_bwd(gx, st, dh, (2 * B * T * H, T * H, H), whh, 2, 2 * B, T, H, dg, st,
+                     cells=lt.get("cells"))
         # W_hh gradient per weight set: rows (seq, t) x history h_{t-1}
         Kh = whp.shape[2]
         dwhh = _empty((2, 4 * H, Kh), dev)

@@ -37,8 +37,10 @@ class StepGraph:
     ahead_layout = False
 
     def __init__(self, kd, X, y, warmup=1):
-        if not isinstance(kd, KnowledgeDistillation):
-            raise TypeError("StepGraph captures a clskd.distill.KnowledgeDistillation step")
+        from .distill import SPKDDistillation
+        if not isinstance(kd, (KnowledgeDistillation, SPKDDistillation)):
+            raise TypeError("StepGraph captures a clskd.distill.KnowledgeDistillation (C2) or "
+                            "SPKDDistillation (C4) step")
         if not X.is_cuda:
             raise RuntimeError("StepGraph needs device-resident inputs")
         self.kd = kd
@@ -54,7 +56,7 @@ class StepGraph:
     # graph each step are excluded: their re-init and repack are recorded)
     def _baked(self):
         mods = [self.kd.teacher, self.kd.student]
-        if self.kd.abf_reinit != "step":
+        if getattr(self.kd, "abf_reinit", "step") != "step":  # C4 (SPKD) has no ReviewKD modules
             mods += [self.kd.review_encoder, self.kd.review_decoder]
         return [p for m in mods for p in m.parameters()]
 
@@ -246,11 +248,43 @@ class StepExecutor(StepGraph):
         _lib.check(_lib.load().clskd_exec_launch(self._ex, _lib.stream_ptr()), "exec_launch")
         self._mark_done()
 
+    def census(self):
+        """One replay of the captured step in program order on the current stream with every
+        kernel node event-timed (clskd_exec_census): {host function: [launches, total ms]} — the
+        isolated per-kernel view of a serialised step, over ALL kernels (library and torch).
+        A real step; synchronises."""
+        return exec_census(self._ex, self.info["kernels"])
+
     def __del__(self):
         try:
             self._release()
         except Exception:
             pass
+
+
+def exec_census(handle, nkernels):
+    import ctypes as C
+    from . import _lib
+    fns = (C.c_void_p * nkernels)()
+    ms = (C.c_float * nkernels)()
+    n = C.c_int32(0)
+    _lib.check(_lib.load().clskd_exec_census(handle, _lib.stream_ptr(), nkernels, fns, ms,
+                                             C.byref(n)), "exec_census")
+    out = {}
+    for i in range(n.value):
+        a = out.setdefault(fns[i], [0, 0.0])
+        a[0] += 1
+        a[1] += float(ms[i])
+    return out
+
+
+def kernel_name(fn):
+    """Demangled name of a kernel host function (clskd_kernel_name)."""
+    import ctypes as C
+    from . import _lib
+    buf = C.create_string_buffer(4096)
+    n = _lib.load().clskd_kernel_name(C.c_void_p(fn), buf, 4096)
+    return buf.value.decode() if n >= 0 else hex(fn or 0)
 
 
 class AheadStepExecutor:
@@ -329,6 +363,17 @@ class AheadStepExecutor:
         self.i ^= 1
         return e.out["loss"]
 
+    def census(self, X=None, y=None):
+        """StepExecutor.census of the capture the next call would replay (after the batch is
+        copied into its static inputs); the alternation is unchanged."""
+        torch.cuda.synchronize()
+        e = self.ex[self.i]
+        if X is not None:
+            e.X.copy_(X)
+        if y is not None:
+            e.y.copy_(y.reshape(e.y.shape))
+        return e.census()
+
 
 class TrainStepGraph(StepGraph):
     """Configuration C3 as one captured step: ``kd.train_step`` — fwd+loss with the autograd
@@ -397,6 +442,13 @@ class TrainStepGraph(StepGraph):
         # packed weights, DCCRN._packed — rebuild on the next eager forward instead of serving
         # weights packed before this replay
         self.flat.bump_versions()
+
+    def census(self):
+        """StepExecutor.census of the training step (TrainStepExecutor); the replayed Adam (one
+        rank) rewrote the parameters: their versions advance as after any replay."""
+        out = super().census()
+        self.flat.bump_versions()
+        return out
 
     def _capture(self):
         self._release()

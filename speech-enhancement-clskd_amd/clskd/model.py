@@ -159,6 +159,9 @@ def _pv(*tensors):
 # the gather reproduces the real build bitwise (fp32 outputs; a + b summed in the build's order).
 # CLSKD_PACK_MAPS=0 disables it (A/B).
 _PACK_MAPS_ON = os.environ.get("CLSKD_PACK_MAPS", "1") == "1"
+# the taped H = 32 recurrence stores its cell states for the backward (round 6; CLSKD_LSTM_CELLS=0:
+# the backward re-derives them with its serial scan, A/B)
+_LSTM_CELLS = os.environ.get("CLSKD_LSTM_CELLS", "1") == "1"
 
 
 def _flat_root(params):
@@ -614,10 +617,17 @@ class DCCRN(nn.Module):
             hs = torch.empty(2, 2 * B, T, H, **f32)
             # taped: the recurrence leaves the gate pre-activations in gx (the backward's `pre`)
             pre = tape is not None and ops.lstm_pre_capable(H)
-            (ops.lstm_recurrent_pre if pre else ops.lstm_recurrent)(
-                gx, 4 * H, T * 8 * H, 8 * H, whh, 2, 2 * B, T, H, hs, 2 * B * T * H, T * H, H)
+            cells = None
+            if pre:  # ... and its cell states (the backward then skips its cell-state scan)
+                cells = torch.empty(2 * 2 * B * T * H, **f32) if _LSTM_CELLS else None
+                ops.lstm_recurrent_pre(gx, 4 * H, T * 8 * H, 8 * H, whh, 2, 2 * B, T, H, hs,
+                                       2 * B * T * H, T * H, H, cbuf=cells)
+            else:
+                ops.lstm_recurrent(gx, 4 * H, T * 8 * H, 8 * H, whh, 2, 2 * B, T, H, hs,
+                                   2 * B * T * H, T * H, H)
             if tape is not None:
-                tape.setdefault("lstm", []).append(dict(gx=gx, hs=hs, r_in=r_in, pre=pre))
+                tape.setdefault("lstm", []).append(dict(gx=gx, hs=hs, r_in=r_in, pre=pre,
+                                                        cells=cells))
             # a 16-bit model (the frozen teacher in precision 'mixed' / 'fp16') stores the layer
             # output as the 16-bit operand of the next layer's input GEMM and the projection
             # (one rounding, as every other teacher activation); fp32 models and taped

@@ -36,6 +36,17 @@ class KernelTimer:
     only = None  # optional kernel-instance name: time just that kernel's launches
     fns = {}  # kernel-instance name -> host function (clskd_exec_profile key)
     nbytes = {}  # kernel-instance name -> [launches, summed compulsory bytes]
+    # non-conv kernels (round 6): canonical instance name -> [launches, summed algorithmic bytes,
+    # summed algorithmic FLOPs], noted by their wrappers while the timer is on (census step)
+    work = {}
+
+    @classmethod
+    def note_work(cls, name, nbytes, flops=0.0):
+        if cls.active and not torch.cuda.is_current_stream_capturing():
+            w = cls.work.setdefault(name, [0, 0.0, 0.0])
+            w[0] += 1
+            w[1] += float(nbytes)
+            w[2] += float(flops)
 
     @classmethod
     def start(cls, only=None):
@@ -93,10 +104,10 @@ def direct_weight(wpacked):
     fp32 [Kp][NP]; bf16 [Kp/2][NP][2].  Cached per packed tensor (pointer + version; the cache
     holds the source alive so a pointer is never reused while its entry exists)."""
     tok = capture_token()
-    # an entry built inside a capture holds its values only in that graph's replays (key below)
-    key = (wpacked.data_ptr(), wpacked._version, tuple(wpacked.shape), wpacked.dtype, id(tok))
+    key = (wpacked.data_ptr(), wpacked._version, tuple(wpacked.shape), wpacked.dtype)
     ent = _DIRECT_W.get(key)
-    if ent is not None and ent[2] is tok:
+    # an entry built inside a capture holds its values only in that graph's replays
+    if ent is not None and cache_entry_usable(ent[2], tok):
         _DIRECT_W.move_to_end(key)
         capture_keep(ent, tok)
         return ent[1]
@@ -510,6 +521,93 @@ _CAPTURE_TOKEN = None  # the CaptureScope being recorded on this process's captu
 _ANON_CAPTURE = object()  # a capture without a CaptureScope (nothing kept alive for it)
 
 
+_MANGLED_TYPES = {"f": "float", "d": "double", "i": "int", "j": "unsigned", "b": "bool",
+                  "l": "long", "m": "unsigned long", "DF16b": "bf16", "bf16": "bf16", "DF16_": "f16",
+                  "Dh": "f16", "h": "unsigned char", "s": "short", "t": "unsigned short"}
+
+
+def _demangle_simple(m):
+    """'_ZN5clskd19abf_fuse_bwd_kernelIbf16EEvPKT_...' -> 'clskd::abf_fuse_bwd_kernel<bf16>':
+    nested name + template arguments of the forms kernel instances use (types, L<type><n>E
+    literals); anything else is returned unchanged."""
+    try:
+        i = 2
+        if m[i] != "N":
+            return m
+        i += 1
+        parts = []
+        while m[i].isdigit():
+            j = i
+            while m[j].isdigit():
+                j += 1
+            n = int(m[i:j])
+            parts.append(m[j:j + n])
+            i = j + n
+        args = []
+        if m[i] == "I":
+            i += 1
+            while m[i] != "E":
+                if m[i] == "L":  # literal: L <type> <value> E
+                    j = m.index("E", i)
+                    lit = m[i + 1:j]
+                    for t in ("i", "j", "l", "m", "b"):
+                        if lit.startswith(t) and (lit[1:].lstrip("n").isdigit()):
+                            v = lit[1:].replace("n", "-", 1)
+                            args.append(("true" if v == "1" else "false") if t == "b" else v)
+                            break
+                    else:
+                        return m
+                    i = j + 1
+                    continue
+                for code in sorted(_MANGLED_TYPES, key=len, reverse=True):
+                    if m.startswith(code, i):
+                        args.append(_MANGLED_TYPES[code])
+                        i += len(code)
+                        break
+                else:
+                    return m
+        return "::".join(parts) + ("<" + ",".join(args) + ">" if args else "")
+    except (IndexError, ValueError):
+        return m
+
+
+def canonical_kernel_name(name):
+    """Kernel instance name in one canonical form, for matching demangled names
+    (clskd_kernel_name), rocprofv3's kernel names and the conv engines' note_kernel names: return
+    type, namespaces and the argument list dropped, 16-bit float types spelled bf16 / f16, no
+    spaces ('void clskd::abf_fuse_bwd_kernel<__bf16>(__bf16 const*, ...)' ->
+    'abf_fuse_bwd_kernel<bf16>')."""
+    s = name.strip()
+    if s.startswith("_Z"):  # a mangled name the demangler refused (HIP spells __bf16 "bf16")
+        s = _demangle_simple(s)
+    if s.startswith("void "):
+        s = s[5:]
+    s = s.replace("(anonymous namespace)::", "")
+    depth, cut = 0, len(s)
+    for i, ch in enumerate(s):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            cut = i
+            break
+    s = s[:cut]
+    depth, start = 0, 0
+    for i, ch in enumerate(s):  # namespace qualifiers of the name (not inside template args)
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == ":" and depth == 0 and i + 1 < len(s) and s[i + 1] == ":":
+            start = i + 2
+    s = s[start:]
+    for a, b in (("std::bfloat16_t", "bf16"), ("__bf16", "bf16"), ("DF16b", "bf16"),
+                 ("std::float16_t", "f16"), ("_Float16", "f16"), ("clskd::", ""), (" ", "")):
+        s = s.replace(a, b)
+    return s
+
+
 def capture_token():
     """None outside graph capture; else the identity of the capture being recorded."""
     if not (torch.cuda.is_initialized() and torch.cuda.is_current_stream_capturing()):
@@ -773,10 +871,14 @@ def lstm_pre_capable(H):
     return bool(lib().clskd_lstm_pre_capable(H))
 
 
-def lstm_recurrent_pre(gx, gx_ws, gx_seq, gx_t, whh, nws, nseq, T, H, out, o_ws, o_seq, o_t):
-    """lstm_recurrent that also overwrites gx with the gate pre-activations (taped forward)."""
+def lstm_recurrent_pre(gx, gx_ws, gx_seq, gx_t, whh, nws, nseq, T, H, out, o_ws, o_seq, o_t,
+                       cbuf=None):
+    """lstm_recurrent that also overwrites gx with the gate pre-activations (taped forward) and,
+    given cbuf (nws*nseq*T*H fp32), stores the cell states there for lstm_bwd."""
+    assert cbuf is None or (cbuf.dtype == torch.float32 and cbuf.numel() == nws * nseq * T * H)
     check(lib().clskd_lstm_recurrent_pre(ptr(gx), gx_ws, gx_seq, gx_t, ptr(whh), nws, nseq, T, H,
-                                         ptr(out), o_ws, o_seq, o_t, _stream()), "lstm_pre")
+                                         ptr(out), o_ws, o_seq, o_t, ptr(cbuf), _stream()),
+          "lstm_pre")
     return out
 
 
@@ -1053,6 +1155,14 @@ class GramSlabs:
         self.refs = [(base + 4096 * f, n) for f, n in spans]
         # job table is a host array passed as kernel arguments (no upload, capturable)
         check(lib().clskd_gram_partial(jobs, len(views), B, base, _stream()), "gram_partial")
+        if KernelTimer.active:  # algorithmic bytes: every tap once (+ the fused apply's write)
+            nb = self.slabs.numel() * 4
+            fl = 0.0
+            for v in views:
+                n = B * v.P * v.Cs * v.tensor.element_size()
+                nb += n * (2 if v.out is not None else 1)
+                fl += 2.0 * B * B * v.P * v.Cs
+            KernelTimer.note_work(f"gram_partial_kernel<{1 if B <= 16 else 2}>", nb, fl)
 
 
 # fused BatchNorm-apply + Gram (bn_apply_gram): slabs per tap.  The launch sits on the producing
@@ -1244,6 +1354,11 @@ def abf_fuse_bwd(x1, res, w, b, x_coef, dout, dx, dyup, dnext=None, mv1=None, ep
                                ptr(mv1[0]) if mv1 is not None else None,
                                ptr(mv1[1]) if mv1 is not None else None, eps, ptr(part),
                                _dt(x1), _stream()), "abf_fuse_bwd")
+    if KernelTimer.active:  # algorithmic bytes: every operand once
+        es, npix = x1.element_size(), B * F * T
+        nb = (npix * Cm * es + B * Fr * Tr * Cm * es + npix * Cm * 4 * (2 + (dyup is not None))
+              + (B * F2 * T2 * Cm * 4 if dnext is not None else 0) + nblk * Cm * 3 * 8)
+        KernelTimer.note_work(f"abf_fuse_bwd_kernel<{'bf16' if es == 2 else 'float'}>", nb)
     return part, nblk
 
 
@@ -1296,10 +1411,14 @@ def complex_combine_bwd(dre, dim, dh):
                                           _stream()), "complex_combine_bwd")
 
 
-def lstm_bwd(pre, p_strides, dh, d_strides, whh, nws, nseq, T, H, dgates, g_strides):
-    cbuf = torch.empty(nws * nseq * T * H, dtype=torch.float32, device=pre.device)
+def lstm_bwd(pre, p_strides, dh, d_strides, whh, nws, nseq, T, H, dgates, g_strides, cells=None):
+    """cells: the forward's cell states (lstm_recurrent_pre's cbuf), else recomputed here."""
+    c_ready = cells is not None
+    cbuf = cells if c_ready else torch.empty(nws * nseq * T * H, dtype=torch.float32, device=pre.device)
+    assert cbuf.numel() == nws * nseq * T * H
     check(lib().clskd_lstm_bwd(ptr(pre), *p_strides, ptr(dh), *d_strides, ptr(whh), nws, nseq, T, H,
-                               ptr(cbuf), ptr(dgates), *g_strides, _stream()), "lstm_bwd")
+                               ptr(cbuf), int(c_ready), ptr(dgates), *g_strides, _stream()),
+          "lstm_bwd")
 
 
 def spkd_grad(s_refs, t_refs, B, batchmean=True, scale=1.0, out=None, device=None):
@@ -1347,6 +1466,15 @@ def spkd_bn_bwd(raw, coef_bn, coef_m, mean, var, eps, gamma, draw, dgamma=None, 
     check(L.clskd_spkd_bn_bwd(ptr(raw), _dt(raw), P * Cn, P, Cn, B, sc, sc + 4 * Cn, ptr(coef_m),
                               ptr(mean), ptr(var), eps, ptr(gamma), ptr(work), nblk, ptr(dgamma),
                               ptr(dbeta), ptr(draw), _dt(draw), _stream()), "spkd_bn_bwd")
+    if KernelTimer.active:  # algorithmic bytes: the reduce reads raw once, the apply raw + draw
+        t = {2: "bf16", 4: "float"}
+        bm = 32 if B > 16 else 16
+        n = raw.numel()
+        KernelTimer.note_work(f"spkd_bn_bwd_reduce_kernel<{t[raw.element_size()]},{bm}>",
+                              n * raw.element_size() + nblk * Cn * 3 * 8)
+        KernelTimer.note_work(f"spkd_bn_bwd_apply_kernel<{t[raw.element_size()]},"
+                              f"{t[draw.element_size()]},{bm}>",
+                              n * (raw.element_size() + draw.element_size()))
     return draw
 
 

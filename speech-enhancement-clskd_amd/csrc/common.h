@@ -38,7 +38,7 @@ int experiment_guard(const char* what, int value);
 // build only; always false in the product library): the entry point returns without launching.
 enum SkipBit {
   SKIP_BN_FINALIZE = 1, SKIP_BN_APPLY = 2, SKIP_CONV_F32 = 4, SKIP_LSTM = 8, SKIP_ABF = 16,
-  SKIP_GRAM = 32, SKIP_CONV_LOWP = 64, SKIP_CONV_DIRECT = 128
+  SKIP_GRAM = 32, SKIP_CONV_LOWP = 64, SKIP_CONV_DIRECT = 128, SKIP_LSTM_PRE = 256, SKIP_LSTM_BWD = 512
 };
 bool skip_kernel(int bit);
 template <typename T> inline const char* type_name();

@@ -1128,52 +1128,11 @@ int launch_conv_gemm8(const clskd_conv_desc& d, hipStream_t st, bool* launched) 
     }
 #undef G8A
   }
-  if (mode >= 10 && mode < 100 && !f32 && d.in_dtype == CLSKD_BF16) {
-    const int cfg = mode / 10, dbg = mode % 10;
-#define G8X(BM_, BN_, WM_, BK_, NS_, PHI_)                                    \
-  switch (dbg) {                                                              \
-    case 1: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 1>(d, st);  \
-    case 2: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 2>(d, st);  \
-    case 3: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 3>(d, st);  \
-    case 4: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 4>(d, st);  \
-    case 5: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 5>(d, st);  \
-    case 6: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 6>(d, st);  \
-    case 7: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 7>(d, st);  \
-    case 8: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 8>(d, st);  \
-    case 9: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 9>(d, st);  \
-    default: return launch_g8<BM_, BN_, WM_, BK_, NS_, PHI_, __bf16, 0>(d, st); \
-  }
-    const int nk64 = d.K / 64;
-    switch (cfg) {
-      case 2:  // BK 32, four stages (three K-tiles in flight)
-        if (d.N <= 128) { G8X(256, 128, 4, 32, 5, 1) }
-        G8X(256, 256, 2, 32, 4, 1)
-      case 3:  // BK 32, three stages
-        if (d.N <= 128) { G8X(256, 128, 4, 32, 4, 1) }
-        G8X(256, 256, 2, 32, 3, 1)
-      case 4:  // BK 32, pieces over both substeps
-        if (d.N <= 128) { G8X(256, 128, 4, 32, 5, 2) }
-        G8X(256, 256, 2, 32, 4, 2)
-      case 5:  // 256 x 128 tiles everywhere, BK 32 four stages
-        G8X(256, 128, 4, 32, 5, 1)
-      case 6:  // fragment prefetch two substeps ahead (three register sets)
-        if (d.N <= 128) return launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 2>(d, st);
-        return launch_g8<256, 256, 2, 64, 2, 2, __bf16, 0, 2>(d, st);
-      case 7:  // prefetch two ahead, 256 x 128 tiles everywhere
-        return launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 2>(d, st);
-      case 8:  // prefetch three ahead, 256 x 128 tiles everywhere
-        return launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 3>(d, st);
-      case 9:  // dbg 0: K-tile boundary before the last substep (EB); 1: four waves (one per
-               // SIMD), each a 128 x 64 block (measured 1.4-1.9x slower)
-        if (dbg == 1) return launch_g8<256, 128, 2, 64, 2, 2, __bf16, 0, 1, 4>(d, st);
-        if (d.N <= 128) return launch_g8<256, 128, 4, 64, 2, 2, __bf16, 0, 1, 8, 1>(d, st);
-        return launch_g8<256, 256, 2, 64, 2, 2, __bf16, 0, 1, 8, 1>(d, st);
-      default:  // BK 64, two stages
-        (void)nk64;
-        if (d.N <= 128) { G8X(256, 128, 4, 64, 2, 2) }
-        G8X(256, 256, 2, 64, 2, 2)
-    }
-#undef G8X
+  if (mode >= 10 && mode < 100) {
+    // rounds 2-4's tile / stage / prefetch variants (CLSKD_G8 = 10 * cfg + dbg) were measured and
+    // not adopted; round 6 dropped them from the experiments library
+    set_error("CLSKD_G8=%d: the round 2-4 variants are no longer built (TA ablations: 100 + flags)", mode);
+    return CLSKD_E_ARG;
   }
 #endif
   // default: BK 64, two stages, the K-tile boundary before the last substep (EB; 3-5 % on the

@@ -17,8 +17,11 @@
 // The graph is borrowed: the kernels' captured arguments live in its nodes, and the buffers they
 // point to in the capture's memory pool, so the caller keeps both alive while the executor is
 // used (clskd.graph.StepExecutor owns the torch CUDAGraph for this).
+#include <cxxabi.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 #include <time.h>
 
 #include <algorithm>
@@ -636,6 +639,100 @@ extern "C" int clskd_exec_profile_read(clskd_exec* ex, double* total_ms, int32_t
   *total_ms = tot;
   *count = ex->t_used;
   return CLSKD_OK;
+}
+
+// Per-kernel census of one replay (round 6; bench.py picks the dominant kernel instance from it):
+// the program's nodes in program order (a topological order) on ONE stream, the caller's, with an
+// event pair around every kernel node — each kernel's isolated duration, the view a rocprofv3
+// kernel trace of a serialised step has.  The replay is a real step of the captured computation.
+// fns / ms receive one entry per kernel node in program order (*n = the node count; cap too small:
+// CLSKD_E_ARG with *n set).  Synchronises the stream.
+extern "C" int clskd_exec_census(clskd_exec* ex, void* stream, int32_t cap, const void** fns, float* ms,
+                                 int32_t* n) {
+  CLSKD_CHECK_ARG(ex && n, "exec_census: null argument");
+  const int nk = (int)ex->kernels.size();
+  *n = nk;
+  CLSKD_CHECK_ARG(cap >= nk && fns && ms, "exec_census: %d kernel nodes, room for %d", nk, cap);
+  const hipStream_t s = as_stream(stream);
+  std::vector<hipEvent_t> ev(2 * (size_t)nk, nullptr);
+  auto cleanup = [&]() {
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+  };
+  for (auto& e : ev) {
+    const hipError_t r = hipEventCreate(&e);
+    if (r != hipSuccess) {
+      e = nullptr;
+      cleanup();
+      return hip_fail("hipEventCreate", r);
+    }
+  }
+  int k = 0;
+  for (const Op& op : ex->program) {
+    hipError_t e = hipSuccess;
+    if (op.kind == OP_KERNEL) {
+      const KNode& kn = ex->kernels[op.idx];
+      (void)hipEventRecord(ev[2 * k], s);
+      e = hipLaunchKernel(kn.func, kn.grid, kn.block, kn.args, kn.shmem, s);
+      (void)hipEventRecord(ev[2 * k + 1], s);
+      fns[k++] = kn.func;
+    } else if (op.kind == OP_MEMSET) {
+      const hipMemsetParams& p = ex->memsets[op.idx];
+      if (p.height > 1)
+        e = hipMemset2DAsync(p.dst, p.pitch, (int)p.value, p.width, p.height, s);
+      else if (p.elementSize == 4)
+        e = hipMemsetD32Async((hipDeviceptr_t)p.dst, (int)p.value, p.width, s);
+      else if (p.elementSize == 2)
+        e = hipMemsetD16Async((hipDeviceptr_t)p.dst, (unsigned short)p.value, p.width, s);
+      else
+        e = hipMemsetD8Async((hipDeviceptr_t)p.dst, (unsigned char)p.value, p.width, s);
+    } else if (op.kind == OP_MEMCPY) {
+      const clskd_exec::Flat& f = ex->flat[op.idx];
+      e = f.bytes ? hipMemcpyAsync(f.dst, f.src, f.bytes, f.kind, s) : hipMemcpy3DAsync(&ex->memcpys[op.idx], s);
+    }  // waits / records: one stream in program order needs none
+    if (e != hipSuccess) {
+      (void)hipStreamSynchronize(s);
+      cleanup();
+      return hip_fail("exec_census launch", e);
+    }
+  }
+  hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    cleanup();
+    return hip_fail("hipStreamSynchronize", e);
+  }
+  for (int i = 0; i < k; ++i) {
+    float t = 0.f;
+    e = hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]);
+    if (e != hipSuccess) {
+      cleanup();
+      return hip_fail("hipEventElapsedTime", e);
+    }
+    ms[i] = t;
+  }
+  cleanup();
+  return CLSKD_OK;
+}
+
+// Demangled name of a kernel's host stub (the function pointers exec_census reports).  Returns
+// the name's length (buf: NUL-terminated, truncated to cap), -1 when HIP does not know the
+// function.
+extern "C" int32_t clskd_kernel_name(const void* fn, char* buf, int32_t cap) {
+  const char* m = fn ? hipKernelNameRefByPtr(fn, nullptr) : nullptr;
+  if (!m) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  int st = 0;
+  char* dm = abi::__cxa_demangle(m, nullptr, nullptr, &st);
+  const std::string out = (st == 0 && dm) ? std::string(dm) : std::string(m);
+  free(dm);
+  if (buf && cap > 0) {
+    const size_t nb = out.size() < (size_t)cap - 1 ? out.size() : (size_t)cap - 1;
+    memcpy(buf, out.data(), nb);
+    buf[nb] = 0;
+  }
+  return (int32_t)out.size();
 }
 
 extern "C" void clskd_exec_destroy(clskd_exec* ex) {

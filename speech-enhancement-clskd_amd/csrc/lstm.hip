@@ -191,7 +191,7 @@ template <int H>
 __global__ __launch_bounds__(64) void lstm_wave_kernel(
     const float* gx, int64_t gx_ws, int64_t gx_seq, int64_t gx_t,
     const float* __restrict__ whh, int T, float* __restrict__ out, int64_t o_ws, int64_t o_seq,
-    int64_t o_t, int prio, float* pre) {
+    int64_t o_t, int prio, float* pre, float* __restrict__ cout = nullptr) {
   if (prio) __builtin_amdgcn_s_setprio(3);
   constexpr int S = 64 / H;   // k-slices per unit
   constexpr int KW = H / S;   // k-slice width
@@ -214,6 +214,8 @@ __global__ __launch_bounds__(64) void lstm_wave_kernel(
   const float* gp = gx + ws * gx_ws + seq * gx_seq + u;
   float* pp = pre ? pre + ws * gx_ws + seq * gx_seq + u : nullptr;
   float* op = out + ws * o_ws + seq * o_seq + u;
+  // taped forward: the cell states c_t too, [ws][seq][T][H] (the backward's cell scan input)
+  float* cq = cout ? cout + ((int64_t)ws * gridDim.x + seq) * (int64_t)T * H + u : nullptr;
   auto load_g = [&](int t, float& g0, float& g1) {
     const float* q = gp + (int64_t)min(t, T - 1) * gx_t;
     g0 = q[ks * H];
@@ -282,6 +284,7 @@ __global__ __launch_bounds__(64) void lstm_wave_kernel(
       const float hn = og * tanh_fast(cstate);
       hb[t & 1][u] = hn;
       op[(int64_t)t * o_t] = hn;
+      if (cq) cq[(int64_t)t * H] = cstate;
     }
     // one wave: its LDS write completes before its next read is served (in-order LDS queue);
     // the wait + clobber keep the compiler from moving the next step's reads above the write
@@ -427,7 +430,7 @@ __global__ __launch_bounds__(64) void lstm_bwd_wave_kernel(
     const float* __restrict__ pre, int64_t p_ws, int64_t p_seq, int64_t p_t,
     const float* __restrict__ dh, int64_t d_ws, int64_t d_seq, int64_t d_t,
     const float* __restrict__ whh, int T, float* __restrict__ cbuf,
-    float* __restrict__ dg, int64_t g_ws, int64_t g_seq, int64_t g_t) {
+    float* __restrict__ dg, int64_t g_ws, int64_t g_seq, int64_t g_t, int c_ready) {
   constexpr int G = 4 * H;
   constexpr int S = 64 / H;  // lanes per unit
   constexpr int GW = G / S;  // gate rows per lane in the W_hh^T reduction
@@ -444,8 +447,9 @@ __global__ __launch_bounds__(64) void lstm_bwd_wave_kernel(
   float* cp = cbuf + ((int64_t)ws * gridDim.x + seq) * (int64_t)T * H + u;
   float* gp = dg + ws * g_ws + seq * g_seq + u;
   // phase 1: the cell scan, by every lane of the unit (identical values to the same address;
-  // each lane reads back only what it wrote itself)
-  {
+  // each lane reads back only what it wrote itself) — unless the taped forward stored the cell
+  // states already (c_ready: lstm_wave_kernel's cout; the serial scan is ~half of this kernel)
+  if (!c_ready) {
     float c = 0.f;
 #pragma unroll 4
     for (int t = 0; t < T; ++t) {
@@ -646,15 +650,16 @@ extern "C" int clskd_lstm_recurrent(const float* gx, int64_t gx_ws, int64_t gx_s
 extern "C" int clskd_lstm_recurrent_pre(float* gx, int64_t gx_ws, int64_t gx_seq, int64_t gx_t,
                                         const float* whh, int32_t nws, int32_t nseq, int32_t T,
                                         int32_t H, float* out, int64_t o_ws, int64_t o_seq,
-                                        int64_t o_t, void* stream) {
+                                        int64_t o_t, float* cbuf, void* stream) {
   CLSKD_CHECK_ARG(gx && whh && out, "lstm_pre: null pointer");
   CLSKD_CHECK_SHAPE(nws >= 1 && nseq >= 1 && T >= 1, "lstm_pre: empty shape");
   CLSKD_CHECK_ARG(((uintptr_t)whh & 15) == 0, "lstm_pre: whh must be 16-byte aligned");
   CLSKD_CHECK_SHAPE(clskd_lstm_pre_capable(H), "lstm_pre: H=%d runs on a kernel without the "
                     "pre-activation output (clskd_lstm_pre_capable)", H);
+  if (skip_kernel(SKIP_LSTM_PRE)) return CLSKD_OK;
   hipLaunchKernelGGL(lstm_wave_kernel<32>, dim3(nseq, nws), dim3(64), 0, as_stream(stream), gx,
                      gx_ws, gx_seq, gx_t, whh, T, out, o_ws, o_seq, o_t,
-                     knob(KNOB_LSTM_PRIO) == 1 ? 1 : 0, gx);
+                     knob(KNOB_LSTM_PRIO) == 1 ? 1 : 0, gx, cbuf);
   CLSKD_LAUNCH_CHECK("lstm_recurrent_pre");
   return CLSKD_OK;
 }
@@ -662,10 +667,11 @@ extern "C" int clskd_lstm_recurrent_pre(float* gx, int64_t gx_ws, int64_t gx_seq
 extern "C" int clskd_lstm_bwd(const float* pre, int64_t p_ws, int64_t p_seq, int64_t p_t,
                               const float* dh, int64_t d_ws, int64_t d_seq, int64_t d_t,
                               const float* whh, int32_t nws, int32_t nseq, int32_t T, int32_t H,
-                              float* cbuf, float* dgates, int64_t g_ws, int64_t g_seq,
-                              int64_t g_t, void* stream) {
+                              float* cbuf, int32_t c_ready, float* dgates, int64_t g_ws,
+                              int64_t g_seq, int64_t g_t, void* stream) {
   CLSKD_CHECK_ARG(pre && dh && whh && cbuf && dgates, "lstm_bwd: null pointer");
   CLSKD_CHECK_SHAPE(nws >= 1 && nseq >= 1 && T >= 1, "lstm_bwd: empty shape");
+  if (skip_kernel(SKIP_LSTM_BWD)) return CLSKD_OK;
   dim3 grid(nseq, nws);
   hipStream_t st = as_stream(stream);
 #define LSTM_BWD(H_, NKS_)                                                                     \
@@ -676,10 +682,10 @@ extern "C" int clskd_lstm_bwd(const float* pre, int64_t p_ws, int64_t p_seq, int
   if (wave && (H == 16 || H == 32)) {
     if (H == 16)
       hipLaunchKernelGGL(lstm_bwd_wave_kernel<16>, grid, dim3(64), 0, st, pre, p_ws, p_seq, p_t, dh,
-                         d_ws, d_seq, d_t, whh, T, cbuf, dgates, g_ws, g_seq, g_t);
+                         d_ws, d_seq, d_t, whh, T, cbuf, dgates, g_ws, g_seq, g_t, c_ready);
     else
       hipLaunchKernelGGL(lstm_bwd_wave_kernel<32>, grid, dim3(64), 0, st, pre, p_ws, p_seq, p_t, dh,
-                         d_ws, d_seq, d_t, whh, T, cbuf, dgates, g_ws, g_seq, g_t);
+                         d_ws, d_seq, d_t, whh, T, cbuf, dgates, g_ws, g_seq, g_t, c_ready);
     CLSKD_LAUNCH_CHECK("lstm_bwd");
     return CLSKD_OK;
   }

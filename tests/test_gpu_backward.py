@@ -493,3 +493,43 @@ def test_lstm_recurrent_pre_writes_gate_preactivations():
     hprev = torch.cat([torch.zeros(2, 2 * B, 1, H, dtype=torch.float64), h[:, :, :-1]], 2)
     exp = gx.double().cpu() + torch.einsum("wstk,wgk->wstg", hprev, whh.double().cpu())
     np.testing.assert_allclose(gx2.double().cpu().numpy(), exp.numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_lstm_forward_cell_states_feed_the_backward():
+    """Round 6: clskd_lstm_recurrent_pre with a cell-state buffer stores c_t of every step, and
+    clskd_lstm_bwd with c_ready = 1 (no cell-state scan of its own) gives the gate gradients of
+    the scanning backward: c_t within 1e-6 relative of the backward's own scan (the same gate
+    functions; only the compiler's FMA contraction of c = f c + i g may differ), dgates within
+    1e-5 relative."""
+    from clskd import ops
+    H, B, T = 32, 3, 41
+    if not ops.lstm_pre_capable(H):
+        pytest.skip("pre-activation output disabled (CLSKD_LSTM_PRE=0)")
+    g = torch.Generator().manual_seed(7)
+    gx = torch.randn(2, 2 * B, T, 4 * H, generator=g).to(DEV)
+    whh = (torch.randn(2, 4 * H, H, generator=g) * 0.3).to(DEV)
+    dh = torch.randn(2, 2 * B, T, H, generator=g).to(DEV)
+    st = (2 * B * T * 4 * H, T * 4 * H, 4 * H)
+    hs = torch.empty(2, 2 * B, T, H, device=DEV)
+    cells = torch.full((2 * 2 * B * T * H,), float("nan"), device=DEV)
+    ops.lstm_recurrent_pre(gx, *st, whh, 2, 2 * B, T, H, hs, 2 * B * T * H, T * H, H, cbuf=cells)
+    dg_scan = torch.empty(2, 2 * B, T, 4 * H, device=DEV)
+    dg_fwd = torch.empty_like(dg_scan)
+    ds = (2 * B * T * H, T * H, H)
+    ops.lstm_bwd(gx, st, dh, ds, whh, 2, 2 * B, T, H, dg_scan, st)  # its own cell-state scan
+    ops.lstm_bwd(gx, st, dh, ds, whh, 2, 2 * B, T, H, dg_fwd, st, cells=cells)
+    torch.cuda.synchronize()
+    assert torch.isfinite(cells).all()
+    # c_t from the pre-activations in fp64
+    pre = gx.double().cpu()
+    c = torch.zeros(2, 2 * B, H, dtype=torch.float64)
+    ref = []
+    for t in range(T):
+        q = pre[:, :, t]
+        ig, fg = torch.sigmoid(q[..., :H]), torch.sigmoid(q[..., H:2 * H])
+        gg = torch.tanh(q[..., 2 * H:3 * H])
+        c = fg * c + ig * gg
+        ref.append(c.clone())
+    ref = torch.stack(ref, 2).reshape(-1)
+    np.testing.assert_allclose(cells.double().cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(dg_fwd.cpu().numpy(), dg_scan.cpu().numpy(), rtol=1e-5, atol=1e-6)

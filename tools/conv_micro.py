@@ -57,6 +57,7 @@ def make(kind, ci, co, fi, B=B, T=T, dev=None):
 
     def run():
         ops.conv([seg], taps, B, Fo, To, co, wp, bias, out, omap, stride_f=sf, stats=st)
+    run.out = out
     return run, 2.0 * B * Fo * To * co * K, (B * Fo * To, co, K)
 
 

@@ -36,6 +36,11 @@ for st in ${STEPS:-suite bench}; do
         rc=0; timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/fetch.log 2>&1 || rc=$?; ok $rc fetch
         rc=0; timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/write.log 2>&1 || rc=$?; ok $rc write ) || exit $?
       python3 $R/tools/pmc_traffic.py $O/fetch/run_counter_collection.csv $O/write/run_counter_collection.csv $O/pmc_traffic.json > $O/traffic.txt;;
+    pmc_train)  # the C3 leg's own FETCH_SIZE / WRITE_SIZE passes (round 6: the C3 line's traffic)
+      ( cd /tmp && export TMPDIR=/tmp
+        rc=0; timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/tfetch -o run -- python3 $R/bench.py --train --steps 2 --warmup 2 --no-cpu-baseline > $O/tfetch.log 2>&1 || rc=$?; ok $rc tfetch
+        rc=0; timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/twrite -o run -- python3 $R/bench.py --train --steps 2 --warmup 2 --no-cpu-baseline > $O/twrite.log 2>&1 || rc=$?; ok $rc twrite ) || exit $?
+      python3 $R/tools/pmc_traffic.py $O/tfetch/run_counter_collection.csv $O/twrite/run_counter_collection.csv $O/train_pmc_traffic.json > $O/train_traffic.txt;;
     sq)  # MFMA utilisation / wait counters of the conv_gemm8 instances inside the C2 bench: three
          # --pmc passes (the per-block slot limits), kernel filter, summarised by tools/sq_summary.py
       ( cd /tmp && export TMPDIR=/tmp; i=0
@@ -82,6 +87,16 @@ for st in ${STEPS:-suite bench}; do
         --only ${ABL_LAYERS:-enc3,enc4,enc5,dec1,dec3,abf3,abf4,pw64k} \
         --ab CLSKD_G8=${ABL_MODES:-100,101,102,103,104,106,107,108,111,115,116,132,164} > $O/abl.txt 2>&1 || rc=$?
       cat $O/abl.txt | grep -v amdgpu.ids; ok $rc abl;;
+    skip)  # "what if this kernel family were free" (CLSKD_SKIP bit mask, experiments library,
+           # wrong results, step time only): SKIP_MODES interleaved over 3 passes, BENCH_ARGS
+           # selects the leg (e.g. --train).  Bits: 8 LSTM recurrence (plain), 256 taped H=32
+           # recurrence (lstm_recurrent_pre), 512 LSTM backward, 32 Gram partials
+      for pass in 1 2 3; do
+        for m in ${SKIP_MODES:-0 8 256 512 776}; do
+          rc=0; CLSKD_LIB=exp CLSKD_SKIP=$m timeout -k 10 200 python $R/bench.py --no-cpu-baseline --steps 20 --warmup 5 $BENCH_ARGS > $O/skip_${m}_p$pass.log 2>&1 || rc=$?; ok $rc skip
+          echo "skip=$m pass $pass: $(grep '^{' $O/skip_${m}_p$pass.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], "ms")')" | tee -a $O/skip_summary.txt
+        done
+      done;;
     *) echo "unknown step $st"; exit 2;;
   esac
 done
