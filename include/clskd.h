@@ -557,7 +557,11 @@ int clskd_bn_bwd(const void* x, const float* dy, int64_t rows, int32_t C, const 
                  int32_t accumulate_params, int32_t dtype, void* stream);
 
 /* ABF fusion backward (framework.py:209-219): from dout = dL/d(fused x), dx = dL/d(conv1 BN
- * output) and dyup = dL/d(upsampled residual) (fp32 [B][F][T][64]); operands as clskd_abf_fuse.
+ * output) and dyup = dL/d(upsampled residual) ([B][F][T][64]); operands as clskd_abf_fuse.
+ * grad_dtype (CLSKD_F32 or CLSKD_BF16) is the storage type of all four gradient maps (dout,
+ * dnext, dx, dyup); arithmetic is fp32 either way.  With bf16 storage the bn_partial sums are
+ * taken over the stored (rounded) dx, so clskd_bn_bwd_from_partials reading that dx back
+ * (dy_dtype CLSKD_BF16) applies statistics consistent with its input.
  * clskd_nearest_down_sum folds a gradient of a nearest upsampling (F.interpolate 'nearest',
  * framework.py:213-222) back onto the source grid: out[b][fr][tr][c] (+)= sum of g over the
  * destination pixels whose nearest source is (fr, tr).
@@ -570,20 +574,22 @@ int clskd_bn_bwd(const void* x, const float* dy, int64_t rows, int32_t C, const 
 int32_t clskd_abf_fuse_bwd_blocks(int32_t B, int32_t F, int32_t T);
 int clskd_abf_fuse_bwd(const void* x1, const void* res, int32_t B, int32_t F, int32_t T,
                        int32_t Fr, int32_t Tr, const float* w, const float* b,
-                       const float* x_scale, const float* x_shift, const float* dout, float* dx,
-                       float* dyup, const float* dnext, int32_t F2, int32_t T2,
+                       const float* x_scale, const float* x_shift, const void* dout, void* dx,
+                       void* dyup, const void* dnext, int32_t F2, int32_t T2,
                        const float* mean1, const float* var1, float eps, double* bn_partial,
-                       int32_t dtype, void* stream);
+                       int32_t dtype, int32_t grad_dtype, void* stream);
 /* BatchNorm backward whose statistics partials [nblk][C][3] were produced by a fused producer
  * (clskd_abf_fuse_bwd): finalize + apply of clskd_bn_bwd (no PReLU).  kbuf: 3*C floats. */
-int clskd_bn_bwd_from_partials(const void* x, const float* dy, int64_t rows, int32_t C,
+int clskd_bn_bwd_from_partials(const void* x, const void* dy, int64_t rows, int32_t C,
                                const float* scale, const float* shift, const float* mean,
                                const float* var, float eps, const float* gamma,
                                double* partial, int32_t nblk, float* kbuf, float* dgamma,
                                float* dbeta, float* dx, int32_t accumulate_dx, int32_t dtype,
-                               void* stream);
-int clskd_nearest_down_sum(const float* g, int32_t B, int32_t F, int32_t T, int32_t Fr,
-                           int32_t Tr, int32_t C, float* out, int32_t accumulate, void* stream);
+                               int32_t dy_dtype, void* stream);
+/* g_dtype: storage type of g (CLSKD_F32 or CLSKD_BF16); out is fp32. */
+int clskd_nearest_down_sum(const void* g, int32_t B, int32_t F, int32_t T, int32_t Fr,
+                           int32_t Tr, int32_t C, float* out, int32_t accumulate, int32_t g_dtype,
+                           void* stream);
 
 /* Masking mode 'E' backward (DCCRN.py:207-226): d est [B][T][ldest] -> d mask [B][256][Tm][2]
  * (time 0 of the decoder output gets zero).  ConviSTFT OLA + clamp backward (tools_for_model.py:

@@ -191,10 +191,11 @@ SIGNATURES = {
                             _p, _p, _i32, _i32, _i32, _p]),
     "clskd_abf_fuse_bwd_blocks": (_i32, [_i32, _i32, _i32]),
     "clskd_abf_fuse_bwd": (_i32, [_p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,
-                                  _p, _p, _i32, _i32, _p, _p, _f32, _p, _i32, _p]),
+                                  _p, _p, _i32, _i32, _p, _p, _f32, _p, _i32, _i32, _p]),
     "clskd_bn_bwd_from_partials": (_i32, [_p, _p, _i64, _i32, _p, _p, _p, _p, _f32, _p, _p, _i32,
-                                          _p, _p, _p, _p, _i32, _i32, _p]),
-    "clskd_nearest_down_sum": (_i32, [_p, _i32, _i32, _i32, _i32, _i32, _i32, _p, _i32, _p]),
+                                          _p, _p, _p, _p, _i32, _i32, _i32, _p]),
+    "clskd_nearest_down_sum": (_i32, [_p, _i32, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32,
+                                      _p]),
     "clskd_mask_e_bwd": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _i32, _p, _p]),
     "clskd_ola_bwd": (_i32, [_p, _p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p]),
     "clskd_frame_pad_bwd": (_i32, [_p, _i32, _i32, _i32, _i32, _i32, _p, _i64, _i32, _p]),

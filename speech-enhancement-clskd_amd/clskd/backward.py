@@ -154,6 +154,9 @@ def _tw(key, src, build):
 # too, or change dtype, keep `build`.  CLSKD_TW_MAPS=0 disables the maps (A/B).
 _TW_MAPS_ON = os.environ.get("CLSKD_TW_MAPS", "1") == "1"
 _BATCH_SCATTERS = os.environ.get("CLSKD_BATCH_SCATTERS", "1") == "1"  # A/B: 0 = one launch each
+# mixed-precision ReviewKD backward: the mid-channel gradient maps (conv2 data gradient, ABF
+# fusion dx / dyup) stored bf16 (A/B: 0 = fp32 storage)
+_RKD_GRAD_BF16 = os.environ.get("CLSKD_RKD_GRAD_BF16", "1") == "1"
 _TWMAP = {}
 
 
@@ -533,7 +536,10 @@ def review_backward(review, tape, coef_m, d_feats, acc_feats):
         d_oraw = torch.empty(out_raw.shape, device=dev, dtype=out_raw.dtype if lowp else f32)
         ops.spkd_bn_bwd(out_raw, tp["coef2"], coef_m[j], tp["mv2"][0], tp["mv2"][1], bn2.eps,
                         bn2.weight, d_oraw)
-        d_xf = _empty((Bn, Fn, Tn, mid), dev)
+        # levels with an attention fusion hand d_xf only to abf_fuse_bwd (any storage type);
+        # the level without one accumulates the residual gradient into it (fp32)
+        gdt = torch.bfloat16 if (lowp and _RKD_GRAD_BF16 and abf.att_conv is not None) else f32
+        d_xf = torch.empty((Bn, Fn, Tn, mid), device=dev, dtype=gdt)
         w2 = abf.conv2[0].weight
         w2t = _tw(("abf2_t", id(abf), lowp), w2, lambda: ops.pack_weight(
             w2.permute(1, 2, 3, 0).reshape(mid, 9, Cout).contiguous().float(), 9 * Cout,
@@ -546,8 +552,8 @@ def review_backward(review, tape, coef_m, d_feats, acc_feats):
         if abf.att_conv is not None:
             # one pass: residual path of level j+1 folded in on load, the attention-fusion
             # backward, and the conv1-BN statistics partials (no down-sum / BN-reduce passes)
-            dxn = _empty(d_xf.shape, dev)
-            dyup = _empty(d_xf.shape, dev)
+            dxn = torch.empty(d_xf.shape, device=dev, dtype=gdt)
+            dyup = torch.empty(d_xf.shape, device=dev, dtype=gdt)
             aw = abf.att_conv[0].weight.reshape(2, -1).float().contiguous()
             ab = abf.att_conv[0].bias.float().contiguous()
             part, nblk = ops.abf_fuse_bwd(tp["x1"], tp["res"], aw, ab, c1, d_xf, dxn, dyup,

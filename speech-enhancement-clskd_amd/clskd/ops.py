@@ -1334,8 +1334,13 @@ def bn_bwd(x, dy, scale, shift, mean, var, eps, gamma, alpha, dx, dgamma=None, d
 def abf_fuse_bwd(x1, res, w, b, x_coef, dout, dx, dyup, dnext=None, mv1=None, eps=1e-5):
     """ABF fusion backward.  dnext: the next level's dyup, folded onto this grid and added to
     dout on load.  mv1 = conv1 BN [mean; var]: also returns (partials, nblk) of that BN's
-    backward statistics for bn_bwd_from_partials."""
+    backward statistics for bn_bwd_from_partials.  The gradient maps (dout, dnext, dx, dyup)
+    share one storage type, fp32 or bf16 (dout's)."""
     L = lib()
+    gdt = dout.dtype
+    assert gdt in (torch.float32, torch.bfloat16), gdt
+    for t in (dx, dyup, dnext):
+        assert t is None or t.dtype == gdt, (t.dtype, gdt)
     B, F, T, Cm = x1.shape
     _, Fr, Tr, _ = res.shape
     sc = sh = None
@@ -1353,12 +1358,13 @@ def abf_fuse_bwd(x1, res, w, b, x_coef, dout, dx, dyup, dnext=None, mv1=None, ep
                                ptr(dout), ptr(dx), ptr(dyup), ptr(dnext), F2, T2,
                                ptr(mv1[0]) if mv1 is not None else None,
                                ptr(mv1[1]) if mv1 is not None else None, eps, ptr(part),
-                               _dt(x1), _stream()), "abf_fuse_bwd")
+                               _dt(x1), _dt(dout), _stream()), "abf_fuse_bwd")
     if KernelTimer.active:  # algorithmic bytes: every operand once
-        es, npix = x1.element_size(), B * F * T
-        nb = (npix * Cm * es + B * Fr * Tr * Cm * es + npix * Cm * 4 * (2 + (dyup is not None))
-              + (B * F2 * T2 * Cm * 4 if dnext is not None else 0) + nblk * Cm * 3 * 8)
-        KernelTimer.note_work(f"abf_fuse_bwd_kernel<{'bf16' if es == 2 else 'float'}>", nb)
+        es, gs, npix = x1.element_size(), dout.element_size(), B * F * T
+        nb = (npix * Cm * es + B * Fr * Tr * Cm * es + npix * Cm * gs * (2 + (dyup is not None))
+              + (B * F2 * T2 * Cm * gs if dnext is not None else 0) + nblk * Cm * 3 * 8)
+        tn = lambda e: "bf16" if e == 2 else "float"
+        KernelTimer.note_work(f"abf_fuse_bwd_kernel<{tn(es)},{tn(gs)}>", nb)
     return part, nblk
 
 
@@ -1369,7 +1375,7 @@ def bn_bwd_from_partials(x, dy, scale, shift, mean, var, eps, gamma, partial, nb
     check(lib().clskd_bn_bwd_from_partials(ptr(x), ptr(dy), x.numel() // Cn, Cn, ptr(scale),
                                            ptr(shift), ptr(mean), ptr(var), eps, ptr(gamma),
                                            ptr(partial), nblk, ptr(kbuf), None, None, ptr(dx),
-                                           int(accumulate_dx), _dt(x), _stream()),
+                                           int(accumulate_dx), _dt(x), _dt(dy), _stream()),
           "bn_bwd_from_partials")
     return dx
 
@@ -1377,8 +1383,9 @@ def bn_bwd_from_partials(x, dy, scale, shift, mean, var, eps, gamma, partial, nb
 def nearest_down_sum(g, out, accumulate=False):
     B, F, T, Cn = g.shape
     _, Fr, Tr, _ = out.shape
+    assert out.dtype == torch.float32, out.dtype
     check(lib().clskd_nearest_down_sum(ptr(g), B, F, T, Fr, Tr, Cn, ptr(out), int(accumulate),
-                                       _stream()), "nearest_down_sum")
+                                       _dt(g), _stream()), "nearest_down_sum")
 
 
 def mask_e_bwd(spec, mask, T, dest, dmask):

@@ -149,6 +149,9 @@ __device__ __forceinline__ void gram_store_slab(float (*red)[3][256], const f32x
   }
 }
 
+// store target of lanes without an element (16 B per lane)
+__device__ __attribute__((aligned(256))) unsigned char g_gram_sink[64 * 16];
+
 template <int NB, int MODE, bool OUT>
 __device__ __forceinline__ void gram_accumulate(const clskd_gram_job& j, int B, int64_t nel,
                                                 int64_t p0, int64_t p1, const GramXf& xf,
@@ -187,17 +190,24 @@ __device__ __forceinline__ void gram_accumulate(const clskd_gram_job& j, int B, 
           v1[u] = k1[u] ? *reinterpret_cast<const bf16x8g*>(src + o1[u]) : bf16x8g{};
         }
       }
+      // transforms, then the stores back to back: a store followed by the next transform let the
+      // compiler reuse the store's address registers behind a vmcnt(0) (one store round trip
+      // per 16-B row piece); rows / elements that were not loaded stay zero for the MFMA
+      if constexpr (MODE != 0) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if constexpr (MODE != 0) {
-          // rows / elements that were not loaded stay zero (the MFMA must see zeros for them)
-          v0[u] = k0[u] ? xf8_bf16<MODE>(v0[u], c0[u], sp, xf) : bf16x8g{};
-          if constexpr (OUT)
-            if (k0[u]) *reinterpret_cast<bf16x8g*>(dst + o0[u]) = v0[u];
-          if constexpr (NB == 2) {
-            v1[u] = k1[u] ? xf8_bf16<MODE>(v1[u], c1[u], sp, xf) : bf16x8g{};
-            if constexpr (OUT)
-              if (k1[u]) *reinterpret_cast<bf16x8g*>(dst + o1[u]) = v1[u];
+        for (int u = 0; u < U; ++u) {
+          if (k0[u]) v0[u] = xf8_bf16<MODE>(v0[u], c0[u], sp, xf);
+          if constexpr (NB == 2)
+            if (k1[u]) v1[u] = xf8_bf16<MODE>(v1[u], c1[u], sp, xf);
+        }
+        if constexpr (OUT) {
+          // straight-line stores: lanes without an element write their lane's slot of a sink
+          // page (an exec-masked store per piece compiled to a branch + vmcnt(0) each)
+          __bf16* sink = reinterpret_cast<__bf16*>(g_gram_sink) + lane * 8;
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            *reinterpret_cast<bf16x8g*>(k0[u] ? dst + o0[u] : sink) = v0[u];
+            if constexpr (NB == 2) *reinterpret_cast<bf16x8g*>(k1[u] ? dst + o1[u] : sink) = v1[u];
           }
         }
       }
@@ -233,16 +243,19 @@ __device__ __forceinline__ void gram_accumulate(const clskd_gram_job& j, int B, 
           v1[u] = k1[u] ? *reinterpret_cast<const f32x4*>(src + o1[u]) : f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
+      if constexpr (MODE != 0) {  // transforms, then the stores back to back (as above)
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if constexpr (MODE != 0) {
-          v0[u] = k0[u] ? xf4_f32<MODE>(v0[u], c0[u], sp, xf) : f32x4{0.f, 0.f, 0.f, 0.f};
-          if constexpr (OUT)
-            if (k0[u]) *reinterpret_cast<f32x4*>(dst + o0[u]) = v0[u];
-          if constexpr (NB == 2) {
-            v1[u] = k1[u] ? xf4_f32<MODE>(v1[u], c1[u], sp, xf) : f32x4{0.f, 0.f, 0.f, 0.f};
-            if constexpr (OUT)
-              if (k1[u]) *reinterpret_cast<f32x4*>(dst + o1[u]) = v1[u];
+        for (int u = 0; u < U; ++u) {
+          if (k0[u]) v0[u] = xf4_f32<MODE>(v0[u], c0[u], sp, xf);
+          if constexpr (NB == 2)
+            if (k1[u]) v1[u] = xf4_f32<MODE>(v1[u], c1[u], sp, xf);
+        }
+        if constexpr (OUT) {
+          float* sink = reinterpret_cast<float*>(g_gram_sink) + lane * 4;
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            *reinterpret_cast<f32x4*>(k0[u] ? dst + o0[u] : sink) = v0[u];
+            if constexpr (NB == 2) *reinterpret_cast<f32x4*>(k1[u] ? dst + o1[u] : sink) = v1[u];
           }
         }
       }

@@ -4,6 +4,7 @@
 // complex-LSTM output combine.  HBM-bound passes; statistics reductions in fp64 with fixed
 // orders (no float atomics), so every gradient is bitwise repeatable.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -22,6 +23,21 @@ __device__ __forceinline__ f32x4 ld4<__bf16>(const __bf16* p) {
   const bf16x4b v = *reinterpret_cast<const bf16x4b*>(p);
   return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
+
+// 4 channels as their raw storage vector (loaded without conversion) and its fp32 widening
+template <typename T> struct Raw4;
+template <> struct Raw4<float> {
+  typedef f32x4 V;
+  static __device__ __forceinline__ V ld(const float* p) { return *reinterpret_cast<const V*>(p); }
+  static __device__ __forceinline__ f32x4 cvt(V v) { return v; }
+};
+template <> struct Raw4<__bf16> {
+  typedef bf16x4b V;
+  static __device__ __forceinline__ V ld(const __bf16* p) { return *reinterpret_cast<const V*>(p); }
+  static __device__ __forceinline__ f32x4 cvt(V v) {
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+  }
+};
 
 // ------------------------------------------------------------------------------------------
 // BatchNorm (train) + optional PReLU backward.  Forward: y_bn = x*scale + shift (scale = gamma *
@@ -171,9 +187,9 @@ __global__ void bn_bwd_alpha_kernel(const double* alpha_part, int C, float* dalp
   }
 }
 
-template <typename T>
+template <typename T, typename GT = float>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
-    const T* __restrict__ x, const float* __restrict__ dy, int64_t rows, int C,
+    const T* __restrict__ x, const GT* __restrict__ dy, int64_t rows, int C,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ alpha, const float* __restrict__ k, float* __restrict__ dx,
     int accumulate) {
@@ -187,7 +203,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   int c0 = (int)((q0 * 4) % C);
   for (int64_t q = q0; q < nq; q += stride) {
     const f32x4 xv = ld4<T>(x + q * 4);
-    const f32x4 gv = *reinterpret_cast<const f32x4*>(dy + q * 4);
+    const f32x4 gv = load4<GT>(dy + q * 4);
     const f32x4 k0 = *reinterpret_cast<const f32x4*>(k + c0);
     const f32x4 k1 = *reinterpret_cast<const f32x4*>(k + C + c0);
     const f32x4 k2 = *reinterpret_cast<const f32x4*>(k + 2 * C + c0);
@@ -239,12 +255,14 @@ __device__ __forceinline__ int first_dst_b(int s, int in_size, int out_size) {
 // (nearest upsampling (F, T) -> (F2, T2), framework.py:213-215) — so no separate down-sum pass;
 // when bnpart is given, per-block fp64 partials {sum dx, sum dx*xhat1, 0} of the conv1 BatchNorm
 // backward (xhat1 = (x1 - mean1) * rstd1) are emitted — so no separate BN reduce pass.
-template <typename DT>
+// GT: storage type of the four gradient maps (dout, dnext, dx, dyup): fp32, or bf16 in the
+// mixed-precision step (halves the pass's dominant bytes; arithmetic stays fp32).
+template <typename DT, typename GT>
 __global__ __launch_bounds__(256) void abf_fuse_bwd_kernel(
     const DT* __restrict__ x1, const DT* __restrict__ res, int B, int F, int T, int Fr, int Tr,
     const float* __restrict__ w, const float* __restrict__ bias, const float* __restrict__ xs,
-    const float* __restrict__ xh, const float* __restrict__ dout, float* __restrict__ dx,
-    float* __restrict__ dyup, const float* __restrict__ dnext, int F2, int T2,
+    const float* __restrict__ xh, const GT* __restrict__ dout, GT* __restrict__ dx,
+    GT* __restrict__ dyup, const GT* __restrict__ dnext, int F2, int T2,
     const float* __restrict__ mean1, const float* __restrict__ var1, float eps,
     double* __restrict__ bnpart) {
   const int lane = threadIdx.x & 63;
@@ -276,6 +294,13 @@ __global__ __launch_bounds__(256) void abf_fuse_bwd_kernel(
     w1y[j] = w[192 + c + j];
   }
   const float b0 = bias[0], b1 = bias[1];
+  // next grid an exact 1x / 2x upsampling in each axis (nearest_src_b's fast paths): the children
+  // of (f, t) are {rf*f, rf*f + 1} x {rt*t, rt*t + 1}, no search loop (rf = 0: general grids)
+  int rf = 0, rt = 0;
+  if (dnext && (F2 == F || F2 == 2 * F) && (T2 == T || T2 == 2 * T)) {
+    rf = F2 / F;
+    rt = T2 / T;
+  }
   const int64_t npix = (int64_t)B * F * T;
   const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
   const int64_t nslots = ((int64_t)gridDim.x * blockDim.x) >> 4;
@@ -287,17 +312,40 @@ __global__ __launch_bounds__(256) void abf_fuse_bwd_kernel(
     const int f = (int)(bf - (uint32_t)b * (uint32_t)F);
     const int fr = nearest_src_b(f, Fr, F);
     const int tr = nearest_src_b(t, Tr, T);
-    const f32x4 xraw = ld4<DT>(x1 + p * 64 + c);
+    // every operand of the pixel is loaded before any is used (one memory round trip): raw
+    // vectors, pinned together, converted afterwards
+    const DT* xp = x1 + p * 64 + c;
+    const DT* yp = res + (((int64_t)b * Fr + fr) * Tr + tr) * 64 + c;
+    const GT* gp = dout + p * 64 + c;
+    const GT* q = gp;  // children of a 1x / 2x next grid (rf = 0: dout again, unused)
+    int64_t df = 0, dt = 0;
+    if (rf) {
+      q = dnext + ((((int64_t)b * F2 + f * rf) * T2 + t * rt) * 64) + c;
+      df = rf == 2 ? (int64_t)T2 * 64 : 0;
+      dt = rt == 2 ? 64 : 0;
+    }
+    typename Raw4<DT>::V xr = Raw4<DT>::ld(xp), yr = Raw4<DT>::ld(yp);
+    typename Raw4<GT>::V gr = Raw4<GT>::ld(gp), c00 = Raw4<GT>::ld(q), c01 = Raw4<GT>::ld(q + dt),
+                         c10 = Raw4<GT>::ld(q + df), c11 = Raw4<GT>::ld(q + df + dt);
+    asm volatile("" : "+v"(xr), "+v"(yr), "+v"(gr), "+v"(c00), "+v"(c01), "+v"(c10), "+v"(c11));
+    const f32x4 xraw = Raw4<DT>::cvt(xr);
     f32x4 xv;
 #pragma unroll
     for (int j = 0; j < 4; ++j) xv[j] = fmaf(xraw[j], sx[j], hx[j]);
-    const f32x4 yv = ld4<DT>(res + (((int64_t)b * Fr + fr) * Tr + tr) * 64 + c);
-    f32x4 g = *reinterpret_cast<const f32x4*>(dout + p * 64 + c);
-    if (dnext) {  // children of (f, t) on the next level's grid
+    const f32x4 yv = Raw4<DT>::cvt(yr);
+    f32x4 g = Raw4<GT>::cvt(gr);
+    if (rf) {  // summed in the general loop's order: (f2, t2), (f2, t2+1), (f2+1, t2), ...
+      g += Raw4<GT>::cvt(c00);
+      if (rt == 2) g += Raw4<GT>::cvt(c01);
+      if (rf == 2) {
+        g += Raw4<GT>::cvt(c10);
+        if (rt == 2) g += Raw4<GT>::cvt(c11);
+      }
+    } else if (dnext) {  // children of (f, t) on the next level's grid
       const int fa = first_dst_b(f, F, F2), ta = first_dst_b(t, T, T2);
       for (int f2 = fa; f2 < F2 && nearest_src_b(f2, F, F2) == f; ++f2)
         for (int t2 = ta; t2 < T2 && nearest_src_b(t2, T, T2) == t; ++t2)
-          g += *reinterpret_cast<const f32x4*>(dnext + ((((int64_t)b * F2 + f2) * T2 + t2) * 64) + c);
+          g += load4<GT>(dnext + ((((int64_t)b * F2 + f2) * T2 + t2) * 64) + c);
     }
     float d0 = 0.f, d1 = 0.f, e0 = 0.f, e1 = 0.f;
 #pragma unroll
@@ -324,8 +372,14 @@ __global__ __launch_bounds__(256) void abf_fuse_bwd_kernel(
       ox[j] = g[j] * z0 + a0 * w0x[j] + a1 * w1x[j];
       oy[j] = g[j] * z1 + a0 * w0y[j] + a1 * w1y[j];
     }
-    *reinterpret_cast<f32x4*>(dx + p * 64 + c) = ox;
-    if (dyup) *reinterpret_cast<f32x4*>(dyup + p * 64 + c) = oy;
+    if constexpr (sizeof(GT) == 2) {
+      // the BN partials sum the stored (rounded) dx, so the apply pass that reads it back sees
+      // statistics consistent with its own input
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ox[j] = (float)(GT)ox[j];
+    }
+    store4<GT>(dx + p * 64 + c, ox);
+    if (dyup) store4<GT>(dyup + p * 64 + c, oy);
     if (bnpart) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -366,8 +420,9 @@ __device__ __forceinline__ int first_dst(int s, int in_size, int out_size) {
   return d0;
 }
 
+template <typename GT>
 __global__ __launch_bounds__(256) void nearest_down_sum_kernel(
-    const float* __restrict__ g, int B, int F, int T, int Fr, int Tr, int C,
+    const GT* __restrict__ g, int B, int F, int T, int Fr, int Tr, int C,
     float* __restrict__ out, int accumulate) {
   const int CQ = C / 4;
   const int64_t total = (int64_t)B * Fr * Tr * CQ;
@@ -383,7 +438,7 @@ __global__ __launch_bounds__(256) void nearest_down_sum_kernel(
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
     for (int f = fa; f < F && nearest_src_b(f, Fr, F) == fr; ++f)
       for (int t = ta; t < T && nearest_src_b(t, Tr, T) == tr; ++t)
-        s += *reinterpret_cast<const f32x4*>(g + ((((int64_t)b * F + f) * T + t) * C) + cq * 4);
+        s += load4<GT>(g + ((((int64_t)b * F + f) * T + t) * C) + cq * 4);
     float* op = out + pix * C + cq * 4;
     if (accumulate) s += *reinterpret_cast<const f32x4*>(op);
     *reinterpret_cast<f32x4*>(op) = s;
@@ -558,8 +613,7 @@ __global__ void complex_combine_bwd_kernel(const float* __restrict__ dre, const 
 // d raw = k1*dz + k2*raw + k3.  One thread = (position, 4 channels) over all B samples.
 // ------------------------------------------------------------------------------------------
 template <typename T>
-__device__ __forceinline__ f32x4 z_of(const T* p, const f32x4& sc, const f32x4& sh) {
-  f32x4 v = ld4<T>(p);
+__device__ __forceinline__ f32x4 z_from(f32x4 v, const f32x4& sc, const f32x4& sh) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float z = fmaf(v[i], sc[i], sh[i]);
@@ -568,12 +622,58 @@ __device__ __forceinline__ f32x4 z_of(const T* p, const f32x4& sc, const f32x4& 
   return v;
 }
 
+// The B samples' raw quads of one (position, 4 channels): all BM loads are issued before any is
+// used (sample index clamped to B - 1: the k >= B terms are never read), so a thread has BM
+// loads in flight — a `b < B ? load : 0` form compiles to one load + vmcnt(0) per sample.  The
+// raw values are kept (BM = 16) so the pass does not re-load them.
 template <typename T, int BM>
+struct SampleQuads {
+  static constexpr bool KEEP = BM <= 16;
+  typedef typename std::conditional<sizeof(T) == 2, bf16x4b, f32x4>::type RawV;
+  RawV r[KEEP ? BM : 1];
+  f32x4 z[BM];
+  __device__ __forceinline__ void load(const T* base, int64_t sB, int B, const f32x4& sc,
+                                       const f32x4& sh) {
+    RawV t[BM];
+#pragma unroll
+    for (int b = 0; b < BM; ++b) {
+      const int bb = b < B ? b : B - 1;
+      t[b] = *reinterpret_cast<const RawV*>(base + bb * sB);
+    }
+#pragma unroll
+    for (int b = 0; b < BM; ++b) {
+      f32x4 v;
+      if constexpr (sizeof(T) == 2) {
+        v = f32x4{(float)t[b][0], (float)t[b][1], (float)t[b][2], (float)t[b][3]};
+      } else {
+        v = t[b];
+      }
+      z[b] = z_from<T>(v, sc, sh);
+      if constexpr (KEEP) r[b] = t[b];
+    }
+  }
+  __device__ __forceinline__ f32x4 raw(const T* base, int64_t sB, int b) const {
+    if constexpr (KEEP) {
+      RawV t = r[0];
+#pragma unroll
+      for (int i = 1; i < BM; ++i)
+        if (i == b) t = r[i];
+      if constexpr (sizeof(T) == 2) return f32x4{(float)t[0], (float)t[1], (float)t[2], (float)t[3]};
+      else return t;
+    } else {
+      return ld4<T>(base + b * sB);
+    }
+  }
+};
+
+// EX: B == BM (the benched batch): every sample guard folds away at compile time
+template <typename T, int BM, bool EX = false>
 __global__ __launch_bounds__(256) void spkd_bn_bwd_reduce_kernel(
-    const T* __restrict__ raw, int64_t sB, int64_t P, int C, int B, int64_t ppb,
+    const T* __restrict__ raw, int64_t sB, int64_t P, int C, int Bdyn, int64_t ppb,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ Mc, const float* __restrict__ mean, const float* __restrict__ var,
     float eps, double* __restrict__ partial) {
+  const int B = EX ? BM : Bdyn;
   const int CG = C >> 2;
   const int RP = 256 / CG;
   const int tid = threadIdx.x;
@@ -594,21 +694,23 @@ __global__ __launch_bounds__(256) void spkd_bn_bwd_reduce_kernel(
   double sb[4] = {0, 0, 0, 0}, sg[4] = {0, 0, 0, 0};
   if (rl < RP) {
     for (int64_t p = p0 + rl; p < p1; p += RP) {
-      f32x4 z[BM];
-#pragma unroll
-      for (int b = 0; b < BM; ++b)
-        z[b] = b < B ? z_of<T>(raw + b * sB + p * C + cg * 4, sc, sh) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const T* base = raw + p * C + cg * 4;
+      SampleQuads<T, BM> q;
+      q.load(base, sB, B, sc, sh);
       float fb[4] = {0, 0, 0, 0}, fg[4] = {0, 0, 0, 0};
-      for (int b = 0; b < B; ++b) {
-        f32x4 dz = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < BM; ++k)
-          if (k < B) dz += Mc[b * B + k] * z[k];
-        const f32x4 x = ld4<T>(raw + b * sB + p * C + cg * 4);
+      for (int b = 0; b < BM; ++b) {
+        if (b < B) {
+          f32x4 dz = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          fb[j] += dz[j];
-          fg[j] = fmaf(dz[j], (x[j] - mu[j]) * rs[j], fg[j]);
+          for (int k = 0; k < BM; ++k)
+            if (k < B) dz += Mc[b * B + k] * q.z[k];
+          const f32x4 x = q.raw(base, sB, b);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            fb[j] += dz[j];
+            fg[j] = fmaf(dz[j], (x[j] - mu[j]) * rs[j], fg[j]);
+          }
         }
       }
 #pragma unroll
@@ -645,11 +747,12 @@ __global__ __launch_bounds__(256) void spkd_bn_bwd_reduce_kernel(
   }
 }
 
-template <typename T, typename OT, int BM>
+template <typename T, typename OT, int BM, bool EX = false>
 __global__ __launch_bounds__(256) void spkd_bn_bwd_apply_kernel(
-    const T* __restrict__ raw, int64_t sB, int64_t P, int C, int B,
+    const T* __restrict__ raw, int64_t sB, int64_t P, int C, int Bdyn,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ Mc, const float* __restrict__ k, OT* __restrict__ draw) {
+  const int B = EX ? BM : Bdyn;
   const int CQ = C / 4;
   const int64_t nq = P * CQ;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
@@ -665,16 +768,17 @@ __global__ __launch_bounds__(256) void spkd_bn_bwd_apply_kernel(
       k2[j] = k[C + c0 + j];
       k3[j] = k[2 * C + c0 + j];
     }
-    f32x4 z[BM];
+    const T* base = raw + p * C + c0;
+    SampleQuads<T, BM> sq;
+    sq.load(base, sB, B, sc, sh);
 #pragma unroll
-    for (int b = 0; b < BM; ++b)
-      z[b] = b < B ? z_of<T>(raw + b * sB + p * C + c0, sc, sh) : f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int b = 0; b < B; ++b) {
+    for (int b = 0; b < BM; ++b) {
+      if (b >= B) continue;
       f32x4 dz = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < BM; ++kk)
-        if (kk < B) dz += Mc[b * B + kk] * z[kk];
-      const f32x4 x = ld4<T>(raw + b * sB + p * C + c0);
+        if (kk < B) dz += Mc[b * B + kk] * sq.z[kk];
+      const f32x4 x = sq.raw(base, sB, b);
       f32x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = fmaf(k1[j], dz[j], fmaf(k2[j], x[j], k3[j]));
@@ -757,37 +861,49 @@ extern "C" int32_t clskd_abf_fuse_bwd_blocks(int32_t B, int32_t F, int32_t T) {
 
 extern "C" int clskd_abf_fuse_bwd(const void* x1, const void* res, int32_t B, int32_t F, int32_t T,
                                   int32_t Fr, int32_t Tr, const float* w, const float* b,
-                                  const float* x_scale, const float* x_shift, const float* dout,
-                                  float* dx, float* dyup, const float* dnext, int32_t F2,
+                                  const float* x_scale, const float* x_shift, const void* dout,
+                                  void* dx, void* dyup, const void* dnext, int32_t F2,
                                   int32_t T2, const float* mean1, const float* var1, float eps,
-                                  double* bn_partial, int32_t dtype, void* stream) {
+                                  double* bn_partial, int32_t dtype, int32_t grad_dtype,
+                                  void* stream) {
   CLSKD_CHECK_ARG(x1 && res && w && b && dout && dx, "abf_fuse_bwd: null pointer");
   CLSKD_CHECK_ARG((x_scale == nullptr) == (x_shift == nullptr), "abf_fuse_bwd: scale/shift pair");
   CLSKD_CHECK_ARG(!bn_partial || (mean1 && var1), "abf_fuse_bwd: BN partials need mean1/var1");
   CLSKD_CHECK_SHAPE(!dnext || (F2 >= F && T2 >= T), "abf_fuse_bwd: next grid smaller than this one");
   CLSKD_CHECK_SHAPE(B > 0 && F > 0 && T > 0 && (int64_t)B * F * T < ((int64_t)1 << 31),
                     "abf_fuse_bwd: B*F*T must be positive and below 2^31");
+  CLSKD_CHECK_ARG(grad_dtype == CLSKD_F32 || grad_dtype == CLSKD_BF16,
+                  "abf_fuse_bwd: grad_dtype must be CLSKD_F32 or CLSKD_BF16");
   const unsigned grid = (unsigned)clskd_abf_fuse_bwd_blocks(B, F, T);
-  if (dtype == CLSKD_BF16)
-    hipLaunchKernelGGL(abf_fuse_bwd_kernel<__bf16>, dim3(grid), dim3(256), 0, as_stream(stream),
-                       (const __bf16*)x1, (const __bf16*)res, B, F, T, Fr, Tr, w, b, x_scale,
-                       x_shift, dout, dx, dyup, dnext, F2, T2, mean1, var1, eps, bn_partial);
-  else
-    hipLaunchKernelGGL(abf_fuse_bwd_kernel<float>, dim3(grid), dim3(256), 0, as_stream(stream),
-                       (const float*)x1, (const float*)res, B, F, T, Fr, Tr, w, b, x_scale,
-                       x_shift, dout, dx, dyup, dnext, F2, T2, mean1, var1, eps, bn_partial);
+  hipStream_t st = as_stream(stream);
+#define ABF_BWD_LAUNCH(DT, GT)                                                                   \
+  hipLaunchKernelGGL((abf_fuse_bwd_kernel<DT, GT>), dim3(grid), dim3(256), 0, st,             \
+                     (const DT*)x1, (const DT*)res, B, F, T, Fr, Tr, w, b, x_scale, x_shift,  \
+                     (const GT*)dout, (GT*)dx, (GT*)dyup, (const GT*)dnext, F2, T2, mean1,    \
+                     var1, eps, bn_partial)
+  if (dtype == CLSKD_BF16) {
+    if (grad_dtype == CLSKD_BF16) ABF_BWD_LAUNCH(__bf16, __bf16);
+    else ABF_BWD_LAUNCH(__bf16, float);
+  } else {
+    if (grad_dtype == CLSKD_BF16) ABF_BWD_LAUNCH(float, __bf16);
+    else ABF_BWD_LAUNCH(float, float);
+  }
+#undef ABF_BWD_LAUNCH
   CLSKD_LAUNCH_CHECK("abf_fuse_bwd");
   return CLSKD_OK;
 }
 
-extern "C" int clskd_bn_bwd_from_partials(const void* x, const float* dy, int64_t rows, int32_t C,
+extern "C" int clskd_bn_bwd_from_partials(const void* x, const void* dy, int64_t rows, int32_t C,
                                           const float* scale, const float* shift,
                                           const float* mean, const float* var, float eps,
                                           const float* gamma, double* partial, int32_t nblk,
                                           float* kbuf, float* dgamma, float* dbeta, float* dx,
-                                          int32_t accumulate_dx, int32_t dtype, void* stream) {
+                                          int32_t accumulate_dx, int32_t dtype,
+                                          int32_t dy_dtype, void* stream) {
   CLSKD_CHECK_ARG(x && dy && scale && shift && mean && var && partial && kbuf && dx,
                   "bn_bwd_from_partials: null pointer");
+  CLSKD_CHECK_ARG(dy_dtype == CLSKD_F32 || dy_dtype == CLSKD_BF16,
+                  "bn_bwd_from_partials: dy_dtype must be CLSKD_F32 or CLSKD_BF16");
   CLSKD_CHECK_SHAPE(rows > 0 && C >= 4 && C % 4 == 0 && nblk >= 1, "bn_bwd_from_partials: shape");
   CLSKD_CHECK_ARG(((uintptr_t)kbuf & 15) == 0, "bn_bwd_from_partials: kbuf must be 16-byte aligned");
   hipStream_t st = as_stream(stream);
@@ -795,24 +911,36 @@ extern "C" int clskd_bn_bwd_from_partials(const void* x, const float* dy, int64_
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, nblk, rows, C,
                      gamma, mean, var, eps, dgamma, dbeta, kbuf, nullptr, 0);
   const int64_t nq = rows * C / 4;
-  if (dtype == CLSKD_BF16)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<__bf16>, dim3(grid_of(nq)), dim3(256), 0, st,
-                       (const __bf16*)x, dy, rows, C, scale, shift, nullptr, kbuf, dx, accumulate_dx);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(grid_of(nq)), dim3(256), 0, st,
-                       (const float*)x, dy, rows, C, scale, shift, nullptr, kbuf, dx, accumulate_dx);
+#define BN_APPLY_LAUNCH(T, GT)                                                                  \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, GT>), dim3(grid_of(nq)), dim3(256), 0, st,        \
+                     (const T*)x, (const GT*)dy, rows, C, scale, shift, nullptr, kbuf, dx,     \
+                     accumulate_dx)
+  if (dtype == CLSKD_BF16) {
+    if (dy_dtype == CLSKD_BF16) BN_APPLY_LAUNCH(__bf16, __bf16);
+    else BN_APPLY_LAUNCH(__bf16, float);
+  } else {
+    if (dy_dtype == CLSKD_BF16) BN_APPLY_LAUNCH(float, __bf16);
+    else BN_APPLY_LAUNCH(float, float);
+  }
+#undef BN_APPLY_LAUNCH
   CLSKD_LAUNCH_CHECK("bn_bwd_from_partials");
   return CLSKD_OK;
 }
 
-extern "C" int clskd_nearest_down_sum(const float* g, int32_t B, int32_t F, int32_t T, int32_t Fr,
+extern "C" int clskd_nearest_down_sum(const void* g, int32_t B, int32_t F, int32_t T, int32_t Fr,
                                       int32_t Tr, int32_t C, float* out, int32_t accumulate,
-                                      void* stream) {
+                                      int32_t g_dtype, void* stream) {
   CLSKD_CHECK_ARG(g && out, "nearest_down_sum: null pointer");
+  CLSKD_CHECK_ARG(g_dtype == CLSKD_F32 || g_dtype == CLSKD_BF16,
+                  "nearest_down_sum: g_dtype must be CLSKD_F32 or CLSKD_BF16");
   CLSKD_CHECK_SHAPE(C % 4 == 0 && F >= Fr && T >= Tr, "nearest_down_sum: shape");
   const int64_t total = (int64_t)B * Fr * Tr * (C / 4);
-  hipLaunchKernelGGL(nearest_down_sum_kernel, dim3(grid_of(total)), dim3(256), 0, as_stream(stream),
-                     g, B, F, T, Fr, Tr, C, out, accumulate);
+  if (g_dtype == CLSKD_BF16)
+    hipLaunchKernelGGL(nearest_down_sum_kernel<__bf16>, dim3(grid_of(total)), dim3(256), 0,
+                       as_stream(stream), (const __bf16*)g, B, F, T, Fr, Tr, C, out, accumulate);
+  else
+    hipLaunchKernelGGL(nearest_down_sum_kernel<float>, dim3(grid_of(total)), dim3(256), 0,
+                       as_stream(stream), (const float*)g, B, F, T, Fr, Tr, C, out, accumulate);
   CLSKD_LAUNCH_CHECK("nearest_down_sum");
   return CLSKD_OK;
 }
@@ -848,11 +976,25 @@ extern "C" int clskd_spkd_bn_bwd(const void* raw, int32_t dtype, int64_t sB, int
   const int64_t nq = P * (C / 4);
   const unsigned ga = grid_of(nq, 16384);
 #define SBB_RED(T_, BM_)                                                                            \
-  hipLaunchKernelGGL((spkd_bn_bwd_reduce_kernel<T_, BM_>), dim3(nblk), dim3(256), 0, st,           \
-                     (const T_*)raw, sB, P, C, B, ppb, scale, shift, coef, mean, var, eps, partial)
-#define SBB_APP(T_, OT_, BM_)                                                                        \
-  hipLaunchKernelGGL((spkd_bn_bwd_apply_kernel<T_, OT_, BM_>), dim3(ga), dim3(256), 0, st,          \
-                     (const T_*)raw, sB, P, C, B, scale, shift, coef, k, (OT_*)draw)
+  do {                                                                                              \
+    if (B == BM_)                                                                                   \
+      hipLaunchKernelGGL((spkd_bn_bwd_reduce_kernel<T_, BM_, true>), dim3(nblk), dim3(256), 0, st, \
+                         (const T_*)raw, sB, P, C, B, ppb, scale, shift, coef, mean, var, eps,     \
+                         partial);                                                                  \
+    else                                                                                            \
+      hipLaunchKernelGGL((spkd_bn_bwd_reduce_kernel<T_, BM_, false>), dim3(nblk), dim3(256), 0, st,\
+                         (const T_*)raw, sB, P, C, B, ppb, scale, shift, coef, mean, var, eps,     \
+                         partial);                                                                  \
+  } while (0)
+#define SBB_APP(T_, OT_, BM_)                                                                       \
+  do {                                                                                              \
+    if (B == BM_)                                                                                   \
+      hipLaunchKernelGGL((spkd_bn_bwd_apply_kernel<T_, OT_, BM_, true>), dim3(ga), dim3(256), 0,   \
+                         st, (const T_*)raw, sB, P, C, B, scale, shift, coef, k, (OT_*)draw);      \
+    else                                                                                            \
+      hipLaunchKernelGGL((spkd_bn_bwd_apply_kernel<T_, OT_, BM_, false>), dim3(ga), dim3(256), 0,  \
+                         st, (const T_*)raw, sB, P, C, B, scale, shift, coef, k, (OT_*)draw);      \
+  } while (0)
   const bool big = B > 16;
   if (dtype == CLSKD_BF16) {
     if (big) SBB_RED(__bf16, 32); else SBB_RED(__bf16, 16);

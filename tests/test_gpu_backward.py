@@ -361,7 +361,7 @@ def test_backward_refuses_redrawn_abf_weights():
 def test_clskd_backward_mixed_precision_close_to_fp32():
     """precision='mixed' (teacher + ReviewKD activations in bf16, the bench default): the
     student's gradients stay close to the all-fp32 step's (the ReviewKD backward reads bf16
-    saved activations; gradients themselves are fp32)."""
+    saved activations; the mid-channel ReviewKD gradient maps are stored bf16 too)."""
     from clskd.data import synthetic_pairs
     noisy, clean = synthetic_pairs(2, 8000, seed=23)
     X, y = torch.from_numpy(noisy).to(DEV), torch.from_numpy(clean).to(DEV)
@@ -380,6 +380,93 @@ def test_clskd_backward_mixed_precision_close_to_fp32():
     worst.sort(reverse=True)
     print(worst[:5])
     assert worst[0][0] < 5e-2, worst[:5]
+
+
+def test_reviewkd_backward_bf16_gradient_storage():
+    """The ReviewKD backward's bf16 gradient maps (precision='mixed'): abf_fuse_bwd with bf16
+    dout / dnext / dx / dyup computes in fp32 exactly as the fp32-storage path fed the same
+    (bf16-representable) gradients, so its outputs are that path's outputs rounded once —
+    bitwise; nearest_down_sum of a bf16 map equals the fp32 sum of its upcast, bitwise; the
+    conv1-BN backward from the bf16 path's partials stays within bf16 rounding of fp32's."""
+    from clskd import ops
+    bf = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(5)
+    B, F, T, Fr, Tr, F2, T2, C = 3, 16, 20, 8, 10, 32, 40, 64
+    rn = lambda *s: torch.randn(*s, device=DEV, generator=g)
+    x1 = rn(B, F, T, C).to(bf)
+    res = rn(B, Fr, Tr, C).to(bf)
+    w = (rn(2, 2 * C) * 0.2).contiguous()
+    b = rn(2) * 0.1
+    coef = torch.cat([rn(C).abs() + 0.5, rn(C) * 0.1]).contiguous()
+    mv1 = torch.stack([rn(C) * 0.1, rn(C).abs() + 0.5]).contiguous()
+    dout = rn(B, F, T, C).to(bf)
+    dnext = rn(B, F2, T2, C).to(bf)
+    outs = {}
+    for gdt in (torch.float32, bf):
+        dx = torch.empty(B, F, T, C, device=DEV, dtype=gdt)
+        dyup = torch.empty_like(dx)
+        part, nblk = ops.abf_fuse_bwd(x1, res, w, b, coef, dout.to(gdt), dx, dyup,
+                                      dnext=dnext.to(gdt), mv1=mv1)
+        d_x1 = torch.empty(B, F, T, C, device=DEV)
+        ops.bn_bwd_from_partials(x1, dx, coef[:C], coef[C:], mv1[0], mv1[1], 1e-5,
+                                 torch.ones(C, device=DEV), part, nblk, d_x1)
+        down = torch.empty(B, Fr, Tr, C, device=DEV)
+        ops.nearest_down_sum(dyup, down)
+        outs[gdt] = (dx, dyup, d_x1, down)
+    torch.cuda.synchronize()
+    f, h = outs[torch.float32], outs[bf]
+    assert torch.equal(h[0], f[0].to(bf))
+    assert torch.equal(h[1], f[1].to(bf))
+    ref_down = torch.empty_like(f[3])
+    ops.nearest_down_sum(h[1].float().contiguous(), ref_down)
+    torch.cuda.synchronize()
+    assert torch.equal(h[3], ref_down)
+    assert _rel(_np(h[2]), _np(f[2])) < 8e-3
+
+
+@pytest.mark.parametrize("B,dt", [(16, torch.bfloat16), (16, torch.float32), (5, torch.bfloat16),
+                                  (20, torch.bfloat16)])
+def test_spkd_bn_bwd_against_fp64(B, dt):
+    """clskd_spkd_bn_bwd (the SPKD gradient dz_b = sum_k M[b][k] z_k of the deferred-BN Gram
+    input, fused into that BatchNorm's backward) against fp64 torch on the same rounded z: the
+    exact-batch instance (B = 16), the guarded ones (B = 5, B = 20 on the 32-sample kernel), bf16
+    and fp32 maps; dgamma / dbeta too; bitwise repeatable."""
+    from clskd import ops
+    g = torch.Generator().manual_seed(B)
+    F, T, C, eps = 6, 37, 64, 1e-5
+    raw = (torch.randn(B, F, T, C, generator=g) * 1.3 + 0.2).to(dt)
+    xr = raw.double()
+    mean = xr.mean((0, 1, 2))
+    var = xr.var((0, 1, 2), unbiased=False)
+    gamma = torch.rand(C, generator=g) + 0.5
+    sc = torch.rand(C, generator=g) + 0.5
+    sh = torch.randn(C, generator=g) * 0.1
+    M = torch.randn(B, B, generator=g) * 0.01
+    # the Gram's (rounded) input: fmaf(raw, sc, sh) rounded once to fp32, then to the map's type
+    z = (raw.double() * sc.double() + sh.double()).float().to(dt).double()
+    dz = torch.einsum("bk,kftc->bftc", M.double(), z)
+    rs = 1.0 / torch.sqrt(var + eps)
+    xhat = (xr - mean) * rs
+    n = B * F * T
+    db = dz.sum((0, 1, 2))
+    dgm = (dz * xhat).sum((0, 1, 2))
+    ref = gamma.double() * rs * (dz - db / n - xhat * dgm / n)
+    coef = torch.cat([sc, sh]).to(DEV)
+    outs = []
+    for _ in range(2):
+        draw = torch.empty(B, F, T, C, device=DEV)
+        dgam = torch.empty(C, device=DEV)
+        dbet = torch.empty(C, device=DEV)
+        ops.spkd_bn_bwd(raw.to(DEV), coef, M.to(DEV), mean.float().to(DEV), var.float().to(DEV), eps,
+                        gamma.to(DEV), draw, dgam, dbet)
+        outs.append((draw, dgam, dbet))
+    torch.cuda.synchronize()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    draw, dgam, dbet = outs[0]
+    assert _rel(_np(draw), ref.numpy()) < 2e-5
+    assert _rel(_np(dgam), dgm.numpy()) < 2e-5
+    assert _rel(_np(dbet), db.numpy()) < 2e-5
 
 
 # ------------------------------------------------------------------------------------------

@@ -49,14 +49,22 @@ def main():
         noisy, clean = synthetic_pairs(bench.B_PER_GPU, bench.L, seed=1000 + k)
         Xs.append(torch.from_numpy(noisy).to(dev))
         Ys.append(torch.from_numpy(clean).to(dev))
+    if os.environ.get("TRAIN") == "1":  # the C3 training step (bench.py --train's eager step)
+        from clskd import config as cfg
+        from clskd.train import FlatAdam, FlatParams
+        flat = FlatParams(kd.student)
+        opt = FlatAdam(flat, lr=cfg.learning_rate, device_step=True)
+        step = lambda i: kd.train_step((Xs[i % 2], Ys[i % 2]), flat, opt)
+    else:
+        step = lambda i: kd.training_step((Xs[i % 2], Ys[i % 2]), i)
     with torch.no_grad():
         for i in range(3):
-            kd.training_step((Xs[i % 2], Ys[i % 2]), i)
+            step(i)
         torch.cuda.synchronize()
         cen = Census()
         with cen:
             for i in range(steps):
-                kd.training_step((Xs[i % 2], Ys[i % 2]), i)
+                step(i)
         torch.cuda.synchronize()
     tot = sum(cen.c.values())
     print(f"aten ops per step: {tot / steps:.1f}")
