@@ -155,7 +155,9 @@ def _tw(key, src, build):
 _TW_MAPS_ON = os.environ.get("CLSKD_TW_MAPS", "1") == "1"
 _BATCH_SCATTERS = os.environ.get("CLSKD_BATCH_SCATTERS", "1") == "1"  # A/B: 0 = one launch each
 # mixed-precision ReviewKD backward: the mid-channel gradient maps (conv2 data gradient, ABF
-# fusion dx / dyup) stored bf16 (A/B: 0 = fp32 storage)
+# fusion dx / dyup) stored bf16 — the ABF fusion backward's dominant bytes halved (C3 -0.28 ms;
+# worst C3 parameter gradient vs the oracle 3.04e-3 against 3.23e-3 with fp32 maps,
+# profiles/r6_rkd_grad_bf16.txt).  CLSKD_RKD_GRAD_BF16=0: fp32 storage (A/B)
 _RKD_GRAD_BF16 = os.environ.get("CLSKD_RKD_GRAD_BF16", "1") == "1"
 _TWMAP = {}
 

@@ -97,6 +97,20 @@ def direct_np(N):
 
 
 _DIRECT_W = OrderedDict()
+_DIRECT_MAPS = {}
+
+
+def _direct_map(N, Kp, NP, dev):
+    """index_gather map of the fp32 direct layout: wd[k][n] = w[n][k] for n < N, else 0."""
+    key = (N, Kp, NP, str(dev))
+    m = _DIRECT_MAPS.get(key)
+    if m is None:
+        k = torch.arange(Kp, dtype=torch.int64).view(Kp, 1)
+        n = torch.arange(NP, dtype=torch.int64).view(1, NP)
+        idx = torch.where(n < N, n * Kp + k, torch.full_like(n * k, -1)).to(torch.int32)
+        m = (idx.reshape(-1, 1).to(dev), torch.ones(Kp * NP, 1, dtype=torch.float32, device=dev))
+        _DIRECT_MAPS[key] = m
+    return m
 
 
 def direct_weight(wpacked):
@@ -116,6 +130,13 @@ def direct_weight(wpacked):
     if wpacked.dtype in (torch.bfloat16, torch.float16):
         wd = wpacked.new_zeros(Kp // 2, NP, 2)
         wd[:, :N, :] = wpacked.view(N, Kp // 2, 2).permute(1, 0, 2)
+    elif wpacked.is_cuda and wpacked.is_contiguous() and (
+            (N, Kp, NP, str(wpacked.device)) in _DIRECT_MAPS
+            or not torch.cuda.is_current_stream_capturing()):  # (the map's H2D copy: eager)
+        # fp32 (re-packed every training step): one index gather instead of a fill + strided copy
+        idx, sgn = _direct_map(N, Kp, NP, wpacked.device)
+        wd = torch.empty(Kp, NP, dtype=torch.float32, device=wpacked.device)
+        index_gather(wpacked, idx, sgn, wd)
     else:
         wd = wpacked.new_zeros(Kp, NP)
         wd[:, :N] = wpacked.t()
@@ -1476,11 +1497,12 @@ def spkd_bn_bwd(raw, coef_bn, coef_m, mean, var, eps, gamma, draw, dgamma=None, 
     if KernelTimer.active:  # algorithmic bytes: the reduce reads raw once, the apply raw + draw
         t = {2: "bf16", 4: "float"}
         bm = 32 if B > 16 else 16
+        ex = "true" if B == bm else "false"  # the exact-batch instance (no sample guards)
         n = raw.numel()
-        KernelTimer.note_work(f"spkd_bn_bwd_reduce_kernel<{t[raw.element_size()]},{bm}>",
+        KernelTimer.note_work(f"spkd_bn_bwd_reduce_kernel<{t[raw.element_size()]},{bm},{ex}>",
                               n * raw.element_size() + nblk * Cn * 3 * 8)
         KernelTimer.note_work(f"spkd_bn_bwd_apply_kernel<{t[raw.element_size()]},"
-                              f"{t[draw.element_size()]},{bm}>",
+                              f"{t[draw.element_size()]},{bm},{ex}>",
                               n * (raw.element_size() + draw.element_size()))
     return draw
 

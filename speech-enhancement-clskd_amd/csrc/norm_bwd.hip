@@ -304,48 +304,55 @@ __global__ __launch_bounds__(256) void abf_fuse_bwd_kernel(
   const int64_t npix = (int64_t)B * F * T;
   const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
   const int64_t nslots = ((int64_t)gridDim.x * blockDim.x) >> 4;
-  for (int64_t p = gw; p < npix; p += nslots) {
+  // a pixel's operands as loaded (raw vectors) and its grid coordinates
+  struct Px {
+    typename Raw4<DT>::V xr, yr;
+    typename Raw4<GT>::V gr, c00, c01, c10, c11;
+    int b, f, t;
+  };
+  auto load_px = [&](int64_t p, Px& o) {
     // 32-bit index split (npix < 2^31, checked by the host): no 64-bit division per pixel
     const uint32_t p32 = (uint32_t)p, bf = p32 / (uint32_t)T;
-    const int t = (int)(p32 - bf * (uint32_t)T);
-    const int b = (int)(bf / (uint32_t)F);
-    const int f = (int)(bf - (uint32_t)b * (uint32_t)F);
-    const int fr = nearest_src_b(f, Fr, F);
-    const int tr = nearest_src_b(t, Tr, T);
-    // every operand of the pixel is loaded before any is used (one memory round trip): raw
-    // vectors, pinned together, converted afterwards
-    const DT* xp = x1 + p * 64 + c;
-    const DT* yp = res + (((int64_t)b * Fr + fr) * Tr + tr) * 64 + c;
+    o.t = (int)(p32 - bf * (uint32_t)T);
+    o.b = (int)(bf / (uint32_t)F);
+    o.f = (int)(bf - (uint32_t)o.b * (uint32_t)F);
+    const int fr = nearest_src_b(o.f, Fr, F);
+    const int tr = nearest_src_b(o.t, Tr, T);
     const GT* gp = dout + p * 64 + c;
     const GT* q = gp;  // children of a 1x / 2x next grid (rf = 0: dout again, unused)
     int64_t df = 0, dt = 0;
     if (rf) {
-      q = dnext + ((((int64_t)b * F2 + f * rf) * T2 + t * rt) * 64) + c;
+      q = dnext + ((((int64_t)o.b * F2 + o.f * rf) * T2 + o.t * rt) * 64) + c;
       df = rf == 2 ? (int64_t)T2 * 64 : 0;
       dt = rt == 2 ? 64 : 0;
     }
-    typename Raw4<DT>::V xr = Raw4<DT>::ld(xp), yr = Raw4<DT>::ld(yp);
-    typename Raw4<GT>::V gr = Raw4<GT>::ld(gp), c00 = Raw4<GT>::ld(q), c01 = Raw4<GT>::ld(q + dt),
-                         c10 = Raw4<GT>::ld(q + df), c11 = Raw4<GT>::ld(q + df + dt);
-    asm volatile("" : "+v"(xr), "+v"(yr), "+v"(gr), "+v"(c00), "+v"(c01), "+v"(c10), "+v"(c11));
-    const f32x4 xraw = Raw4<DT>::cvt(xr);
+    o.xr = Raw4<DT>::ld(x1 + p * 64 + c);
+    o.yr = Raw4<DT>::ld(res + (((int64_t)o.b * Fr + fr) * Tr + tr) * 64 + c);
+    o.gr = Raw4<GT>::ld(gp);
+    o.c00 = Raw4<GT>::ld(q);
+    o.c01 = Raw4<GT>::ld(q + dt);
+    o.c10 = Raw4<GT>::ld(q + df);
+    o.c11 = Raw4<GT>::ld(q + df + dt);
+  };
+  auto compute_px = [&](int64_t p, const Px& o) {
+    const f32x4 xraw = Raw4<DT>::cvt(o.xr);
     f32x4 xv;
 #pragma unroll
     for (int j = 0; j < 4; ++j) xv[j] = fmaf(xraw[j], sx[j], hx[j]);
-    const f32x4 yv = Raw4<DT>::cvt(yr);
-    f32x4 g = Raw4<GT>::cvt(gr);
+    const f32x4 yv = Raw4<DT>::cvt(o.yr);
+    f32x4 g = Raw4<GT>::cvt(o.gr);
     if (rf) {  // summed in the general loop's order: (f2, t2), (f2, t2+1), (f2+1, t2), ...
-      g += Raw4<GT>::cvt(c00);
-      if (rt == 2) g += Raw4<GT>::cvt(c01);
+      g += Raw4<GT>::cvt(o.c00);
+      if (rt == 2) g += Raw4<GT>::cvt(o.c01);
       if (rf == 2) {
-        g += Raw4<GT>::cvt(c10);
-        if (rt == 2) g += Raw4<GT>::cvt(c11);
+        g += Raw4<GT>::cvt(o.c10);
+        if (rt == 2) g += Raw4<GT>::cvt(o.c11);
       }
     } else if (dnext) {  // children of (f, t) on the next level's grid
-      const int fa = first_dst_b(f, F, F2), ta = first_dst_b(t, T, T2);
-      for (int f2 = fa; f2 < F2 && nearest_src_b(f2, F, F2) == f; ++f2)
-        for (int t2 = ta; t2 < T2 && nearest_src_b(t2, T, T2) == t; ++t2)
-          g += load4<GT>(dnext + ((((int64_t)b * F2 + f2) * T2 + t2) * 64) + c);
+      const int fa = first_dst_b(o.f, F, F2), ta = first_dst_b(o.t, T, T2);
+      for (int f2 = fa; f2 < F2 && nearest_src_b(f2, F, F2) == o.f; ++f2)
+        for (int t2 = ta; t2 < T2 && nearest_src_b(t2, T, T2) == o.t; ++t2)
+          g += load4<GT>(dnext + ((((int64_t)o.b * F2 + f2) * T2 + t2) * 64) + c);
     }
     float d0 = 0.f, d1 = 0.f, e0 = 0.f, e1 = 0.f;
 #pragma unroll
@@ -356,11 +363,11 @@ __global__ __launch_bounds__(256) void abf_fuse_bwd_kernel(
       e1 += g[j] * yv[j];
     }
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) {
-      d0 += __shfl_xor(d0, o, 16);
-      d1 += __shfl_xor(d1, o, 16);
-      e0 += __shfl_xor(e0, o, 16);
-      e1 += __shfl_xor(e1, o, 16);
+    for (int sh = 8; sh > 0; sh >>= 1) {
+      d0 += __shfl_xor(d0, sh, 16);
+      d1 += __shfl_xor(d1, sh, 16);
+      e0 += __shfl_xor(e0, sh, 16);
+      e1 += __shfl_xor(e1, sh, 16);
     }
     const float z0 = sigmoidf_(d0 + b0);
     const float z1 = sigmoidf_(d1 + b1);
@@ -387,6 +394,21 @@ __global__ __launch_bounds__(256) void abf_fuse_bwd_kernel(
         sg[j] += (double)ox[j] * (double)((xraw[j] - mu[j]) * rs[j]);
       }
     }
+  };
+  // two pixels per iteration (p, p + nslots: the same per-thread order as one at a time, so the
+  // partials are bitwise unchanged): their 14 loads issued together, pinned ahead of the uniform
+  // branches (the compiler would sink each child load into its branch behind a vmcnt(0))
+  for (int64_t p = gw; p < npix; p += 2 * nslots) {
+    const int64_t p2 = p + nslots;
+    const bool two = p2 < npix;
+    Px A, Bq;
+    load_px(p, A);
+    load_px(two ? p2 : p, Bq);
+    asm volatile("" : "+v"(A.xr), "+v"(A.yr), "+v"(A.gr), "+v"(A.c00), "+v"(A.c01), "+v"(A.c10),
+                 "+v"(A.c11), "+v"(Bq.xr), "+v"(Bq.yr), "+v"(Bq.gr), "+v"(Bq.c00), "+v"(Bq.c01),
+                 "+v"(Bq.c10), "+v"(Bq.c11));
+    compute_px(p, A);
+    if (two) compute_px(p2, Bq);
   }
   if (bnpart) {  // the block's 16 pixel slots share the channel mapping: fixed-order slot sum
     __shared__ double red[16][64][2];
@@ -622,51 +644,36 @@ __device__ __forceinline__ f32x4 z_from(f32x4 v, const f32x4& sc, const f32x4& s
   return v;
 }
 
-// The B samples' raw quads of one (position, 4 channels): all BM loads are issued before any is
-// used (sample index clamped to B - 1: the k >= B terms are never read), so a thread has BM
-// loads in flight — a `b < B ? load : 0` form compiles to one load + vmcnt(0) per sample.  The
-// raw values are kept (BM = 16) so the pass does not re-load them.
+// z of the B samples of one (position, 4 channels), the BM loads issued together before any
+// use (sample index clamped to B - 1: the k >= B terms are never read) — a `b < B ? load : 0`
+// form compiled to one load + vmcnt(0) per sample.  The per-sample pass then walks b as a loop
+// (M's row b in SGPRs; unrolling it put all B x B coefficients in VGPRs and halved occupancy)
+// and re-reads x_b one sample ahead (cache-resident: it was just loaded).
+// The raw quads are also parked in LDS ([b][thread], conflict-free 8 / 16-B rows) when they fit
+// (xs != nullptr), so the sample loop reads x_b back from LDS instead of re-reading global memory.
 template <typename T, int BM>
-struct SampleQuads {
-  static constexpr bool KEEP = BM <= 16;
-  typedef typename std::conditional<sizeof(T) == 2, bf16x4b, f32x4>::type RawV;
-  RawV r[KEEP ? BM : 1];
-  f32x4 z[BM];
-  __device__ __forceinline__ void load(const T* base, int64_t sB, int B, const f32x4& sc,
-                                       const f32x4& sh) {
-    RawV t[BM];
+__device__ __forceinline__ void load_z(const T* base, int64_t sB, int B, const f32x4& sc,
+                                       const f32x4& sh, f32x4 (&z)[BM],
+                                       typename Raw4<T>::V* xs) {
+  typedef typename Raw4<T>::V V;
+  V t[BM];
 #pragma unroll
-    for (int b = 0; b < BM; ++b) {
-      const int bb = b < B ? b : B - 1;
-      t[b] = *reinterpret_cast<const RawV*>(base + bb * sB);
-    }
+  for (int b = 0; b < BM; ++b) t[b] = Raw4<T>::ld(base + (b < B ? b : B - 1) * sB);
 #pragma unroll
-    for (int b = 0; b < BM; ++b) {
-      f32x4 v;
-      if constexpr (sizeof(T) == 2) {
-        v = f32x4{(float)t[b][0], (float)t[b][1], (float)t[b][2], (float)t[b][3]};
-      } else {
-        v = t[b];
-      }
-      z[b] = z_from<T>(v, sc, sh);
-      if constexpr (KEEP) r[b] = t[b];
-    }
+  for (int b = 0; b < BM; ++b) {
+    z[b] = z_from<T>(Raw4<T>::cvt(t[b]), sc, sh);
+    if (xs) xs[b * 256] = t[b];
   }
-  __device__ __forceinline__ f32x4 raw(const T* base, int64_t sB, int b) const {
-    if constexpr (KEEP) {
-      RawV t = r[0];
-#pragma unroll
-      for (int i = 1; i < BM; ++i)
-        if (i == b) t = r[i];
-      if constexpr (sizeof(T) == 2) return f32x4{(float)t[0], (float)t[1], (float)t[2], (float)t[3]};
-      else return t;
-    } else {
-      return ld4<T>(base + b * sB);
-    }
-  }
-};
+}
 
-// EX: B == BM (the benched batch): every sample guard folds away at compile time
+// LDS parking space of load_z for a 256-thread block (0 when it does not fit 64 KiB)
+template <typename T, int BM>
+constexpr int park_elems() {
+  return sizeof(typename Raw4<T>::V) * BM * 256 <= 64 * 1024 ? BM * 256 : 1;
+}
+template <typename T, int BM>
+constexpr bool parks() { return park_elems<T, BM>() > 1; }
+
 template <typename T, int BM, bool EX = false>
 __global__ __launch_bounds__(256) void spkd_bn_bwd_reduce_kernel(
     const T* __restrict__ raw, int64_t sB, int64_t P, int C, int Bdyn, int64_t ppb,
@@ -674,6 +681,7 @@ __global__ __launch_bounds__(256) void spkd_bn_bwd_reduce_kernel(
     const float* __restrict__ Mc, const float* __restrict__ mean, const float* __restrict__ var,
     float eps, double* __restrict__ partial) {
   const int B = EX ? BM : Bdyn;
+  __shared__ typename Raw4<T>::V park[park_elems<T, BM>()];
   const int CG = C >> 2;
   const int RP = 256 / CG;
   const int tid = threadIdx.x;
@@ -695,22 +703,21 @@ __global__ __launch_bounds__(256) void spkd_bn_bwd_reduce_kernel(
   if (rl < RP) {
     for (int64_t p = p0 + rl; p < p1; p += RP) {
       const T* base = raw + p * C + cg * 4;
-      SampleQuads<T, BM> q;
-      q.load(base, sB, B, sc, sh);
+      f32x4 z[BM];
+      load_z<T, BM>(base, sB, B, sc, sh, z, parks<T, BM>() ? park + tid : nullptr);
       float fb[4] = {0, 0, 0, 0}, fg[4] = {0, 0, 0, 0};
+#pragma unroll 1
+      for (int b = 0; b < B; ++b) {
+        const f32x4 x = parks<T, BM>() ? Raw4<T>::cvt(park[b * 256 + tid])
+                                         : ld4<T>(base + b * sB);
+        f32x4 dz = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int b = 0; b < BM; ++b) {
-        if (b < B) {
-          f32x4 dz = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < BM; ++k)
+          if (k < B) dz += Mc[b * B + k] * z[k];
 #pragma unroll
-          for (int k = 0; k < BM; ++k)
-            if (k < B) dz += Mc[b * B + k] * q.z[k];
-          const f32x4 x = q.raw(base, sB, b);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            fb[j] += dz[j];
-            fg[j] = fmaf(dz[j], (x[j] - mu[j]) * rs[j], fg[j]);
-          }
+        for (int j = 0; j < 4; ++j) {
+          fb[j] += dz[j];
+          fg[j] = fmaf(dz[j], (x[j] - mu[j]) * rs[j], fg[j]);
         }
       }
 #pragma unroll
@@ -753,6 +760,7 @@ __global__ __launch_bounds__(256) void spkd_bn_bwd_apply_kernel(
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ Mc, const float* __restrict__ k, OT* __restrict__ draw) {
   const int B = EX ? BM : Bdyn;
+  __shared__ typename Raw4<T>::V park[park_elems<T, BM>()];
   const int CQ = C / 4;
   const int64_t nq = P * CQ;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
@@ -769,16 +777,16 @@ __global__ __launch_bounds__(256) void spkd_bn_bwd_apply_kernel(
       k3[j] = k[2 * C + c0 + j];
     }
     const T* base = raw + p * C + c0;
-    SampleQuads<T, BM> sq;
-    sq.load(base, sB, B, sc, sh);
-#pragma unroll
-    for (int b = 0; b < BM; ++b) {
-      if (b >= B) continue;
+    f32x4 z[BM];
+    load_z<T, BM>(base, sB, B, sc, sh, z, parks<T, BM>() ? park + threadIdx.x : nullptr);
+#pragma unroll 1
+    for (int b = 0; b < B; ++b) {
+      const f32x4 x = parks<T, BM>() ? Raw4<T>::cvt(park[b * 256 + threadIdx.x])
+                                       : ld4<T>(base + b * sB);
       f32x4 dz = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < BM; ++kk)
-        if (kk < B) dz += Mc[b * B + kk] * sq.z[kk];
-      const f32x4 x = sq.raw(base, sB, b);
+        if (kk < B) dz += Mc[b * B + kk] * z[kk];
       f32x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = fmaf(k1[j], dz[j], fmaf(k2[j], x[j], k3[j]));
@@ -856,7 +864,10 @@ extern "C" int64_t clskd_bn_bwd_workspace(int32_t nblk, int32_t C) {
 
 extern "C" int32_t clskd_abf_fuse_bwd_blocks(int32_t B, int32_t F, int32_t T) {
   const int64_t npix = (int64_t)B * F * T;
-  return (int32_t)std::min<int64_t>(cdiv(npix * 16, 256), 16384);
+  // CLSKD_ABF_BWD_BLOCKS (experiments build, A/B): the grid cap — every block writes one row of
+  // BN partials and pays the slot-reduce tail, so fewer blocks trade per-thread pixels for less
+  const int cap = std::max(64, knob(KNOB_ABF_BWD_BLOCKS));
+  return (int32_t)std::min<int64_t>(cdiv(npix * 16, 256), cap);
 }
 
 extern "C" int clskd_abf_fuse_bwd(const void* x1, const void* res, int32_t B, int32_t F, int32_t T,

@@ -361,7 +361,7 @@ def test_backward_refuses_redrawn_abf_weights():
 def test_clskd_backward_mixed_precision_close_to_fp32():
     """precision='mixed' (teacher + ReviewKD activations in bf16, the bench default): the
     student's gradients stay close to the all-fp32 step's (the ReviewKD backward reads bf16
-    saved activations; the mid-channel ReviewKD gradient maps are stored bf16 too)."""
+    saved activations; gradients themselves are fp32 unless CLSKD_RKD_GRAD_BF16=1)."""
     from clskd.data import synthetic_pairs
     noisy, clean = synthetic_pairs(2, 8000, seed=23)
     X, y = torch.from_numpy(noisy).to(DEV), torch.from_numpy(clean).to(DEV)
@@ -533,6 +533,20 @@ def test_bn_bwd_against_torch(prelu):
     assert _rel(_np(db), bd.grad.numpy()) < 1e-5
     if prelu:
         assert _rel(_np(da), ad.grad.numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("N,Kp", [(2, 32), (8, 96), (16, 160), (12, 48)])
+def test_direct_weight_gather_matches_layout(N, Kp):
+    """ops.direct_weight's fp32 repack (one index gather) equals the k-major zero-padded layout
+    of the direct kernel (wd[k][n] = w[n][k], n < N; zeros beyond), bitwise."""
+    from clskd import ops
+    w = torch.randn(N, Kp, device=DEV)
+    wd = ops.direct_weight(w)
+    NP = ops.direct_np(N)
+    ref = torch.zeros(Kp, NP, device=DEV)
+    ref[:, :N] = w.t()
+    torch.cuda.synchronize()
+    assert wd.shape == ref.shape and torch.equal(wd, ref)
 
 
 def test_index_gather_jobs_matches_single_gathers():

@@ -66,6 +66,17 @@ for st in ${STEPS:-suite bench}; do
           echo "[$c] pass $pass: $(grep '^{' $O/ab_c${i}_p$pass.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["ms_per_step"], "ms, host", d["host_enqueue_ms_per_step"], "frac", r["frac"], r.get("kernel"), r.get("isolated_avg_launch_us"), "census", r.get("all_kernels_isolated", {}).get("ms_per_step"))')"
         done
       done;;
+    ab2)  # a second same-box A/B in the same call: AB2_CASES / BENCH2_ARGS (as ab)
+      IFS=';' read -ra CS <<< "$AB2_CASES"
+      for pass in 1 2 3; do
+        i=0
+        for c in "${CS[@]}"; do
+          i=$((i+1)); rc=0
+          ce=${c%%::*}; ca=""; [[ "$c" == *::* ]] && ca=${c#*::}
+          env $ce timeout -k 10 200 python $R/bench.py --no-cpu-baseline --steps 20 --warmup 5 $BENCH2_ARGS $ca > $O/ab2_c${i}_p$pass.log 2>&1 || rc=$?; ok $rc ab2
+          echo "[$c] pass $pass: $(grep '^{' $O/ab2_c${i}_p$pass.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["ms_per_step"], "ms, host", d["host_enqueue_ms_per_step"], "frac", r["frac"], r.get("kernel"), r.get("isolated_avg_launch_us"), "census", r.get("all_kernels_isolated", {}).get("ms_per_step"))')"
+        done
+      done;;
     hostprof) rc=0; timeout -k 10 300 python $R/tools/host_profile.py --steps 20 --top 60 > $O/hostprof.txt 2>&1 || rc=$?; ok $rc hostprof
       head -3 $O/hostprof.txt;;
     trace_train_exec)
