@@ -586,6 +586,17 @@ int clskd_bn_bwd_from_partials(const void* x, const void* dy, int64_t rows, int3
                                double* partial, int32_t nblk, float* kbuf, float* dgamma,
                                float* dbeta, float* dx, int32_t accumulate_dx, int32_t dtype,
                                int32_t dy_dtype, void* stream);
+/* dx == NULL (clskd_bn_bwd_from_partials, clskd_bn_bwd): coefficients only — kbuf (resp. the
+ * floats at work + nblk*C*3 doubles) receives k [3][C] with d = k0*dy + k1*x + k2, for a consumer
+ * that applies them itself (clskd_bn_bwd_conv1x1). */
+/* BatchNorm-backward apply fused with a 1x1 conv's data gradient (the ReviewKD ABF conv1,
+ * framework.py:179-182, no bias): per row, d[c] = k0[c]*dy[c] + k1[c]*x[c] + k2[c] (C = 64), then
+ * out[row][n] (+)= sum_c w[c][n] d[c] (ascending c, fp32), N in {8, 16, 32, 64}.  x: the BN input
+ * (dtype), dy: the BN output gradient (dy_dtype), both [rows][64] contiguous; w [64][N] fp32
+ * (conv1's weight [64][N][1][1]); out [rows][N] fp32; x, dy, k, out 16-byte aligned. */
+int clskd_bn_bwd_conv1x1(const void* x, int32_t dtype, const void* dy, int32_t dy_dtype,
+                         int64_t rows, int32_t C, const float* k, const float* w, int32_t N,
+                         float* out, int32_t accumulate, void* stream);
 /* g_dtype: storage type of g (CLSKD_F32 or CLSKD_BF16); out is fp32. */
 int clskd_nearest_down_sum(const void* g, int32_t B, int32_t F, int32_t T, int32_t Fr,
                            int32_t Tr, int32_t C, float* out, int32_t accumulate, int32_t g_dtype,

@@ -159,6 +159,9 @@ _BATCH_SCATTERS = os.environ.get("CLSKD_BATCH_SCATTERS", "1") == "1"  # A/B: 0 =
 # worst C3 parameter gradient vs the oracle 3.04e-3 against 3.23e-3 with fp32 maps,
 # profiles/r6_rkd_grad_bf16.txt).  CLSKD_RKD_GRAD_BF16=0: fp32 storage (A/B)
 _RKD_GRAD_BF16 = os.environ.get("CLSKD_RKD_GRAD_BF16", "1") == "1"
+# the ABF conv1 BatchNorm backward fused into conv1's data gradient (clskd_bn_bwd_conv1x1;
+# CLSKD_BN1_CONV1_FUSED=0: apply pass + the fp32 engine, A/B)
+_BN1_CONV1_FUSED = os.environ.get("CLSKD_BN1_CONV1_FUSED", "1") == "1"
 _TWMAP = {}
 
 
@@ -550,7 +553,6 @@ def review_backward(review, tape, coef_m, d_feats, acc_feats):
                  Tn, mid, w2t, None, d_xf, OutMap(Fn * Tn * mid, Tn * mid, mid))
         c1 = tp["coef1"]
         bn1 = abf.conv1[1]
-        d_x1 = _empty(tp["x1"].shape, dev)
         if abf.att_conv is not None:
             # one pass: residual path of level j+1 folded in on load, the attention-fusion
             # backward, and the conv1-BN statistics partials (no down-sum / BN-reduce passes)
@@ -561,17 +563,29 @@ def review_backward(review, tape, coef_m, d_feats, acc_feats):
             part, nblk = ops.abf_fuse_bwd(tp["x1"], tp["res"], aw, ab, c1, d_xf, dxn, dyup,
                                           dnext=dyup_next, mv1=tp["mv1"], eps=bn1.eps)
             dyup_next = dyup
-            ops.bn_bwd_from_partials(tp["x1"], dxn, c1[:mid], c1[mid:], tp["mv1"][0],
-                                     tp["mv1"][1], bn1.eps, bn1.weight, part, nblk, d_x1)
         else:
             if dyup_next is not None:  # residual path of level j+1 (nearest upsampling)
                 ops.nearest_down_sum(dyup_next, d_xf, accumulate=True)
             dxn = d_xf
             dyup_next = None
-            ops.bn_bwd(tp["x1"], dxn, c1[:mid], c1[mid:], tp["mv1"][0], tp["mv1"][1], bn1.eps,
-                       bn1.weight, None, d_x1)
+            part, nblk = None, 0
         w1 = abf.conv1[0].weight  # [mid, Cin, 1, 1]
         Cin = w1.shape[1]
+        w1m = w1.reshape(mid, Cin).float().contiguous()
+        if _BN1_CONV1_FUSED and ops.bn_bwd_conv1x1_ok(tp["x1"], dxn, w1m, d_feats[j]):
+            # conv1 BatchNorm backward applied inside conv1's data gradient: d_x1 (64 channels
+            # at the tap's resolution, fp32) never reaches HBM
+            k = ops.bn_bwd_coeffs(tp["x1"], dxn, c1[:mid], c1[mid:], tp["mv1"][0], tp["mv1"][1],
+                                  bn1.eps, bn1.weight, part, nblk)
+            ops.bn_bwd_conv1x1(tp["x1"], dxn, k, w1m, d_feats[j], accumulate=bool(acc_feats[j]))
+            continue
+        d_x1 = _empty(tp["x1"].shape, dev)
+        if part is not None:
+            ops.bn_bwd_from_partials(tp["x1"], dxn, c1[:mid], c1[mid:], tp["mv1"][0],
+                                     tp["mv1"][1], bn1.eps, bn1.weight, part, nblk, d_x1)
+        else:
+            ops.bn_bwd(tp["x1"], dxn, c1[:mid], c1[mid:], tp["mv1"][0], tp["mv1"][1], bn1.eps,
+                       bn1.weight, None, d_x1)
         w1t = _tw(("abf1_t", id(abf)), w1, lambda: ops.pack_weight(
             w1.reshape(mid, Cin).t().contiguous().unsqueeze(1).float(), mid))
         ops.conv([seg_bftc(d_x1)], [(0, 0)], Bn, Fn, Tn, Cin, w1t, None, d_feats[j],

@@ -49,8 +49,9 @@ _STUDENT_SPLIT = os.environ.get("CLSKD_STUDENT_SPLIT", "1") == "1"
 # the training step of a 'mixed' student (C3): bit 0 — weight gradients on split products
 # (csrc/wgrad_x3.hip, the default: 20.2 -> 19.0 ms per step); bit 1 — the taped forward's and the
 # backward's data-gradient fp32 convs too (measured +0.2 ms on top: the split engine displaces
-# the halo / pointwise kernels of the narrow layers).  CLSKD_TRAIN_SPLIT=0: the whole training
-# step exact (A/B, profiles/r5_train_split_ab.txt)
+# the halo / pointwise kernels of the narrow layers); bit 2 — the taped forward only (the
+# data gradients stay exact).  CLSKD_TRAIN_SPLIT=0: the whole training step exact (A/B,
+# profiles/r5_train_split_ab.txt)
 _TRAIN_SPLIT = int(os.environ.get("CLSKD_TRAIN_SPLIT", "1"))
 _SERIAL = os.environ.get("CLSKD_SERIAL_STREAMS") == "1"  # diagnostic: the whole step on one stream
 # conv_gemm8's persistent grid inside the concurrent four-stream step: 7/8 of the CUs (224 of

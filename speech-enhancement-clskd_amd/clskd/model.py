@@ -519,9 +519,9 @@ class DCCRN(nn.Module):
             tape=None, taps_only=False, mark=None, on_decoder_tap=None, gram_taps=None):
         """See _run.  compute 'f32x3' (the student in precision 'mixed'): the fp32 convs of a
         forward without a tape run as 3 x bf16 split products (CLSKD_F32X3); a taped (training)
-        forward too when train_split bit 1 is set (KnowledgeDistillation.set_precision), else on
-        the exact fp32 engines."""
-        split = self.compute == "f32x3" and (tape is None or bool(self.train_split & 2))
+        forward too when train_split bit 1 or 2 is set (KnowledgeDistillation.set_precision),
+        else on the exact fp32 engines."""
+        split = self.compute == "f32x3" and (tape is None or bool(self.train_split & 6))
         with ops.split_products(split):
             return self._run(x, train, bn_updates, spec, want_masks, on_encoder, tape, taps_only,
                              mark, on_decoder_tap, gram_taps)

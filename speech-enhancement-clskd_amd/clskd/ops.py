@@ -1401,6 +1401,57 @@ def bn_bwd_from_partials(x, dy, scale, shift, mean, var, eps, gamma, partial, nb
     return dx
 
 
+def bn_bwd_coeffs(x, dy, scale, shift, mean, var, eps, gamma, partial=None, nblk=0):
+    """The BatchNorm-backward coefficients k [3][C] (d = k0*dy + k1*x + k2) without the apply
+    pass: from a fused producer's partials (clskd_bn_bwd_from_partials with dx NULL), else by
+    the reduce + finalize of clskd_bn_bwd (dx NULL)."""
+    L = lib()
+    Cn = x.shape[-1]
+    rows = x.numel() // Cn
+    if partial is not None:
+        kbuf = torch.empty(3 * Cn, dtype=torch.float32, device=x.device)
+        check(L.clskd_bn_bwd_from_partials(ptr(x), ptr(dy), rows, Cn, ptr(scale), ptr(shift),
+                                           ptr(mean), ptr(var), eps, ptr(gamma), ptr(partial),
+                                           nblk, ptr(kbuf), None, None, None, 0, _dt(x), _dt(dy),
+                                           _stream()), "bn_bwd_coeffs")
+        return kbuf
+    assert dy.dtype == torch.float32, dy.dtype
+    nb = int(L.clskd_bn_bwd_blocks(rows, Cn))
+    work = torch.empty(int(L.clskd_bn_bwd_workspace(nb, Cn)), dtype=torch.float64, device=x.device)
+    check(L.clskd_bn_bwd(ptr(x), ptr(dy), rows, Cn, ptr(scale), ptr(shift), ptr(mean), ptr(var), eps,
+                         ptr(gamma), None, ptr(work), nb, None, None, None, None, 0, 0, _dt(x),
+                         _stream()), "bn_bwd_coeffs")
+    return work.view(torch.float32)[nb * Cn * 6:nb * Cn * 6 + 3 * Cn]
+
+
+def bn_bwd_conv1x1_ok(x, dy, w, out):
+    C = x.shape[-1]
+    N = w.shape[1]
+    return (C == 64 and N in (8, 16, 32, 64) and x.is_contiguous() and dy.is_contiguous()
+            and w.is_contiguous() and w.dtype == torch.float32 and out.dtype == torch.float32
+            and out.is_contiguous() and out.numel() == x.numel() // C * N
+            and all(t.data_ptr() % 16 == 0 for t in (x, dy, out)))
+
+
+def bn_bwd_conv1x1(x, dy, k, w, out, accumulate=False):
+    """out [rows][N] (+)= (k0*dy + k1*x + k2) @ w [64][N]: a BatchNorm-backward apply fused with
+    the 1x1 conv's data gradient (clskd_bn_bwd_conv1x1)."""
+    C = x.shape[-1]
+    rows = x.numel() // C
+    assert k.data_ptr() % 16 == 0 and k.numel() >= 3 * C
+    check(lib().clskd_bn_bwd_conv1x1(ptr(x), _dt(x), ptr(dy), _dt(dy), rows, C, ptr(k), ptr(w),
+                                     w.shape[1], ptr(out), int(bool(accumulate)), _stream()),
+          "bn_bwd_conv1x1")
+    if KernelTimer.active:  # algorithmic bytes: x, dy, out (read + write when accumulating)
+        n = w.shape[1]
+        tn = lambda e: "bf16" if e == 2 else "float"
+        KernelTimer.note_work(f"bn_bwd_conv1x1_kernel<{tn(x.element_size())},"
+                              f"{tn(dy.element_size())},{n}>",
+                              rows * (C * (x.element_size() + dy.element_size())
+                                      + n * 4 * (2 if accumulate else 1)))
+    return out
+
+
 def nearest_down_sum(g, out, accumulate=False):
     B, F, T, Cn = g.shape
     _, Fr, Tr, _ = out.shape

@@ -803,6 +803,66 @@ __global__ __launch_bounds__(256) void spkd_bn_bwd_apply_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// ABF conv1 BatchNorm backward apply fused with conv1's data gradient (framework.py:179-182:
+// conv1 = 1x1 Cin -> 64, no bias).  Per row: d[c] = k0[c]*dy[c] + k1[c]*x[c] + k2[c] (the
+// bn_bwd_apply of a finalize's coefficients, no PReLU), then out[n] (+)= sum_c w[c][n] * d[c] in
+// ascending c — the 64-channel gradient d never reaches HBM (the two-pass form wrote and re-read
+// it in fp32: 2 x rows x 256 B).  TPR = N / 8 threads per row, each owning 8 output channels;
+// every operand of a row is loaded before use; coefficients and weights broadcast from LDS.
+// ------------------------------------------------------------------------------------------
+template <typename XT, typename GT, int N>
+__global__ __launch_bounds__(256) void bn_bwd_conv1x1_kernel(
+    const XT* __restrict__ x, const GT* __restrict__ dy, int64_t rows, const float* __restrict__ k,
+    const float* __restrict__ w, float* __restrict__ out, int accumulate) {
+  constexpr int C = 64;
+  constexpr int TPR = N / 8;
+  constexpr int RPP = 256 / TPR;  // rows per block pass
+  __shared__ __attribute__((aligned(16))) float kl[3 * C];
+  __shared__ __attribute__((aligned(16))) float wl[C * N];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 3 * C; i += 256) kl[i] = k[i];
+  for (int i = tid; i < C * N; i += 256) wl[i] = w[i];
+  __syncthreads();
+  const int cg = tid % TPR, rg = tid / TPR;
+  const int n0 = cg * 8;
+  // 8 channels per step (one 16-B bf16 / two 16-B fp32 loads per operand), two steps' loads in
+  // flight: few registers, full occupancy (the whole row held at once spilled)
+  for (int64_t m = (int64_t)blockIdx.x * RPP + rg; m < rows; m += (int64_t)gridDim.x * RPP) {
+    f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
+    const XT* xrow = x + m * C;
+    const GT* grow = dy + m * C;
+#pragma unroll 2
+    for (int c8 = 0; c8 < C; c8 += 8) {
+      const f32x4 xa = Raw4<XT>::cvt(Raw4<XT>::ld(xrow + c8));
+      const f32x4 xb = Raw4<XT>::cvt(Raw4<XT>::ld(xrow + c8 + 4));
+      const f32x4 ga = Raw4<GT>::cvt(Raw4<GT>::ld(grow + c8));
+      const f32x4 gb = Raw4<GT>::cvt(Raw4<GT>::ld(grow + c8 + 4));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c8 + j;
+        const float xv = j < 4 ? xa[j & 3] : xb[j & 3];
+        const float gv = j < 4 ? ga[j & 3] : gb[j & 3];
+        const float dv = fmaf(kl[c], gv, fmaf(kl[C + c], xv, kl[2 * C + c]));
+        const f32x4 wa = *reinterpret_cast<const f32x4*>(&wl[c * N + n0]);
+        const f32x4 wb = *reinterpret_cast<const f32x4*>(&wl[c * N + n0 + 4]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o0[e] = fmaf(dv, wa[e], o0[e]);
+          o1[e] = fmaf(dv, wb[e], o1[e]);
+        }
+      }
+    }
+    float* op = out + m * N + n0;
+    if (accumulate) {
+      o0 += *reinterpret_cast<const f32x4*>(op);
+      o1 += *reinterpret_cast<const f32x4*>(op + 4);
+    }
+    *reinterpret_cast<f32x4*>(op) = o0;
+    *reinterpret_cast<f32x4*>(op + 4) = o1;
+  }
+}
+
 inline unsigned grid_of(int64_t n, int64_t cap = 8192) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n, 256), cap));
 }
@@ -822,7 +882,7 @@ extern "C" int clskd_bn_bwd(const void* x, const float* dy, int64_t rows, int32_
                             double* work, int32_t nblk, float* dgamma, float* dbeta,
                             float* dalpha, float* dx, int32_t accumulate_dx,
                             int32_t accumulate_params, int32_t dtype, void* stream) {
-  CLSKD_CHECK_ARG(x && dy && scale && shift && mean && var && work && dx, "bn_bwd: null pointer");
+  CLSKD_CHECK_ARG(x && dy && scale && shift && mean && var && work, "bn_bwd: null pointer");
   CLSKD_CHECK_SHAPE(rows > 0 && C >= 4 && C % 4 == 0 && C <= 1024 && nblk >= 1,
                     "bn_bwd: rows=%lld C=%d nblk=%d", (long long)rows, C, nblk);
   CLSKD_CHECK_ARG(dtype == CLSKD_F32 || dtype == CLSKD_BF16, "bn_bwd: dtype");
@@ -847,6 +907,10 @@ extern "C" int clskd_bn_bwd(const void* x, const float* dy, int64_t rows, int32_
   if (alpha && dalpha)
     hipLaunchKernelGGL(bn_bwd_alpha_kernel, dim3(1), dim3(64), 0, st, apart, C, dalpha,
                        accumulate_params);
+  if (!dx) {  // coefficients only (k at work + nblk*C*3 doubles): the apply runs in a consumer
+    CLSKD_LAUNCH_CHECK("bn_bwd");
+    return CLSKD_OK;
+  }
   const int64_t nq = rows * C / 4;
   if (dtype == CLSKD_BF16)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<__bf16>, dim3(grid_of(nq)), dim3(256), 0, st,
@@ -904,6 +968,47 @@ extern "C" int clskd_abf_fuse_bwd(const void* x1, const void* res, int32_t B, in
   return CLSKD_OK;
 }
 
+extern "C" int clskd_bn_bwd_conv1x1(const void* x, int32_t dtype, const void* dy,
+                                    int32_t dy_dtype, int64_t rows, int32_t C, const float* k,
+                                    const float* w, int32_t N, float* out, int32_t accumulate,
+                                    void* stream) {
+  CLSKD_CHECK_ARG(x && dy && k && w && out, "bn_bwd_conv1x1: null pointer");
+  CLSKD_CHECK_SHAPE(C == 64 && (N == 8 || N == 16 || N == 32 || N == 64) && rows > 0,
+                    "bn_bwd_conv1x1: C=%d (64) N=%d (8/16/32/64)", C, N);
+  CLSKD_CHECK_ARG((dtype == CLSKD_F32 || dtype == CLSKD_BF16) &&
+                      (dy_dtype == CLSKD_F32 || dy_dtype == CLSKD_BF16),
+                  "bn_bwd_conv1x1: dtype");
+  CLSKD_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 &&
+                      ((uintptr_t)out & 15) == 0 && ((uintptr_t)k & 15) == 0,
+                  "bn_bwd_conv1x1: x, dy, k, out must be 16-byte aligned");
+  hipStream_t st = as_stream(stream);
+  const int rpp = 256 / (N / 8);
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(rows, rpp), 4096));
+#define BC1_N(XT_, GT_)                                                                           \
+  do {                                                                                            \
+    if (N == 8)                                                                                   \
+      hipLaunchKernelGGL((bn_bwd_conv1x1_kernel<XT_, GT_, 8>), dim3(grid), dim3(256), 0, st,     \
+                         (const XT_*)x, (const GT_*)dy, rows, k, w, out, accumulate);             \
+    else if (N == 16)                                                                             \
+      hipLaunchKernelGGL((bn_bwd_conv1x1_kernel<XT_, GT_, 16>), dim3(grid), dim3(256), 0, st,    \
+                         (const XT_*)x, (const GT_*)dy, rows, k, w, out, accumulate);             \
+    else if (N == 32)                                                                             \
+      hipLaunchKernelGGL((bn_bwd_conv1x1_kernel<XT_, GT_, 32>), dim3(grid), dim3(256), 0, st,    \
+                         (const XT_*)x, (const GT_*)dy, rows, k, w, out, accumulate);             \
+    else                                                                                          \
+      hipLaunchKernelGGL((bn_bwd_conv1x1_kernel<XT_, GT_, 64>), dim3(grid), dim3(256), 0, st,    \
+                         (const XT_*)x, (const GT_*)dy, rows, k, w, out, accumulate);             \
+  } while (0)
+  if (dtype == CLSKD_BF16) {
+    if (dy_dtype == CLSKD_BF16) BC1_N(__bf16, __bf16); else BC1_N(__bf16, float);
+  } else {
+    if (dy_dtype == CLSKD_BF16) BC1_N(float, __bf16); else BC1_N(float, float);
+  }
+#undef BC1_N
+  CLSKD_LAUNCH_CHECK("bn_bwd_conv1x1");
+  return CLSKD_OK;
+}
+
 extern "C" int clskd_bn_bwd_from_partials(const void* x, const void* dy, int64_t rows, int32_t C,
                                           const float* scale, const float* shift,
                                           const float* mean, const float* var, float eps,
@@ -911,7 +1016,7 @@ extern "C" int clskd_bn_bwd_from_partials(const void* x, const void* dy, int64_t
                                           float* kbuf, float* dgamma, float* dbeta, float* dx,
                                           int32_t accumulate_dx, int32_t dtype,
                                           int32_t dy_dtype, void* stream) {
-  CLSKD_CHECK_ARG(x && dy && scale && shift && mean && var && partial && kbuf && dx,
+  CLSKD_CHECK_ARG(x && dy && scale && shift && mean && var && partial && kbuf,
                   "bn_bwd_from_partials: null pointer");
   CLSKD_CHECK_ARG(dy_dtype == CLSKD_F32 || dy_dtype == CLSKD_BF16,
                   "bn_bwd_from_partials: dy_dtype must be CLSKD_F32 or CLSKD_BF16");
@@ -921,6 +1026,10 @@ extern "C" int clskd_bn_bwd_from_partials(const void* x, const void* dy, int64_t
   nblk = fold_partials(partial, nblk, 3 * C, 1, st);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, nblk, rows, C,
                      gamma, mean, var, eps, dgamma, dbeta, kbuf, nullptr, 0);
+  if (!dx) {  // coefficients only (kbuf): the apply runs fused into its consumer
+    CLSKD_LAUNCH_CHECK("bn_bwd_from_partials");
+    return CLSKD_OK;
+  }
   const int64_t nq = rows * C / 4;
 #define BN_APPLY_LAUNCH(T, GT)                                                                  \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<T, GT>), dim3(grid_of(nq)), dim3(256), 0, st,        \

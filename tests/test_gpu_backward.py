@@ -535,6 +535,54 @@ def test_bn_bwd_against_torch(prelu):
         assert _rel(_np(da), ad.grad.numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("N", [8, 16, 32, 64])
+@pytest.mark.parametrize("dts", [(torch.bfloat16, torch.bfloat16), (torch.bfloat16, torch.float32),
+                                 (torch.float32, torch.float32)])
+def test_bn_bwd_conv1x1_against_fp64(N, dts):
+    """clskd_bn_bwd_conv1x1 (ABF conv1 BatchNorm backward applied inside conv1's data gradient)
+    against fp64 torch: coefficients from the partials path and from the reduce path, overwrite
+    and accumulate; bitwise repeatable."""
+    from clskd import ops
+    xdt, gdt = dts
+    g = torch.Generator().manual_seed(N)
+    rows, C, eps = 4 * 9 * 37, 64, 1e-5
+    x = (torch.randn(rows, C, generator=g) * 1.2 + 0.1).to(xdt)
+    dy = torch.randn(rows, C, generator=g).to(gdt)
+    w = torch.randn(C, N, generator=g) * 0.1
+    gamma = torch.rand(C, generator=g) + 0.5
+    xd = x.double()
+    mean, var = xd.mean(0), xd.var(0, unbiased=False)
+    rs = 1.0 / torch.sqrt(var + eps)
+    xh = (xd - mean) * rs
+    dd = dy.double()
+    dx = gamma.double() * rs * (dd - dd.mean(0) - xh * (dd * xh).mean(0))
+    base = torch.randn(rows, N, generator=g)
+    ref = dx @ w.double()
+    scale = (gamma / torch.sqrt(var.float() + eps)).contiguous()
+    shift = (-mean.float() * scale).contiguous()
+    X, DY = x.to(DEV).contiguous(), dy.to(DEV).contiguous()
+    args = (X, DY, scale.to(DEV), shift.to(DEV), mean.float().to(DEV), var.float().to(DEV), eps,
+            gamma.to(DEV))
+    outs = []
+    for rep in range(2):
+        if gdt == torch.float32:
+            k = ops.bn_bwd_coeffs(*args)
+        else:  # partials of the fused producer's layout: {sum dy, sum dy*xhat, 0} per block
+            part = torch.zeros(1, C, 3, dtype=torch.float64)
+            part[0, :, 0] = dd.sum(0)
+            part[0, :, 1] = (dd * xh).sum(0)
+            k = ops.bn_bwd_coeffs(*args, partial=part.reshape(-1).to(DEV), nblk=1)
+        o1 = torch.empty(rows, N, device=DEV)
+        ops.bn_bwd_conv1x1(X, DY, k, w.to(DEV), o1)
+        o2 = base.to(DEV).clone()
+        ops.bn_bwd_conv1x1(X, DY, k, w.to(DEV), o2, accumulate=True)
+        outs.append((o1, o2))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert _rel(_np(outs[0][0]), ref.numpy()) < 2e-5
+    assert _rel(_np(outs[0][1]), (ref + base.double()).numpy()) < 2e-5
+
+
 @pytest.mark.parametrize("N,Kp", [(2, 32), (8, 96), (16, 160), (12, 48)])
 def test_direct_weight_gather_matches_layout(N, Kp):
     """ops.direct_weight's fp32 repack (one index gather) equals the k-major zero-padded layout
