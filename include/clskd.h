@@ -131,9 +131,10 @@ typedef struct {
   int32_t seg_c[CLSKD_MAX_SEGS];
   int16_t tap_df[16];
   int16_t tap_dt[16];
-  /* 1: out += result (read-modify-write, fp32 `out`, fp32 compute, no statistics: the fp32 MFMA
-     engines with wlayout NK, or the direct kernel with wlayout DIRECT for narrow N / short K) —
-     lets several data-gradient contributions of one tensor sum in place. */
+  /* 1: out += result (read-modify-write, fp32 `out`, no statistics: the fp32 MFMA engines with
+     wlayout NK, the direct kernel with wlayout DIRECT for narrow N / short K, or — bf16 compute —
+     the bf16 LDS-DMA engine) — lets several data-gradient contributions of one tensor sum in
+     place. */
   int32_t accumulate;
   int32_t reserved_;
   /* Optional folded BatchNorm finalize (HOST pointer, read at launch; NULL = none): the launch
@@ -597,6 +598,15 @@ int clskd_bn_bwd_from_partials(const void* x, const void* dy, int64_t rows, int3
 int clskd_bn_bwd_conv1x1(const void* x, int32_t dtype, const void* dy, int32_t dy_dtype,
                          int64_t rows, int32_t C, const float* k, const float* w, int32_t N,
                          float* out, int32_t accumulate, void* stream);
+/* Split-product data gradients on the bf16 engines (round 6): clskd_split_planes writes an fp32
+ * map [rows][C] as bf16 planes [rows][2C] (hi = bf16(x) in channels [0, C), lo = bf16(x - hi) in
+ * [C, 2C)); clskd_pack_split3 turns a packed fp32 weight [N][ntaps*C] (K order tap, channel) into
+ * the bf16 weight [N][Kp] (Kp = ntaps*3C padded to 64) of the two-segment K table (tap, [planes
+ * 2C | planes' hi C], channel): per tap [W_hi | W_hi | W_lo], so one bf16 implicit GEMM sums
+ * hi*W_hi + lo*W_hi + hi*W_lo — the CLSKD_F32X3 split product as three K segments. */
+int clskd_split_planes(const float* src, int64_t rows, int32_t C, void* dst, void* stream);
+int clskd_pack_split3(const float* w, int32_t N, int32_t ldw, int32_t ntaps, int32_t C, int32_t Kp,
+                      void* out, void* stream);
 /* g_dtype: storage type of g (CLSKD_F32 or CLSKD_BF16); out is fp32. */
 int clskd_nearest_down_sum(const void* g, int32_t B, int32_t F, int32_t T, int32_t Fr,
                            int32_t Tr, int32_t C, float* out, int32_t accumulate, int32_t g_dtype,

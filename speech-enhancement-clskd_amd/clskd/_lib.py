@@ -197,6 +197,8 @@ SIGNATURES = {
     "clskd_nearest_down_sum": (_i32, [_p, _i32, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32,
                                       _p]),
     "clskd_bn_bwd_conv1x1": (_i32, [_p, _i32, _p, _i32, _i64, _i32, _p, _p, _i32, _p, _i32, _p]),
+    "clskd_split_planes": (_i32, [_p, _i64, _i32, _p, _p]),
+    "clskd_pack_split3": (_i32, [_p, _i32, _i32, _i32, _i32, _i32, _p, _p]),
     "clskd_mask_e_bwd": (_i32, [_p, _i32, _p, _i32, _i32, _i32, _p, _i32, _p, _p]),
     "clskd_ola_bwd": (_i32, [_p, _p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p]),
     "clskd_frame_pad_bwd": (_i32, [_p, _i32, _i32, _i32, _i32, _i32, _p, _i64, _i32, _p]),

@@ -162,7 +162,34 @@ _RKD_GRAD_BF16 = os.environ.get("CLSKD_RKD_GRAD_BF16", "1") == "1"
 # the ABF conv1 BatchNorm backward fused into conv1's data gradient (clskd_bn_bwd_conv1x1;
 # CLSKD_BN1_CONV1_FUSED=0: apply pass + the fp32 engine, A/B)
 _BN1_CONV1_FUSED = os.environ.get("CLSKD_BN1_CONV1_FUSED", "1") == "1"
+# split-product data gradients on the bf16 LDS-DMA engine (round 6): the raw-output gradient as
+# bf16 hi / lo planes, the transposed weight tripled [W_hi | W_hi | W_lo] per tap (CLSKD_DGRAD_PLANES)
+_DGRAD_PLANES = os.environ.get("CLSKD_DGRAD_PLANES", "1") == "1"
 _TWMAP = {}
+
+
+def _planes_of(draw, geom):
+    """draw [..][C] fp32 (channel-contiguous rows) -> (bf16 planes [..][2C], the two segments of
+    the split K table: planes (hi | lo) and planes' hi half), or None when not eligible."""
+    C = geom.C
+    if not (_DGRAD_PLANES and C % 32 == 0 and draw.dtype == f32 and draw.is_contiguous()
+            and geom.sT == C and draw.data_ptr() % 16 == 0):
+        return None
+    planes = torch.empty(draw.shape[:-1] + (2 * C,), dtype=torch.bfloat16, device=draw.device)
+    ops.split_planes(draw, planes)
+    g2 = SegGeom(2 * C, geom.sB * 2, geom.sF * 2, geom.sT * 2, geom.F, geom.T)
+    g1 = SegGeom(C, geom.sB * 2, geom.sF * 2, geom.sT * 2, geom.F, geom.T)
+    return planes, [Seg(planes, 0, g2), Seg(planes, 0, g1)]
+
+
+def _split3_weight(wt, ntaps, C):
+    """Packed fp32 data-gradient weight [N][ntaps*C (+pad)] -> bf16 [N][Kp] of the planes' K
+    table (per tap [W_hi | W_hi | W_lo], Kp = ntaps*3C padded to 64)."""
+    N = wt.shape[0]
+    Kp = -(-ntaps * 3 * C // 64) * 64
+    out = torch.empty(N, Kp, dtype=torch.bfloat16, device=wt.device)
+    ops.pack_split3(wt, ntaps, C, out)
+    return out
 
 
 def _tw_build(key, src, build):
@@ -267,8 +294,11 @@ def dccrn_backward(m, tape, enc, dec, dec_in, lstm_io, g, pg, acc_params=False, 
         wt = _tw(("istft_t", id(m)), winv,
                  lambda: ops.pack_weight(winv[:, :516].t().contiguous().unsqueeze(1), 400))
         dest = _empty((B, T, 516), dev)
-        ops.conv([Seg(dframes, 0, SegGeom(400, T * 400, 0, 400, 1, T))], [(0, 0)], B, 1, T, 516, wt,
-                 None, dest, OutMap(T * 516, 0, 516), mfma_only=True)
+        # (N = 516 on the exact engine: split products with the planes' data gradients)
+        with ops.split_products(_DGRAD_PLANES and getattr(m, "compute", "fp32") == "f32x3",
+                                wgrad=getattr(ops._SPLIT, "wgrad", False)):
+            ops.conv([Seg(dframes, 0, SegGeom(400, T * 400, 0, 400, 1, T))], [(0, 0)], B, 1, T, 516,
+                     wt, None, dest, OutMap(T * 516, 0, 516), mfma_only=True)
         dmask = _empty(dec[-1].shape, dev)
         ops.mask_e_bwd(tape["spec"], dec[-1], T, dest, dmask)
 
@@ -316,12 +346,19 @@ def dccrn_backward(m, tape, enc, dec, dec_in, lstm_io, g, pg, acc_params=False, 
             join()
             join = None
         # data gradients: one stride-2 gather over the raw-output gradient, per destination
-        dseg = Seg(draw, 0, SegGeom(Co, 2 * F * (T + 1) * Co, (T + 1) * Co, Co, 2 * F, T + 1))
+        dgeom = SegGeom(Co, 2 * F * (T + 1) * Co, (T + 1) * Co, Co, 2 * F, T + 1)
+        dseg = Seg(draw, 0, dgeom)
         taps_b = [(p - 2 * dF, kt) for p in (0, 1) for _, dF in DCCRN._DEC_TAPS[p] for kt in (0, 1)]
+        pl = _planes_of(draw, dgeom)
         for s0, Cs, dst, t0, Tt in ((0, Cof, g["dec_in"] if d == 0 else g["dec"][d - 1], out_t0,
                                      out_t.shape[2]),
                                     (Cof, Csk, g["enc"][nl - 1 - d], 0, T)):
             wt = _tw(("dec_t", id(m), d, s0), packs[0][0], lambda: _dec_dgrad_w(packs, Ci, s0, Cs))
+            if pl is not None:  # split products on the bf16 engine
+                ops.conv(pl[1], taps_b, B, F, T, Cs, _split3_weight(wt, len(taps_b), Co), None, dst,
+                         OutMap(F * Tt * Cs, Tt * Cs, Cs), out_offset=t0 * Cs, stride_f=2,
+                         accumulate=True)
+                continue
             ops.conv([dseg], taps_b, B, F, T, Cs, wt, None, dst, OutMap(F * Tt * Cs, Tt * Cs, Cs),
                      out_offset=t0 * Cs, stride_f=2, accumulate=True)
 
@@ -451,7 +488,9 @@ def dccrn_backward(m, tape, enc, dec, dec_in, lstm_io, g, pg, acc_params=False, 
         _scatter(db, bmaps, [pg.get(cc.real_conv.bias), pg.get(cc.imag_conv.bias)], acc_params)
         if i == 0:
             continue
-        dseg = Seg(draw, 0, SegGeom(Co, Fo * T * Co, T * Co, Co, Fo, T))
+        dgeom = SegGeom(Co, Fo * T * Co, T * Co, Co, Fo, T)
+        dseg = Seg(draw, 0, dgeom)
+        pl = _planes_of(draw, dgeom)
         for p in (0, 1):
             kfs = [kf for kf in range(5) if kf % 2 == p]
             taps_b = [((p - kf + 2) // 2, 1 - kt) for kf in kfs for kt in range(2)]
@@ -460,6 +499,11 @@ def dccrn_backward(m, tape, enc, dec, dec_in, lstm_io, g, pg, acc_params=False, 
             wt = _tw(("enc_t", id(m), i, p), wp, lambda: ops.pack_weight(
                 wp[:, :10 * Ci].reshape(Co, 5, 2, Ci)[:, p::2].permute(3, 1, 2, 0)
                 .reshape(Ci, len(kfs) * 2, Co).contiguous(), len(kfs) * 2 * Co))
+            if pl is not None:  # split products on the bf16 engine
+                ops.conv(pl[1], taps_b, B, Fo, T, Ci, _split3_weight(wt, len(taps_b), Co), None,
+                         g["enc"][i - 1], OutMap(2 * Fo * T * Ci, T * Ci, Ci, of_mul=2, of_add=p),
+                         accumulate=True)
+                continue
             ops.conv([dseg], taps_b, B, Fo, T, Ci, wt, None, g["enc"][i - 1],
                      OutMap(2 * Fo * T * Ci, T * Ci, Ci, of_mul=2, of_add=p), accumulate=True)
 
@@ -678,7 +722,12 @@ def clskd_backward(res, student, review_encoder, review_decoder, pg, acc_params=
         review_backward(review_encoder, tp["re"], [M[n - 1 - j] for j in range(n)],
                         [g["enc"][n - 1 - j] for j in range(n)], [False] * n)
     # MRSTFT log-magnitude base loss (distill.py:100-101) -> d student waveform
-    mrstft_backward(tp["ms"], g["wav"], upstream)
+    # the spectrum gradient's frame GEMM (N = hop, K = taps x 516: 23 TF/s on the exact engine,
+    # at the head of the waveform tail every student gradient waits for) on split products when
+    # the data gradients are (CLSKD_DGRAD_PLANES with a 'mixed' student)
+    with ops.split_products(_DGRAD_PLANES and getattr(student, "compute", "fp32") == "f32x3",
+                            wgrad=getattr(ops._SPLIT, "wgrad", False)):
+        mrstft_backward(tp["ms"], g["wav"], upstream)
 
     def join():
         main.wait_stream(s_dec)

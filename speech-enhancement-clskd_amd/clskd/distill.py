@@ -52,7 +52,9 @@ _STUDENT_SPLIT = os.environ.get("CLSKD_STUDENT_SPLIT", "1") == "1"
 # the halo / pointwise kernels of the narrow layers); bit 2 — the taped forward only (the
 # data gradients stay exact).  CLSKD_TRAIN_SPLIT=0: the whole training step exact (A/B,
 # profiles/r5_train_split_ab.txt)
-_TRAIN_SPLIT = int(os.environ.get("CLSKD_TRAIN_SPLIT", "1"))
+# default 5 = weight gradients + the taped forward (round 6: 14.93-15.04 -> 14.74-14.87 ms,
+# profiles/r6_train_split_ab.txt); 1 = weight gradients only
+_TRAIN_SPLIT = int(os.environ.get("CLSKD_TRAIN_SPLIT", "5"))
 _SERIAL = os.environ.get("CLSKD_SERIAL_STREAMS") == "1"  # diagnostic: the whole step on one stream
 # conv_gemm8's persistent grid inside the concurrent four-stream step: 7/8 of the CUs (224 of
 # 256), so the wide teacher / ReviewKD GEMMs leave a CU per XCD group to the other streams'

@@ -1334,6 +1334,14 @@ def conv_wgrad(segs, taps, B, Fo, To, N, dy, omap, dw, dbias=None, dy_offset=0, 
     check(lib().clskd_conv2d_wgrad(d, dy.data_ptr() + 4 * dy_offset, ptr(dw), ptr(dbias), ptr(work),
                                    ws, int(bool(accumulate)) | (int(bool(acc_b)) << 1), _stream()),
           "conv2d_wgrad")
+    if KernelTimer.active and split:  # the split engine names its instance (conv_wgrad_x3<...>)
+        name = lib().clskd_conv_last_kernel().decode()
+        if name.startswith("conv_wgrad_x3"):
+            K = sum(len(taps) * g.C for g in geoms)
+            # algorithmic work: the GEMM's fp32-equivalent FLOPs; bytes: every operand once
+            KernelTimer.note_work(name, 4 * (sum(B * g.F * g.T * g.C for g in geoms)
+                                             + B * Fo * To * N + N * Kp),
+                                  2.0 * B * Fo * To * N * K)
     return dw
 
 
@@ -1450,6 +1458,22 @@ def bn_bwd_conv1x1(x, dy, k, w, out, accumulate=False):
                               rows * (C * (x.element_size() + dy.element_size())
                                       + n * 4 * (2 if accumulate else 1)))
     return out
+
+
+def split_planes(x, planes):
+    """fp32 [..][C] -> bf16 planes [..][2C]: hi = bf16(x) | lo = bf16(x - hi) (clskd_split_planes)."""
+    C = x.shape[-1]
+    assert planes.shape[-1] == 2 * C and planes.dtype == torch.bfloat16 and x.is_contiguous()
+    check(lib().clskd_split_planes(ptr(x), x.numel() // C, C, ptr(planes), _stream()),
+          "split_planes")
+
+
+def pack_split3(w, ntaps, C, out):
+    """fp32 [N][ldw] (K order tap, channel) -> bf16 [N][Kp]: per tap [W_hi | W_hi | W_lo]."""
+    N, ldw = w.shape
+    assert w.dtype == torch.float32 and w.is_contiguous() and out.dtype == torch.bfloat16
+    check(lib().clskd_pack_split3(ptr(w), N, ldw, ntaps, C, out.shape[1], ptr(out), _stream()),
+          "pack_split3")
 
 
 def nearest_down_sum(g, out, accumulate=False):

@@ -379,8 +379,16 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
       const int rr = q / CPRW, cc = q % CPRW;
       const int64_t ro = out_row[wm * WR + rr];
       const int n = n0 + wn * WC + cc * CH;
-      if (q < WR * CPRW && ro >= 0 && n < d.N)
-        *reinterpret_cast<uint4*>(out + ro + n) = *reinterpret_cast<const uint4*>(wt + rr * WC + cc * CH);
+      if (q < WR * CPRW && ro >= 0 && n < d.N) {
+        uint4 v = *reinterpret_cast<const uint4*>(wt + rr * WC + cc * CH);
+        if constexpr (sizeof(OutT) == 4) {
+          if (d.accumulate) {  // data-gradient sums (fp32 out): out += conv
+            const f32x4 o = *reinterpret_cast<const f32x4*>(out + ro + n);
+            v = __builtin_bit_cast(uint4, __builtin_bit_cast(f32x4, v) + o);
+          }
+        }
+        *reinterpret_cast<uint4*>(out + ro + n) = v;
+      }
     }
     return;
   }
@@ -395,7 +403,12 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_bf16_dma(const ConvArgsV2 
       for (int r = 0; r < 16; ++r) {
         const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int64_t ro = out_row[row];
-        if (DBG != 3 && ro >= 0) store_out<OutT>(out + ro + coff, acc[i][j][r]);
+        if (DBG != 3 && ro >= 0) {
+          float v = acc[i][j][r];
+          if constexpr (sizeof(OutT) == 4)
+            if (d.accumulate) v += reinterpret_cast<const float*>(out)[ro + coff];
+          store_out<OutT>(out + ro + coff, v);
+        }
       }
     }
   }
@@ -463,6 +476,13 @@ int launch_conv_halow(const clskd_conv_desc& d, hipStream_t st, bool* launched);
 
 int launch_conv_bf16(const clskd_conv_desc& d, hipStream_t st) {
   const bool no_halo = knob(KNOB_NO_HALO) == 1;  // A/B switch: 1 keeps narrow layers on the engine
+  // accumulating launches (fp32 out += conv: the split-product data gradients over bf16 hi / lo
+  // planes) run the LDS-DMA engine, the one with the read-add-write epilogue
+  if (d.accumulate) {
+    CLSKD_CHECK_ARG(d.out_dtype == CLSKD_F32 && !d.stats && !d.bn_fold && d.in_dtype == CLSKD_BF16,
+                    "conv2d(bf16): accumulate needs an fp32 output, bf16 operands, no statistics");
+    return launch_nw<8, 3>(d, st);
+  }
   if (!no_halo) {
     bool launched = false;
     const int rc = launch_conv_halo(d, st, &launched);

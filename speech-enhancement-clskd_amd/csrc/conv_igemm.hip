@@ -437,9 +437,10 @@ extern "C" int clskd_conv2d_fwd(const clskd_conv_desc* dp, void* stream) {
                     "conv2d: kvec=%d", d.kvec);
   CLSKD_CHECK_ARG(d.wlayout == CLSKD_WLAYOUT_NK || d.wlayout == CLSKD_WLAYOUT_DIRECT,
                   "conv2d: wlayout=%d", d.wlayout);
-  CLSKD_CHECK_ARG(!d.accumulate || (d.compute == CLSKD_F32 && d.out_dtype == CLSKD_F32),
-                  "conv2d: accumulate needs fp32 compute and an fp32 output (the fp32 engines or "
-                  "the direct kernel)");
+  CLSKD_CHECK_ARG(!d.accumulate || ((d.compute == CLSKD_F32 || d.compute == CLSKD_BF16) &&
+                                     d.out_dtype == CLSKD_F32),
+                  "conv2d: accumulate needs fp32 or bf16 compute and an fp32 output (the fp32 "
+                  "engines, the direct kernel, the bf16 LDS-DMA engine)");
   if (d.wlayout == CLSKD_WLAYOUT_DIRECT) {
     if (skip_kernel(SKIP_CONV_DIRECT)) return CLSKD_OK;
     const int rc = launch_conv_direct(d, st);

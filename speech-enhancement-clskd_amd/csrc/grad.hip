@@ -461,3 +461,84 @@ extern "C" int clskd_axpy_f32(const float* x, float* y, int64_t n, float alpha, 
   CLSKD_LAUNCH_CHECK("axpy_f32");
   return CLSKD_OK;
 }
+
+// ------------------------------------------------------------------------------------------
+// Split-product data gradients on the bf16 engines (include/clskd.h, clskd_split_planes /
+// clskd_pack_split3).  x = hi + lo + r with hi = bf16_rne(x), lo = bf16_rne(x - hi) (x - hi exact
+// in fp32), |r| <= 2^-18 |x| — the split of the CLSKD_F32X3 engines (conv_split.hip), here
+// materialised once so the LDS-DMA bf16 engine stages it like any bf16 map.
+// ------------------------------------------------------------------------------------------
+namespace clskd {
+
+__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ src,
+                                                           int64_t rows, int C,
+                                                           __bf16* __restrict__ dst) {
+  const int CQ = C / 4;
+  const int64_t nq = rows * CQ;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = q / CQ;
+    const int c = (int)(q - r * CQ) * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(src + r * C + c);
+    bf16x4 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      hi[j] = (__bf16)v[j];
+      lo[j] = (__bf16)(v[j] - (float)hi[j]);
+    }
+    *reinterpret_cast<bf16x4*>(dst + r * 2 * C + c) = hi;
+    *reinterpret_cast<bf16x4*>(dst + r * 2 * C + C + c) = lo;
+  }
+}
+
+// out[n][t*3C + s*C + c] = {hi, hi, lo}[s] of w[n][t*C + c]; zero for k >= ntaps*3C
+__global__ __launch_bounds__(256) void pack_split3_kernel(const float* __restrict__ w, int N,
+                                                          int ldw, int ntaps, int C, int Kp,
+                                                          __bf16* __restrict__ out) {
+  const int64_t total = (int64_t)N * Kp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int n = (int)(i / Kp);
+    const int k = (int)(i - (int64_t)n * Kp);
+    float v = 0.f;
+    int part = 0;
+    if (k < ntaps * 3 * C) {
+      const int t = k / (3 * C);
+      const int r = k - t * 3 * C;
+      part = r / C;
+      v = w[(int64_t)n * ldw + t * C + (r - part * C)];
+    }
+    const __bf16 hi = (__bf16)v;
+    out[i] = part == 2 ? (__bf16)(v - (float)hi) : hi;
+  }
+}
+
+}  // namespace clskd
+
+extern "C" int clskd_split_planes(const float* src, int64_t rows, int32_t C, void* dst,
+                                  void* stream) {
+  CLSKD_CHECK_ARG(src && dst, "split_planes: null pointer");
+  CLSKD_CHECK_SHAPE(rows >= 0 && C > 0 && C % 4 == 0, "split_planes: C=%d must be a multiple of 4", C);
+  CLSKD_CHECK_ARG(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 7) == 0,
+                  "split_planes: src 16-B / dst 8-B alignment");
+  const int64_t nq = rows * (C / 4);
+  if (nq == 0) return CLSKD_OK;
+  hipLaunchKernelGGL(clskd::split_planes_kernel, dim3(clskd::grid_for(nq)), dim3(256), 0,
+                     clskd::as_stream(stream), src, rows, C, reinterpret_cast<__bf16*>(dst));
+  CLSKD_LAUNCH_CHECK("split_planes");
+  return CLSKD_OK;
+}
+
+extern "C" int clskd_pack_split3(const float* w, int32_t N, int32_t ldw, int32_t ntaps, int32_t C,
+                                 int32_t Kp, void* out, void* stream) {
+  CLSKD_CHECK_ARG(w && out, "pack_split3: null pointer");
+  CLSKD_CHECK_SHAPE(N > 0 && ntaps > 0 && C > 0 && ldw >= ntaps * C && Kp >= ntaps * 3 * C &&
+                        Kp % 64 == 0,
+                    "pack_split3: N=%d ldw=%d ntaps=%d C=%d Kp=%d", N, ldw, ntaps, C, Kp);
+  const int64_t total = (int64_t)N * Kp;
+  hipLaunchKernelGGL(clskd::pack_split3_kernel, dim3(clskd::grid_for(total)), dim3(256), 0,
+                     clskd::as_stream(stream), w, N, ldw, ntaps, C, Kp,
+                     reinterpret_cast<__bf16*>(out));
+  CLSKD_LAUNCH_CHECK("pack_split3");
+  return CLSKD_OK;
+}

@@ -394,7 +394,7 @@ void launch_wgrad_x3(const clskd_conv_desc& d, const float* dy, float* work, int
     if (v) depth == 2 ? launch_x3<64, true, 2>(grid, st, a) : launch_x3<64, true, 1>(grid, st, a);
     else depth == 2 ? launch_x3<64, false, 2>(grid, st, a) : launch_x3<64, false, 1>(grid, st, a);
   }
-  note_kernel("conv_wgrad_x3<%d,%d,%d>", tn, v ? 1 : 0, depth);
+  note_kernel("conv_wgrad_x3<%d,%s,%d>", tn, v ? "true" : "false", depth);
 }
 
 }  // namespace clskd

@@ -535,6 +535,39 @@ def test_bn_bwd_against_torch(prelu):
         assert _rel(_np(da), ad.grad.numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("C,N", [(64, 64), (32, 64), (64, 32)])
+def test_split_plane_data_gradient_matches_fp32(C, N):
+    """A data-gradient conv on bf16 hi / lo planes with the tripled weight [W_hi | W_hi | W_lo]
+    (bf16 LDS-DMA engine, accumulate epilogue) against the exact fp32 engine on the same taps:
+    the split product's error (<= ~3 * 2^-18 per product) and the read-add-write."""
+    from clskd import backward as bw
+    from clskd import ops
+    from clskd.ops import OutMap, Seg, SegGeom
+    g = torch.Generator(device=DEV).manual_seed(C + N)
+    B, F, T = 2, 12, 45
+    draw = torch.randn(B, F, T, C, device=DEV, generator=g)
+    geom = SegGeom(C, F * T * C, T * C, C, F, T)
+    taps = [(dF, dT) for dF in (-1, 0, 1) for dT in (0, 1)]
+    wt = ops.pack_weight(torch.randn(N, len(taps), C, device=DEV, generator=g), len(taps) * C)
+    ref = torch.empty(B, F, T, N, device=DEV)
+    ops.conv([Seg(draw, 0, geom)], taps, B, F, T, N, wt, None, ref, OutMap(F * T * N, T * N, N))
+    base = torch.randn(B, F, T, N, device=DEV, generator=g)
+    out = base.clone()
+    prev = bw._DGRAD_PLANES
+    bw._DGRAD_PLANES = True
+    try:
+        planes, segs = bw._planes_of(draw, geom)
+        w3 = bw._split3_weight(wt, len(taps), C)
+        ops.conv(segs, taps, B, F, T, N, w3, None, out, OutMap(F * T * N, T * N, N), accumulate=True)
+    finally:
+        bw._DGRAD_PLANES = prev
+    torch.cuda.synchronize()
+    hi = draw.to(torch.bfloat16)
+    assert torch.equal(planes[..., :C], hi)
+    assert torch.equal(planes[..., C:], (draw - hi.float()).to(torch.bfloat16))
+    assert _rel(_np(out - base), _np(ref)) < 2e-5
+
+
 @pytest.mark.parametrize("N", [8, 16, 32, 64])
 @pytest.mark.parametrize("dts", [(torch.bfloat16, torch.bfloat16), (torch.bfloat16, torch.float32),
                                  (torch.float32, torch.float32)])
