@@ -165,6 +165,7 @@ _BN1_CONV1_FUSED = os.environ.get("CLSKD_BN1_CONV1_FUSED", "1") == "1"
 # split-product data gradients on the bf16 LDS-DMA engine (round 6): the raw-output gradient as
 # bf16 hi / lo planes, the transposed weight tripled [W_hi | W_hi | W_lo] per tap (CLSKD_DGRAD_PLANES)
 _DGRAD_PLANES = os.environ.get("CLSKD_DGRAD_PLANES", "1") == "1"
+_PLANES_MIN_N = int(os.environ.get("CLSKD_PLANES_MIN_N", "33"))  # narrowest output on planes
 _TWMAP = {}
 
 
@@ -349,12 +350,14 @@ def dccrn_backward(m, tape, enc, dec, dec_in, lstm_io, g, pg, acc_params=False, 
         dgeom = SegGeom(Co, 2 * F * (T + 1) * Co, (T + 1) * Co, Co, 2 * F, T + 1)
         dseg = Seg(draw, 0, dgeom)
         taps_b = [(p - 2 * dF, kt) for p in (0, 1) for _, dF in DCCRN._DEC_TAPS[p] for kt in (0, 1)]
-        pl = _planes_of(draw, dgeom)
+        # planes where a destination is wider than 32 channels (the bf16 engine's 32-wide tile
+        # loses to the exact engine: profiles/r6_planes_micro.txt)
+        pl = _planes_of(draw, dgeom) if max(Cof, Csk) >= _PLANES_MIN_N else None
         for s0, Cs, dst, t0, Tt in ((0, Cof, g["dec_in"] if d == 0 else g["dec"][d - 1], out_t0,
                                      out_t.shape[2]),
                                     (Cof, Csk, g["enc"][nl - 1 - d], 0, T)):
             wt = _tw(("dec_t", id(m), d, s0), packs[0][0], lambda: _dec_dgrad_w(packs, Ci, s0, Cs))
-            if pl is not None:  # split products on the bf16 engine
+            if pl is not None and Cs >= _PLANES_MIN_N:  # split products on the bf16 engine
                 ops.conv(pl[1], taps_b, B, F, T, Cs, _split3_weight(wt, len(taps_b), Co), None, dst,
                          OutMap(F * Tt * Cs, Tt * Cs, Cs), out_offset=t0 * Cs, stride_f=2,
                          accumulate=True)
@@ -490,7 +493,7 @@ def dccrn_backward(m, tape, enc, dec, dec_in, lstm_io, g, pg, acc_params=False, 
             continue
         dgeom = SegGeom(Co, Fo * T * Co, T * Co, Co, Fo, T)
         dseg = Seg(draw, 0, dgeom)
-        pl = _planes_of(draw, dgeom)
+        pl = _planes_of(draw, dgeom) if Ci >= _PLANES_MIN_N else None
         for p in (0, 1):
             kfs = [kf for kf in range(5) if kf % 2 == p]
             taps_b = [((p - kf + 2) // 2, 1 - kt) for kf in kfs for kt in range(2)]

@@ -43,6 +43,7 @@ struct WgradX3Args {
   int rows_per_split;
   int S;
   int want_bias;
+  int xcd;  // XCD-major work order (CLSKD_WGRAD_XCD): the k-tiles of a row chunk on one XCD
 };
 
 template <int R> struct RowVec;
@@ -104,9 +105,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(const WgradX3Args a) {
   extern __shared__ __attribute__((aligned(16))) short lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   short* const wl = lds + wave * WAVE_E;  // this wave's planes: A hi, A lo, dY hi, dY lo
-  const int split = blockIdx.x;
-  const int n0 = blockIdx.y * TN;
-  const int k0 = blockIdx.z * X3_TK;
+  // work item (row chunk, n-tile, k-tile).  The hardware deals workgroups round-robin over the
+  // eight XCDs; with a.xcd each XCD instead walks one contiguous run of work items, k-tile
+  // fastest, so the k-tiles re-reading one row chunk's dY and gathered rows share its L2
+  int split = blockIdx.x, ty = blockIdx.y, tz = blockIdx.z;
+  if (a.xcd) {
+    const int ny = gridDim.y, nz = gridDim.z;
+    const int total = gridDim.x * ny * nz;
+    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + ny * blockIdx.z);
+    const int v = xcd_tile(lin, total);
+    split = v / (ny * nz);
+    const int rem = v - split * (ny * nz);
+    ty = rem / nz;
+    tz = rem - ty * nz;
+  }
+  const int n0 = ty * TN;
+  const int k0 = tz * X3_TK;
   const unsigned M = (unsigned)d.B * d.Fo * d.To;
   const unsigned FoTo = (unsigned)d.Fo * d.To;
   const unsigned r_begin = (unsigned)split * a.rows_per_split;
@@ -139,7 +153,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_x3(const WgradX3Args a) {
 
   float av[8][4], dv[RPL][4], av2[8][4], dv2[RPL][4];  // av2 / dv2: the second set (DEPTH 2)
   f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
-  const bool bias_lane = a.want_bias && blockIdx.z == 0;
+  const bool bias_lane = a.want_bias && tz == 0;
 
   // loop-invariant parts of the addressing: the vec4 quad's base and row strides, the dY
   // column offsets of this lane's n-quad
@@ -374,7 +388,7 @@ bool wgrad_x3_takes(const clskd_conv_desc& d) {
 
 void launch_wgrad_x3(const clskd_conv_desc& d, const float* dy, float* work, int S, int64_t rps,
                      int want_bias, hipStream_t st) {
-  WgradX3Args a{d, dy, work, (int)rps, S, want_bias};
+  WgradX3Args a{d, dy, work, (int)rps, S, want_bias, knob(KNOB_WGRAD_XCD) != 0 ? 1 : 0};
   const int tn = x3_tn(d.N);
   // chunks in flight per wave (CLSKD_WGRAD_DEPTH 1 / 2; 0 = by instance): two for the vec4
   // gathers of the narrow tiles, where the second register set keeps the occupancy and the

@@ -114,6 +114,32 @@ def test_conv_wgrad_split_products_against_fp64(case, depth):
         _lib.set_knob("CLSKD_WGRAD_DEPTH", prev)
 
 
+@pytest.mark.parametrize("case", sorted(X3_CASES))
+def test_conv_wgrad_xcd_order_is_bitwise_identical(case):
+    """CLSKD_WGRAD_XCD (each XCD walks a contiguous run of (row chunk, n-tile, k-tile) work items)
+    only reassigns work items to workgroups: dW and dbias bitwise equal to the grid order."""
+    from clskd import _lib, ops
+    segc, N, taps, sf, B, Fi, Fo, T = X3_CASES[case]
+    g = torch.Generator().manual_seed(9)
+    dsegs = [ops.seg_bftc((torch.randn(B, Fi, T, c, generator=g) * 1.3).to(DEV)) for c in segc]
+    dyd = torch.randn(B, Fo, T, N, generator=g).to(DEV)
+    Kp = -(-len(taps) * sum(segc) // 16) * 16
+    outs = []
+    for xcd in (0, 1):
+        prev = _lib.set_knob("CLSKD_WGRAD_XCD", xcd)
+        try:
+            dw = torch.empty(N, Kp, device=DEV)
+            db = torch.empty(N, device=DEV)
+            with ops.split_products(False, wgrad=True):
+                ops.conv_wgrad(dsegs, taps, B, Fo, T, N, dyd, ops.OutMap(Fo * T * N, T * N, N), dw,
+                               db, stride_f=sf)
+            torch.cuda.synchronize()
+            outs.append((dw, db))
+        finally:
+            _lib.set_knob("CLSKD_WGRAD_XCD", prev)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 def _x3_case(case):
     from clskd import ops
     segc, N, taps, sf, B, Fi, Fo, T = X3_CASES[case]
