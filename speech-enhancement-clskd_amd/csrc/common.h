@@ -198,4 +198,18 @@ __device__ __forceinline__ int nearest_src(int dst, int in_size, int out_size) {
   return s < in_size - 1 ? s : in_size - 1;
 }
 
+// masking mode 'E' (norm.hip mask_e_kernel, norm_bwd.hip mask_e_bwd_kernel): MASK_TT frames per
+// block; the mask columns [256][2 * MASK_TT] staged in LDS with a padded row (MASK_LD floats: the
+// bins of one wave's float2 reads fall on distinct banks)
+constexpr int MASK_TT = 16;
+constexpr int MASK_LD = 2 * MASK_TT + 2;
+// ml[fm][r] = mcol[fm * Tm * 2 + r] for r < 2 * nt (mcol: the block's first column of bin 0)
+__device__ __forceinline__ void mask_tile_load(const float* __restrict__ mcol, int Tm, int nt,
+                                               float* ml) {
+  for (int i = threadIdx.x; i < 256 * 2 * MASK_TT; i += blockDim.x) {
+    const int fm = i / (2 * MASK_TT), r = i - fm * 2 * MASK_TT;
+    if (r < 2 * nt) ml[fm * MASK_LD + r] = mcol[(int64_t)fm * Tm * 2 + r];
+  }
+}
+
 }  // namespace clskd

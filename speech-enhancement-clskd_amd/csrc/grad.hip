@@ -167,12 +167,24 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32(const WgradArgs a) {
 // four 64-B runs per load); split lane sl sums splits sl, sl + 16, ... (eight loads in flight per
 // round), then the 16 lane sums are added in a fixed order in LDS (deterministic for a given S).
 // Round 4's 32 x 8 layout read 8 splits of one element per 8 lanes (32-B pieces) and carried a
-// chain of S / 8 dependent loads: 16.8 us per launch in the C3 census.
+// chain of S / 8 dependent loads: 16.8 us per launch in the C3 census.  The bias partials
+// ([S][N] after the weight partials) are reduced by the blocks past the weight's wblocks in the
+// same launch (round 6: one launch per weight gradient instead of two).
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ work, int S,
                                                           int64_t per, float* __restrict__ dw,
-                                                          int accumulate) {
+                                                          int accumulate, int64_t wblocks,
+                                                          int64_t nbias, float* __restrict__ dbias,
+                                                          int acc_bias) {
   const int e = threadIdx.x & 15, sl = threadIdx.x >> 4;
-  const int64_t i = (int64_t)blockIdx.x * 16 + e;
+  int64_t blk = blockIdx.x;
+  if (blk >= wblocks) {  // block-uniform: the bias segment
+    blk -= wblocks;
+    work += (int64_t)S * per;
+    per = nbias;
+    dw = dbias;
+    accumulate = acc_bias;
+  }
+  const int64_t i = blk * 16 + e;
   float s = 0.f;
   if (i < per) {
     int j = sl;
@@ -378,11 +390,10 @@ extern "C" int clskd_conv2d_wgrad(const clskd_conv_desc* dp, const float* dy, fl
   }
   CLSKD_LAUNCH_CHECK("conv2d_wgrad");
   const int64_t per = (int64_t)d.N * d.K;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(per, 16)), dim3(256), 0, st, work, S,
-                     per, dw, accumulate & 1);
-  if (dbias)
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv(d.N, 16)), dim3(256), 0, st,
-                       work + (int64_t)S * per, S, (int64_t)d.N, dbias, (accumulate >> 1) & 1);
+  const int64_t wblocks = cdiv(per, 16), bblocks = dbias ? cdiv((int64_t)d.N, 16) : 0;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(256), 0, st,
+                     work, S, per, dw, accumulate & 1, wblocks, (int64_t)d.N, dbias,
+                     (accumulate >> 1) & 1);
   CLSKD_LAUNCH_CHECK("conv2d_wgrad_reduce");
   return CLSKD_OK;
 }

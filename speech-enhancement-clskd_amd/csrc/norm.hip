@@ -221,26 +221,32 @@ __global__ void frame_pad_kernel(const float* __restrict__ x, int64_t ldx, int B
 // ------------------------------------------------------------------------------------------
 // masking mode 'E' (DCCRN.py:150-159, 207-226)
 // ------------------------------------------------------------------------------------------
-__global__ void mask_e_kernel(const float* __restrict__ spec, int ldspec,
-                              const float* __restrict__ mask, int Tm, int B, int T,
-                              float* __restrict__ est, int ldest, float* __restrict__ mask_r,
-                              float* __restrict__ mask_i) {
-  const int64_t total = (int64_t)B * T * 257;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int f = (int)(i % 257);
-    const int64_t bt = i / 257;
-    const int t = (int)(bt % T);
-    const int b = (int)(bt / T);
+// The mask is time-minor ([B][256][Tm][2]) and the spectrum / estimate frequency-minor
+// ([B][T][ld]): a block owns MASK_TT frames of one utterance and stages their mask columns in LDS
+// (one 128-B run per bin), so both sides are read and written in contiguous runs.  Round 6: the
+// one-thread-per-bin form gathered the mask with a 3.2-KB stride (PMC 195 MB read per launch at
+// C2's shape against ~40 MB algorithmic).
+__global__ __launch_bounds__(256) void mask_e_kernel(const float* __restrict__ spec, int ldspec,
+                                                     const float* __restrict__ mask, int Tm, int B,
+                                                     int T, float* __restrict__ est, int ldest,
+                                                     float* __restrict__ mask_r,
+                                                     float* __restrict__ mask_i) {
+  __shared__ __attribute__((aligned(16))) float ml[256 * MASK_LD];
+  const int b = blockIdx.y, t0 = blockIdx.x * MASK_TT;
+  const int nt = min(MASK_TT, T - t0);
+  mask_tile_load(mask + ((int64_t)b * 256 * Tm + t0 + 1) * 2, Tm, nt, ml);
+  __syncthreads();
+  for (int i = threadIdx.x; i < nt * 257; i += 256) {
+    const int tt = i / 257, f = i - tt * 257;
+    const int64_t bt = (int64_t)b * T + t0 + tt;
     const float re = spec[bt * ldspec + f];
     const float im = spec[bt * ldspec + 257 + f];
     const float mags = sqrtf(re * re + im * im + 1e-8f);
     const float phase = atan2f(im, re);
     float mr = 0.f, mi = 0.f;
     if (f > 0) {
-      const float* mp = mask + (((int64_t)b * 256 + (f - 1)) * Tm + (t + 1)) * 2;
-      mr = mp[0];
-      mi = mp[1];
+      mr = ml[(f - 1) * MASK_LD + 2 * tt];
+      mi = ml[(f - 1) * MASK_LD + 2 * tt + 1];
     }
     const float mm = sqrtf(mr * mr + mi * mi);
     const float rp = mr / (mm + 1e-8f);
@@ -648,7 +654,8 @@ extern "C" int clskd_mask_e(const float* spec, int32_t ldspec, const float* mask
   CLSKD_CHECK_ARG(spec && mask && est, "mask_e: null pointer");
   CLSKD_CHECK_SHAPE(ldspec >= 514 && ldest >= 514 && ldest - 514 <= 257 && Tm >= T + 1,
                     "mask_e: bad strides");
-  hipLaunchKernelGGL(mask_e_kernel, dim3(grid_for((int64_t)B * T * 257)), dim3(256), 0,
+  CLSKD_CHECK_SHAPE(B > 0 && B <= 65535 && T > 0, "mask_e: B=%d T=%d", B, T);
+  hipLaunchKernelGGL(mask_e_kernel, dim3((unsigned)cdiv(T, MASK_TT), (unsigned)B), dim3(256), 0,
                      as_stream(stream), spec, ldspec, mask, Tm, B, T, est, ldest, mask_r, mask_i);
   CLSKD_LAUNCH_CHECK("mask_e");
   return CLSKD_OK;

@@ -475,45 +475,66 @@ __global__ __launch_bounds__(256) void nearest_down_sum_kernel(
 //   dmr = dA |S| (1 - tanh^2|M|) mr/|M| - dpsi mi/|M|^2,  dmi = ... mi/|M| + dpsi mr/|M|^2
 // (the atan2 of the 1/(|M|+1e-8)-scaled pair is scale invariant, so its derivative is atan2's).
 // ------------------------------------------------------------------------------------------
-__global__ void mask_e_bwd_kernel(const float* __restrict__ spec, int ldspec,
-                                  const float* __restrict__ mask, int Tm, int B, int T,
-                                  const float* __restrict__ dest, int ldest,
-                                  float* __restrict__ dmask) {
-  const int64_t total = (int64_t)B * 256 * Tm;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int tm = (int)(i % Tm);
-    const int64_t bf = i / Tm;
-    const int fm = (int)(bf % 256);
-    const int b = (int)(bf / 256);
+// The block tiling of mask_e_kernel (norm.hip): MASK_TT frames per block, the mask columns staged
+// in LDS and the mask gradient written back through the same tile in 128-B runs per bin; block 0
+// of each utterance writes the zero columns (tm = 0 and tm > T).  Round 6: the thread-per-column
+// form read the spectrum and its gradient with a 2-KB stride (PMC 380 MB read per launch at C3's
+// shape against ~40 MB algorithmic).
+__global__ __launch_bounds__(256) void mask_e_bwd_kernel(const float* __restrict__ spec, int ldspec,
+                                                         const float* __restrict__ mask, int Tm,
+                                                         int B, int T,
+                                                         const float* __restrict__ dest, int ldest,
+                                                         float* __restrict__ dmask) {
+  __shared__ __attribute__((aligned(16))) float ml[256 * MASK_LD];
+  const int b = blockIdx.y, t0 = blockIdx.x * MASK_TT;
+  const int nt = min(MASK_TT, T - t0);
+  const int64_t col0 = ((int64_t)b * 256 * Tm + t0 + 1) * 2;
+  mask_tile_load(mask + col0, Tm, nt, ml);
+  __syncthreads();
+  for (int i = threadIdx.x; i < nt * 256; i += 256) {
+    const int tt = i >> 8, fm = i & 255;
+    const int f = fm + 1;
+    const int64_t bt = (int64_t)b * T + t0 + tt;
+    const float re = spec[bt * ldspec + f];
+    const float im = spec[bt * ldspec + 257 + f];
+    const float mags = sqrtf(re * re + im * im + 1e-8f);
+    const float phase = atan2f(im, re);
+    float* mp = ml + fm * MASK_LD + 2 * tt;  // read, then overwritten by this thread only
+    const float mr = mp[0], mi = mp[1];
+    const float m2 = mr * mr + mi * mi;
+    const float mm = sqrtf(m2);
+    const float rp = mr / (mm + 1e-8f);
+    const float ip = mi / (mm + 1e-8f);
+    const float th = tanhf(mm);
+    const float A = th * mags;
+    const float psi = phase + atan2f(ip, rp);
+    const float cp = cosf(psi), sp = sinf(psi);
+    const float dre = dest[bt * ldest + f], dim = dest[bt * ldest + 257 + f];
+    const float dA = dre * cp + dim * sp;
+    const float dpsi = A * (dim * cp - dre * sp);
     float gr = 0.f, gi = 0.f;
-    if (tm >= 1 && tm - 1 < T) {
-      const int t = tm - 1, f = fm + 1;
-      const int64_t bt = (int64_t)b * T + t;
-      const float re = spec[bt * ldspec + f];
-      const float im = spec[bt * ldspec + 257 + f];
-      const float mags = sqrtf(re * re + im * im + 1e-8f);
-      const float phase = atan2f(im, re);
-      const float mr = mask[i * 2], mi = mask[i * 2 + 1];
-      const float m2 = mr * mr + mi * mi;
-      const float mm = sqrtf(m2);
-      const float rp = mr / (mm + 1e-8f);
-      const float ip = mi / (mm + 1e-8f);
-      const float th = tanhf(mm);
-      const float A = th * mags;
-      const float psi = phase + atan2f(ip, rp);
-      const float cp = cosf(psi), sp = sinf(psi);
-      const float dre = dest[bt * ldest + f], dim = dest[bt * ldest + 257 + f];
-      const float dA = dre * cp + dim * sp;
-      const float dpsi = A * (dim * cp - dre * sp);
-      if (mm > 0.f) {
-        const float dmm = dA * mags * (1.f - th * th);
-        gr = dmm * mr / mm - dpsi * mi / m2;
-        gi = dmm * mi / mm + dpsi * mr / m2;
-      }
+    if (mm > 0.f) {
+      const float dmm = dA * mags * (1.f - th * th);
+      gr = dmm * mr / mm - dpsi * mi / m2;
+      gi = dmm * mi / mm + dpsi * mr / m2;
     }
-    dmask[i * 2] = gr;
-    dmask[i * 2 + 1] = gi;
+    mp[0] = gr;
+    mp[1] = gi;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 256 * 2 * MASK_TT; i += 256) {
+    const int fm = i / (2 * MASK_TT), r = i - fm * 2 * MASK_TT;
+    if (r < 2 * nt) dmask[col0 + (int64_t)fm * Tm * 2 + r] = ml[fm * MASK_LD + r];
+  }
+  if (blockIdx.x == 0) {  // columns without a gradient: tm = 0 and T < tm < Tm
+    const int nz = Tm - T;
+    for (int i = threadIdx.x; i < 256 * nz; i += 256) {
+      const int fm = i / nz, j = i - fm * nz;
+      const int tm = j == 0 ? 0 : T + j;
+      float* dp = dmask + (((int64_t)b * 256 + fm) * Tm + tm) * 2;
+      dp[0] = 0.f;
+      dp[1] = 0.f;
+    }
   }
 }
 
@@ -806,60 +827,99 @@ __global__ __launch_bounds__(256) void spkd_bn_bwd_apply_kernel(
 // ------------------------------------------------------------------------------------------
 // ABF conv1 BatchNorm backward apply fused with conv1's data gradient (framework.py:179-182:
 // conv1 = 1x1 Cin -> 64, no bias).  Per row: d[c] = k0[c]*dy[c] + k1[c]*x[c] + k2[c] (the
-// bn_bwd_apply of a finalize's coefficients, no PReLU), then out[n] (+)= sum_c w[c][n] * d[c] in
-// ascending c — the 64-channel gradient d never reaches HBM (the two-pass form wrote and re-read
-// it in fp32: 2 x rows x 256 B).  TPR = N / 8 threads per row, each owning 8 output channels;
-// every operand of a row is loaded before use; coefficients and weights broadcast from LDS.
+// bn_bwd_apply of a finalize's coefficients, no PReLU), then out[n] (+)= sum_c w[c][n] * d[c] —
+// the 64-channel gradient d never reaches HBM (the two-pass form wrote and re-read it in fp32:
+// 2 x rows x 256 B).  Eight lanes per row, lane q owning channels 8q..8q+7: one wave load
+// instruction reads 8 whole rows (1 KB contiguous).  Round 6's first form (a thread per row,
+// 16 B of its 128-B row per step) fetched every line from HBM several times (PMC 1,197 MB per
+// launch at N = 8 against 263 MB algorithmic: the lines left L2 between the row's steps).  Each
+// lane forms its 8 channels' partial sums of all N outputs (weights from LDS, a padded stride per
+// 8-channel chunk: the 8 chunks of one instruction hit disjoint banks), then the 8 lanes
+// reduce-scatter them over xor 4 / 2 / 1, lane q ending with outputs q*N/8 .. (q+1)*N/8 - 1.
 // ------------------------------------------------------------------------------------------
 template <typename XT, typename GT, int N>
 __global__ __launch_bounds__(256) void bn_bwd_conv1x1_kernel(
     const XT* __restrict__ x, const GT* __restrict__ dy, int64_t rows, const float* __restrict__ k,
     const float* __restrict__ w, float* __restrict__ out, int accumulate) {
   constexpr int C = 64;
-  constexpr int TPR = N / 8;
-  constexpr int RPP = 256 / TPR;  // rows per block pass
-  __shared__ __attribute__((aligned(16))) float kl[3 * C];
-  __shared__ __attribute__((aligned(16))) float wl[C * N];
+  constexpr int WS = 8 * N + 4;  // floats per 8-channel chunk of the weights in LDS (padded)
+  constexpr int RPB = 32;        // rows per block pass
+  constexpr int NO = N / 8;      // outputs per lane after the reduce-scatter
+  __shared__ __attribute__((aligned(16))) float wl[8 * WS];
   const int tid = threadIdx.x;
-  for (int i = tid; i < 3 * C; i += 256) kl[i] = k[i];
-  for (int i = tid; i < C * N; i += 256) wl[i] = w[i];
+  for (int i = tid; i < C * N; i += 256) {
+    const int c = i / N;
+    wl[(c >> 3) * WS + (c & 7) * N + (i - c * N)] = w[i];
+  }
+  const int q = tid & 7;
+  float k0[8], k1[8], k2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    k0[j] = k[q * 8 + j];
+    k1[j] = k[C + q * 8 + j];
+    k2[j] = k[2 * C + q * 8 + j];
+  }
   __syncthreads();
-  const int cg = tid % TPR, rg = tid / TPR;
-  const int n0 = cg * 8;
-  // 8 channels per step (one 16-B bf16 / two 16-B fp32 loads per operand), two steps' loads in
-  // flight: few registers, full occupancy (the whole row held at once spilled)
-  for (int64_t m = (int64_t)blockIdx.x * RPP + rg; m < rows; m += (int64_t)gridDim.x * RPP) {
-    f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
-    const XT* xrow = x + m * C;
-    const GT* grow = dy + m * C;
-#pragma unroll 2
-    for (int c8 = 0; c8 < C; c8 += 8) {
-      const f32x4 xa = Raw4<XT>::cvt(Raw4<XT>::ld(xrow + c8));
-      const f32x4 xb = Raw4<XT>::cvt(Raw4<XT>::ld(xrow + c8 + 4));
-      const f32x4 ga = Raw4<GT>::cvt(Raw4<GT>::ld(grow + c8));
-      const f32x4 gb = Raw4<GT>::cvt(Raw4<GT>::ld(grow + c8 + 4));
+  int woff = q * WS;
+  for (int64_t m = (int64_t)blockIdx.x * RPB + (tid >> 3); m < rows;
+       m += (int64_t)gridDim.x * RPB) {
+    // an opaque per-row offset: the weight reads stay inside the loop (hoisted, N = 8 alone held
+    // 64 weights per lane in VGPRs and the wide instances spilled)
+    asm volatile("" : "+v"(woff));
+    const float* wq = wl + woff;
+    const f32x4 xa = Raw4<XT>::cvt(Raw4<XT>::ld(x + m * C + q * 8));
+    const f32x4 xb = Raw4<XT>::cvt(Raw4<XT>::ld(x + m * C + q * 8 + 4));
+    const f32x4 ga = Raw4<GT>::cvt(Raw4<GT>::ld(dy + m * C + q * 8));
+    const f32x4 gb = Raw4<GT>::cvt(Raw4<GT>::ld(dy + m * C + q * 8 + 4));
+    float o[N];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = c8 + j;
-        const float xv = j < 4 ? xa[j & 3] : xb[j & 3];
-        const float gv = j < 4 ? ga[j & 3] : gb[j & 3];
-        const float dv = fmaf(kl[c], gv, fmaf(kl[C + c], xv, kl[2 * C + c]));
-        const f32x4 wa = *reinterpret_cast<const f32x4*>(&wl[c * N + n0]);
-        const f32x4 wb = *reinterpret_cast<const f32x4*>(&wl[c * N + n0 + 4]);
+    for (int n = 0; n < N; ++n) o[n] = 0.f;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          o0[e] = fmaf(dv, wa[e], o0[e]);
-          o1[e] = fmaf(dv, wb[e], o1[e]);
-        }
+    for (int j = 0; j < 8; ++j) {
+      const float xv = j < 4 ? xa[j & 3] : xb[j & 3];
+      const float gv = j < 4 ? ga[j & 3] : gb[j & 3];
+      const float dv = fmaf(k0[j], gv, fmaf(k1[j], xv, k2[j]));
+#pragma unroll
+      for (int n4 = 0; n4 < N; n4 += 4) {
+        const f32x4 w4 = *reinterpret_cast<const f32x4*>(&wq[j * N + n4]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[n4 + e] = fmaf(dv, w4[e], o[n4 + e]);
       }
     }
-    float* op = out + m * N + n0;
-    if (accumulate) {
-      o0 += *reinterpret_cast<const f32x4*>(op);
-      o1 += *reinterpret_cast<const f32x4*>(op + 4);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {  // reduce-scatter over the row's 8 lanes
+      const int mask = 4 >> s;
+      const int H = N >> (s + 1);
+      const bool hi = (q & mask) != 0;
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        // both values loaded first: `hi ? o[H + i] : o[i]` selects an address, and the array
+        // then lived as a dynamically indexed one (a compare / select chain per access)
+        const float lo_v = o[i], hi_v = o[H + i];
+        const float keep = hi ? hi_v : lo_v;
+        const float send = hi ? lo_v : hi_v;
+        o[i] = keep + __shfl_xor(send, mask);
+      }
     }
-    *reinterpret_cast<f32x4*>(op) = o0;
-    *reinterpret_cast<f32x4*>(op + 4) = o1;
+    float* op = out + m * N + q * NO;
+    if constexpr (NO == 1) {
+      *op = accumulate ? *op + o[0] : o[0];
+    } else if constexpr (NO == 2) {
+      float2 v = make_float2(o[0], o[1]);
+      if (accumulate) {
+        const float2 p = *reinterpret_cast<const float2*>(op);
+        v.x += p.x;
+        v.y += p.y;
+      }
+      *reinterpret_cast<float2*>(op) = v;
+    } else {
+#pragma unroll
+      for (int i = 0; i < NO; i += 4) {
+        f32x4 v = {o[i], o[i + 1], o[i + 2], o[i + 3]};
+        if (accumulate) v += *reinterpret_cast<const f32x4*>(op + i);
+        *reinterpret_cast<f32x4*>(op + i) = v;
+      }
+    }
   }
 }
 
@@ -982,8 +1042,7 @@ extern "C" int clskd_bn_bwd_conv1x1(const void* x, int32_t dtype, const void* dy
                       ((uintptr_t)out & 15) == 0 && ((uintptr_t)k & 15) == 0,
                   "bn_bwd_conv1x1: x, dy, k, out must be 16-byte aligned");
   hipStream_t st = as_stream(stream);
-  const int rpp = 256 / (N / 8);
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(rows, rpp), 4096));
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(rows, 32), 8192));
 #define BC1_N(XT_, GT_)                                                                           \
   do {                                                                                            \
     if (N == 8)                                                                                   \
@@ -1070,9 +1129,9 @@ extern "C" int clskd_mask_e_bwd(const float* spec, int32_t ldspec, const float* 
                                 float* dmask, void* stream) {
   CLSKD_CHECK_ARG(spec && mask && dest && dmask, "mask_e_bwd: null pointer");
   CLSKD_CHECK_SHAPE(Tm >= T + 1, "mask_e_bwd: Tm=%d < T+1", Tm);
-  const int64_t total = (int64_t)B * 256 * Tm;
-  hipLaunchKernelGGL(mask_e_bwd_kernel, dim3(grid_of(total)), dim3(256), 0, as_stream(stream), spec,
-                     ldspec, mask, Tm, B, T, dest, ldest, dmask);
+  CLSKD_CHECK_SHAPE(B > 0 && B <= 65535 && T > 0, "mask_e_bwd: B=%d T=%d", B, T);
+  hipLaunchKernelGGL(mask_e_bwd_kernel, dim3((unsigned)cdiv(T, MASK_TT), (unsigned)B), dim3(256), 0,
+                     as_stream(stream), spec, ldspec, mask, Tm, B, T, dest, ldest, dmask);
   CLSKD_LAUNCH_CHECK("mask_e_bwd");
   return CLSKD_OK;
 }

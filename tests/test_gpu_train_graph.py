@@ -63,7 +63,8 @@ def test_train_graph_matches_eager_train_steps(precision, launch):
     ex = (TrainStepExecutor if launch == "exec" else TrainStepGraph)(kd_g, fg, og, *batches[0])
     assert og.step_count == 0 and torch.equal(fe.data, fg.data)  # warm-up state restored
     if launch == "exec":
-        assert ex.info["memcpys"] == 0 and ex.info["kernels"] > 500, ex.info
+        # (a whole captured step: ~480 kernels once the packing gathers are batched)
+        assert ex.info["memcpys"] == 0 and ex.info["kernels"] > 400, ex.info
     for i, (X, y) in enumerate(batches):
         le = kd_e.train_step((X, y), fe, oe)
         lg = ex(X, y)
