@@ -134,6 +134,16 @@ def _tw(key, src, build):
         return ent[1]
     with torch.no_grad():
         w = _tw_build(key, src, build)
+    _tw_install(key, src, w, tok)
+    if _TW_PREBUILD and _TWMAP.get(key):  # how to find this entry's source next step
+        from .model import pack_provenance
+        prov = pack_provenance(src)
+        _TW_PLAN[key] = ("pack", weakref.ref(prov[0]), prov[1], prov[2]) if prov else (
+            "tensor", weakref.ref(src))
+    return w
+
+
+def _tw_install(key, src, w, tok):
     k = (src.data_ptr(), src._version)
     _TW.pop(key, None)
     for dead in [kk for kk, e in _TW.items() if e[2]() is None]:
@@ -142,7 +152,48 @@ def _tw(key, src, build):
         del _TW[next(iter(_TW))]
     _TW[key] = (k, w, weakref.ref(src), tok)
     ops.capture_keep(w, tok)
-    return w
+
+
+# Every step re-derives the mapped entries whose sources changed (the packed forward weights an
+# Adam step rewrote, the re-drawn ABF weights), one index_gather each at its first use.
+# tw_prebuild, at the start of the backward, finds each such entry's current source from the
+# previous step's plan (a packed output of the model: model.pack_provenance; else the same
+# tensor object) and gathers them all in one batched launch (CLSKD_TW_PREBUILD=0: A/B).
+_TW_PREBUILD = os.environ.get("CLSKD_TW_PREBUILD", "1") == "1"
+_TW_PLAN = {}
+
+
+def tw_prebuild():
+    if not _TW_PREBUILD or not _TW_PLAN:
+        return
+    from .model import pack_output
+    tok = ops.capture_token()
+    jobs, pend = [], []
+    for key, plan in list(_TW_PLAN.items()):
+        m = _TWMAP.get(key)
+        src = None
+        if plan[0] == "pack":
+            model = plan[1]()
+            src = pack_output(model, plan[2], plan[3], tok) if model is not None else None
+        else:
+            src = plan[1]()
+        if not m or src is None:
+            _TW_PLAN.pop(key, None)
+            continue
+        if m[0] != (tuple(src.shape), src.dtype, str(src.device)):
+            continue
+        ent = _TW.get(key)
+        if (ent is not None and ent[0] == (src.data_ptr(), src._version) and ent[2]() is src
+                and ops.cache_entry_usable(ent[3], tok)):
+            continue
+        out = torch.empty(m[3], dtype=f32, device=src.device)
+        jobs.append((src, m[1], m[2], out))
+        pend.append((key, src, out))
+    if len(jobs) < 2:
+        return
+    ops.index_gather_jobs(jobs)
+    for key, src, out in pend:
+        _tw_install(key, src, out, tok)
 
 
 # A rebuilt entry (every step: Adam rewrote the packed forward weights, the ABFs were re-drawn) is
@@ -714,6 +765,7 @@ def clskd_backward(res, student, review_encoder, review_decoder, pg, acc_params=
     # taps and insert results at the front (framework.py:245-261).
     from .distill import _side_stream
     main = torch.cuda.current_stream(dev)
+    tw_prebuild()  # on main, before the branches fork: every consumer is ordered after it
     s_dec, s_enc = _side_stream(dev, 0), _side_stream(dev, 1)
     n = len(enc)
     for st in (s_dec, s_enc):

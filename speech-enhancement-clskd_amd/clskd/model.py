@@ -10,6 +10,7 @@ Supported configuration = the one the reference trains and distils: masking_mode
 use_clstm=True, use_cbn=False, kernel_size 5, fft 512 / win 400 / hop 100.  Anything else raises.
 """
 import os
+import weakref
 
 import numpy as np
 import torch
@@ -162,6 +163,44 @@ _PACK_MAPS_ON = os.environ.get("CLSKD_PACK_MAPS", "1") == "1"
 # the taped H = 32 recurrence stores its cell states for the backward (round 6; CLSKD_LSTM_CELLS=0:
 # the backward re-derives them with its serial scan, A/B)
 _LSTM_CELLS = os.environ.get("CLSKD_LSTM_CELLS", "1") == "1"
+# the changed parameter groups re-packed in one batched gather at the start of a forward
+# (DCCRN.prepack; CLSKD_PREPACK=0: one gather per group at its first use, A/B)
+_PREPACK = os.environ.get("CLSKD_PREPACK", "1") == "1"
+
+
+# packed outputs -> (model, group, slot): backward.tw_prebuild re-derives the data-gradient weights
+# of the packed forward weights a step just made, all in one batched gather at the start of the
+# backward (id -> (weak output, weak model, group key, slot); verified by identity on lookup)
+_PACK_PROV = {}
+
+
+def _note_pack_outputs(model, key, out):
+    outs = [(out, None)] if isinstance(out, torch.Tensor) else [
+        (t, i) for i, t in enumerate(out) if isinstance(t, torch.Tensor)]
+    if len(_PACK_PROV) > 4096:
+        for k in [k for k, v in _PACK_PROV.items() if v[0]() is None]:
+            del _PACK_PROV[k]
+    mref = weakref.ref(model)
+    for t, i in outs:
+        _PACK_PROV[id(t)] = (weakref.ref(t), mref, key, i)
+
+
+def pack_provenance(t):
+    """(model, group key, slot | None) of a packed output still current in its model's cache."""
+    v = _PACK_PROV.get(id(t))
+    if v is None or v[0]() is not t:
+        return None
+    m = v[1]()
+    return None if m is None else (m, v[2], v[3])
+
+
+def pack_output(model, key, slot, tok):
+    """The model's current packed output (group key, slot) usable under capture token tok."""
+    ent = model._wcache.get(key)
+    if ent is None or not ops.cache_entry_usable(ent[2], tok):
+        return None
+    out = ent[1]
+    return out if slot is None else out[slot]
 
 
 def _flat_root(params):
@@ -303,6 +342,8 @@ class DCCRN(nn.Module):
         self._wcache = {}
         self._pmaps = {}  # parameter group -> packing index map (_pack_group)
         self._pgroups = {}
+        self._pkparams = {}  # parameter group -> its resolved tensors (prepack)
+        self._pkused = set()  # groups used since the last prepack (the next one re-packs these)
         self._refs = None
         self._tap_sinks = []
         # MFMA operand type of the large GEMMs: "fp32" (exact-f32 MFMA), "f32x3" (fp32 storage, 3 x
@@ -355,17 +396,57 @@ class DCCRN(nn.Module):
             if pg is None:
                 pg = self._pgroups[key] = tuple(params())
             params = pg
+        self._pkparams[key] = params
+        self._pkused.add(key)
         ent = self._wcache.get(key)
         ver = _pv(*params)
         tok = ops.capture_token()  # entries built inside a capture serve that capture only
         if ent is None or ent[0] != ver or not ops.cache_entry_usable(ent[2], tok) or (
-                self.repack_in_capture and tok is not None
+                self.repack_in_capture and tok is not None and ent[3] is not tok
                 and any(p.requires_grad for p in params)):
             with torch.no_grad():
-                ent = (_pv(*params), _pack_group(self._pmaps, key, params, build), tok)
+                ent = (_pv(*params), _pack_group(self._pmaps, key, params, build), tok, None)
             self._wcache[key] = ent
+            _note_pack_outputs(self, key, ent[1])
         ops.capture_keep(ent[1], tok)
         return ent[1]
+
+    def prepack(self):
+        """Re-pack every parameter group that has a packing map and changed since its entry (a
+        training step's Adam rewrote them) in one batched gather (clskd_index_gather_jobs) at the
+        start of a forward, instead of one launch per group at its first use.  Entries made
+        here inside a capture are that capture's repacks (the graph replays the gather)."""
+        if not _PREPACK or not self._pmaps:
+            return
+        tok = ops.capture_token()
+        jobs, pend = [], []
+        used, self._pkused = self._pkused, set()
+        for key in used:
+            m = self._pmaps.get(key)
+            params = self._pkparams.get(key)
+            if not m or params is None:
+                continue
+            root, idx, sgn, total, layout, kind = m
+            r = _flat_root(params)
+            if r is None or r.data_ptr() != root.data_ptr() or r.numel() != root.numel():
+                continue
+            ver = _pv(*params)
+            ent = self._wcache.get(key)
+            if not (self.repack_in_capture and tok is not None) and ent is not None and (
+                    ent[0] == ver and ops.cache_entry_usable(ent[2], tok)):
+                continue  # (a captured step re-packs every group: its replays follow Adam)
+            buf = torch.empty(total, dtype=torch.float32, device=root.device)
+            jobs.append((root, idx, sgn, buf))
+            pend.append((key, ver, buf, layout, kind))
+        if len(jobs) < 2:
+            return
+        ops.index_gather_jobs(jobs)
+        for key, ver, buf, layout, kind in pend:
+            outs = [buf[o:o + n].view(sh) for o, n, sh in layout]
+            out = outs[0] if kind == "tensor" else kind(outs)
+            self._wcache[key] = (ver, out, tok, tok)
+            _note_pack_outputs(self, key, out)
+            ops.capture_keep(out, tok)
 
     def _layer_refs(self):
         """Per-layer module references, resolved once: encoder (conv, bn, prelu), decoder
@@ -522,6 +603,7 @@ class DCCRN(nn.Module):
         forward too when train_split bit 1 or 2 is set (KnowledgeDistillation.set_precision),
         else on the exact fp32 engines."""
         split = self.compute == "f32x3" and (tape is None or bool(self.train_split & 6))
+        self.prepack()
         with ops.split_products(split):
             return self._run(x, train, bn_updates, spec, want_masks, on_encoder, tape, taps_only,
                              mark, on_decoder_tap, gram_taps)

@@ -741,3 +741,43 @@ def test_lstm_forward_cell_states_feed_the_backward():
     ref = torch.stack(ref, 2).reshape(-1)
     np.testing.assert_allclose(cells.double().cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(dg_fwd.cpu().numpy(), dg_scan.cpu().numpy(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,T,extra", [(3, 37, 2), (2, 16, 0), (1, 1, 0)])
+def test_mask_e_tiles_against_fp64(B, T, extra):
+    """Masking mode 'E' (DCCRN.py:207-226) forward and backward, the LDS-tiled kernels (16 frames
+    per block): ragged last tile, mask columns past T (zero gradient), against fp64 autograd of
+    the same formula."""
+    from clskd import ops
+    g = torch.Generator().manual_seed(B * 100 + T)
+    Tm = T + 1 + extra
+    spec = torch.randn(B, T, 520, generator=g, dtype=torch.float64)
+    mask = torch.randn(B, 256, Tm, 2, generator=g, dtype=torch.float64)
+    dest = torch.randn(B, T, 600, generator=g, dtype=torch.float64)
+    # fp64 reference of the forward (bins 1..256 masked with the mask at frame t + 1)
+    mr_ = mask[:, :, 1:T + 1, 0].transpose(1, 2).clone().requires_grad_(True)
+    mi_ = mask[:, :, 1:T + 1, 1].transpose(1, 2).clone().requires_grad_(True)
+    re, im = spec[..., :257], spec[..., 257:514]
+    mags = torch.sqrt(re * re + im * im + 1e-8)
+    phase = torch.atan2(im, re)
+    z = torch.zeros(B, T, 1, dtype=torch.float64)
+    mr = torch.cat([z, mr_], -1)
+    mi = torch.cat([z, mi_], -1)
+    mm = torch.sqrt(mr * mr + mi * mi)
+    mphase = torch.atan2(mi / (mm + 1e-8), mr / (mm + 1e-8))
+    em = torch.tanh(mm) * mags
+    e_re, e_im = em * torch.cos(phase + mphase), em * torch.sin(phase + mphase)
+    (e_re * dest[..., :257] + e_im * dest[..., 257:514]).sum().backward()
+    f32 = lambda t: t.to(DEV, torch.float32).contiguous()
+    est = torch.full((B, T, 600), 7.0, device=DEV)
+    ops.mask_e(f32(spec), f32(mask), T, est)
+    dmask = torch.full((B, 256, Tm, 2), 7.0, device=DEV)
+    ops.mask_e_bwd(f32(spec), f32(mask), T, f32(dest), dmask)
+    torch.cuda.synchronize()
+    est, dmask = est.cpu().double(), dmask.cpu().double()
+    assert _rel(est[..., :257], e_re.detach()) < 1e-5
+    assert _rel(est[..., 257:514], e_im.detach()) < 1e-5
+    assert torch.all(est[..., 514:600] == 0)
+    assert _rel(dmask[:, :, 1:T + 1, 0], mr_.grad.transpose(1, 2)) < 1e-4
+    assert _rel(dmask[:, :, 1:T + 1, 1], mi_.grad.transpose(1, 2)) < 1e-4
+    assert torch.all(dmask[:, :, 0] == 0) and torch.all(dmask[:, :, T + 1:] == 0)
