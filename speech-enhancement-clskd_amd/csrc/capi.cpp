@@ -63,6 +63,7 @@ static const KnobDef kKnobs[KNOB_COUNT] = {
     {"CLSKD_LSTM_PRE", 1, true},
     {"CLSKD_ABF_BWD_BLOCKS", 2048, false},
     {"CLSKD_WGRAD_XCD", 1, true},
+    {"CLSKD_LSTM_BWD_PIN", 1, true},
     {"CLSKD_LSTM128_TDIV", 0, false},
     {"CLSKD_LSTM32_TDIV", 0, false}, {"CLSKD_BF16_DEBUG_MODE", 0, false}, {"CLSKD_SKIP", 0, false},
     {"CLSKD_H32_DEBUG_MODE", 0, false},

@@ -21,7 +21,7 @@ enum KnobId {
   KNOB_G8, KNOB_G8_GRID, KNOB_HALO_GRID, KNOB_LSTM_NKS, KNOB_LSTM_NKS32,
   KNOB_WGRAD_WG, KNOB_NO_HALO, KNOB_BF16_WAVES, KNOB_BF16_STAGES, KNOB_BF16_TILE,
   KNOB_NO_POINTWISE, KNOB_ABF_MOMENT_DIV, KNOB_F32_WAVES, KNOB_EXEC_GATE,
-  KNOB_NO_HALO32, KNOB_HALO32_SPLIT, KNOB_HALO32_MIN_N, KNOB_G8_KORDER, KNOB_G8_PP, KNOB_F32_SPLIT, KNOB_LSTM_PRIO, KNOB_SPLIT_BK, KNOB_HALOW, KNOB_SPLIT_GRID, KNOB_G8_TA, KNOB_G8_SK, KNOB_SPLIT_PD, KNOB_SPLIT_OCC, KNOB_WGRAD_DEPTH, KNOB_LSTM_BWD_WAVE, KNOB_SPLIT_NS2, KNOB_BN_PFOLD, KNOB_LSTM_PRE, KNOB_ABF_BWD_BLOCKS, KNOB_WGRAD_XCD,
+  KNOB_NO_HALO32, KNOB_HALO32_SPLIT, KNOB_HALO32_MIN_N, KNOB_G8_KORDER, KNOB_G8_PP, KNOB_F32_SPLIT, KNOB_LSTM_PRIO, KNOB_SPLIT_BK, KNOB_HALOW, KNOB_SPLIT_GRID, KNOB_G8_TA, KNOB_G8_SK, KNOB_SPLIT_PD, KNOB_SPLIT_OCC, KNOB_WGRAD_DEPTH, KNOB_LSTM_BWD_WAVE, KNOB_SPLIT_NS2, KNOB_BN_PFOLD, KNOB_LSTM_PRE, KNOB_ABF_BWD_BLOCKS, KNOB_WGRAD_XCD, KNOB_LSTM_BWD_PIN,
   // timing-only experiment modes (wrong results): -DCLSKD_EXPERIMENTS builds only
   KNOB_LSTM128_TDIV, KNOB_LSTM32_TDIV, KNOB_BF16_DEBUG_MODE, KNOB_SKIP, KNOB_H32_DEBUG_MODE,
   KNOB_COUNT

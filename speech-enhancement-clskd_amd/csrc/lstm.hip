@@ -98,6 +98,11 @@ __global__ __launch_bounds__(NKS * H) void lstm_recurrent_kernel(
     f32x4 hv[KW / 4];
 #pragma unroll
     for (int j = 0; j < KW / 4; ++j) hv[j] = reinterpret_cast<const f32x4*>(hp)[j];
+    // every h read issued before the first FMA: the compiler split the 8 reads of H = 128 into
+    // three dependent groups (one register quad reused); the memory clobber keeps all reads
+    // above the pins, and the pins make each value live at once (FMAs start as they arrive)
+#pragma unroll
+    for (int j = 0; j < KW / 4; ++j) asm volatile("" : "+v"(hv[j]) : : "memory");
     f32x2l acc[4][2] = {};
 #pragma unroll
     for (int j = 0; j < KW / 4; ++j) {
@@ -423,9 +428,12 @@ __global__ __launch_bounds__(NKS * H) void lstm_bwd_kernel(
 // into (W_hh^T da_t)_u.  A step's operands (4 pre-activations, c_t, c_{t-1}, dh_in) are fetched
 // four steps ahead into a register ring, so the serial chain waits on no global load.  The
 // 4-wave kernel above spent ~820 ns per step (its barrier and the 8-lane reduction); this one is
-// bound by the chain's VALU / LDS latency (tools/lstm_micro.py).
+// bound by the chain's VALU / LDS latency (tools/lstm_micro.py).  PIN (round 6,
+// CLSKD_LSTM_BWD_PIN): the lane's GW / 4 gate-gradient reads are issued back to back and waited
+// once — the compiler interleaved each ds_read_b128 with the FMAs of the previous one, a chain of
+// 16 LDS round trips per step at H = 32.
 // ------------------------------------------------------------------------------------------
-template <int H>
+template <int H, bool PIN>
 __global__ __launch_bounds__(64) void lstm_bwd_wave_kernel(
     const float* __restrict__ pre, int64_t p_ws, int64_t p_seq, int64_t p_t,
     const float* __restrict__ dh, int64_t d_ws, int64_t d_seq, int64_t d_t,
@@ -502,12 +510,25 @@ __global__ __launch_bounds__(64) void lstm_bwd_wave_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local: da of step t written
     f32x2l a0 = {0.f, 0.f}, a1 = {0.f, 0.f};  // four independent chains, two per packed FMA
     const f32x4* dv = reinterpret_cast<const f32x4*>(&das[buf][ks * GW]);
+    if constexpr (PIN) {
+      f32x4 v[GW / 4];
 #pragma unroll
-    for (int j = 0; j < GW / 4; ++j) {
-      const f32x4 v = dv[j];
-      const f32x2l v01 = {v[0], v[1]}, v23 = {v[2], v[3]};
-      a0 = wc[2 * j] * v01 + a0;
-      a1 = wc[2 * j + 1] * v23 + a1;
+      for (int j = 0; j < GW / 4; ++j) v[j] = dv[j];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read in flight, one wait
+#pragma unroll
+      for (int j = 0; j < GW / 4; ++j) {
+        const f32x2l v01 = {v[j][0], v[j][1]}, v23 = {v[j][2], v[j][3]};
+        a0 = wc[2 * j] * v01 + a0;
+        a1 = wc[2 * j + 1] * v23 + a1;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < GW / 4; ++j) {
+        const f32x4 v = dv[j];
+        const f32x2l v01 = {v[0], v[1]}, v23 = {v[2], v[3]};
+        a0 = wc[2 * j] * v01 + a0;
+        a1 = wc[2 * j + 1] * v23 + a1;
+      }
     }
     const f32x2l a = a0 + a1;
     float s = a[0] + a[1];
@@ -680,12 +701,16 @@ extern "C" int clskd_lstm_bwd(const float* pre, int64_t p_ws, int64_t p_seq, int
   // H = 16 / 32: the single-wave kernel unless CLSKD_LSTM_BWD_WAVE=0 (A/B)
   const bool wave = knob(KNOB_LSTM_BWD_WAVE) != 0;
   if (wave && (H == 16 || H == 32)) {
-    if (H == 16)
-      hipLaunchKernelGGL(lstm_bwd_wave_kernel<16>, grid, dim3(64), 0, st, pre, p_ws, p_seq, p_t, dh,
-                         d_ws, d_seq, d_t, whh, T, cbuf, dgates, g_ws, g_seq, g_t, c_ready);
-    else
-      hipLaunchKernelGGL(lstm_bwd_wave_kernel<32>, grid, dim3(64), 0, st, pre, p_ws, p_seq, p_t, dh,
-                         d_ws, d_seq, d_t, whh, T, cbuf, dgates, g_ws, g_seq, g_t, c_ready);
+    const bool pin = knob(KNOB_LSTM_BWD_PIN) != 0;
+#define LSTM_BWD_WAVE(H_, PIN_)                                                                   \
+  hipLaunchKernelGGL((lstm_bwd_wave_kernel<H_, PIN_>), grid, dim3(64), 0, st, pre, p_ws, p_seq,   \
+                     p_t, dh, d_ws, d_seq, d_t, whh, T, cbuf, dgates, g_ws, g_seq, g_t, c_ready)
+    if (H == 16) {
+      if (pin) LSTM_BWD_WAVE(16, true); else LSTM_BWD_WAVE(16, false);
+    } else {
+      if (pin) LSTM_BWD_WAVE(32, true); else LSTM_BWD_WAVE(32, false);
+    }
+#undef LSTM_BWD_WAVE
     CLSKD_LAUNCH_CHECK("lstm_bwd");
     return CLSKD_OK;
   }

@@ -781,3 +781,27 @@ def test_mask_e_tiles_against_fp64(B, T, extra):
     assert _rel(dmask[:, :, 1:T + 1, 0], mr_.grad.transpose(1, 2)) < 1e-4
     assert _rel(dmask[:, :, 1:T + 1, 1], mi_.grad.transpose(1, 2)) < 1e-4
     assert torch.all(dmask[:, :, 0] == 0) and torch.all(dmask[:, :, T + 1:] == 0)
+
+
+@pytest.mark.parametrize("H", [16, 32])
+def test_lstm_bwd_pinned_reads_are_bitwise_identical(H):
+    """CLSKD_LSTM_BWD_PIN only changes when the single-wave BPTT kernel issues its LDS reads (all
+    of a step's gate-gradient reads together): dgates bitwise equal to the unpinned schedule."""
+    from clskd import _lib, ops
+    B, T = 3, 37
+    g = torch.Generator().manual_seed(H)
+    pre = (torch.randn(2, 2 * B, T, 4 * H, generator=g) * 0.5).to(DEV)
+    dh = torch.randn(2, 2 * B, T, H, generator=g).to(DEV)
+    whh = (torch.randn(2, 4 * H, H, generator=g) * 0.05).to(DEV)
+    st = (2 * B * T * 4 * H, T * 4 * H, 4 * H)
+    outs = []
+    for pin in (0, 1):
+        prev = _lib.set_knob("CLSKD_LSTM_BWD_PIN", pin)
+        try:
+            dg = torch.empty_like(pre)
+            ops.lstm_bwd(pre, st, dh, (2 * B * T * H, T * H, H), whh, 2, 2 * B, T, H, dg, st)
+            torch.cuda.synchronize()
+            outs.append(dg)
+        finally:
+            _lib.set_knob("CLSKD_LSTM_BWD_PIN", prev)
+    assert torch.equal(outs[0], outs[1])

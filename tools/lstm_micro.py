@@ -55,6 +55,23 @@ def main():
         print(f"bwd H={H} wave={wave}: {us:8.1f} us per layer, {us / T * 1e3:7.1f} ns per step",
               flush=True)
     _lib.set_knob("CLSKD_LSTM_BWD_WAVE", 1)
+    # the single-wave kernel with its gate-gradient reads issued together (CLSKD_LSTM_BWD_PIN)
+    for pin in (0, 1, 0, 1):
+        _lib.set_knob("CLSKD_LSTM_BWD_PIN", pin)
+        run = lambda: ops.lstm_bwd(pre, st, dh, (2 * B * T * H, T * H, H), whh, 2, 2 * B, T, H, dg, st)
+        for _ in range(2):
+            run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / 10
+        print(f"bwd H={H} wave=1 pin={pin}: {us:8.1f} us per layer, {us / T * 1e3:7.1f} ns per step",
+              flush=True)
+    _lib.set_knob("CLSKD_LSTM_BWD_PIN", 1)
 
 
 if __name__ == "__main__":
