@@ -306,6 +306,8 @@ int clskd_complex_combine_dt(const float* rr, const float* ii, const float* ir, 
  *                  bins 0..256 at 0.., imag at 257..) and the last decoder output
  *                  mask[B][256][Tm][2] read at time t+1; writes est [B][T][ldest] (real at 0..,
  *                  imag at 257.., zero tail) and optionally mask_r/mask_i [B][T][257].
+ *                  1 <= B <= 65535, T >= 1 (a block per utterance and 16 frames); the same
+ *                  bounds hold for clskd_mask_e_bwd.
  * clskd_ola:       ConviSTFT overlap-add (tools_for_model.py:95-107): frames [B][T][400] ->
  *                  wav[b][n] = (sum frames) / (sum window^2 + 1e-8), trimmed, clamp(-1,1)
  *                  (DCCRN.py:235-237) when clamp != 0.  window == NULL: the plain sum
