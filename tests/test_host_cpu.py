@@ -112,3 +112,34 @@ def test_bench_standalone_multi_gpu_launch_command():
     i = cmd.index("--master-addr")
     assert cmd[i + 1] == "127.0.0.1" and cmd[cmd.index("--master-port") + 1] == "29512"
     assert cmd[-4:] == ["--gpus", "8", "--steps", "5"] and cmd[-5].endswith("bench.py")
+
+
+def test_pack_provenance_follows_the_current_cache_entry():
+    """model.pack_provenance / pack_output (backward.tw_prebuild's source lookup): an output is
+    traced to (model, group, slot) only while it is the object the registry recorded, and
+    pack_output returns the model's current entry's slot (a re-pack replaces it)."""
+    from clskd import model as M
+
+    class Holder:
+        def __init__(self):
+            self._wcache = {}
+
+    h = Holder()
+    a, b = torch.zeros(3), torch.ones(2)
+    h._wcache["g"] = ((), (a, b), None, None)
+    M._note_pack_outputs(h, "g", (a, b))
+    assert M.pack_provenance(b) == (h, "g", 1)
+    assert M.pack_provenance(torch.zeros(2)) is None
+    assert M.pack_output(h, "g", 1, None) is b
+    a2, b2 = torch.zeros(3), torch.full((2,), 2.0)  # the next step's re-pack
+    h._wcache["g"] = ((), (a2, b2), None, None)
+    M._note_pack_outputs(h, "g", (a2, b2))
+    assert M.pack_output(h, "g", 1, None) is b2
+    assert M.pack_provenance(b2) == (h, "g", 1)
+    t = torch.zeros(4)
+    h._wcache["t"] = ((), t, None, None)
+    M._note_pack_outputs(h, "t", t)
+    assert M.pack_provenance(t) == (h, "t", None) and M.pack_output(h, "t", None, None) is t
+    tok = object()  # an entry built inside a capture serves only that capture
+    h._wcache["c"] = ((), t, tok, tok)
+    assert M.pack_output(h, "c", None, None) is None and M.pack_output(h, "c", None, tok) is t
